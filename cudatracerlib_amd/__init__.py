@@ -1,0 +1,197 @@
+"""cudatracerlib_amd — MI355X-native traversal backend for the CudaTracerLib
+hot path (BVH traversal + Woop ray/triangle intersection driven by the
+PathTracer pass loop).
+
+The product is ``_lib/libctl_trace.so`` (hand-written gfx950 HIP kernels plus
+the C-ABI of ``include/ctl_trace.h``).  This module is a thin host-side mirror
+of the reference's surface for that path:
+
+  reference                                   here
+  ------------------------------------------- ---------------------------------
+  DynamicScene (host scene, Engine/DynamicScene.h:40-188)   HostScene
+  UpdateKernel / KernelDynamicScene upload                  Tracer.upload_scene
+  __internal__IntersectBuffers (TraceHelper.cu:736-746)     Tracer.intersect_buffers
+  PathTracer::DoPass (Kernel/Tracer.h:209-248)              PathTracer.do_pass
+  k_getNumRaysTraced (TraceHelper.cu:309-314)               Tracer.rays_traced
+
+Device memory, streams and torch.distributed come from PyTorch; no torch type
+crosses the C-ABI (device pointers are passed as integers).  There is no CPU
+fallback: every compute call goes through the HIP library and raises if it is
+missing or fails.
+"""
+import ctypes as C
+
+from . import _abi
+from ._abi import (PTParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK,
+                   CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION)
+
+__all__ = ["HostScene", "Tracer", "PathTracer", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
+           "CTL_SCENE_HALF_HOST_QUIRK", "lib", "diffuse_material"]
+
+
+def lib():
+    return _abi.load()
+
+
+class CTLError(RuntimeError):
+    pass
+
+
+def _check(status, ctx=None, what=""):
+    if status != 0:
+        L = lib()
+        msg = L.ctl_last_error(ctx) if ctx is not None else L.ctl_host_last_error()
+        raise CTLError(f"{what} failed (status {status}): {msg.decode() if msg else ''}")
+
+
+def diffuse_material(r, g, b, two_sided=True):
+    m = Material()
+    m.bsdf_type = CTL_BSDF_DIFFUSE
+    m.combined_type = CTL_EDIFFUSE_REFLECTION
+    m.two_sided = 1 if two_sided else 0
+    m.node_light_index = 0xFFFFFFFF
+    m.reflectance[:] = [r, g, b]
+    return m
+
+
+class HostScene:
+    """Host-side scene compiler (the reference's DynamicScene + Mesh compile)."""
+
+    def __init__(self):
+        self._L = lib()
+        self._h = self._L.ctl_host_scene_create()
+        self.desc = None
+
+    def close(self):
+        if self._h:
+            self._L.ctl_host_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def generate(self, config, scale=1.0, width=256, height=256):
+        _check(self._L.ctl_host_scene_generate(self._h, int(config), float(scale), int(width), int(height)),
+               None, "ctl_host_scene_generate")
+        return self
+
+    def add_mesh(self, vertices, indices, materials, mat_index=None, normals=None, uvs=None):
+        import numpy as np
+        v = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+        i = np.ascontiguousarray(indices, dtype=np.uint32).reshape(-1, 3)
+        mats = (Material * len(materials))(*materials)
+        mi = None if mat_index is None else np.ascontiguousarray(mat_index, dtype=np.uint8)
+        n = None if normals is None else np.ascontiguousarray(normals, dtype=np.float32)
+        uv = None if uvs is None else np.ascontiguousarray(uvs, dtype=np.float32)
+        self._keep = getattr(self, "_keep", []) + [v, i, mi, n, uv, mats]
+        r = self._L.ctl_host_scene_add_mesh(
+            self._h, v.ctypes.data, v.shape[0], i.ctypes.data, i.shape[0],
+            None if n is None else n.ctypes.data, None if uv is None else uv.ctypes.data,
+            None if mi is None else mi.ctypes.data, mats, len(materials))
+        if r < 0:
+            _check(1, None, "add_mesh")
+        return r
+
+    def add_node(self, mesh, xf16=None):
+        arr = None
+        if xf16 is not None:
+            arr = (C.c_float * 16)(*[float(x) for x in xf16])
+        r = self._L.ctl_host_scene_add_node(self._h, mesh, arr)
+        if r < 0:
+            _check(1, None, "add_node")
+        return r
+
+    def add_area_light(self, node, local_material, radiance):
+        arr = (C.c_float * 3)(*radiance)
+        r = self._L.ctl_host_scene_add_area_light(self._h, node, local_material, arr)
+        if r < 0:
+            _check(1, None, "add_area_light")
+        return r
+
+    def set_camera(self, pos, target, up, fov_deg, width, height, near=1.0, far=100000.0):
+        f3 = C.c_float * 3
+        _check(self._L.ctl_host_scene_set_camera(self._h, f3(*pos), f3(*target), f3(*up), fov_deg, near, far,
+                                                  width, height), None, "set_camera")
+
+    def set_flags(self, flags):
+        _check(self._L.ctl_host_scene_set_flags(self._h, flags), None, "set_flags")
+
+    def compile(self, threads=0):
+        d = SceneDesc()
+        _check(self._L.ctl_host_scene_compile(self._h, threads, C.byref(d)), None, "ctl_host_scene_compile")
+        self.desc = d
+        return d
+
+
+class Tracer:
+    """Per-GPU traversal context (InitializeKernel/UpdateKernel/IntersectBuffers)."""
+
+    def __init__(self, device=0):
+        self._L = lib()
+        self._ctx = self._L.ctl_create(int(device))
+        if not self._ctx:
+            raise CTLError("ctl_create failed: " + (self._L.ctl_last_error(None) or b"").decode())
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            self._L.ctl_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload_scene(self, desc):
+        _check(self._L.ctl_scene_upload(self._ctx, C.byref(desc)), self._ctx, "ctl_scene_upload")
+
+    def generate_samples(self, pass_index, stream=0):
+        _check(self._L.ctl_sampler_generate(self._ctx, int(pass_index), stream), self._ctx, "ctl_sampler_generate")
+
+    def intersect_buffers(self, n, rays_ptr, hits_ptr, any_hit=False, stream=0):
+        _check(self._L.ctl_intersect(self._ctx, int(n), rays_ptr, hits_ptr, 1 if any_hit else 0, stream),
+               self._ctx, "ctl_intersect")
+
+    def intersect_stats(self, n, rays_ptr, hits_ptr, any_hit=False, stream=0):
+        out = (C.c_uint64 * 4)()
+        _check(self._L.ctl_intersect_stats(self._ctx, int(n), rays_ptr, hits_ptr, 1 if any_hit else 0, out, stream),
+               self._ctx, "ctl_intersect_stats")
+        return list(out)
+
+    def rays_traced(self):
+        return int(self._L.ctl_rays_traced(self._ctx))
+
+    def reset_rays(self, stream=0):
+        _check(self._L.ctl_reset_rays(self._ctx, stream), self._ctx, "ctl_reset_rays")
+
+    def sync(self, stream=0):
+        _check(self._L.ctl_sync(self._ctx, stream), self._ctx, "ctl_sync")
+
+
+class PathTracer(Tracer):
+    """PathTracer (Integrators/PathTracer.h:7-24) parameters and pass loop.
+    Defaults: Direct=1, MaxPathLength=50, RRStartDepth=5 (PathTracer.h:16-19)."""
+
+    def __init__(self, device=0, max_path_length=50, rr_start_depth=5, shadow_any_hit=True, tile_size=64,
+                 num_ranks=1, rank=0):
+        super().__init__(device)
+        self.params = PTParams(1, max_path_length, rr_start_depth, 1 if shadow_any_hit else 0, tile_size,
+                               num_ranks, rank, 0)
+
+    def do_pass(self, fb_ptr, pass_index, stream=0):
+        """UpdateKernel's sampler regeneration + one render pass into fb (device PixelData[w*h])."""
+        self.generate_samples(pass_index, stream)
+        _check(self._L.ctl_render_pass(self._ctx, C.byref(self.params), fb_ptr, stream), self._ctx,
+               "ctl_render_pass")
+
+    def pass_stats(self, fb_ptr, pass_index, stream=0):
+        self.generate_samples(pass_index, stream)
+        out = (C.c_uint64 * 4)()
+        _check(self._L.ctl_render_pass_stats(self._ctx, C.byref(self.params), fb_ptr, out, stream), self._ctx,
+               "ctl_render_pass_stats")
+        return list(out)

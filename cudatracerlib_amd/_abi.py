@@ -1,0 +1,161 @@
+"""ctypes mirror of include/ctl_trace.h (the C-ABI drop-in boundary).
+
+Layouts are byte-identical to the reference structures named in the header;
+``tests/test_abi.py`` checks every size against the C side.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libctl_trace.so")
+
+CTL_OK = 0
+CTL_SCENE_HALF_HOST_QUIRK = 1
+CTL_BSDF_DIFFUSE = 1
+CTL_EDIFFUSE_REFLECTION = 0x2
+CTL_MAX_NUM_LIGHTS = 16
+
+
+class BVHNode(C.Structure):          # BVHNodeData, 64 B
+    _fields_ = [("v", C.c_float * 16)]
+
+
+class WoopTri(C.Structure):          # TriIntersectorData, 48 B
+    _fields_ = [("v", C.c_float * 12)]
+
+
+class TriangleData(C.Structure):     # TriangleData (EXT_TRI), 32 B
+    _fields_ = [("w", C.c_uint32 * 8)]
+
+
+class KernelMesh(C.Structure):       # KernelMesh, 20 B
+    _fields_ = [("triangle_offset", C.c_uint32), ("bvh_node_offset", C.c_uint32),
+                ("bvh_triangle_offset", C.c_uint32), ("bvh_indices_offset", C.c_uint32),
+                ("std_material_offset", C.c_uint32)]
+
+
+class Node(C.Structure):             # Node, 24 B
+    _fields_ = [("mesh_index", C.c_uint32), ("material_offset", C.c_uint32),
+                ("instanced_material", C.c_uint32), ("lights", C.c_uint32 * 2), ("num_lights", C.c_uint32)]
+
+
+class Float4x4(C.Structure):
+    _fields_ = [("m", C.c_float * 16)]
+
+
+class Ray(C.Structure):              # traversalRay, 32 B
+    _fields_ = [("o", C.c_float * 3), ("tmin", C.c_float), ("d", C.c_float * 3), ("tmax", C.c_float)]
+
+
+class Hit(C.Structure):              # traversalResult, 16 B
+    _fields_ = [("dist", C.c_float), ("node_idx", C.c_int32), ("tri_idx", C.c_int32), ("bary", C.c_int32)]
+
+
+class Pixel(C.Structure):            # PixelData, 28 B
+    _fields_ = [("rgb", C.c_float * 3), ("rgb_splat", C.c_float * 3), ("weight_sum", C.c_float)]
+
+
+class Material(C.Structure):
+    _fields_ = [("bsdf_type", C.c_uint32), ("combined_type", C.c_uint32), ("two_sided", C.c_uint32),
+                ("node_light_index", C.c_uint32), ("reflectance", C.c_float * 3), ("pad", C.c_float)]
+
+
+class LightTri(C.Structure):         # ShapeSet::triData, 64 B
+    _fields_ = [("p", (C.c_float * 3) * 3), ("n", C.c_float * 3), ("area", C.c_float),
+                ("i_dat", C.c_uint32), ("t_dat", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class Light(C.Structure):
+    _fields_ = [("radiance", C.c_float * 3), ("orthogonal", C.c_uint32), ("tri_first", C.c_uint32),
+                ("tri_count", C.c_uint32), ("cdf_first", C.c_uint32), ("sum_area", C.c_float),
+                ("node_idx", C.c_uint32), ("pad", C.c_uint32 * 3)]
+
+
+class Camera(C.Structure):
+    _fields_ = [("to_world", Float4x4), ("sample_to_camera", Float4x4), ("dx", C.c_float * 3),
+                ("dy", C.c_float * 3), ("inv_resolution", C.c_float * 2), ("width", C.c_uint32),
+                ("height", C.c_uint32)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [
+        ("tri_data", C.POINTER(TriangleData)), ("n_tri_data", C.c_uint64),
+        ("woop_tris", C.POINTER(WoopTri)), ("n_woop_tris", C.c_uint64),
+        ("bvh_nodes", C.POINTER(BVHNode)), ("n_bvh_nodes", C.c_uint64),
+        ("tri_indices", C.POINTER(C.c_uint32)), ("n_tri_indices", C.c_uint64),
+        ("materials", C.POINTER(Material)), ("n_materials", C.c_uint32),
+        ("meshes", C.POINTER(KernelMesh)), ("n_meshes", C.c_uint32),
+        ("nodes", C.POINTER(Node)), ("n_nodes", C.c_uint32),
+        ("scene_bvh_nodes", C.POINTER(BVHNode)), ("n_scene_bvh_nodes", C.c_uint32),
+        ("scene_start_node", C.c_int32),
+        ("node_xf", C.POINTER(Float4x4)), ("node_inv_xf", C.POINTER(Float4x4)),
+        ("lights", C.POINTER(Light)), ("n_lights", C.c_uint32),
+        ("light_tris", C.POINTER(LightTri)), ("n_light_tris", C.c_uint32),
+        ("light_tri_cdf", C.POINTER(C.c_float)), ("n_light_tri_cdf", C.c_uint32),
+        ("light_cdf", C.c_float * CTL_MAX_NUM_LIGHTS),
+        ("env_map_index", C.c_uint32),
+        ("box_min", C.c_float * 3), ("box_max", C.c_float * 3),
+        ("ray_eps", C.c_float),
+        ("camera", Camera),
+        ("flags", C.c_uint32),
+    ]
+
+
+class PTParams(C.Structure):
+    _fields_ = [("direct", C.c_int32), ("max_path_length", C.c_int32), ("rr_start_depth", C.c_int32),
+                ("shadow_any_hit", C.c_int32), ("tile_size", C.c_uint32), ("num_ranks", C.c_uint32),
+                ("rank", C.c_uint32), ("flags", C.c_uint32)]
+
+
+# Every symbol include/ctl_trace.h declares: (name, restype, argtypes)
+_vp = C.c_void_p
+SYMBOLS = [
+    ("ctl_abi_version", C.c_int32, []),
+    ("ctl_create", _vp, [C.c_int32]),
+    ("ctl_destroy", None, [_vp]),
+    ("ctl_last_error", C.c_char_p, [_vp]),
+    ("ctl_scene_upload", C.c_int32, [_vp, C.POINTER(SceneDesc)]),
+    ("ctl_sampler_generate", C.c_int32, [_vp, C.c_uint64, _vp]),
+    ("ctl_sampler_upload", C.c_int32, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
+    ("ctl_intersect", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, _vp]),
+    ("ctl_render_pass", C.c_int32, [_vp, C.POINTER(PTParams), _vp, _vp]),
+    ("ctl_rays_traced", C.c_uint64, [_vp]),
+    ("ctl_reset_rays", C.c_int32, [_vp, _vp]),
+    ("ctl_sync", C.c_int32, [_vp, _vp]),
+    ("ctl_intersect_stats", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, C.POINTER(C.c_uint64), _vp]),
+    ("ctl_render_pass_stats", C.c_int32, [_vp, C.POINTER(PTParams), _vp, C.POINTER(C.c_uint64), _vp]),
+    ("ctl_woop_set", None, [_vp, _vp, _vp, C.POINTER(WoopTri)]),
+    ("ctl_host_sampler_tables", C.c_int32, [C.c_uint64, C.c_uint32, C.c_uint32, _vp, _vp]),
+    ("ctl_host_scene_create", _vp, []),
+    ("ctl_host_scene_destroy", None, [_vp]),
+    ("ctl_host_scene_add_mesh", C.c_int32, [_vp, _vp, C.c_uint32, _vp, C.c_uint32, _vp, _vp, _vp,
+                                            C.POINTER(Material), C.c_uint32]),
+    ("ctl_host_scene_add_node", C.c_int32, [_vp, C.c_uint32, _vp]),
+    ("ctl_host_scene_add_area_light", C.c_int32, [_vp, C.c_uint32, C.c_uint32, _vp]),
+    ("ctl_host_scene_set_camera", C.c_int32, [_vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
+                                              C.c_uint32, C.c_uint32]),
+    ("ctl_host_scene_set_flags", C.c_int32, [_vp, C.c_uint32]),
+    ("ctl_host_scene_compile", C.c_int32, [_vp, C.c_uint32, C.POINTER(SceneDesc)]),
+    ("ctl_host_last_error", C.c_char_p, []),
+    ("ctl_host_scene_generate", C.c_int32, [_vp, C.c_int32, C.c_double, C.c_uint32, C.c_uint32]),
+]
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libctl_trace.so and bind every declared symbol.  Raises loudly if
+    the HIP extension was not built: there is no fallback path."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libctl_trace.so not built ({path}); run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(path)
+    for name, res, args in SYMBOLS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path == LIB_PATH:
+        _lib = lib
+    return lib

@@ -1,0 +1,281 @@
+// traverse.h — gfx950 two-level BVH traversal + Woop intersection.
+//
+// Semantics are those of the reference's __traceRay_internal__<false>
+// (Kernel/TraceHelper.cu:88-172) and intersectKernel<ANY_HIT>
+// (TraceHelper.cu:326-734): Aila–Laine while-while traversal of the instance
+// BVH, per-instance ray transform by the inverse node matrix, while-while
+// traversal of the mesh BVH, Woop test per leaf entry until the last-in-leaf
+// flag, postponing one leaf, wave-wide exit of the inner-node loop once every
+// active lane holds a postponed leaf (ballot; reference: vote.ballot,
+// BVHTraversal.h:92-105).  Box spans use the same integer min/max on the fp32
+// bit patterns (kepler_math, Math/MathFunc.h:402-445 -> v_min3/v_max3_i32).
+//
+// MI355X-specific structure:
+//  * one traversal stack per lane for BOTH levels; the 16 most recent entries
+//    live in LDS ([entry][thread] layout: consecutive lanes hit consecutive
+//    banks), deeper entries spill to a private scratch array;
+//  * level switch without a second stack: entering an instance pushes the
+//    pending top-level node and a sentinel; the mesh level ends when that
+//    sentinel (or a sentinel child, as in the reference) comes up;
+//  * node = 4 x 16-B loads, Woop triangle = 3 x 16-B loads (dwordx4);
+//  * no FMA contraction (-ffp-contract=off) => bit-identical to the CPU oracle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "../ctl_shade.h"
+
+namespace ctl {
+
+#define CTL_SENTINEL 0x76543210
+
+constexpr int kLdsStack = 16;
+constexpr int kStackMax = 128;
+
+struct DevScene {
+    const float4* bvh;          // mesh BVHNodeData, float4 units
+    const float4* woop;         // TriIntersectorData, float4 units
+    const uint32_t* tri_idx;    // TriIntersectorData2
+    const ctl_triangle_data* tri_data;
+    const ctl_material* mats;
+    const ctl_kernel_mesh* meshes;
+    const ctl_node* nodes;
+    const float4* scene_bvh;    // instance BVH
+    const float4* xf;           // node transforms, 4 float4 rows each
+    const float4* inv_xf;
+    const ctl_light* lights;
+    const ctl_light_tri* light_tris;
+    const float* light_tri_cdf;
+    const float4* normal_lut;   // 65536 decoded spherical normals (Compression.h:20-31)
+    uint32_t n_nodes;
+    int32_t start_node;
+    uint32_t n_lights;
+    uint32_t flags;
+    float ray_eps;
+    float light_cdf[CTL_MAX_NUM_LIGHTS];
+    ctl_camera camera;
+};
+
+struct TraceStats { uint32_t nodes, tris, inst; };
+
+struct HitRec {
+    float t, u, v;
+    uint32_t tri, node;
+};
+
+__device__ __forceinline__ int imin3(int a, int b, int c) { return min(min(a, b), c); }
+__device__ __forceinline__ int imax3(int a, int b, int c) { return max(max(a, b), c); }
+
+__device__ __forceinline__ float span_begin(float a0, float a1, float b0, float b1, float c0, float c1, float d) {
+    return __int_as_float(imax3(__float_as_int(tmin(a0, a1)), __float_as_int(tmin(b0, b1)),
+                                max(min(__float_as_int(c0), __float_as_int(c1)), __float_as_int(d))));
+}
+__device__ __forceinline__ float span_end(float a0, float a1, float b0, float b1, float c0, float c1, float d) {
+    return __int_as_float(imin3(__float_as_int(tmax(a0, a1)), __float_as_int(tmax(b0, b1)),
+                                min(max(__float_as_int(c0), __float_as_int(c1)), __float_as_int(d))));
+}
+
+struct LaneStack {
+    int* lds;       // &s_stack[0][tid], stride = block size
+    int stride;
+    int spill[kStackMax - kLdsStack];
+    int sp;
+    bool overflow;
+    __device__ __forceinline__ void push(int v) {
+        if (sp < kLdsStack) lds[sp * stride] = v;
+        else if (sp < kStackMax) spill[sp - kLdsStack] = v;
+        else overflow = true;
+        sp++;
+    }
+    __device__ __forceinline__ int pop() {
+        --sp;
+        if (sp < 0) { sp = 0; return CTL_SENTINEL; }
+        if (sp < kLdsStack) return lds[sp * stride];
+        if (sp < kStackMax) return spill[sp - kLdsStack];
+        return CTL_SENTINEL;
+    }
+};
+
+struct RayLocal {
+    float ox, oy, oz, dx, dy, dz;
+    float idx, idy, idz, oodx, oody, oodz;
+    __device__ __forceinline__ void set(float px, float py, float pz, float qx, float qy, float qz) {
+        ox = px; oy = py; oz = pz; dx = qx; dy = qy; dz = qz;
+        const float ooeps = 0x1p-80f;   // exp2(-80), TraceHelper.cu:412
+        idx = 1.0f / (fabsf(qx) > ooeps ? qx : copysign_ref(ooeps, qx));
+        idy = 1.0f / (fabsf(qy) > ooeps ? qy : copysign_ref(ooeps, qy));
+        idz = 1.0f / (fabsf(qz) > ooeps ? qz : copysign_ref(ooeps, qz));
+        oodx = ox * idx; oody = oy * idy; oodz = oz * idz;
+    }
+};
+
+// Transform by a row-major float4x4 given as 4 float4 rows (float4x4.h:398-408).
+__device__ __forceinline__ void xform_rows(const float4* M, f3 p, f3 d, f3& po, f3& doo) {
+    float4 r0 = M[0], r1 = M[1], r2 = M[2], r3 = M[3];
+    m44 m;
+    m.d[0] = r0.x; m.d[1] = r0.y; m.d[2] = r0.z; m.d[3] = r0.w;
+    m.d[4] = r1.x; m.d[5] = r1.y; m.d[6] = r1.z; m.d[7] = r1.w;
+    m.d[8] = r2.x; m.d[9] = r2.y; m.d[10] = r2.z; m.d[11] = r2.w;
+    m.d[12] = r3.x; m.d[13] = r3.y; m.d[14] = r3.z; m.d[15] = r3.w;
+    doo = xform_dir(m, d);
+    po = xform_point(m, p);
+}
+
+// Closest (ANY=false) or any (ANY=true) hit with tmin_tri < t < h.t.  Box
+// spans start at span_tmin.  h must be initialised by the caller (t = tmax,
+// tri = node = UINT_MAX).  Returns false if the lane overflowed its stack.
+template <bool ANY, bool STATS>
+__device__ bool trace_ray_dev(const DevScene& S, f3 ori, f3 dir, float span_tmin, float tri_tmin, HitRec& h,
+                              LaneStack& st, TraceStats* stats) {
+    if (S.n_nodes == 0) return true;
+    RayLocal world, cur;
+    world.set(ori.x, ori.y, ori.z, dir.x, dir.y, dir.z);
+    cur = world;
+    st.sp = 0;
+    st.overflow = false;
+    st.push(CTL_SENTINEL);
+    int level = 0;
+    int meshSent = 0;
+    int nodeAddr, leafAddr;
+    if (S.start_node < 0) { leafAddr = S.start_node; nodeAddr = CTL_SENTINEL; }
+    else { leafAddr = 0; nodeAddr = S.start_node; }
+    const float4* nodes = S.scene_bvh;
+    uint32_t nodeBase = 0, triBase = 0, idxBase = 0, triOffset = 0, instIdx = 0;
+    bool done = false;
+    bool resumeLeaves = false;   // back from an instance with a second postponed top-level leaf
+
+    while (!done) {
+        // ---- inner nodes until every active lane holds a postponed leaf
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
+            const float4* n = nodes + nodeBase + nodeAddr;
+            const float4 n0xy = n[0];
+            const float4 n1xy = n[1];
+            const float4 nz = n[2];
+            const float4 tmp = n[3];
+            if (STATS) stats->nodes++;
+            int c0i = __float_as_int(tmp.x), c1i = __float_as_int(tmp.y);
+            const float c0lox = n0xy.x * cur.idx - cur.oodx;
+            const float c0hix = n0xy.y * cur.idx - cur.oodx;
+            const float c0loy = n0xy.z * cur.idy - cur.oody;
+            const float c0hiy = n0xy.w * cur.idy - cur.oody;
+            const float c0loz = nz.x * cur.idz - cur.oodz;
+            const float c0hiz = nz.y * cur.idz - cur.oodz;
+            const float c1loz = nz.z * cur.idz - cur.oodz;
+            const float c1hiz = nz.w * cur.idz - cur.oodz;
+            const float c0min = span_begin(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, span_tmin);
+            const float c0max = span_end(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, h.t);
+            const float c1lox = n1xy.x * cur.idx - cur.oodx;
+            const float c1hix = n1xy.y * cur.idx - cur.oodx;
+            const float c1loy = n1xy.z * cur.idy - cur.oody;
+            const float c1hiy = n1xy.w * cur.idy - cur.oody;
+            const float c1min = span_begin(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, span_tmin);
+            const float c1max = span_end(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, h.t);
+            bool swp = (c1min < c0min);
+            bool tc0 = (c0max >= c0min);
+            bool tc1 = (c1max >= c1min);
+            if (!tc0 && !tc1) {
+                nodeAddr = st.pop();
+            } else {
+                nodeAddr = tc0 ? c0i : c1i;
+                if (tc0 && tc1) {
+                    if (swp) { int t = nodeAddr; nodeAddr = c1i; c1i = t; }
+                    st.push(c1i);
+                }
+            }
+            if (nodeAddr < 0 && leafAddr >= 0) {
+                leafAddr = nodeAddr;
+                nodeAddr = st.pop();
+            }
+            if (!__any(leafAddr >= 0)) break;
+        }
+        // ---- postponed leaves
+        resumeLeaves = false;
+        bool entered = false;
+        while (leafAddr < 0) {
+            if (level == 1) {
+                if (leafAddr != -214783648) {
+                    for (int triAddr = ~leafAddr;; triAddr++) {
+                        const float4* tv = S.woop + triBase + (uint32_t)triAddr * 3u;
+                        const float4 v00 = tv[0];
+                        const float4 v11 = tv[1];
+                        const float4 v22 = tv[2];
+                        const uint32_t index = S.tri_idx[idxBase + (uint32_t)triAddr];
+                        if (STATS) stats->tris++;
+                        float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
+                        float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
+                        float t = Oz * invDz;
+                        if (t > tri_tmin && t < h.t) {
+                            float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
+                            float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
+                            float u = Ox + t * Dx;
+                            if (u >= 0.0f) {
+                                float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
+                                float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
+                                float v = Oy + t * Dy;
+                                if (v >= 0.0f && u + v <= 1.0f) {
+                                    h.node = instIdx;
+                                    h.tri = (index >> 1) + triOffset;
+                                    h.u = u;
+                                    h.v = v;
+                                    h.t = t;
+                                    if (ANY) { done = true; break; }
+                                }
+                            }
+                        }
+                        if (index & 1) break;
+                    }
+                    if (done) break;
+                }
+                leafAddr = nodeAddr;
+                if (nodeAddr < 0) nodeAddr = st.pop();
+            } else {
+                if (leafAddr != -214783648) {
+                    // enter instance ~leafAddr (TraceHelper.cu:91-100, 528-561)
+                    instIdx = (uint32_t)(~leafAddr);
+                    if (STATS) stats->inst++;
+                    const ctl_node& N = S.nodes[instIdx];
+                    const ctl_kernel_mesh& M = S.meshes[N.mesh_index];
+                    nodeBase = M.bvh_node_offset;
+                    triBase = M.bvh_triangle_offset;
+                    idxBase = M.bvh_indices_offset;
+                    triOffset = M.triangle_offset;
+                    f3 o2, d2;
+                    xform_rows(S.inv_xf + 4 * instIdx, mk3(world.ox, world.oy, world.oz),
+                               mk3(world.dx, world.dy, world.dz), o2, d2);
+                    cur.set(o2.x, o2.y, o2.z, d2.x, d2.y, d2.z);
+                    st.push(nodeAddr);        // pending top-level work
+                    meshSent = st.sp;
+                    st.push(CTL_SENTINEL);    // bottom of the mesh-level stack
+                    nodes = S.bvh;
+                    level = 1;
+                    nodeAddr = 0;             // mesh root (TraceHelper.cu:170)
+                    leafAddr = 0;
+                    entered = true;
+                    break;
+                }
+                leafAddr = nodeAddr;
+                if (nodeAddr < 0) nodeAddr = st.pop();
+            }
+        }
+        if (done) break;
+        if (entered) continue;
+        if (nodeAddr == CTL_SENTINEL) {
+            if (level == 1) {
+                // mesh traversal finished (bottom sentinel or a sentinel child)
+                st.sp = meshSent;
+                int saved = st.pop();
+                level = 0;
+                nodes = S.scene_bvh;
+                nodeBase = 0;
+                cur = world;
+                leafAddr = saved;
+                nodeAddr = saved;
+                if (saved < 0) nodeAddr = st.pop();
+                resumeLeaves = leafAddr < 0;   // the reference's leaf loop continues right away
+            } else {
+                break;
+            }
+        }
+    }
+    return !st.overflow;
+}
+
+}  // namespace ctl

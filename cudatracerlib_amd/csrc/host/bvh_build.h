@@ -1,0 +1,39 @@
+// bvh_build.h — parallel binned-SAH BVH builder emitting the reference's
+// BVHNodeData / TriIntersectorData2 layout (Engine/TriIntersectorData.h:8-117)
+// in the DFS order of SplitBVHBuilder's handleNode (SplitBVHBuilder.cpp:163-203):
+//   inner node k -> child value 4*k (float4 offset), leaf -> ~first leaf entry,
+//   leaf entries numbered in DFS order, last entry of a leaf flagged (bit 0),
+//   a root that is a single leaf -> one inner node {leaf, 0x76543210} whose
+//   right box is the zero box (handleNode's level-0 branch).
+#pragma once
+#include <cstdint>
+#include <vector>
+#include "../../../include/ctl_trace.h"
+
+namespace ctl {
+
+struct Box { float lo[3], hi[3]; };
+
+struct BvhBuildParams {
+    uint32_t max_leaf = 8;        // Platform::m_maxLeafSize = 8 (BVHBuilderHelper.cpp:119,136)
+    uint32_t bins = 32;           // binned SAH (the reference sweeps sorted refs)
+    uint32_t threads = 0;         // 0 = hardware concurrency
+    uint32_t median_depth = 40;   // beyond this depth: median splits (bounds depth <= 64)
+    bool leaf_size_one = false;   // top-level (instance) BVH: one object per leaf, leaf = ~object
+};
+
+struct BvhOutput {
+    std::vector<ctl_bvh_node> nodes;     // inner nodes
+    std::vector<uint32_t> leaf_objects;  // object id of each leaf entry (DFS order)
+    std::vector<uint8_t> leaf_last;      // 1 if entry is the last of its leaf
+    int32_t start_node = 0x76543210;     // root value (inner: 0, single object w/ leaf_size_one: ~obj)
+    uint32_t max_depth = 0;
+    Box root_box;
+};
+
+// Builds over object boxes (`boxes[i]`), `n` objects.  Degenerate boxes
+// (min extent < 0 or a line/point: sum(size)==max(size)) are dropped like the
+// reference's "Remove degenerates" step (SplitBVHBuilder.cpp:296-303).
+void build_bvh(const Box* boxes, uint32_t n, const BvhBuildParams& p, BvhOutput& out);
+
+}  // namespace ctl

@@ -1,0 +1,457 @@
+// scene.cpp — host scene compiler (ctl_host_scene_* of include/ctl_trace.h).
+// Produces exactly the arrays the reference's host code hands to the device:
+//   Mesh::CompileMesh / ConstructBVH  (Engine/Mesh.cpp:199-290, BVHBuilderHelper.cpp:129-147)
+//   TriangleData(P, mat, T, N)        (Engine/TriangleData.cu:10-68)
+//   DynamicScene::CreateLight/Shape   (Engine/DynamicScene.cpp:689-766), ShapeSet (Engine/ShapeSet.cpp)
+//   SceneBVH transforms               (Engine/SceneBVH.cpp:56-100)
+//   LightStream::fillDeviceData       (Engine/DynamicScene.cpp:173-196)
+//   getKernelSceneData eps            (Engine/DynamicScene.cpp:587)
+#include "scene.h"
+#include "bvh_build.h"
+#include "../ctl_shade.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <thread>
+
+namespace ctl {
+
+static thread_local std::string g_host_error;
+void set_host_error(const std::string& s) { g_host_error = s; }
+
+void woop_set(f3 a, f3 b, f3 c, ctl_woop_tri& out) {
+    m44 m;
+    m.set_col(0, mk4(a - c, 0));
+    m.set_col(1, mk4(b - c, 0));
+    m.set_col(2, mk4(cross(a - c, b - c), 0));
+    m.set_col(3, mk4(c, 1));
+    m = inverse(m);
+    f4 A = mk4(m.at(2, 0), m.at(2, 1), m.at(2, 2), -m.at(2, 3));
+    f4 B = m.row(0), C = m.row(1);
+    float v[12] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, C.x, C.y, C.z, C.w};
+    memcpy(out.v, v, sizeof(v));
+}
+
+void woop_get(const ctl_woop_tri& in, f3& v0, f3& v1, f3& v2) {
+    m44 m = m44_identity();
+    m.set_row(0, mk4(in.v[4], in.v[5], in.v[6], in.v[7]));
+    m.set_row(1, mk4(in.v[8], in.v[9], in.v[10], in.v[11]));
+    m.set_row(2, mk4(in.v[0], in.v[1], in.v[2], in.v[3]));
+    m.at(2, 3) *= -1.0f;
+    m = inverse(m);
+    f3 e02 = xyz(m.col(0)), e12 = xyz(m.col(1));
+    v2 = xyz(m.col(3));
+    v0 = v2 + e02;
+    v1 = v2 + e12;
+}
+
+void camera_setup(const float pos[3], const float tar[3], const float up[3], float fov_deg, float nearc, float farc,
+                  uint32_t w, uint32_t h, ctl_camera& out) {
+    f3 p = mk3(pos[0], pos[1], pos[2]), t = mk3(tar[0], tar[1], tar[2]), u = mk3(up[0], up[1], up[2]);
+    f3 f = normalize(t - p);
+    f3 r = normalize(cross(f, u));
+    m44 view = m44_identity();
+    view.set_col(0, mk4(r, 0)); view.set_col(1, mk4(u, 0)); view.set_col(2, mk4(f, 0));
+    view.set_col(3, mk4(0, 0, 0, 1)); view.set_row(3, mk4(0, 0, 0, 1));
+    m44 tr = m44_identity(); tr.at(0, 3) = p.x; tr.at(1, 3) = p.y; tr.at(2, 3) = p.z;
+    m44 toWorld = matmul(tr, view);                                  // Translate(pos) % rot
+    float resx = (float)w, resy = (float)h;
+    float invx = 1.0f / resx, invy = 1.0f / resy;                    // Vec2f(1) / m_resolution
+    float aspect = resx / resy;
+    float fov = ((float)CTL_PI / 180.f) * fov_deg;                   // math::Radians
+    m44 sc = m44_identity(); sc.at(0, 0) = -0.5f; sc.at(1, 1) = -0.5f * aspect; sc.at(2, 2) = 1.0f;
+    m44 tl = m44_identity(); tl.at(0, 3) = -1.0f; tl.at(1, 3) = -1.0f / aspect; tl.at(2, 3) = 0.0f;
+    float recip = 1.0f / (farc - nearc);                             // float4x4::Perspective
+    float cot = 1.0f / cr_tan(fov / 2.0f);
+    m44 pe = m44_zero();
+    pe.at(0, 0) = cot; pe.at(1, 1) = cot; pe.at(2, 2) = farc * recip; pe.at(2, 3) = -nearc * farc * recip;
+    pe.at(3, 2) = 1;
+    m44 c2s = matmul(matmul(sc, tl), pe);
+    m44 s2c = inverse(c2s);
+    f3 dx = xform_point(s2c, mk3(invx, 0.0f, 0.0f)) - xform_point(s2c, mk3s(0.0f));
+    f3 dy = xform_point(s2c, mk3(0.0f, invy, 0.0f)) - xform_point(s2c, mk3s(0.0f));
+    memcpy(out.to_world.m, toWorld.d, 64);
+    memcpy(out.sample_to_camera.m, s2c.d, 64);
+    out.dx[0] = dx.x; out.dx[1] = dx.y; out.dx[2] = dx.z;
+    out.dy[0] = dy.x; out.dy[1] = dy.y; out.dy[2] = dy.z;
+    out.inv_resolution[0] = invx; out.inv_resolution[1] = invy;
+    out.width = w; out.height = h;
+}
+
+namespace {
+
+uint16_t float_to_half(float f) {   // Math/half.h:21-60, host branch
+    uint32_t ia; memcpy(&ia, &f, 4);
+    uint16_t ir = (ia >> 16) & 0x8000;
+    if ((ia & 0x7f800000) == 0x7f800000) {
+        if ((ia & 0x7fffffff) == 0x7f800000) ir |= 0x7c00;
+        else ir = 0x7fff;
+    } else if ((ia & 0x7f800000) >= 0x33000000) {
+        int shift = (int)((ia >> 23) & 0xff) - 127;
+        if (shift > 15) ir |= 0x7c00;
+        else {
+            ia = (ia & 0x007fffff) | 0x00800000;
+            if (shift < -14) { ir |= ia >> (-1 - shift); ia = ia << (32 - (-1 - shift)); }
+            else { ir |= ia >> (24 - 11); ia = ia << (32 - (24 - 11)); ir = ir + ((14 + shift) << 10); }
+            if ((ia > 0x80000000u) || ((ia == 0x80000000u) && (ir & 1))) ir++;
+        }
+    }
+    return ir;
+}
+
+uint16_t normal_encode16(f3 v) {   // NormalizedFloat3ToUchar2_Spherical (Math/Compression.h:12-18)
+    float theta = (cr_acos(v.z) * (255.0f / CTL_PI));
+    float phi = (cr_atan2(v.y, v.x) * (255.0f / (2.0f * CTL_PI)));
+    phi = phi < 0 ? (phi + 255) : phi;
+    return (uint16_t)(((uint16_t)theta << 8) | (uint16_t)phi);
+}
+
+// TriangleData(P, matIndex, T, N) (TriangleData.cu:10-68); UVs decoded with the
+// host half decode, as the reference's compile step always runs on the host.
+void triangle_data(const f3 P[3], uint8_t mat, const f2 T[3], const f3 N[3], ctl_triangle_data& out) {
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    w[1] = (uint32_t)mat << 16;
+    for (int i = 0; i < 3; i++)
+        w[5 + i] = (uint32_t)float_to_half(T[i].x) | ((uint32_t)float_to_half(T[i].y) << 16);
+    f2 t0 = mk2(half_to_float(w[5] & 0xffff, true), half_to_float(w[5] >> 16, true));
+    f2 t1 = mk2(half_to_float(w[6] & 0xffff, true), half_to_float(w[6] >> 16, true));
+    f2 t2 = mk2(half_to_float(w[7] & 0xffff, true), half_to_float(w[7] >> 16, true));
+    f3 dP1 = P[1] - P[0], dP2 = P[2] - P[0];
+    f2 dUV1 = t1 - t0, dUV2 = t2 - t0;
+    float determinant = dUV1.x * dUV2.y - dUV1.y * dUV2.x;
+    f3 dpdu, dpdv;
+    if (determinant == 0) {
+        f3 a, b, n = normalize(cross(dP1, dP2));
+        coordinate_system(n, a, b);
+        dpdu = a; dpdv = b;
+    } else {
+        float invDet = 1.0f / determinant;
+        dpdu = ((dUV2.y * dP1 - dUV1.y * dP2) * invDet);
+        dpdv = ((-dUV2.x * dP1 + dUV1.x * dP2) * invDet);
+    }
+    w[0] = (uint32_t)normal_encode16(N[0]) | ((uint32_t)normal_encode16(N[1]) << 16);
+    w[1] = (uint32_t)normal_encode16(N[2]) | (w[1] & 0xffff0000u);
+    w[2] = float_to_half(dpdu.x) | ((uint32_t)float_to_half(dpdu.y) << 16);
+    w[3] = float_to_half(dpdu.z) | ((uint32_t)float_to_half(dpdv.x) << 16);
+    w[4] = float_to_half(dpdv.y) | ((uint32_t)float_to_half(dpdv.z) << 16);
+    memcpy(out.w, w, 32);
+}
+
+template <class F>
+void parallel_for(uint64_t n, uint32_t threads, F f) {
+    if (threads <= 1 || n < 4096) { f(0, n); return; }
+    std::vector<std::thread> ts;
+    uint64_t chunk = (n + threads - 1) / threads;
+    for (uint32_t t = 0; t < threads; t++) {
+        uint64_t b = std::min(n, (uint64_t)t * chunk), e = std::min(n, b + chunk);
+        if (b < e) ts.emplace_back([=] { f(b, e); });
+    }
+    for (auto& t : ts) t.join();
+}
+
+struct NormalDecodeHost {
+    f3 operator()(uint32_t c) const { return normal_decode16(c); }
+};
+
+}  // namespace
+}  // namespace ctl
+
+using namespace ctl;
+
+extern "C" {
+
+CTL_API const char* ctl_host_last_error(void) { return g_host_error.c_str(); }
+
+CTL_API void ctl_woop_set(const float v0[3], const float v1[3], const float v2[3], ctl_woop_tri* out) {
+    woop_set(mk3(v0[0], v0[1], v0[2]), mk3(v1[0], v1[1], v1[2]), mk3(v2[0], v2[1], v2[2]), *out);
+}
+
+CTL_API ctl_host_scene* ctl_host_scene_create(void) { return new ctl_host_scene(); }
+CTL_API void ctl_host_scene_destroy(ctl_host_scene* s) { delete s; }
+
+CTL_API int32_t ctl_host_scene_add_mesh(ctl_host_scene* s, const float* vertices, uint32_t n_vertices,
+                                        const uint32_t* indices, uint32_t n_triangles, const float* normals,
+                                        const float* uvs, const uint8_t* mat_index, const ctl_material* materials,
+                                        uint32_t n_materials) {
+    if (!s || !vertices || !indices || n_materials == 0 || n_materials > 255) {
+        set_host_error("add_mesh: invalid arguments (need vertices, indices, 1..255 materials)");
+        return -1;
+    }
+    for (uint64_t i = 0; i < 3ull * n_triangles; i++)
+        if (indices[i] >= n_vertices) { set_host_error("add_mesh: index out of range"); return -1; }
+    if (mat_index)
+        for (uint32_t i = 0; i < n_triangles; i++)
+            if (mat_index[i] >= n_materials) { set_host_error("add_mesh: material index out of range"); return -1; }
+    ctl_host_scene::Mesh m;
+    m.v.assign(vertices, vertices + 3ull * n_vertices);
+    m.idx.assign(indices, indices + 3ull * n_triangles);
+    if (normals) m.n.assign(normals, normals + 3ull * n_vertices);
+    if (uvs) m.uv.assign(uvs, uvs + 2ull * n_vertices);
+    if (mat_index) m.mat.assign(mat_index, mat_index + n_triangles);
+    m.materials.assign(materials, materials + n_materials);
+    s->meshes.push_back(std::move(m));
+    return (int32_t)s->meshes.size() - 1;
+}
+
+CTL_API int32_t ctl_host_scene_add_node(ctl_host_scene* s, uint32_t mesh, const float* xf16) {
+    if (!s || mesh >= s->meshes.size()) { set_host_error("add_node: bad mesh index"); return -1; }
+    ctl_host_scene::Node n;
+    n.mesh = mesh;
+    n.has_xf = xf16 != nullptr;
+    n.xf = m44_identity();
+    if (xf16) memcpy(n.xf.d, xf16, 64);
+    s->nodes.push_back(n);
+    return (int32_t)s->nodes.size() - 1;
+}
+
+CTL_API int32_t ctl_host_scene_add_area_light(ctl_host_scene* s, uint32_t node, uint32_t local_material,
+                                              const float radiance[3]) {
+    if (!s || node >= s->nodes.size()) { set_host_error("add_area_light: bad node"); return -1; }
+    const auto& mesh = s->meshes[s->nodes[node].mesh];
+    if (local_material >= mesh.materials.size()) { set_host_error("add_area_light: bad material"); return -1; }
+    uint32_t perNode = 0;
+    for (auto& l : s->lights) perNode += l.node == node;
+    if (perNode >= 2) { set_host_error("add_area_light: MAX_AREALIGHT_NUM (2) lights per node"); return -1; }
+    if (s->lights.size() >= CTL_MAX_NUM_LIGHTS) { set_host_error("add_area_light: MAX_NUM_LIGHTS (16)"); return -1; }
+    ctl_host_scene::Light l{node, local_material, {radiance[0], radiance[1], radiance[2]}};
+    s->lights.push_back(l);
+    return (int32_t)s->lights.size() - 1;
+}
+
+CTL_API ctl_status ctl_host_scene_set_camera(ctl_host_scene* s, const float pos[3], const float target[3],
+                                             const float up[3], float fov_deg, float near_clip, float far_clip,
+                                             uint32_t width, uint32_t height) {
+    if (!s || width == 0 || height == 0) return CTL_ERR_INVALID;
+    memcpy(s->cam_pos, pos, 12); memcpy(s->cam_tar, target, 12); memcpy(s->cam_up, up, 12);
+    s->cam_fov = fov_deg; s->cam_near = near_clip; s->cam_far = far_clip;
+    s->cam_w = width; s->cam_h = height;
+    s->has_camera = true;
+    return CTL_OK;
+}
+
+CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags) {
+    if (!s) return CTL_ERR_INVALID;
+    s->flags = flags;
+    return CTL_OK;
+}
+
+CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, ctl_scene_desc* out) {
+    if (!s || !out) return CTL_ERR_INVALID;
+    if (!s->has_camera) { set_host_error("compile: no camera"); return CTL_ERR_INVALID; }
+    if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
+    s->tri_data.clear(); s->woop.clear(); s->bvh_nodes.clear(); s->tri_indices.clear(); s->materials.clear();
+    s->kmeshes.clear(); s->knodes.clear(); s->scene_bvh.clear(); s->xf.clear(); s->inv_xf.clear();
+    s->klights.clear(); s->light_tris.clear(); s->light_tri_cdf.clear();
+    s->max_mesh_depth = 0;
+
+    std::vector<Box> meshBox(s->meshes.size());
+    // --- per mesh: BVH, Woop entries, TriangleData, materials
+    for (size_t mi = 0; mi < s->meshes.size(); mi++) {
+        const auto& M = s->meshes[mi];
+        uint32_t ntri = (uint32_t)(M.idx.size() / 3);
+        auto V = [&](uint32_t vi) { return mk3(M.v[3 * vi], M.v[3 * vi + 1], M.v[3 * vi + 2]); };
+        std::vector<Box> boxes(ntri);
+        parallel_for(ntri, threads, [&](uint64_t b, uint64_t e) {
+            for (uint64_t t = b; t < e; t++) {
+                Box& bx = boxes[t];
+                for (int k = 0; k < 3; k++) { bx.lo[k] = FLT_MAX; bx.hi[k] = -FLT_MAX; }
+                for (int c = 0; c < 3; c++) {
+                    f3 p = V(M.idx[3 * t + c]);
+                    float q[3] = {p.x, p.y, p.z};
+                    for (int k = 0; k < 3; k++) { bx.lo[k] = tmin(bx.lo[k], q[k]); bx.hi[k] = tmax(bx.hi[k], q[k]); }
+                }
+            }
+        });
+        BvhBuildParams bp;
+        bp.threads = threads;
+        BvhOutput bo;
+        build_bvh(boxes.data(), ntri, bp, bo);
+        s->max_mesh_depth = std::max(s->max_mesh_depth, bo.max_depth);
+        meshBox[mi] = bo.root_box;
+
+        ctl_kernel_mesh km;
+        km.triangle_offset = (uint32_t)s->tri_data.size();
+        km.bvh_node_offset = (uint32_t)(s->bvh_nodes.size() * 4);
+        km.bvh_triangle_offset = (uint32_t)(s->woop.size() * 3);
+        km.bvh_indices_offset = (uint32_t)s->woop.size();
+        km.std_material_offset = (uint32_t)s->materials.size();
+        s->kmeshes.push_back(km);
+
+        s->bvh_nodes.insert(s->bvh_nodes.end(), bo.nodes.begin(), bo.nodes.end());
+        size_t e0 = s->woop.size(), ne = bo.leaf_objects.size();
+        s->woop.resize(e0 + ne);
+        s->tri_indices.resize(e0 + ne);
+        parallel_for(ne, threads, [&](uint64_t b, uint64_t e) {
+            for (uint64_t i = b; i < e; i++) {
+                uint32_t t = bo.leaf_objects[i];
+                woop_set(V(M.idx[3 * t]), V(M.idx[3 * t + 1]), V(M.idx[3 * t + 2]), s->woop[e0 + i]);
+                s->tri_indices[e0 + i] = (t << 1) | (bo.leaf_last[i] ? 1u : 0u);
+            }
+        });
+        size_t t0 = s->tri_data.size();
+        s->tri_data.resize(t0 + ntri);
+        parallel_for(ntri, threads, [&](uint64_t b, uint64_t e) {
+            for (uint64_t t = b; t < e; t++) {
+                f3 P[3]; f2 T[3]; f3 N[3];
+                for (int c = 0; c < 3; c++) {
+                    uint32_t vi = M.idx[3 * t + c];
+                    P[c] = V(vi);
+                    T[c] = M.uv.empty() ? mk2(0, 0) : mk2(M.uv[2 * vi], M.uv[2 * vi + 1]);
+                }
+                f3 fn = normalize(cross(P[1] - P[0], P[2] - P[0]));
+                for (int c = 0; c < 3; c++) {
+                    uint32_t vi = M.idx[3 * t + c];
+                    N[c] = M.n.empty() ? fn : mk3(M.n[3 * vi], M.n[3 * vi + 1], M.n[3 * vi + 2]);
+                }
+                triangle_data(P, M.mat.empty() ? 0 : M.mat[t], T, N, s->tri_data[t0 + t]);
+            }
+        });
+        for (auto m : M.materials) {
+            m.node_light_index = 0xffffffffu;
+            s->materials.push_back(m);
+        }
+    }
+
+    // --- nodes (instances), transforms, top-level BVH
+    Box sceneBox;
+    for (int k = 0; k < 3; k++) { sceneBox.lo[k] = FLT_MAX; sceneBox.hi[k] = -FLT_MAX; }
+    std::vector<Box> nodeBox(s->nodes.size());
+    for (size_t ni = 0; ni < s->nodes.size(); ni++) {
+        const auto& N = s->nodes[ni];
+        ctl_node kn{};
+        kn.mesh_index = N.mesh;
+        kn.material_offset = s->kmeshes[N.mesh].std_material_offset;
+        kn.instanced_material = 0;
+        kn.lights[0] = kn.lights[1] = 0xffffffffu;
+        kn.num_lights = 0;
+        s->knodes.push_back(kn);
+        ctl_float4x4 a, b;
+        memcpy(a.m, N.xf.d, 64);
+        m44 inv = N.has_xf ? inverse(N.xf) : m44_identity();   // SceneBVH::setTransform / ctor identity
+        memcpy(b.m, inv.d, 64);
+        s->xf.push_back(a);
+        s->inv_xf.push_back(b);
+        const Box& mb = meshBox[N.mesh];
+        Box wb;
+        for (int k = 0; k < 3; k++) { wb.lo[k] = FLT_MAX; wb.hi[k] = -FLT_MAX; }
+        for (int c = 0; c < 8; c++) {
+            f3 p = mk3((c & 1) ? mb.hi[0] : mb.lo[0], (c & 2) ? mb.hi[1] : mb.lo[1], (c & 4) ? mb.hi[2] : mb.lo[2]);
+            f3 q = xform_point(N.xf, p);
+            float qq[3] = {q.x, q.y, q.z};
+            for (int k = 0; k < 3; k++) { wb.lo[k] = tmin(wb.lo[k], qq[k]); wb.hi[k] = tmax(wb.hi[k], qq[k]); }
+        }
+        // conservative slack against rounding of the corner transform
+        for (int k = 0; k < 3; k++) {
+            float ext = tmax(fabsf(wb.lo[k]), fabsf(wb.hi[k])) * 1e-6f + 1e-30f;
+            wb.lo[k] -= ext; wb.hi[k] += ext;
+        }
+        nodeBox[ni] = wb;
+        for (int k = 0; k < 3; k++) { sceneBox.lo[k] = tmin(sceneBox.lo[k], wb.lo[k]); sceneBox.hi[k] = tmax(sceneBox.hi[k], wb.hi[k]); }
+    }
+    int32_t startNode = 0x76543210;
+    if (!s->nodes.empty()) {
+        BvhBuildParams bp;
+        bp.leaf_size_one = true;
+        bp.threads = 1;
+        BvhOutput bo;
+        build_bvh(nodeBox.data(), (uint32_t)nodeBox.size(), bp, bo);
+        s->scene_bvh = bo.nodes;
+        startNode = bo.start_node;
+    }
+
+    // --- lights (CreateLight -> CreateShape -> ShapeSet)
+    NormalDecodeHost ndec;
+    for (size_t li = 0; li < s->lights.size(); li++) {
+        const auto& L = s->lights[li];
+        ctl_node& kn = s->knodes[L.node];
+        const ctl_kernel_mesh& km = s->kmeshes[kn.mesh_index];
+        ctl_material& mat = s->materials[kn.material_offset + L.local_mat];
+        if (mat.node_light_index == 0xffffffffu) {
+            mat.node_light_index = kn.num_lights;
+            kn.lights[kn.num_lights++] = (uint32_t)li;
+        }
+        ctl_light kl{};
+        kl.radiance[0] = L.L[0]; kl.radiance[1] = L.L[1]; kl.radiance[2] = L.L[2];
+        kl.orthogonal = 0;
+        kl.tri_first = (uint32_t)s->light_tris.size();
+        kl.cdf_first = (uint32_t)s->light_tri_cdf.size();
+        kl.node_idx = L.node;
+        const auto& M = s->meshes[kn.mesh_index];
+        uint32_t ntri = (uint32_t)(M.idx.size() / 3);
+        // entries of this mesh: [bvh_indices_offset, next mesh)
+        uint64_t e0 = km.bvh_indices_offset;
+        uint64_t e1 = (kn.mesh_index + 1 < s->kmeshes.size()) ? s->kmeshes[kn.mesh_index + 1].bvh_indices_offset
+                                                              : s->woop.size();
+        std::vector<uint32_t> seen;
+        std::vector<char> used(ntri, 0);
+        m44 mxf = s->nodes[L.node].xf;
+        float sumArea = 0;
+        std::vector<float> areas;
+        for (uint64_t e = e0; e < e1; e++) {
+            uint32_t i2 = s->tri_indices[e] >> 1;
+            const ctl_triangle_data& td = s->tri_data[km.triangle_offset + i2];
+            if (((td.w[1] >> 16) & 0xff) != L.local_mat || used[i2]) continue;
+            used[i2] = 1;
+            ctl_light_tri lt{};
+            f3 p[3];
+            woop_get(s->woop[e], p[0], p[1], p[2]);
+            dgeom dg;
+            fill_dg(td, mxf, mk2(1.0f / 3.0f, 1.0f / 3.0f), true, ndec, dg);   // host fillDG
+            for (int i = 0; i < 3; i++) p[i] = xform_point(mxf, p[i]);
+            float area = 0.5f * length(cross(p[2] - p[0], p[1] - p[0]));
+            for (int i = 0; i < 3; i++) { lt.p[i][0] = p[i].x; lt.p[i][1] = p[i].y; lt.p[i][2] = p[i].z; }
+            lt.n[0] = dg.sys.n.x; lt.n[1] = dg.sys.n.y; lt.n[2] = dg.sys.n.z;
+            lt.area = area;
+            lt.i_dat = (uint32_t)e;
+            lt.t_dat = km.triangle_offset + i2;
+            s->light_tris.push_back(lt);
+            areas.push_back(area);
+        }
+        kl.tri_count = (uint32_t)areas.size();
+        if (kl.tri_count == 0) { set_host_error("compile: area light material has no triangles"); return CTL_ERR_INVALID; }
+        std::vector<float> cdf(kl.tri_count + 1);
+        cdf[0] = 0.0f;
+        for (uint32_t i = 0; i < kl.tri_count; i++) { sumArea += areas[i]; cdf[i + 1] = cdf[i] + areas[i]; }
+        for (uint32_t i = 0; i <= kl.tri_count; i++) cdf[i] = cdf[i] / sumArea;
+        kl.sum_area = sumArea;
+        s->light_tri_cdf.insert(s->light_tri_cdf.end(), cdf.begin(), cdf.end());
+        s->klights.push_back(kl);
+    }
+
+    ctl_scene_desc& d = s->desc;
+    d = ctl_scene_desc{};
+    d.tri_data = s->tri_data.data(); d.n_tri_data = s->tri_data.size();
+    d.woop_tris = s->woop.data(); d.n_woop_tris = s->woop.size();
+    d.bvh_nodes = s->bvh_nodes.data(); d.n_bvh_nodes = s->bvh_nodes.size();
+    d.tri_indices = s->tri_indices.data(); d.n_tri_indices = s->tri_indices.size();
+    d.materials = s->materials.data(); d.n_materials = (uint32_t)s->materials.size();
+    d.meshes = s->kmeshes.data(); d.n_meshes = (uint32_t)s->kmeshes.size();
+    d.nodes = s->knodes.data(); d.n_nodes = (uint32_t)s->knodes.size();
+    d.scene_bvh_nodes = s->scene_bvh.data(); d.n_scene_bvh_nodes = (uint32_t)s->scene_bvh.size();
+    d.scene_start_node = startNode;
+    d.node_xf = s->xf.data(); d.node_inv_xf = s->inv_xf.data();
+    d.lights = s->klights.data(); d.n_lights = (uint32_t)s->klights.size();
+    d.light_tris = s->light_tris.data(); d.n_light_tris = (uint32_t)s->light_tris.size();
+    d.light_tri_cdf = s->light_tri_cdf.data(); d.n_light_tri_cdf = (uint32_t)s->light_tri_cdf.size();
+    {   // LightStream::fillDeviceData with unit weights
+        uint32_t n = (uint32_t)s->klights.size();
+        float accum = 0;
+        for (uint32_t i = 0; i < n; i++) accum += 1.0f;
+        for (uint32_t i = 0; i < n; i++) {
+            float pdf = 1.0f / accum;
+            d.light_cdf[i] = (i > 0 ? d.light_cdf[i - 1] : 0.0f) + pdf;
+        }
+    }
+    d.env_map_index = 0xffffffffu;
+    for (int k = 0; k < 3; k++) { d.box_min[k] = sceneBox.lo[k]; d.box_max[k] = sceneBox.hi[k]; }
+    f3 size = mk3(sceneBox.hi[0] - sceneBox.lo[0], sceneBox.hi[1] - sceneBox.lo[1], sceneBox.hi[2] - sceneBox.lo[2]);
+    d.ray_eps = 1e-4f * length(size);   // MIN_RAYTRACE_DISTANCE_RELATIVE * |box|
+    camera_setup(s->cam_pos, s->cam_tar, s->cam_up, s->cam_fov, s->cam_near, s->cam_far, s->cam_w, s->cam_h, d.camera);
+    d.flags = s->flags;
+    *out = d;
+    return CTL_OK;
+}
+
+}  // extern "C"

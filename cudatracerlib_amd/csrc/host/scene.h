@@ -1,0 +1,57 @@
+// scene.h — host scene compiler: the product-side equivalent of the
+// reference's DynamicScene / Mesh::CompileMesh / SceneBVH host code that
+// produces the KernelDynamicScene arrays (Engine/DynamicScene.cpp:567-589,
+// Engine/Mesh.cpp:199-290, Engine/SceneBVH.cpp).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+#include "../../../include/ctl_trace.h"
+#include "../ctl_math.h"
+
+struct ctl_host_scene {
+    struct Mesh {
+        std::vector<float> v;         // xyz
+        std::vector<uint32_t> idx;    // 3 per triangle
+        std::vector<float> n;         // per-vertex normals (may be empty)
+        std::vector<float> uv;        // per-vertex uv (may be empty)
+        std::vector<uint8_t> mat;     // per triangle (may be empty)
+        std::vector<ctl_material> materials;
+    };
+    struct Node { uint32_t mesh; bool has_xf; ctl::m44 xf; };
+    struct Light { uint32_t node; uint32_t local_mat; float L[3]; };
+    std::vector<Mesh> meshes;
+    std::vector<Node> nodes;
+    std::vector<Light> lights;
+    bool has_camera = false;
+    float cam_pos[3], cam_tar[3], cam_up[3], cam_fov, cam_near, cam_far;
+    uint32_t cam_w = 0, cam_h = 0;
+    uint32_t flags = 0;
+
+    // compiled arrays (owned)
+    std::vector<ctl_triangle_data> tri_data;
+    std::vector<ctl_woop_tri> woop;
+    std::vector<ctl_bvh_node> bvh_nodes;
+    std::vector<ctl_tri_index> tri_indices;
+    std::vector<ctl_material> materials;
+    std::vector<ctl_kernel_mesh> kmeshes;
+    std::vector<ctl_node> knodes;
+    std::vector<ctl_bvh_node> scene_bvh;
+    std::vector<ctl_float4x4> xf, inv_xf;
+    std::vector<ctl_light> klights;
+    std::vector<ctl_light_tri> light_tris;
+    std::vector<float> light_tri_cdf;
+    ctl_scene_desc desc{};
+    uint32_t max_mesh_depth = 0;
+};
+
+namespace ctl {
+// TriIntersectorData::setData (Engine/TriIntersectorData.cu:5-18)
+void woop_set(f3 a, f3 b, f3 c, ctl_woop_tri& out);
+// TriIntersectorData::getData (Engine/TriIntersectorData.cu:20-32)
+void woop_get(const ctl_woop_tri& in, f3& v0, f3& v1, f3& v2);
+// PerspectiveSensor::Update + Sensor::SetToWorld(pos, tar, up)
+void camera_setup(const float pos[3], const float tar[3], const float up[3], float fov_deg, float nearc, float farc,
+                  uint32_t w, uint32_t h, ctl_camera& out);
+void set_host_error(const std::string& s);
+}  // namespace ctl

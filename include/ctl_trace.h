@@ -1,0 +1,337 @@
+/*
+ * ctl_trace.h — C-ABI drop-in boundary of the MI355X-native traversal backend.
+ *
+ * This header is the ONLY contract between a host renderer (the reference's
+ * Tracer / KernelDynamicScene / BSDF plugin surface, or our own Python/C++ host
+ * code) and the hand-written gfx950 HIP kernels in libctl_trace.so.
+ * Plain C, plain pointers and sizes; no torch, no HIP types in the signatures
+ * (streams are passed as `void*` = hipStream_t).
+ *
+ * Citations are `file:line` in the reference (Ilinite/CudaTracerLib).
+ *
+ *   reference entry point                               replaced by
+ *   --------------------------------------------------- --------------------------------
+ *   InitializeKernel / DeinitializeKernel               ctl_create / ctl_destroy
+ *     Kernel/TraceHelper.h:41-42, TraceHelper.cu:253-272
+ *   UpdateKernel(DynamicScene*, ISamplingSeq...&)       ctl_scene_upload + ctl_sampler_generate
+ *     Kernel/TraceHelper.h:44, TraceHelper.cu:182-217
+ *   __internal__IntersectBuffers(N, rays, res, skip, any_hit)
+ *     Kernel/TraceHelper.h:71, TraceHelper.cu:736-746  ctl_intersect
+ *   PathTracer::RenderBlock / pathKernel2 per pass      ctl_render_pass
+ *     Integrators/PathTracer.cu:182-217, Kernel/Tracer.h:209-248
+ *   k_getNumRaysTraced / k_setNumRaysTraced             ctl_rays_traced / ctl_reset_rays
+ *     Kernel/TraceHelper.h:52-53, TraceHelper.cu:309-320
+ *   ThrowCudaErrors (Defines.cpp:15-29)                 ctl_status + ctl_last_error (never throws)
+ *
+ * Ownership: the caller owns every host array passed in a ctl_scene_desc (the
+ * backend copies and may re-layout them) and every device buffer passed to
+ * ctl_intersect / ctl_render_pass (rays, hits, framebuffer).  The context owns
+ * its device copy of the scene and sampler tables.  All state is per context
+ * (no process globals), so one context per GPU / rank is re-entrant.
+ */
+#ifndef CTL_TRACE_H
+#define CTL_TRACE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CTL_ABI_VERSION 1
+
+#if defined(_WIN32)
+#define CTL_API __declspec(dllexport)
+#else
+#define CTL_API __attribute__((visibility("default")))
+#endif
+
+typedef int32_t ctl_status;
+enum {
+    CTL_OK = 0,
+    CTL_ERR_INVALID = 1,   /* bad argument / inconsistent scene description  */
+    CTL_ERR_HIP = 2,       /* a HIP runtime call failed (see ctl_last_error)  */
+    CTL_ERR_NOMEM = 3,     /* device or host allocation failed                */
+    CTL_ERR_STATE = 4,     /* call order violated (e.g. render before upload) */
+    CTL_ERR_NODEVICE = 5   /* no usable gfx950 device / HIP code object       */
+};
+
+/* ------------------------------------------------------------------------ */
+/* Byte-identical reference data layouts (static_assert'ed in the sources).  */
+/* ------------------------------------------------------------------------ */
+
+/* BVHNodeData, 64 B (Engine/TriIntersectorData.h:42-117):
+ *   v[0..3]  = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
+ *   v[4..7]  = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+ *   v[8..11] = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
+ *   v[12..13]= int child0, child1 : >=0 inner node as float4 offset (=index*4),
+ *              <0 leaf (= ~first leaf entry), 0x76543210 = empty/sentinel
+ *   v[14]    = parent (uint), v[15] unused                                   */
+typedef struct { float v[16]; } ctl_bvh_node;
+
+/* TriIntersectorData, 48 B Woop unit-triangle transform
+ * (Engine/TriIntersectorData.h:30-40, setData TriIntersectorData.cu:5-18).   */
+typedef struct { float v[12]; } ctl_woop_tri;
+
+/* TriIntersectorData2, 4 B: (local triangle index << 1) | last-in-leaf flag
+ * (Engine/TriIntersectorData.h:8-28).                                        */
+typedef uint32_t ctl_tri_index;
+
+/* TriangleData (EXT_TRI), 32 B (Engine/TriangleData.h:10-36):
+ *   w[0..1] NorMatExtra: 3 x 16-bit spherical normals, u8 material, u8 extra
+ *   w[2..4] DpduDpdv   : dpdu, dpdv as 6 x half
+ *   w[5..7] UVSets[0]  : 3 x half2 texture coordinates                        */
+typedef struct { uint32_t w[8]; } ctl_triangle_data;
+
+/* KernelMesh, 20 B (Engine/Mesh.h:12-19).  bvh_node_offset is in float4 units
+ * (Mesh.cpp:104), bvh_triangle_offset in float4 units (= entry*3, Mesh.cpp:105). */
+typedef struct {
+    uint32_t triangle_offset;
+    uint32_t bvh_node_offset;
+    uint32_t bvh_triangle_offset;
+    uint32_t bvh_indices_offset;
+    uint32_t std_material_offset;
+} ctl_kernel_mesh;
+
+/* Node, 24 B (SceneTypes/Node.h:13-24; m_uLights is a FixedSizeArray<uint,2>). */
+typedef struct {
+    uint32_t mesh_index;
+    uint32_t material_offset;
+    uint32_t instanced_material;
+    uint32_t lights[2];
+    uint32_t num_lights;
+} ctl_node;
+
+/* float4x4, row-major, 64 B (Math/float4x4.h:12-17, idx(i,j) = i*4+j). */
+typedef struct { float m[16]; } ctl_float4x4;
+
+/* traversalRay, 32 B (Kernel/TraceHelper.h:55-59): {o.xyz, tmin ; d.xyz, tmax} */
+typedef struct { float o[3]; float tmin; float d[3]; float tmax; } ctl_ray;
+
+/* traversalResult, 16 B (Kernel/TraceHelper.h:61-69, written TraceHelper.cu:722-731):
+ *   hit : {t, node, tri(global), (v16 << 16) | u16}   miss : {tmax, -1, -1, 0} */
+typedef struct { float dist; int32_t node_idx; int32_t tri_idx; int32_t bary; } ctl_hit;
+
+/* PixelData, 28 B (Engine/Image.h:10-29). */
+typedef struct { float rgb[3]; float rgb_splat[3]; float weight_sum; } ctl_pixel;
+
+/* ------------------------------------------------------------------------ */
+/* Flattened plugin data (the fields of Material / DiffuseLight / Sensor the */
+/* path reads; the reference keeps them in CudaVirtualAggregate unions).     */
+/* ------------------------------------------------------------------------ */
+
+enum {                        /* BSDF TYPE_FUNC ids (SceneTypes/BSDF_Simple.h) */
+    CTL_BSDF_DIFFUSE = 1,         /* diffuse, BSDF_Simple.cu:7-75             */
+    CTL_BSDF_ROUGHDIELECTRIC = 5  /* reserved (config C5, not yet supported) */
+};
+
+/* EBSDFType bits used by the path (SceneTypes/Samples.h:32-60). */
+enum {
+    CTL_EDIFFUSE_REFLECTION = 0x00002,
+    CTL_EDIFFUSE_TRANSMISSION = 0x00004
+};
+
+typedef struct {
+    uint32_t bsdf_type;          /* CTL_BSDF_*                                   */
+    uint32_t combined_type;      /* BSDF::m_combinedType (EDiffuseReflection)    */
+    uint32_t two_sided;          /* BSDF::m_enableTwoSided                       */
+    uint32_t node_light_index;   /* Material::NodeLightIndex, 0xFFFFFFFF = none  */
+    float reflectance[3];        /* ConstantTexture value of diffuse::m_reflectance */
+    float pad;
+} ctl_material;
+
+/* ShapeSet::triData, 64 B (Engine/ShapeSet.h:17-27), world space. */
+typedef struct {
+    float p[3][3];
+    float n[3];
+    float area;
+    uint32_t i_dat;
+    uint32_t t_dat;
+    uint32_t pad;
+} ctl_light_tri;
+
+/* DiffuseLight (SceneTypes/Light.h:96-143) with a ConstantTexture radiance and
+ * its ShapeSet: triangles [tri_first, tri_first+tri_count) of the light_tris
+ * array and area CDF entries [cdf_first, cdf_first+tri_count+1).             */
+typedef struct {
+    float radiance[3];
+    uint32_t orthogonal;         /* m_bOrthogonal (must be 0; reserved)          */
+    uint32_t tri_first;
+    uint32_t tri_count;
+    uint32_t cdf_first;
+    float sum_area;              /* ShapeSet::sumArea                            */
+    uint32_t node_idx;           /* m_uNodeIdx                                   */
+    uint32_t pad[3];
+} ctl_light;
+
+/* PerspectiveSensor device state after Update() (SceneTypes/Sensor.cu:76-96). */
+typedef struct {
+    ctl_float4x4 to_world;          /* SensorBase::toWorld                      */
+    ctl_float4x4 sample_to_camera;  /* m_sampleToCamera                         */
+    float dx[3];                    /* m_dx                                     */
+    float dy[3];                    /* m_dy                                     */
+    float inv_resolution[2];        /* m_invResolution                          */
+    uint32_t width, height;
+} ctl_camera;
+
+#define CTL_MAX_NUM_LIGHTS 16   /* KernelDynamicScene.h:26 */
+
+/* scene flags */
+enum {
+    /* decode half floats like the reference's HOST path (Math/half.h:72-84,
+     * ((h & 0x7fff) << 13) + 0x38000000, i.e. +0 -> 2^-15); off = IEEE decode
+     * like its CUDA path (__half2float).  The oracle supports both.          */
+    CTL_SCENE_HALF_HOST_QUIRK = 1u << 0
+};
+
+/* Everything KernelDynamicScene (Engine/KernelDynamicScene.h:28-57) holds that
+ * the traversal + PathTracer path reads. */
+typedef struct {
+    const ctl_triangle_data* tri_data;  uint64_t n_tri_data;    /* m_sTriData    */
+    const ctl_woop_tri* woop_tris;      uint64_t n_woop_tris;   /* m_sBVHIntData */
+    const ctl_bvh_node* bvh_nodes;      uint64_t n_bvh_nodes;   /* m_sBVHNodeData */
+    const ctl_tri_index* tri_indices;   uint64_t n_tri_indices; /* m_sBVHIndexData */
+    const ctl_material* materials;      uint32_t n_materials;   /* m_sMatData    */
+    const ctl_kernel_mesh* meshes;      uint32_t n_meshes;      /* m_sMeshData   */
+    const ctl_node* nodes;              uint32_t n_nodes;       /* m_sNodeData   */
+    /* KernelSceneBVH (Engine/SceneBVH_device.h:8-15) */
+    const ctl_bvh_node* scene_bvh_nodes; uint32_t n_scene_bvh_nodes;
+    int32_t scene_start_node;           /* m_sStartNode (<0: single leaf ~node) */
+    const ctl_float4x4* node_xf;        /* m_pNodeTransforms[n_nodes]           */
+    const ctl_float4x4* node_inv_xf;    /* m_pInvNodeTransforms[n_nodes]        */
+    /* lights (m_sLightBuf + ShapeSet data held in m_sAnimData) */
+    const ctl_light* lights;            uint32_t n_lights;
+    const ctl_light_tri* light_tris;    uint32_t n_light_tris;
+    const float* light_tri_cdf;         uint32_t n_light_tri_cdf;
+    float light_cdf[CTL_MAX_NUM_LIGHTS];/* m_pLightCDF (lights are active, identity index map) */
+    uint32_t env_map_index;             /* must be 0xFFFFFFFF (no environment)  */
+    float box_min[3], box_max[3];       /* m_sBox                               */
+    float ray_eps;                      /* m_rayTraceEps, DynamicScene.cpp:587  */
+    ctl_camera camera;                  /* m_Camera                             */
+    uint32_t flags;                     /* CTL_SCENE_*                          */
+} ctl_scene_desc;
+
+/* PathTracer parameters (Integrators/PathTracer.h:10-19) + multi-GPU tiling. */
+typedef struct {
+    int32_t direct;            /* KEY_Direct, default 1                       */
+    int32_t max_path_length;   /* KEY_MaxPathLength, default 50               */
+    int32_t rr_start_depth;    /* KEY_RRStartDepth, default 5                 */
+    int32_t shadow_any_hit;    /* 1: Occluded() as any-hit over (eps,tmax-eps)
+                                  (identical boolean, KernelDynamicScene.cu:70-80);
+                                  0: closest-hit like the reference           */
+    uint32_t tile_size;        /* image tile edge (64 = BLOCK_SAMPLER_BlockSize) */
+    uint32_t num_ranks;        /* tiles with (tile_id % num_ranks) == rank are */
+    uint32_t rank;             /*   rendered by this call                      */
+    uint32_t flags;            /* reserved, 0                                  */
+} ctl_pt_params;
+
+/* ------------------------------------------------------------------------ */
+/* Device API (needs a gfx950 GPU)                                           */
+/* ------------------------------------------------------------------------ */
+
+typedef struct ctl_ctx ctl_ctx;
+
+CTL_API int32_t ctl_abi_version(void);
+/* Creates a context bound to HIP device `device`.  Returns NULL on failure;
+ * the reason is then available from ctl_last_error(NULL). */
+CTL_API ctl_ctx* ctl_create(int32_t device);
+CTL_API void ctl_destroy(ctl_ctx* ctx);
+/* Last error message of ctx (or of the last failed ctl_create when ctx==NULL). */
+CTL_API const char* ctl_last_error(const ctl_ctx* ctx);
+
+/* Copies the scene to the device (synchronous).  Replaces any previous scene. */
+CTL_API ctl_status ctl_scene_upload(ctl_ctx* ctx, const ctl_scene_desc* desc);
+
+/* Generates the SequenceSamplerData tables of render pass `pass_index` (the
+ * pass-th UpdateKernel call, Kernel/Sampler.h:36-55 + 63-85) on the host and
+ * copies them asynchronously on `stream` (double-buffered; safe to call while
+ * the previous pass still renders).  num_sequences=4096, length=30 as
+ * InitializeKernel (TraceHelper.cu:253-257). */
+CTL_API ctl_status ctl_sampler_generate(ctl_ctx* ctx, uint64_t pass_index, void* stream);
+/* Uploads caller-provided tables instead (element-major: [k*num_seq + s]). */
+CTL_API ctl_status ctl_sampler_upload(ctl_ctx* ctx, const float* seq1d, const float* seq2d,
+                                      uint32_t num_sequences, uint32_t sequence_length, void* stream);
+
+/* Batched closest/any-hit over device buffers; asynchronous on `stream`.
+ * Semantics of intersectKernel<ANY_HIT> (TraceHelper.cu:326-734): triangle
+ * accepted when tmin < t < current tmax, result layout as ctl_hit. */
+CTL_API ctl_status ctl_intersect(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays, ctl_hit* d_hits,
+                                 int32_t any_hit, void* stream);
+
+/* One progressive PathTracer pass (one sample per owned pixel) accumulated
+ * into the caller's device framebuffer d_fb[width*height] (PixelData,
+ * Engine/Image.cu:22-44).  Uses the tables from the last ctl_sampler_generate /
+ * ctl_sampler_upload on the same stream.  Asynchronous on `stream`. */
+CTL_API ctl_status ctl_render_pass(ctl_ctx* ctx, const ctl_pt_params* params, ctl_pixel* d_fb,
+                                   void* stream);
+
+/* Number of traceRay-equivalent queries (camera + bounce + shadow rays +
+ * batched rays) since the last reset; 64-bit (the reference's counter is a
+ * 32-bit atomicInc, Base/Platform.cu:12-21).  Synchronises the device. */
+CTL_API uint64_t ctl_rays_traced(ctl_ctx* ctx);
+CTL_API ctl_status ctl_reset_rays(ctl_ctx* ctx, void* stream);
+CTL_API ctl_status ctl_sync(ctl_ctx* ctx, void* stream);
+
+/* Traversal statistics for the roofline's algorithmic byte count (same kernel
+ * compiled with counters; off in the timed path).  out[0]=rays,
+ * out[1]=inner-node visits, out[2]=triangle tests, out[3]=instance entries. */
+CTL_API ctl_status ctl_intersect_stats(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays, ctl_hit* d_hits,
+                                       int32_t any_hit, uint64_t out[4], void* stream);
+CTL_API ctl_status ctl_render_pass_stats(ctl_ctx* ctx, const ctl_pt_params* params, ctl_pixel* d_fb,
+                                         uint64_t out[4], void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Host helpers (no GPU needed): the reference's host-side compile step      */
+/* ------------------------------------------------------------------------ */
+
+/* TriIntersectorData::setData (Engine/TriIntersectorData.cu:5-18). */
+CTL_API void ctl_woop_set(const float v0[3], const float v1[3], const float v2[3], ctl_woop_tri* out);
+
+/* The SequenceSamplerData tables of pass `pass_index`
+ * (seq1d/seq2d: num_sequences*length floats / float2, element-major). */
+CTL_API ctl_status ctl_host_sampler_tables(uint64_t pass_index, uint32_t num_sequences,
+                                           uint32_t sequence_length, float* seq1d, float* seq2d);
+
+/* Host scene compiler: triangle soups -> the arrays of ctl_scene_desc
+ * (BVH build = parallel binned SAH emitting the reference BVHNodeData layout,
+ * leaf <= 8 tris as ConstructBVH, BVHBuilderHelper.cpp:129-147). */
+typedef struct ctl_host_scene ctl_host_scene;
+CTL_API ctl_host_scene* ctl_host_scene_create(void);
+CTL_API void ctl_host_scene_destroy(ctl_host_scene* s);
+/* Adds a mesh; returns its index (or -1).  normals/uvs may be NULL (flat /
+ * zero), mat_index per triangle may be NULL (all 0).  Materials are local to
+ * the mesh (Mesh::m_sMatInfo). */
+CTL_API int32_t ctl_host_scene_add_mesh(ctl_host_scene* s, const float* vertices, uint32_t n_vertices,
+                                        const uint32_t* indices, uint32_t n_triangles,
+                                        const float* normals, const float* uvs,
+                                        const uint8_t* mat_index,
+                                        const ctl_material* materials, uint32_t n_materials);
+/* Adds a node (instance) of a mesh with an object->world transform (row-major
+ * 4x4, NULL = identity); returns the node index or -1. */
+CTL_API int32_t ctl_host_scene_add_node(ctl_host_scene* s, uint32_t mesh, const float* xf16);
+/* Marks material `local_material` of `node` as a DiffuseLight with constant
+ * radiance (DynamicScene::CreateLight on a mesh part). Returns the light index. */
+CTL_API int32_t ctl_host_scene_add_area_light(ctl_host_scene* s, uint32_t node, uint32_t local_material,
+                                              const float radiance[3]);
+/* PerspectiveSensor: position, target, up, fov (degrees), near/far, resolution. */
+CTL_API ctl_status ctl_host_scene_set_camera(ctl_host_scene* s, const float pos[3], const float target[3],
+                                             const float up[3], float fov_deg, float near_clip,
+                                             float far_clip, uint32_t width, uint32_t height);
+CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags);
+/* Builds BVHs (threads=0: all hardware threads) and fills *out; the arrays
+ * stay owned by `s` until it is destroyed or compiled again. */
+CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, ctl_scene_desc* out);
+CTL_API const char* ctl_host_last_error(void);
+
+/* Synthetic workloads of BASELINE.json (seed 0x5EED): 1 = C1 Cornell box
+ * (32 tris), 2 = C2 100k-tri field, 3 = C3 ~10M-tri "San-Miguel-scale".
+ * `scale` multiplies the triangle budget (1.0 = the named size).  The camera
+ * resolution is width x height. */
+CTL_API ctl_status ctl_host_scene_generate(ctl_host_scene* s, int32_t config, double scale,
+                                           uint32_t width, uint32_t height);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CTL_TRACE_H */

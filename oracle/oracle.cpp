@@ -1,0 +1,962 @@
+// oracle.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the reference (Ilinite/CudaTracerLib) algorithm for the
+// hot path: two-level Aila–Laine BVH traversal + Woop ray/triangle test
+// (Kernel/TraceHelper.cu:88-180, Engine/SpatialStructures/BVH/BVHTraversal.h:122-232),
+// the batch intersectKernel semantics (TraceHelper.cu:326-746), the
+// SequenceSampler / CudaRNG (XORWOW) streams (Kernel/Sampler*.h,
+// Base/CudaRandom.{h,cu}), PerspectiveSensor (SceneTypes/Sensor.cu:76-144),
+// diffuse BSDF (SceneTypes/BSDF_Simple.cu:7-75), DiffuseLight + ShapeSet
+// (SceneTypes/Light.cu:55-155, Engine/ShapeSet.cu:11-68), the PathTrace<true>
+// integrator loop (Integrators/PathTracer.cu:10-113,182-194) and
+// Image::AddSample (Engine/Image.cu:22-44).
+//
+// It is the CHECKER for the HIP kernels and the cpu_baseline of bench.py.
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may load it;
+// the product library (libctl_trace.so) never links or calls it.
+//
+// Parity pinning: the reference cannot be built here (it needs the CUDA
+// toolkit and empty submodules; a build would need stand-in CUDA headers,
+// which this project does not write), and it ships no tests or fixtures.  The
+// sampler stream is pinned by the reference outputs recorded in SURVEY.md §8c
+// (tests/golden/sampler_reference_values.json); everything else is "parity
+// unpinned" against the reference binary and is checked by properties
+// (brute-force closest hit, Woop round trip) — see DESIGN.md §Parity.
+#include "oracle_math.h"
+#include "../include/ctl_trace.h"
+
+#include <vector>
+#include <thread>
+#include <atomic>
+#include <mutex>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+using namespace oracle;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Woop unit-triangle transform (Engine/TriIntersectorData.cu:5-32)
+// ---------------------------------------------------------------------------
+void woop_set(V3 a, V3 b, V3 c, float out[12]) {
+    M44 m;
+    m.setCol(0, v4(a - c, 0));
+    m.setCol(1, v4(b - c, 0));
+    m.setCol(2, v4(cross(a - c, b - c), 0));
+    m.setCol(3, v4(c, 1));
+    m = inverse(m);
+    V4 A = v4(m(2, 0), m(2, 1), m(2, 2), -m(2, 3));
+    V4 B = m.row(0), C = m.row(1);
+    float tmp[12] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, C.x, C.y, C.z, C.w};
+    std::memcpy(out, tmp, sizeof(tmp));
+}
+void woop_get(const float in[12], V3& v0, V3& v1, V3& v2) {
+    M44 m = M44::identity();
+    m.setRow(0, v4(in[4], in[5], in[6], in[7]));   // b
+    m.setRow(1, v4(in[8], in[9], in[10], in[11])); // c
+    m.setRow(2, v4(in[0], in[1], in[2], in[3]));   // a
+    m(2, 3) *= -1.0f;
+    m = inverse(m);
+    V3 e02 = xyz(m.col(0)), e12 = xyz(m.col(1));
+    v2 = xyz(m.col(3));
+    v0 = v2 + e02;
+    v1 = v2 + e12;
+}
+
+// ---------------------------------------------------------------------------
+// kepler_math spans on float bit patterns (Math/MathFunc.h:402-445, host branch)
+// ---------------------------------------------------------------------------
+inline int imin3(int a, int b, int c) { return omin(omin(a, b), c); }
+inline int imax3(int a, int b, int c) { return omax(omax(a, b), c); }
+inline int imin_max(int a, int b, int c) { return omax(omin(a, b), c); }
+inline int imax_min(int a, int b, int c) { return omin(omax(a, b), c); }
+inline float spanBegin(float a0, float a1, float b0, float b1, float c0, float c1, float d) {
+    return as_float(imax3(as_int(omin(a0, a1)), as_int(omin(b0, b1)), imin_max(as_int(c0), as_int(c1), as_int(d))));
+}
+inline float spanEnd(float a0, float a1, float b0, float b1, float c0, float c1, float d) {
+    return as_float(imin3(as_int(omax(a0, a1)), as_int(omax(b0, b1)), imax_min(as_int(c0), as_int(c1), as_int(d))));
+}
+
+const int EntrypointSentinel = 0x76543210;
+
+struct Stats { uint64_t nodes = 0, tris = 0, inst = 0; };
+
+// TracerayTemplate, pointer overload (BVHTraversal.h:122-232).  spanTmin is 0
+// for traceRay and the ray's tmin for the batch kernel (TraceHelper.cu:469).
+template <class CLB>
+bool traceray_template(V3 ori, V3 dir, float& rayT, float spanTmin, const CLB& clb, const float* nodes4,
+                       int bvhNodesOffset, int startNode, Stats* st) {
+    if (startNode < 0) return clb(~startNode);
+    bool found = false;
+    // index 1 holds the sentinel; index 0 only absorbs the pop of an already
+    // popped sentinel (the reference would read before its array there)
+    int traversalStack[64 + 3];
+    traversalStack[0] = EntrypointSentinel;
+    traversalStack[1] = EntrypointSentinel;
+    const float ooeps = powf(2.0f, -80.0f);   // math::exp2 host branch (MathFunc.h:240-245)
+    float idirx = 1.0f / (fabsf(dir.x) > ooeps ? dir.x : o_copysign(ooeps, dir.x));
+    float idiry = 1.0f / (fabsf(dir.y) > ooeps ? dir.y : o_copysign(ooeps, dir.y));
+    float idirz = 1.0f / (fabsf(dir.z) > ooeps ? dir.z : o_copysign(ooeps, dir.z));
+    float origx = ori.x, origy = ori.y, origz = ori.z;
+    float oodx = origx * idirx, oody = origy * idiry, oodz = origz * idirz;
+    int sp = 1;
+    int leafAddr = 0;
+    int nodeAddr = startNode;
+    while (nodeAddr != EntrypointSentinel) {
+        while ((unsigned int)nodeAddr < (unsigned int)EntrypointSentinel) {
+            const float* n = nodes4 + 4 * (size_t)(bvhNodesOffset + nodeAddr);
+            if (st) st->nodes++;
+            int c0i, c1i;
+            std::memcpy(&c0i, n + 12, 4);
+            std::memcpy(&c1i, n + 13, 4);
+            const float c0lox = n[0] * idirx - oodx;
+            const float c0hix = n[1] * idirx - oodx;
+            const float c0loy = n[2] * idiry - oody;
+            const float c0hiy = n[3] * idiry - oody;
+            const float c0loz = n[8] * idirz - oodz;
+            const float c0hiz = n[9] * idirz - oodz;
+            const float c1loz = n[10] * idirz - oodz;
+            const float c1hiz = n[11] * idirz - oodz;
+            const float c0min = spanBegin(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, spanTmin);
+            const float c0max = spanEnd(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, rayT);
+            const float c1lox = n[4] * idirx - oodx;
+            const float c1hix = n[5] * idirx - oodx;
+            const float c1loy = n[6] * idiry - oody;
+            const float c1hiy = n[7] * idiry - oody;
+            const float c1min = spanBegin(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, spanTmin);
+            const float c1max = spanEnd(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, rayT);
+            bool swp = (c1min < c0min);
+            bool traverseChild0 = (c0max >= c0min);
+            bool traverseChild1 = (c1max >= c1min);
+            if (!traverseChild0 && !traverseChild1) {
+                nodeAddr = traversalStack[sp--];
+            } else {
+                nodeAddr = traverseChild0 ? c0i : c1i;
+                if (traverseChild0 && traverseChild1) {
+                    if (swp) std::swap(nodeAddr, c1i);
+                    traversalStack[++sp] = c1i;
+                    if (sp > 65) { std::fprintf(stderr, "oracle: traversal stack overflow\n"); std::abort(); }
+                }
+            }
+            if (nodeAddr < 0 && leafAddr >= 0) {
+                leafAddr = nodeAddr;
+                nodeAddr = traversalStack[sp--];
+            }
+            if (!(leafAddr >= 0)) break;   // host branch: mask = leafAddr >= 0
+        }
+        while (leafAddr < 0) {
+            if (leafAddr != -214783648) found |= clb(~leafAddr);   // sic, BVHTraversal.h:221
+            leafAddr = nodeAddr;
+            if (nodeAddr < 0) nodeAddr = traversalStack[sp--];
+        }
+    }
+    return found;
+}
+
+// ---------------------------------------------------------------------------
+// Scene view (the ctl_scene_desc arrays)
+// ---------------------------------------------------------------------------
+struct SceneView {
+    const ctl_scene_desc* d;
+    M44 xf(uint32_t i) const { M44 m; std::memcpy(m.d, d->node_xf[i].m, 64); return m; }
+    M44 inv(uint32_t i) const { M44 m; std::memcpy(m.d, d->node_inv_xf[i].m, 64); return m; }
+    bool quirk() const { return (d->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0; }
+};
+
+enum TieMode { TIE_FIRST_FOUND = 0, TIE_MIN_INDEX = 1 };
+
+struct Hit {
+    float t; float u, v; uint32_t tri; uint32_t node;
+};
+
+// Generic two-level closest/any hit.  traceRay (TraceHelper.cu:88-180):
+// spanTmin=0, triTmin=rayEps, t0=FLT_MAX.  Batch (TraceHelper.cu:326-734):
+// spanTmin=triTmin=ray.tmin, t0=ray.tmax.
+bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
+                     int tie, Stats* st) {
+    const ctl_scene_desc* d = S.d;
+    if (d->n_nodes == 0) return false;
+    const float* sceneNodes = reinterpret_cast<const float*>(d->scene_bvh_nodes);
+    const float* meshNodes = reinterpret_cast<const float*>(d->bvh_nodes);
+    const float* tris = reinterpret_cast<const float*>(d->woop_tris);
+    bool done = false;   // any-hit termination
+    auto instClb = [&](int nodeIdx) -> bool {
+        if (done) return false;
+        if (st) st->inst++;
+        const ctl_node& N = d->nodes[nodeIdx];
+        const ctl_kernel_mesh& mesh = d->meshes[N.mesh_index];
+        M44 modl = S.inv(nodeIdx);
+        V3 dl = transformDirection(modl, dir), ol = transformPoint(modl, ori);
+        auto triClb = [&](int triIdx) -> bool {
+            bool found = false;
+            for (int triAddr = triIdx;; triAddr++) {
+                if (done) break;
+                const float* v = tris + 4 * ((size_t)mesh.bvh_triangle_offset + (size_t)triAddr * 3);
+                unsigned int index = d->tri_indices[mesh.bvh_indices_offset + triAddr];
+                if (st) st->tris++;
+                float Oz = v[3] - ol.x * v[0] - ol.y * v[1] - ol.z * v[2];
+                float invDz = 1.0f / (dl.x * v[0] + dl.y * v[1] + dl.z * v[2]);
+                float t = Oz * invDz;
+                unsigned int gtri = (index >> 1) + mesh.triangle_offset;
+                bool closer = t < h.t || (tie == TIE_MIN_INDEX && t == h.t && gtri < h.tri);
+                if (t > triTmin && closer) {
+                    float Ox = v[7] + ol.x * v[4] + ol.y * v[5] + ol.z * v[6];
+                    float Dx = dl.x * v[4] + dl.y * v[5] + dl.z * v[6];
+                    float u = Ox + t * Dx;
+                    if (u >= 0.0f) {
+                        float Oy = v[11] + ol.x * v[8] + ol.y * v[9] + ol.z * v[10];
+                        float Dy = dl.x * v[8] + dl.y * v[9] + dl.z * v[10];
+                        float vv = Oy + t * Dy;
+                        if (vv >= 0.0f && u + vv <= 1.0f) {
+                            h.node = (uint32_t)nodeIdx;
+                            h.tri = gtri;
+                            h.u = u; h.v = vv;
+                            h.t = t;
+                            found = true;
+                            if (anyHit) { done = true; break; }
+                        }
+                    }
+                }
+                if (index & 1) break;
+            }
+            return found;
+        };
+        return traceray_template(ol, dl, h.t, spanTmin, triClb, meshNodes, (int)mesh.bvh_node_offset, 0, st);
+    };
+    return traceray_template(ori, dir, h.t, spanTmin, instClb, sceneNodes, 0, d->scene_start_node, st);
+}
+
+// traceRay(dir, ori, TraceResult*) (TraceHelper.cu:174-180) on an Init()'ed result
+bool trace_ray(const SceneView& S, V3 ori, V3 dir, Hit& h, int tie, Stats* st) {
+    h.t = FLT_MAX; h.tri = UINT_MAX; h.node = UINT_MAX; h.u = h.v = 0;
+    trace_two_level(S, ori, dir, 0.0f, S.d->ray_eps, h, false, tie, st);
+    return h.tri != UINT_MAX;
+}
+
+// ---------------------------------------------------------------------------
+// XORWOW / CudaRNG (Base/CudaRandom.h:112-282, CudaRandom.cu:8-36)
+// curand_init(1234, subsequence, 0): subsequence jump = 2^67 steps (published
+// cuRAND XORWOW definition).  Jumps use powers of the GF(2) step matrix.
+// ---------------------------------------------------------------------------
+struct Xorwow { uint32_t v[5]; uint32_t d; };
+
+struct Gf2 { uint32_t col[160][5]; };
+void gf2_apply(const Gf2& M, const uint32_t x[5], uint32_t y[5]) {
+    uint32_t r[5] = {0, 0, 0, 0, 0};
+    for (int j = 0; j < 160; j++)
+        if ((x[j >> 5] >> (j & 31)) & 1u)
+            for (int k = 0; k < 5; k++) r[k] ^= M.col[j][k];
+    for (int k = 0; k < 5; k++) y[k] = r[k];
+}
+void xorwow_linear_step(uint32_t v[5]) {
+    uint32_t t = (v[0] ^ (v[0] >> 2));
+    v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+    v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+}
+const std::vector<Gf2>& gf2_powers() {   // P[k] = M^(2^k), k < 128
+    static std::vector<Gf2> P;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        P.resize(128);
+        for (int j = 0; j < 160; j++) {
+            uint32_t v[5] = {0, 0, 0, 0, 0};
+            v[j >> 5] = 1u << (j & 31);
+            xorwow_linear_step(v);
+            for (int k = 0; k < 5; k++) P[0].col[j][k] = v[k];
+        }
+        for (int p = 1; p < 128; p++)
+            for (int j = 0; j < 160; j++) gf2_apply(P[p - 1], P[p - 1].col[j], P[p].col[j]);
+    });
+    return P;
+}
+Xorwow curand_init(uint64_t seed, uint64_t subsequence, uint64_t offset) {
+    Xorwow s;
+    uint32_t s0 = ((uint32_t)seed) ^ 0xaad26b49UL;
+    uint32_t s1 = (uint32_t)(seed >> 32) ^ 0xf7dcefddUL;
+    uint32_t t0 = 1099087573UL * s0;
+    uint32_t t1 = 2591861531UL * s1;
+    s.d = 6615241 + t1 + t0;
+    s.v[0] = 123456789UL + t0;
+    s.v[1] = 362436069UL ^ t0;
+    s.v[2] = 521288629UL + t1;
+    s.v[3] = 88675123UL ^ t1;
+    s.v[4] = 5783321UL + t0;
+    const auto& P = gf2_powers();
+    for (int b = 0; b < 64; b++)
+        if ((subsequence >> b) & 1) gf2_apply(P[67 + b], s.v, s.v);
+    for (int b = 0; b < 64; b++)
+        if ((offset >> b) & 1) gf2_apply(P[b], s.v, s.v);
+    s.d += 362437u * (uint32_t)offset;
+    return s;
+}
+inline uint32_t xorwow_next(Xorwow& s) {   // curand2 (CudaRandom.h:118-129)
+    uint32_t t = (s.v[0] ^ (s.v[0] >> 2));
+    s.v[0] = s.v[1]; s.v[1] = s.v[2]; s.v[2] = s.v[3]; s.v[3] = s.v[4];
+    s.v[4] = (s.v[4] ^ (s.v[4] << 4)) ^ (t ^ (t << 1));
+    s.d += 362437;
+    return s.v[4] + s.d;
+}
+inline float xorwow_uniform(Xorwow& s) {   // randomFloat (CudaRandom.cu:8-17)
+    const float INV = 2.3283064e-10f;       // CURAND_2POW32_INV
+    float f = (float)xorwow_next(s) * INV + (INV / 2.0f);
+    return f * (1 - 1e-5f);
+}
+
+const uint32_t kSamplerSeed = 7539414;       // IndependantSamplingSequenceGenerator (Sampler.h:68)
+void sampler_tables(uint64_t pass, uint32_t nseq, uint32_t len, float* seq1d, float* seq2d) {
+    // One CudaRNG stream continued across passes (Sampler.h:36-55,63-85):
+    // per sequence `len` 1-D draws then `len` 2-D pairs (x drawn first).
+    uint64_t perPass = (uint64_t)nseq * len * 3;
+    Xorwow s = curand_init(1234, kSamplerSeed, pass * perPass);
+    for (uint32_t q = 0; q < nseq; q++) {
+        for (uint32_t i = 0; i < len; i++) seq1d[(size_t)i * nseq + q] = xorwow_uniform(s);
+        for (uint32_t i = 0; i < len; i++) {
+            float x = xorwow_uniform(s);
+            float y = xorwow_uniform(s);
+            seq2d[2 * ((size_t)i * nseq + q) + 0] = x;
+            seq2d[2 * ((size_t)i * nseq + q) + 1] = y;
+        }
+    }
+}
+
+struct Sampler {   // SequenceSampler (Sampler_device.h:59-113)
+    const float* s1; const float* s2; uint32_t nseq, len;
+    uint32_t idx, d1 = 0, d2 = 0;
+    float randomFloat() {
+        uint32_t k = d1 % len;
+        float val = 0.0f;
+        val += s1[(size_t)k * nseq + idx % nseq];
+        val += s1[(size_t)k * nseq + (idx / nseq) % nseq];
+        d1++;
+        return frac(val);
+    }
+    V2 randomFloat2() {
+        uint32_t k = d2 % len;
+        size_t a = (size_t)k * nseq + idx % nseq, b = (size_t)k * nseq + (idx / nseq) % nseq;
+        float x = 0.0f, y = 0.0f;
+        x += s2[2 * a]; y += s2[2 * a + 1];
+        x += s2[2 * b]; y += s2[2 * b + 1];
+        d2++;
+        return v2(frac(x), frac(y));
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Shading (diffuse + DiffuseLight), EXT_TRI TriangleData
+// ---------------------------------------------------------------------------
+using Spec = V3;   // RGB Spectrum, SPECTRUM_SAMPLES 3 (Math/Spectrum.h:10)
+inline float spec_max(Spec s) { float r = s.x; r = omax(r, s.y); r = omax(r, s.z); return r; }
+inline bool spec_zero(Spec s) { return s.x == 0.0f && s.y == 0.0f && s.z == 0.0f; }
+inline Spec spec_div(Spec s, float f) { float recip = 1.0f / f; return s * recip; }   // Spectrum.h:122-128
+
+struct DG {   // DifferentialGeometry subset
+    V3 P; Frame sys; V3 n; V3 dpdu, dpdv; V2 bary;
+};
+
+void fill_dg(const SceneView& S, V2 bary, uint32_t triIdx, uint32_t nodeIdx, DG& dg, bool quirk) {
+    // TriangleData::fillDG (Engine/TriangleData.cu:75-103) via fillDG (TraceHelper.cu:274-307)
+    M44 L2W = S.xf(nodeIdx);
+    dg.bary = bary;
+    const uint32_t* w = S.d->tri_data[triIdx].w;
+    auto hf = [&](uint16_t h) { return quirk ? half_to_float_host(h) : half_to_float_ieee(h); };
+    V3 na = normal_decode((uint16_t)(w[0] & 0xffff)), nb = normal_decode((uint16_t)(w[0] >> 16)),
+       nc = normal_decode((uint16_t)(w[1] & 0xffff));
+    float ww = 1.0f - dg.bary.x - dg.bary.y, u = dg.bary.x, v = dg.bary.y;
+    V3 n = normalize(u * na + v * nb + ww * nc);
+    V3 dpdu = v3(hf(w[2] & 0xffff), hf(w[2] >> 16), hf(w[3] & 0xffff));
+    V3 dpdv = v3(hf(w[3] >> 16), hf(w[4] & 0xffff), hf(w[4] >> 16));
+    V3 s = dpdu - n * dot(n, dpdu);
+    V3 t = cross(s, n);
+    s = transformDirection(L2W, s); t = transformDirection(L2W, t);
+    dg.sys.s = normalize(s); dg.sys.t = normalize(t); dg.sys.n = normalize(cross(t, s));
+    dg.dpdu = transformDirection(L2W, dpdu);
+    dg.dpdv = transformDirection(L2W, dpdv);
+    dg.n = normalize(cross(dg.dpdu, dg.dpdv));
+    if (dot(dg.n, dg.sys.n) < 0.0f) dg.n = -dg.n;
+}
+
+struct BRec {   // BSDFSamplingRecord subset
+    DG dg; V3 wi, wo; uint32_t sampledType; uint32_t typeMask;
+};
+
+const uint32_t EAll = 0x1ff, EDelta = 0x61, ESmooth = 0x1e;
+
+uint32_t mat_index(const SceneView& S, uint32_t tri, uint32_t node) {   // TraceResult.cu:83-86
+    return ((S.d->tri_data[tri].w[1] >> 16) & 0xff) + S.d->nodes[node].material_offset;
+}
+uint32_t light_index(const SceneView& S, uint32_t tri, uint32_t node) {  // TraceResult.cu:53-59
+    const ctl_material& m = S.d->materials[mat_index(S, tri, node)];
+    if (m.node_light_index == UINT_MAX) return UINT_MAX;
+    return S.d->nodes[node].lights[m.node_light_index];
+}
+
+// diffuse (BSDF_Simple.cu:7-75) under BSDFALL two-sided wrapper (BSDF.h:147-208)
+Spec diffuse_sample(const ctl_material& m, BRec& b, float& pdf, V2 sample) {
+    bool flip = b.wi.z < 0 && m.two_sided;
+    if (flip) b.wi.z *= -1.0f;
+    Spec res;
+    if (!(b.typeMask & m.combined_type) || (m.combined_type == CTL_EDIFFUSE_REFLECTION && b.wi.z <= 0)) {
+        res = v3s(0.0f);
+    } else {
+        b.sampledType = m.combined_type;
+        // Warp::squareToCosineHemisphere (Warp.h:61-66) + concentric disk (Warp.h:102-125)
+        float r1 = 2.0f * sample.x - 1.0f, r2 = 2.0f * sample.y - 1.0f;
+        float phi, r;
+        if (r1 == 0 && r2 == 0) { r = phi = 0; }
+        else if (r1 * r1 > r2 * r2) { r = r1; phi = (O_PI / 4.0f) * (r2 / r1); }
+        else { r = r2; phi = (O_PI / 2.0f) - (r1 / r2) * (O_PI / 4.0f); }
+        float sinPhi = cr_sin(phi), cosPhi = cr_cos(phi);
+        V2 p = v2(r * cosPhi, r * sinPhi);
+        float z = sqrtf(1.0f - p.x * p.x - p.y * p.y);
+        b.wo = v3(p.x, p.y, z);
+        pdf = fabsf(O_INV_PI * b.wo.z) * 1.0f;
+        res = v3(m.reflectance[0], m.reflectance[1], m.reflectance[2]) * 1.0f;
+    }
+    if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
+    return res;
+}
+Spec diffuse_f(const ctl_material& m, BRec& b) {
+    bool flip = b.wi.z < 0 && m.two_sided;
+    if (flip) b.wi.z *= -1.0f;
+    Spec res = v3s(0.0f);
+    if (b.typeMask & m.combined_type) {
+        bool validRefl = m.combined_type == CTL_EDIFFUSE_REFLECTION && b.wi.z > 0 && b.wo.z > 0;
+        bool validTrans = m.combined_type == CTL_EDIFFUSE_TRANSMISSION && b.wi.z * b.wo.z < 0;
+        Spec s = v3(m.reflectance[0], m.reflectance[1], m.reflectance[2]) * (O_INV_PI * fabsf(b.wo.z));
+        if (validRefl || validTrans) res = s;
+        else if (m.combined_type == (CTL_EDIFFUSE_REFLECTION | CTL_EDIFFUSE_TRANSMISSION)) res = s * 0.5f;
+    }
+    if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
+    return res;
+}
+float diffuse_pdf(const ctl_material& m, BRec& b) {
+    bool flip = b.wi.z < 0 && m.two_sided;
+    if (flip) b.wi.z *= -1.0f;
+    float res = 0.0f;
+    if (b.typeMask & m.combined_type) {
+        bool validRefl = m.combined_type == CTL_EDIFFUSE_REFLECTION && b.wi.z > 0 && b.wo.z > 0;
+        bool validTrans = m.combined_type == CTL_EDIFFUSE_TRANSMISSION && b.wi.z * b.wo.z < 0;
+        float f = fabsf(O_INV_PI * b.wo.z);
+        if (validRefl || validTrans) res = f;
+        else if (m.combined_type == (CTL_EDIFFUSE_REFLECTION | CTL_EDIFFUSE_TRANSMISSION)) res = f * 0.5f;
+    }
+    if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
+    return res;
+}
+
+struct DRec {   // DirectSamplingRecord
+    V3 p; V3 n; float pdf; int measure; V2 uv; V3 ref; V3 refN; V3 d; float dist;
+};
+const int ESolidAngle = 1, EArea = 3, EDiscrete = 4;
+
+// MonteCarlo::sampleReuse (Math/MonteCarlo.cu:7-14) with STL_lower_bound (Base/STL.h:39-56)
+uint32_t sample_reuse(const float* cdf, uint32_t size, float& sample, float& pdf) {
+    const float* first = cdf;
+    uint32_t count = size + 1;
+    while (count > 0) {
+        uint32_t c2 = count / 2;
+        const float* mid = first + c2;
+        if (*mid < sample) { first = ++mid; count -= c2 + 1; }
+        else count = c2;
+    }
+    uint32_t index = (uint32_t)omin(omax(0, int(first - cdf) - 1), int(size - 1));
+    pdf = cdf[index + 1] - cdf[index];
+    sample = (sample - cdf[index]) / pdf;
+    return index;
+}
+
+// DiffuseLight::sampleDirect, non-orthogonal (Light.cu:84-135) + ShapeSet::SamplePosition (ShapeSet.cu:51-69)
+Spec light_sample_direct(const SceneView& S, const ctl_light& L, DRec& dRec, V2 _sample) {
+    V2 sample = _sample;
+    const float* cdf = S.d->light_tri_cdf + L.cdf_first;
+    float pdf;
+    uint32_t index = sample_reuse(cdf, L.tri_count, sample.y, pdf);
+    const ctl_light_tri& sn = S.d->light_tris[L.tri_first + index];
+    float a = sqrtf(1.0f - sample.x);                      // Warp::squareToUniformTriangle
+    V2 bary = v2(1 - a, a * sample.y);
+    V3 p0 = v3(sn.p[0][0], sn.p[0][1], sn.p[0][2]), p1 = v3(sn.p[1][0], sn.p[1][1], sn.p[1][2]),
+       p2 = v3(sn.p[2][0], sn.p[2][1], sn.p[2][2]);
+    dRec.p = bary.x * p0 + bary.y * p1 + (1.f - bary.x - bary.y) * p2;
+    dRec.n = v3(sn.n[0], sn.n[1], sn.n[2]);
+    dRec.pdf = 1.0f / L.sum_area;
+    dRec.measure = EArea;
+    dRec.uv = bary;
+    V3 dir = dRec.p - dRec.ref;
+    float distSquared = lenSqr(dir);
+    dRec.dist = sqrtf(distSquared);
+    dRec.d = dir / dRec.dist;
+    float dp = absdot(dRec.d, dRec.n);
+    dRec.pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
+    dRec.measure = ESolidAngle;
+    if (dot(dRec.d, dRec.refN) >= 0 && dot(dRec.d, dRec.n) < 0 && dRec.pdf != 0) {
+        Spec rad = v3(L.radiance[0], L.radiance[1], L.radiance[2]);
+        return spec_div(rad, dRec.pdf) * 1.0f;
+    }
+    dRec.pdf = 0.0f;
+    return v3s(0.0f);
+}
+float light_pdf_direct(const ctl_light& L, const DRec& dRec) {   // Light.cu:137-155
+    if (dot(dRec.d, dRec.refN) >= 0 && dot(dRec.d, dRec.n) < 0) {
+        float pdfPos = 1.0f / L.sum_area;
+        if (dRec.measure == ESolidAngle) return pdfPos * (dRec.dist * dRec.dist) / absdot(dRec.d, dRec.n);
+        else if (dRec.measure == EArea) return pdfPos;
+        return 0.0f;
+    }
+    return 0.0f;
+}
+float pdf_emitter(const SceneView& S, uint32_t idx) {   // KernelDynamicScene.cu:41-45
+    return S.d->light_cdf[idx] - (idx == 0 ? 0.0f : S.d->light_cdf[idx - 1]);
+}
+inline float power_heuristic(float fPdf, float gPdf) {   // MonteCarlo.h:29-33 with nf=ng=1
+    float f = 1 * fPdf, g = 1 * gPdf;
+    return (f * f) / (f * f + g * g);
+}
+
+struct RenderCtx {
+    SceneView S;
+    Sampler* rng;
+    int tie;
+    bool quirk;
+    bool anyHitShadow;
+    uint64_t rays = 0;
+    Stats st;
+};
+
+bool occluded(RenderCtx& C, V3 ori, V3 dir, float tmax) {   // KernelDynamicScene.cu:70-80 with tmin=0
+    C.rays++;
+    float eps = C.S.d->ray_eps;
+    Hit h;
+    if (C.anyHitShadow) {
+        h.t = tmax - eps; h.tri = UINT_MAX; h.node = UINT_MAX;
+        if (C.S.d->n_nodes == 0) return false;
+        trace_two_level(C.S, ori, dir, 0.0f, eps, h, true, C.tie, &C.st);
+        return h.tri != UINT_MAX;
+    }
+    trace_ray(C.S, ori, dir, h, C.tie, &C.st);
+    bool end = h.t < tmax - eps;
+    return h.t > 0 + eps && end;
+}
+
+Spec estimate_direct(RenderCtx& C, BRec bRec, const ctl_material& mat, const ctl_light& light, float light_pdf) {
+    // TraceAlgorithms.cu:44-73 (flags = EAll & ~EDelta, attenuated, use_mis)
+    DRec dRec;
+    dRec.p = bRec.dg.P; dRec.n = bRec.dg.sys.n; dRec.measure = EArea;
+    dRec.ref = bRec.dg.P; dRec.refN = bRec.dg.sys.n;
+    Spec value = light_sample_direct(C.S, light, dRec, C.rng->randomFloat2());
+    Spec retVal = v3s(0.0f);
+    if (!spec_zero(value)) {
+        bRec.wo = toLocal(bRec.dg.sys, dRec.d);
+        bRec.typeMask = EAll & ~EDelta;
+        Spec bsdfVal = diffuse_f(mat, bRec);
+        if (!spec_zero(bsdfVal) && !occluded(C, dRec.ref, dRec.d, dRec.dist)) {
+            float weight = 1.0f;
+            if (dRec.measure != EDiscrete) {
+                const float bsdfPdf = diffuse_pdf(mat, bRec);
+                const float directPdf = dRec.pdf * light_pdf;   // measure is ESolidAngle
+                weight = power_heuristic(directPdf, bsdfPdf);
+            }
+            retVal = value * bsdfVal * weight;
+            retVal = retVal * v3s(1.0f);   // Transmittance() without volumes
+        }
+    }
+    return retVal;
+}
+
+Spec uniform_sample_one_light(RenderCtx& C, const BRec& bRec, const ctl_material& mat) {
+    // TraceAlgorithms.cu:92-101 + sampleEmitter (KernelDynamicScene.cu:25-39)
+    const ctl_scene_desc* d = C.S.d;
+    if (!d->n_lights) return v3s(0.0f);
+    V2 sample = C.rng->randomFloat2();
+    uint32_t n = omin(d->n_lights, (uint32_t)CTL_MAX_NUM_LIGHTS);
+    const float* cdf = d->light_cdf;
+    const float* first = cdf; uint32_t count = n;   // STL_upper_bound
+    while (count > 0) {
+        uint32_t c2 = count / 2; const float* mid = first + c2;
+        if (!(sample.x < *mid)) { first = ++mid; count -= c2 + 1; } else count = c2;
+    }
+    uint32_t idx = (uint32_t)(first - cdf);
+    if (idx >= n) idx = n - 1;
+    float fU = cdf[idx], fL = idx > 0 ? cdf[idx - 1] : 0.0f;
+    sample.x = (sample.x - fL) / (fU - fL);
+    float pdf = fU - fL;
+    return spec_div(estimate_direct(C, bRec, mat, d->lights[idx], pdf), pdf);
+}
+
+// PathTrace<true> restricted to surfaces without media / env map (PathTracer.cu:10-113)
+Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, int maxPathLength, int rrStartDepth) {
+    const ctl_scene_desc* d = C.S.d;
+    Spec cl = v3s(0.0f), cf = v3s(1.0f);
+    int depth = 0;
+    bool specularBounce = false;
+    BRec bRec;
+    bRec.wo = v3(0, 0, 1);   // reference leaves it uninitialised before the first sample
+    float brdf_scattering_pdf = 0;
+    V3 last_nor = v3(0, 0, 0);
+    Hit r2;
+    while (depth++ < maxPathLength) {
+        C.rays++;
+        trace_ray(C.S, rori, rdir, r2, C.tie, &C.st);
+        if (r2.tri != UINT_MAX) {
+            // TraceResult::getBsdfSample (TraceResult.cu:16-45)
+            bRec.sampledType = 0;
+            bRec.typeMask = EAll;
+            bRec.dg.P = rori + r2.t * rdir;
+            fill_dg(C.S, v2(r2.u, r2.v), r2.tri, r2.node, bRec.dg, C.quirk);
+            bRec.wi = toLocal(bRec.dg.sys, -rdir);
+            const ctl_material& mat = d->materials[mat_index(C.S, r2.tri, r2.node)];
+            if (mat.two_sided && bRec.wi.z < 0) {
+                bRec.dg.n = -bRec.dg.n;
+                bRec.dg.sys.n = -bRec.dg.sys.n;
+                bRec.wi.z *= -1.0f;
+            }
+            uint32_t li = light_index(C.S, r2.tri, r2.node);
+            if (li != UINT_MAX) {
+                float misWeight = 1.0f;
+                const ctl_light& L = d->lights[li];
+                if (!(depth == 1 || specularBounce)) {
+                    DRec dRec;   // DirectSamplingRecFromRay (TraceAlgorithms.cu:33-42)
+                    dRec.ref = rori; dRec.refN = last_nor; dRec.p = bRec.dg.P; dRec.n = bRec.dg.n;
+                    dRec.d = rdir; dRec.dist = r2.t; dRec.measure = ESolidAngle;
+                    float direct_pdf = light_pdf_direct(L, dRec) * pdf_emitter(C.S, li);
+                    misWeight = power_heuristic(brdf_scattering_pdf, direct_pdf);
+                }
+                // DiffuseLight::eval (Light.cu:67-82)
+                V3 w = -rdir;
+                Spec Le = (dot(bRec.dg.sys.n, w) <= 0) ? v3s(0.0f) : v3(L.radiance[0], L.radiance[1], L.radiance[2]);
+                cl = cl + (cf * misWeight) * Le;
+            }
+            Spec f = diffuse_sample(mat, bRec, brdf_scattering_pdf, C.rng->randomFloat2());
+            last_nor = bRec.dg.sys.n;
+            if ((mat.combined_type & ESmooth) != 0) cl = cl + cf * uniform_sample_one_light(C, bRec, mat);
+            specularBounce = (bRec.sampledType & EDelta) != 0;
+            cf = cf * f;
+            rori = bRec.dg.P;
+            rdir = toWorld(bRec.dg.sys, bRec.wo);
+        }
+        if (r2.tri == UINT_MAX) break;
+        if (depth > rrStartDepth && !specularBounce) {
+            if (C.rng->randomFloat() >= spec_max(cf)) break;
+            cf = spec_div(cf, spec_max(cf));
+        }
+    }
+    if (r2.tri == UINT_MAX) cl = cl + (cf * 1.0f) * v3s(0.0f);   // EvalEnvironment without env map
+    return cl;
+}
+
+void sensor_ray(const ctl_camera& cam, V2 pixelSample, V3& ori, V3& dir) {
+    // PerspectiveSensor::sampleRayDifferential (Sensor.cu:130-144)
+    M44 s2c, tw;
+    std::memcpy(s2c.d, cam.sample_to_camera.m, 64);
+    std::memcpy(tw.d, cam.to_world.m, 64);
+    V3 nearP = transformPoint(s2c, v3(pixelSample.x * cam.inv_resolution[0], pixelSample.y * cam.inv_resolution[1], 0.0f));
+    V3 dd = normalize(nearP);
+    ori = transformPoint(tw, v3s(0.0f));
+    dir = transformDirection(tw, dd);
+}
+
+void add_sample(ctl_pixel* fb, uint32_t w, uint32_t h, float sx, float sy, Spec L) {   // Image.cu:22-44
+    L.x = omax(0.0f, L.x); L.y = omax(0.0f, L.y); L.z = omax(0.0f, L.z);
+    int x = floor2int(sx), y = floor2int(sy);
+    auto bad = [](float f) { return std::isnan(f); };
+    auto invalid = [](float f) { return !std::isfinite(f) || f < 0.0f; };
+    if (x < 0 || x >= (int)w || y < 0 || y >= (int)h || bad(L.x) || bad(L.y) || bad(L.z) || invalid(L.x) ||
+        invalid(L.y) || invalid(L.z))
+        return;
+    ctl_pixel& p = fb[(size_t)y * w + x];
+    p.rgb[0] += L.x; p.rgb[1] += L.y; p.rgb[2] += L.z;
+    p.weight_sum += 1.0f;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C API for tests (ctypes)
+// ===========================================================================
+extern "C" {
+
+void oracle_woop_set(const float* v0, const float* v1, const float* v2, float* out12) {
+    woop_set(v3(v0[0], v0[1], v0[2]), v3(v1[0], v1[1], v1[2]), v3(v2[0], v2[1], v2[2]), out12);
+}
+void oracle_woop_get(const float* in12, float* v0, float* v1, float* v2) {
+    V3 a, b, c;
+    woop_get(in12, a, b, c);
+    v0[0] = a.x; v0[1] = a.y; v0[2] = a.z;
+    v1[0] = b.x; v1[1] = b.y; v1[2] = b.z;
+    v2[0] = c.x; v2[1] = c.y; v2[2] = c.z;
+}
+
+void oracle_xorwow_uniforms(uint64_t subsequence, uint64_t offset, uint64_t n, float* out) {
+    Xorwow s = curand_init(1234, subsequence, offset);
+    for (uint64_t i = 0; i < n; i++) out[i] = xorwow_uniform(s);
+}
+void oracle_xorwow_raw(uint64_t seed, uint64_t subsequence, uint64_t offset, uint64_t n, uint32_t* out) {
+    Xorwow s = curand_init(seed, subsequence, offset);
+    for (uint64_t i = 0; i < n; i++) out[i] = xorwow_next(s);
+}
+void oracle_sampler_tables(uint64_t pass, uint32_t nseq, uint32_t len, float* seq1d, float* seq2d) {
+    sampler_tables(pass, nseq, len, seq1d, seq2d);
+}
+// Draws of SequenceSampler(idx): n1 randomFloat() then n2 randomFloat2().
+void oracle_sampler_draws(const float* seq1d, const float* seq2d, uint32_t nseq, uint32_t len, uint32_t idx,
+                          uint32_t n1, float* out1, uint32_t n2, float* out2) {
+    Sampler s{seq1d, seq2d, nseq, len, idx};
+    for (uint32_t i = 0; i < n1; i++) out1[i] = s.randomFloat();
+    for (uint32_t i = 0; i < n2; i++) { V2 v = s.randomFloat2(); out2[2 * i] = v.x; out2[2 * i + 1] = v.y; }
+}
+
+// PerspectiveSensor::Update + Sensor::SetToWorld(pos, tar, up) (Sensor.cu:76-96,674-699)
+void oracle_camera(const float* pos, const float* tar, const float* up, float fov_deg, float nearc, float farc,
+                   uint32_t w, uint32_t h, ctl_camera* out) {
+    V3 p = v3(pos[0], pos[1], pos[2]), t = v3(tar[0], tar[1], tar[2]), u = v3(up[0], up[1], up[2]);
+    V3 f = normalize(t - p);
+    V3 r = normalize(cross(f, u));
+    M44 view = M44::identity();
+    view.setCol(0, v4(r, 0)); view.setCol(1, v4(u, 0)); view.setCol(2, v4(f, 0));
+    view.setCol(3, v4(0, 0, 0, 1)); view.setRow(3, v4(0, 0, 0, 1));
+    M44 tr = M44::identity(); tr(0, 3) = p.x; tr(1, 3) = p.y; tr(2, 3) = p.z;
+    M44 toWorld = matmul(tr, view);
+    float resx = (float)w, resy = (float)h;
+    float invx = 1.0f / resx, invy = 1.0f / resy;
+    float aspect = resx / resy;
+    float fov = ((float)O_PI / 180.f) * fov_deg;
+    M44 sc = M44::identity(); sc(0, 0) = -0.5f; sc(1, 1) = -0.5f * aspect; sc(2, 2) = 1.0f;
+    M44 tl = M44::identity(); tl(0, 3) = -1.0f; tl(1, 3) = -1.0f / aspect; tl(2, 3) = 0.0f;
+    float recip = 1.0f / (farc - nearc);
+    float cot = 1.0f / cr_tan(fov / 2.0f);
+    M44 pe = M44::zeros();
+    pe(0, 0) = cot; pe(1, 1) = cot; pe(2, 2) = farc * recip; pe(2, 3) = -nearc * farc * recip; pe(3, 2) = 1;
+    M44 camToSample = matmul(matmul(sc, tl), pe);
+    M44 s2c = inverse(camToSample);
+    V3 dx = transformPoint(s2c, v3(invx, 0.0f, 0.0f)) - transformPoint(s2c, v3s(0.0f));
+    V3 dy = transformPoint(s2c, v3(0.0f, invy, 0.0f)) - transformPoint(s2c, v3s(0.0f));
+    std::memcpy(out->to_world.m, toWorld.d, 64);
+    std::memcpy(out->sample_to_camera.m, s2c.d, 64);
+    out->dx[0] = dx.x; out->dx[1] = dx.y; out->dx[2] = dx.z;
+    out->dy[0] = dy.x; out->dy[1] = dy.y; out->dy[2] = dy.z;
+    out->inv_resolution[0] = invx; out->inv_resolution[1] = invy;
+    out->width = w; out->height = h;
+}
+
+// traceRay semantics (mode 0) or batch semantics (mode 1 closest, 2 any-hit).
+// Outputs t,u,v,tri,node per ray; stats[0..3] = rays, inner nodes, tri tests, instance entries.
+void oracle_trace(const ctl_scene_desc* desc, int64_t n, const ctl_ray* rays, int32_t mode, int32_t tie,
+                  float* out_t, float* out_u, float* out_v, uint32_t* out_tri, uint32_t* out_node, uint64_t* stats,
+                  int32_t threads) {
+    SceneView S{desc};
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+    std::atomic<int64_t> next{0};
+    std::mutex mtx;
+    uint64_t acc[4] = {0, 0, 0, 0};
+    auto worker = [&]() {
+        Stats st;
+        uint64_t nr = 0;
+        for (;;) {
+            int64_t base = next.fetch_add(256);
+            if (base >= n) break;
+            int64_t end = std::min<int64_t>(n, base + 256);
+            for (int64_t i = base; i < end; i++) {
+                const ctl_ray& r = rays[i];
+                V3 o = v3(r.o[0], r.o[1], r.o[2]), dd = v3(r.d[0], r.d[1], r.d[2]);
+                Hit h;
+                if (mode == 0) {
+                    trace_ray(S, o, dd, h, tie, &st);
+                } else {
+                    h.t = r.tmax; h.tri = UINT_MAX; h.node = UINT_MAX; h.u = h.v = 0;
+                    trace_two_level(S, o, dd, r.tmin, r.tmin, h, mode == 2, tie, &st);
+                }
+                nr++;
+                out_t[i] = h.t; out_u[i] = h.u; out_v[i] = h.v; out_tri[i] = h.tri; out_node[i] = h.node;
+            }
+        }
+        std::lock_guard<std::mutex> g(mtx);
+        acc[0] += nr; acc[1] += st.nodes; acc[2] += st.tris; acc[3] += st.inst;
+    };
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; i++) ts.emplace_back(worker);
+    for (auto& t : ts) t.join();
+    if (stats) for (int i = 0; i < 4; i++) stats[i] = acc[i];
+}
+
+// Batch kernel output layout (ctl_hit), TraceHelper.cu:722-731.
+void oracle_intersect(const ctl_scene_desc* desc, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit,
+                      int32_t tie, int32_t threads) {
+    std::vector<float> t(n), u(n), v(n);
+    std::vector<uint32_t> tri(n), node(n);
+    oracle_trace(desc, n, rays, any_hit ? 2 : 1, tie, t.data(), u.data(), v.data(), tri.data(), node.data(), nullptr,
+                 threads);
+    for (int64_t i = 0; i < n; i++) {
+        ctl_hit& h = hits[i];
+        h.dist = t[i];
+        if (tri[i] == UINT_MAX) { h.node_idx = -1; h.tri_idx = -1; h.bary = 0; }
+        else {
+            h.node_idx = (int32_t)node[i]; h.tri_idx = (int32_t)tri[i];
+            uint16_t xd = (uint16_t)(u[i] * 65535), yd = (uint16_t)(v[i] * 65535);
+            h.bary = (int32_t)(((uint32_t)yd << 16) | (uint32_t)xd);
+        }
+    }
+}
+
+// Closest hit by scanning every leaf entry of every node (BVH-independent truth).
+void oracle_brute_force(const ctl_scene_desc* d, int64_t n, const ctl_ray* rays, float* out_t, uint32_t* out_tri,
+                        int32_t threads) {
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+    std::atomic<int64_t> next{0};
+    auto worker = [&]() {
+        for (;;) {
+            int64_t i = next.fetch_add(1);
+            if (i >= n) break;
+            const ctl_ray& r = rays[i];
+            V3 o = v3(r.o[0], r.o[1], r.o[2]), dd = v3(r.d[0], r.d[1], r.d[2]);
+            float best = FLT_MAX; uint32_t bt = UINT_MAX;
+            for (uint32_t ni = 0; ni < d->n_nodes; ni++) {
+                const ctl_kernel_mesh& mesh = d->meshes[d->nodes[ni].mesh_index];
+                M44 modl; std::memcpy(modl.d, d->node_inv_xf[ni].m, 64);
+                V3 dl = transformDirection(modl, dd), ol = transformPoint(modl, o);
+                // entries of this mesh: [bvh_indices_offset, next mesh offset)
+                uint64_t e0 = mesh.bvh_indices_offset, e1 = d->n_tri_indices;
+                for (uint32_t m = 0; m < d->n_meshes; m++)
+                    if (d->meshes[m].bvh_indices_offset > e0 && d->meshes[m].bvh_indices_offset < e1) e1 = d->meshes[m].bvh_indices_offset;
+                for (uint64_t e = e0; e < e1; e++) {
+                    const float* v = reinterpret_cast<const float*>(d->woop_tris) + 12 * e;
+                    float Oz = v[3] - ol.x * v[0] - ol.y * v[1] - ol.z * v[2];
+                    float invDz = 1.0f / (dl.x * v[0] + dl.y * v[1] + dl.z * v[2]);
+                    float t = Oz * invDz;
+                    uint32_t gtri = (d->tri_indices[e] >> 1) + mesh.triangle_offset;
+                    if (t > d->ray_eps && (t < best || (t == best && gtri < bt))) {
+                        float u = (v[7] + ol.x * v[4] + ol.y * v[5] + ol.z * v[6]) + t * (dl.x * v[4] + dl.y * v[5] + dl.z * v[6]);
+                        if (u >= 0.0f) {
+                            float vv = (v[11] + ol.x * v[8] + ol.y * v[9] + ol.z * v[10]) + t * (dl.x * v[8] + dl.y * v[9] + dl.z * v[10]);
+                            if (vv >= 0.0f && u + vv <= 1.0f) { best = t; bt = gtri; }
+                        }
+                    }
+                }
+            }
+            out_t[i] = best; out_tri[i] = bt;
+        }
+    };
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; i++) ts.emplace_back(worker);
+    for (auto& t : ts) t.join();
+}
+
+// One PathTracer pass (pathKernel2 semantics, PathTracer.cu:182-194) over the
+// pixels of the tiles owned by (rank, num_ranks), accumulating into fb.
+// Returns the number of traceRay calls.  pixel_stride > 1 renders only every
+// pixel_stride-th pixel (bounded CPU-baseline samples); stats may be NULL.
+uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm, uint64_t pass_index,
+                            ctl_pixel* fb, int32_t tie, int32_t threads, uint32_t pixel_stride, uint64_t* stats) {
+    const uint32_t nseq = 4096, len = 30;
+    std::vector<float> s1((size_t)nseq * len), s2((size_t)nseq * len * 2);
+    sampler_tables(pass_index, nseq, len, s1.data(), s2.data());
+    const ctl_camera& cam = desc->camera;
+    uint32_t W = cam.width, H = cam.height;
+    uint32_t ts = prm->tile_size ? prm->tile_size : 64;
+    uint32_t tilesX = (W + ts - 1) / ts;
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+    if (pixel_stride == 0) pixel_stride = 1;
+    std::atomic<int64_t> nextRow{0};
+    std::mutex mtx;
+    uint64_t totalRays = 0, acc[3] = {0, 0, 0};
+    auto worker = [&]() {
+        RenderCtx C{SceneView{desc}, nullptr, tie, (desc->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0,
+                    prm->shadow_any_hit != 0};
+        for (;;) {
+            int64_t y = nextRow.fetch_add(1);
+            if (y >= (int64_t)H) break;
+            for (uint32_t x = 0; x < W; x++) {
+                uint64_t lin = (uint64_t)y * W + x;
+                if (lin % pixel_stride) continue;
+                uint32_t tile = (uint32_t)(y / ts) * tilesX + x / ts;
+                if (prm->num_ranks > 1 && tile % prm->num_ranks != prm->rank) continue;
+                Sampler rng{s1.data(), s2.data(), nseq, len, (uint32_t)(y * W + x)};
+                C.rng = &rng;
+                V2 pX = v2((float)x, (float)y) + rng.randomFloat2();
+                V2 aperture = rng.randomFloat2();
+                (void)aperture;
+                V3 o, dd;
+                sensor_ray(cam, pX, o, dd);
+                Spec col = v3s(1.0f) * path_trace(C, o, dd, prm->max_path_length, prm->rr_start_depth);
+                add_sample(fb, W, H, pX.x, pX.y, col);
+            }
+        }
+        std::lock_guard<std::mutex> g(mtx);
+        totalRays += C.rays;
+        acc[0] += C.st.nodes; acc[1] += C.st.tris; acc[2] += C.st.inst;
+    };
+    std::vector<std::thread> tv;
+    for (int i = 0; i < threads; i++) tv.emplace_back(worker);
+    for (auto& t : tv) t.join();
+    if (stats) { stats[0] = totalRays; stats[1] = acc[0]; stats[2] = acc[1]; stats[3] = acc[2]; }
+    return totalRays;
+}
+
+// Host-side compile pieces, for checking the product's scene compiler.
+void oracle_triangle_data_set(const float* P9, uint8_t mat, const float* T6, const float* N9, uint32_t* out8) {
+    // TriangleData::TriangleData + setUvSetData + setData (TriangleData.cu:10-68), EXT_TRI
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // MatIndex byte (byte 6)
+    w[1] = (w[1] & 0xff00ffffu) | ((uint32_t)mat << 16);
+    uint16_t a0 = float_to_half(T6[0]), a1 = float_to_half(T6[1]);
+    uint16_t b0 = float_to_half(T6[2]), b1 = float_to_half(T6[3]);
+    uint16_t c0 = float_to_half(T6[4]), c1 = float_to_half(T6[5]);
+    w[5] = a0 | ((uint32_t)a1 << 16);
+    w[6] = b0 | ((uint32_t)b1 << 16);
+    w[7] = c0 | ((uint32_t)c1 << 16);
+    V2 t0 = v2(half_to_float_host(w[5] & 0xffff), half_to_float_host(w[5] >> 16));
+    V2 t1 = v2(half_to_float_host(w[6] & 0xffff), half_to_float_host(w[6] >> 16));
+    V2 t2 = v2(half_to_float_host(w[7] & 0xffff), half_to_float_host(w[7] >> 16));
+    V3 v0 = v3(P9[0], P9[1], P9[2]), v1 = v3(P9[3], P9[4], P9[5]), v2_ = v3(P9[6], P9[7], P9[8]);
+    V3 dP1 = v1 - v0, dP2 = v2_ - v0;
+    V2 dUV1 = t1 - t0, dUV2 = t2 - t0;
+    float determinant = dUV1.x * dUV2.y - dUV1.y * dUV2.x;
+    V3 dpdu, dpdv;
+    if (determinant == 0) {
+        V3 a, b, n = normalize(cross(dP1, dP2));
+        coordinateSystem(n, a, b);
+        dpdu = a; dpdv = b;
+    } else {
+        float invDet = 1.0f / determinant;
+        dpdu = ((dUV2.y * dP1 - dUV1.y * dP2) * invDet);
+        dpdv = ((-dUV2.x * dP1 + dUV1.x * dP2) * invDet);
+    }
+    V3 n0 = v3(N9[0], N9[1], N9[2]), n1 = v3(N9[3], N9[4], N9[5]), n2 = v3(N9[6], N9[7], N9[8]);
+    w[0] = (uint32_t)normal_encode(n0) | ((uint32_t)normal_encode(n1) << 16);
+    w[1] = (uint32_t)normal_encode(n2) | (w[1] & 0xffff0000u);
+    uint16_t ax = float_to_half(dpdu.x), ay = float_to_half(dpdu.y), az = float_to_half(dpdu.z);
+    uint16_t bx = float_to_half(dpdv.x), by = float_to_half(dpdv.y), bz = float_to_half(dpdv.z);
+    w[2] = ax | ((uint32_t)ay << 16);
+    w[3] = az | ((uint32_t)bx << 16);
+    w[4] = by | ((uint32_t)bz << 16);
+    std::memcpy(out8, w, 32);
+}
+
+// ShapeSet::triData::Recalculate (ShapeSet.cu:11-22), host decode.
+void oracle_light_tri(const float* woop12, const uint32_t* tri_data8, const float* xf16, float* p9, float* n3,
+                      float* area) {
+    M44 mat; std::memcpy(mat.d, xf16, 64);
+    V3 p[3];
+    woop_get(woop12, p[0], p[1], p[2]);
+    // fillDG with bary (1/3, 1/3) on the host path
+    ctl_triangle_data td; std::memcpy(td.w, tri_data8, 32);
+    ctl_scene_desc dd{}; dd.tri_data = &td; dd.n_tri_data = 1;
+    ctl_float4x4 xfm; std::memcpy(xfm.m, xf16, 64);
+    dd.node_xf = &xfm;
+    SceneView S{&dd};
+    DG dg;
+    fill_dg(S, v2(1.0f / 3.0f, 1.0f / 3.0f), 0, 0, dg, true);
+    for (int i = 0; i < 3; i++) p[i] = transformPoint(mat, p[i]);
+    float a = 0.5f * length(cross(p[2] - p[0], p[1] - p[0]));
+    for (int i = 0; i < 3; i++) { p9[3 * i] = p[i].x; p9[3 * i + 1] = p[i].y; p9[3 * i + 2] = p[i].z; }
+    n3[0] = dg.sys.n.x; n3[1] = dg.sys.n.y; n3[2] = dg.sys.n.z;
+    *area = a;
+}
+
+void oracle_matrix_inverse(const float* in16, float* out16) {
+    M44 m; std::memcpy(m.d, in16, 64);
+    M44 r = inverse(m);
+    std::memcpy(out16, r.d, 64);
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+"""Shared helpers for the parity tests (test infrastructure)."""
+import ctypes as C
+
+import numpy as np
+
+import oracle
+
+
+def random_rays(desc, n, seed=0, tmin=0.0, tmax=3.0e38, inside=True):
+    """Rays with origins inside the scene box and uniformly random directions (ctl_ray layout)."""
+    rng = np.random.default_rng(seed)
+    lo = np.array(desc.box_min[:], np.float64)
+    hi = np.array(desc.box_max[:], np.float64)
+    o = lo + (hi - lo) * rng.random((n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r = np.zeros((n, 8), np.float32)
+    r[:, 0:3] = o
+    r[:, 3] = tmin
+    r[:, 4:7] = d
+    r[:, 7] = tmax
+    return r
+
+
+def camera_rays(desc, w, h, seed=0):
+    """Primary rays through jittered pixel centres (PerspectiveSensor, numpy fp64: only inputs)."""
+    cam = desc.camera
+    tw = np.array(cam.to_world.m[:], np.float64).reshape(4, 4)
+    s2c = np.array(cam.sample_to_camera.m[:], np.float64).reshape(4, 4)
+    rng = np.random.default_rng(seed)
+    ys, xs = np.mgrid[0:h, 0:w]
+    px = (xs.ravel() + rng.random(w * h)) / w
+    py = (ys.ravel() + rng.random(w * h)) / h
+    p = np.stack([px, py, np.zeros_like(px), np.ones_like(px)], 1) @ s2c.T
+    p = p[:, :3] / p[:, 3:4]
+    d = p / np.linalg.norm(p, axis=1, keepdims=True)
+    d = d @ tw[:3, :3].T
+    r = np.zeros((w * h, 8), np.float32)
+    r[:, 0:3] = tw[:3, 3]
+    r[:, 4:7] = d
+    r[:, 7] = 3.0e38
+    return r
+
+
+def oracle_intersect(orc, desc, rays, any_hit=False, tie=0, threads=0):
+    n = rays.shape[0]
+    hits = np.zeros((n, 4), np.int32)
+    orc.oracle_intersect(C.byref(desc), n, oracle.ptr(rays), oracle.ptr(hits), 1 if any_hit else 0, tie, threads)
+    return hits
+
+
+def oracle_trace(orc, desc, rays, mode=0, tie=0, threads=0):
+    n = rays.shape[0]
+    t = np.zeros(n, np.float32)
+    u = np.zeros(n, np.float32)
+    v = np.zeros(n, np.float32)
+    tri = np.zeros(n, np.uint32)
+    node = np.zeros(n, np.uint32)
+    st = np.zeros(4, np.uint64)
+    orc.oracle_trace(C.byref(desc), n, oracle.ptr(rays), mode, tie, oracle.ptr(t), oracle.ptr(u), oracle.ptr(v),
+                     oracle.ptr(tri), oracle.ptr(node), oracle.ptr(st), threads)
+    return t, u, v, tri, node, st
+
+
+def oracle_render(orc, desc, params, passes, w, h, threads=0, fb=None, first_pass=0):
+    if fb is None:
+        fb = np.zeros((w * h, 7), np.float32)
+    rays = 0
+    for p in range(first_pass, first_pass + passes):
+        rays += orc.oracle_render_pass(C.byref(desc), C.byref(params), p, oracle.ptr(fb), 0, threads, 1, None)
+    return fb, rays
