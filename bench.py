@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""bench.py — Mrays/s (primary + secondary) of the CudaTracerLib PathTracer hot
+path (two-level BVH traversal + Woop intersection driven by the PathTrace<true>
+pass loop) on MI355X.
+
+Workload (BASELINE.json metric "Mrays/s (primary+secondary) at 1920x1080,
+San-Miguel-scale BVH"): configs[2] = PathTracer on the synthetic ~10M-triangle
+scene (seed 0x5EED), 1920x1080, Direct=1, MaxPathLength=50, RRStartDepth=5.
+
+A *step* = one full-image pass-equivalent per GPU: at N GPUs each rank renders
+N progressive passes over the 64x64 image tiles it owns (tile_id % N == rank),
+so per-GPU work is fixed ("weak" scaling) and the job's image after K steps is
+the N*K-spp image, bit-identical to a single-GPU render of the same passes.
+After the last step the PixelData framebuffers are summed to rank 0 with one
+RCCL reduce over xGMI (inside the timed region).  Rays counted exactly as the
+reference's k_getNumRaysTraced (every traceRay incl. NEE shadow rays).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
+torch.distributed.run (one process per GPU, RCCL backend).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3, help="1 Cornell, 2 C2 100k, 3 C3 ~10M tris")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--max-path-length", type=int, default=50)
+    ap.add_argument("--rr-start", type=int, default=5)
+    ap.add_argument("--shadow-any-hit", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--backend", default="nccl")
+    return ap.parse_args()
+
+
+def cpu_baseline(desc, params, seconds, threads):
+    """The oracle (CPU restatement of the reference path, oracle/) timed on the
+    host cores on a bounded sample: every 4th pixel of consecutive passes."""
+    import oracle
+    O = oracle.load()
+    fb = np.zeros((desc.camera.width * desc.camera.height, 7), np.float32)
+    rays = 0
+    passes = 0
+    stats = np.zeros(4, np.uint64)
+    t0 = time.perf_counter()
+    while True:
+        st = np.zeros(4, np.uint64)
+        rays += O.oracle_render_pass(C.byref(desc), C.byref(params), 10_000 + passes, oracle.ptr(fb), 0, threads, 4,
+                                     oracle.ptr(st))
+        stats += st
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or passes >= 64:
+            break
+    return {
+        "value": round(rays / el / 1e6, 4),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle PathTrace<true> on the same scene, every 4th pixel of {passes} pass(es), "
+                  f"{rays} rays in {el:.1f} s",
+        "ref_nodes_per_ray": round(float(stats[1]) / max(1, float(stats[0])), 3),
+        "ref_tris_per_ray": round(float(stats[2]) / max(1, float(stats[0])), 3),
+    }
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        log(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import cudatracerlib_amd as ctl
+
+    if world > 1:
+        dist.init_process_group(a.backend)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    threads = max(1, int(os.environ.get("OMP_NUM_THREADS", "8")))
+
+    t0 = time.perf_counter()
+    hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
+    desc = hs.compile(threads=threads)
+    t_build = time.perf_counter() - t0
+    log(f"[rank {rank}] scene config {a.config}: {desc.n_tri_data} tris, {desc.n_bvh_nodes} BVH nodes, "
+        f"built in {t_build:.1f}s with {threads} threads")
+
+    pt = ctl.PathTracer(local, max_path_length=a.max_path_length, rr_start_depth=a.rr_start,
+                        shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, num_ranks=world, rank=rank)
+    pt.upload_scene(desc)
+    W, H = a.width, a.height
+    fb = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
+
+    # Instrumented pass (same kernel compiled with counters, untimed) for the
+    # roofline's algorithmic bytes: 64 B per inner node visited, 52 B per
+    # triangle tested (48 B Woop + 4 B index), 108 B per instance entry
+    # (SURVEY.md §8d); per-launch = one pass over this rank's tiles.
+    scratch = torch.zeros_like(fb)
+    st = pt.pass_stats(scratch.data_ptr(), 1 << 40, sptr)
+    alg_bytes_per_pass = 64 * st[1] + 52 * st[2] + 108 * st[3]
+    del scratch
+
+    pass_base = 0
+    steps_done = 0
+
+    def step(s):
+        for k in range(world):
+            pt.do_pass(fb.data_ptr(), pass_base + s * world + k, sptr)
+
+    for s in range(a.warmup):
+        step(s)
+    steps_done = a.warmup
+    torch.cuda.synchronize(dev)
+    fb.zero_()
+    pass_base = steps_done * world   # fresh passes for the timed image
+    pt.reset_rays(sptr)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for s in range(a.steps):
+        step(s)
+    ev1.record(stream)
+    if world > 1:
+        dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)   # RCCL over xGMI
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1)
+
+    rays = pt.rays_traced()
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    rr = torch.tensor([rays], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(rr, op=dist.ReduceOp.SUM)
+    elapsed = float(tt.item())
+    total_rays = int(rr.item())
+
+    if rank == 0:
+        passes = a.steps * world
+        img = fb.view(H, W, 7)
+        wsum = float(img[..., 6].sum().item())
+        launches = a.steps * world   # path_kernel launches on this rank in the timed region
+        per_launch_ms = kernel_ms / launches
+        achieved = alg_bytes_per_pass / (per_launch_ms * 1e-3) / 1e9
+        traffic = None
+        tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
+        if os.path.exists(tf):
+            try:
+                j = json.load(open(tf))
+                if j.get("config") == [a.config, a.scale, W, H] and world == 1:
+                    traffic = j.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "Mrays/s (primary+secondary) at 1920x1080, San-Miguel-scale BVH",
+            "value": round(total_rays / elapsed / 1e6, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural scene, seed 0x5EED; SequenceSampler/XORWOW stream of the reference)",
+            "config": {
+                "workload": f"PathTracer C{a.config} (BASELINE.json configs[{a.config - 1}]): "
+                            f"{desc.n_tri_data} tris, {W}x{H}, {passes} spp, Direct=1, MaxPathLength="
+                            f"{a.max_path_length}, RRStartDepth={a.rr_start}, shadow rays any-hit="
+                            f"{a.shadow_any_hit}",
+                "triangles": int(desc.n_tri_data),
+                "bvh_inner_nodes": int(desc.n_bvh_nodes),
+                "resolution": [W, H],
+                "spp": passes,
+                "tile": 64,
+                "parallelism": f"image-tile shard x{world} + RCCL reduce" if world > 1 else "single GPU",
+                "total_rays": total_rays,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": 8000.0,
+                "unit": "GB/s",
+                "frac": round(achieved / 8000.0, 4),
+                "traffic": traffic,
+                "kernel": "path_kernel<false> (megakernel: traversal + shading)",
+                "alg_bytes_per_launch": int(alg_bytes_per_pass),
+                "per_launch_ms": round(per_launch_ms, 3),
+                "visits_per_launch": {"inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3]),
+                                      "rays": int(st[0])},
+            },
+            "image_weight_sum": wsum,
+            "scene_build_s": round(t_build, 2),
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            cores = min(16, os.cpu_count() or 1, threads if threads > 1 else 16)
+            out["cpu_baseline"] = cpu_baseline(desc, pt.params, a.cpu_seconds, cores)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    pt.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -20,6 +20,8 @@
 
 namespace ctl {
 void sampler_tables(uint64_t pass, uint32_t nseq, uint32_t len, float* seq1d, float* seq2d);
+void sampler_pass_state(uint64_t pass, uint32_t nseq, uint32_t len, uint32_t v[5], uint32_t* d);
+void sampler_step_powers(uint32_t* out, int kmax);
 }
 
 using namespace ctl;
@@ -226,6 +228,52 @@ struct PathCtx {
     }
 };
 
+// SequenceSamplerData tables of one pass generated on the device: sequence q
+// starts q*len*3 draws after the pass's first state (host-computed), reached
+// with the GF(2) step powers M^(2^k); then curand_uniform * (1 - 1e-5f)
+// exactly as Base/CudaRandom.cu:8-17 and the CUDA toolkit's XORWOW.
+constexpr int kJumpBits = 24;
+struct XorwowDev { uint32_t v[5]; uint32_t d; };
+
+__global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict__ powers, XorwowDev base,
+                                                      uint32_t nseq, uint32_t len, float* s1, float2* s2) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nseq) return;
+    const uint32_t off = q * len * 3;
+    uint32_t v[5] = {base.v[0], base.v[1], base.v[2], base.v[3], base.v[4]};
+    for (int k = 0; k < kJumpBits; k++) {
+        if (!((off >> k) & 1u)) continue;
+        const uint32_t* M = powers + k * 800;
+        uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+        for (int w = 0; w < 5; w++) {
+            uint32_t bits = v[w];
+            while (bits) {
+                int b = __builtin_ctz(bits);
+                bits &= bits - 1;
+                const uint32_t* c = M + (w * 32 + b) * 5;
+                r0 ^= c[0]; r1 ^= c[1]; r2 ^= c[2]; r3 ^= c[3]; r4 ^= c[4];
+            }
+        }
+        v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
+    }
+    uint32_t d = base.d + 362437u * off;
+    auto next = [&]() -> float {
+        uint32_t t = v[0] ^ (v[0] >> 2);
+        v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
+        v[4] = (v[4] ^ (v[4] << 4)) ^ (t ^ (t << 1));
+        d += 362437u;
+        const float kInv = 2.3283064e-10f;
+        float f = (float)(v[4] + d) * kInv + (kInv / 2.0f);
+        return f * (1 - 1e-5f);
+    };
+    for (uint32_t i = 0; i < len; i++) s1[i * nseq + q] = next();
+    for (uint32_t i = 0; i < len; i++) {
+        float x = next();
+        float y = next();
+        s2[i * nseq + q] = make_float2(x, y);
+    }
+}
+
 __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint64_t v) {
     // one atomic per wave: reduce across the active lanes
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -343,6 +391,8 @@ struct ctl_ctx {
     hipEvent_t ev[2] = {nullptr, nullptr};
     int next_buf = 0, active = -1;
     unsigned long long* d_counters = nullptr;   // [0] rays [1] overflow [2..4] stats
+    uint32_t* d_powers = nullptr;               // XORWOW step powers for sampler_kernel
+    int active_dev = -1;                        // device-generated table buffer in use
 };
 
 static std::mutex g_err_mtx;
@@ -409,6 +459,15 @@ CTL_API ctl_ctx* ctl_create(int32_t device) {
         delete c;
         return fail("ctl_create: counter allocation failed");
     }
+    {
+        std::vector<uint32_t> pw((size_t)kJumpBits * 800);
+        ctl::sampler_step_powers(pw.data(), kJumpBits);
+        if (hipMalloc(&c->d_powers, pw.size() * 4) != hipSuccess ||
+            hipMemcpy(c->d_powers, pw.data(), pw.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            ctl_destroy(c);
+            return fail("ctl_create: sampler power table allocation failed");
+        }
+    }
     for (int i = 0; i < 2; i++) {
         size_t n1 = (size_t)c->nseq * c->len;
         if (hipMalloc(&c->d_s1[i], n1 * sizeof(float)) != hipSuccess ||
@@ -436,6 +495,7 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     }
     if (c->d_counters) (void)hipFree(c->d_counters);
+    if (c->d_powers) (void)hipFree(c->d_powers);
     delete c;
 }
 
@@ -513,16 +573,17 @@ CTL_API ctl_status ctl_sampler_upload(ctl_ctx* c, const float* seq1d, const floa
 }
 
 CTL_API ctl_status ctl_sampler_generate(ctl_ctx* c, uint64_t pass_index, void* stream) {
+    // Generated on the device (sampler_kernel); stream order makes the buffer
+    // reuse safe: the pass that read buffer b two calls ago precedes this launch.
     if (!c) return CTL_ERR_INVALID;
     CTL_HIP(c, hipSetDevice(c->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int b = c->next_buf;
-    size_t n1 = (size_t)c->nseq * c->len;
-    CTL_HIP(c, hipEventSynchronize(c->ev[b]));   // host buffer b no longer read by an earlier copy
-    ctl::sampler_tables(pass_index, c->nseq, c->len, c->h_s1[b], c->h_s2[b]);
-    CTL_HIP(c, hipMemcpyAsync(c->d_s1[b], c->h_s1[b], n1 * sizeof(float), hipMemcpyHostToDevice, s));
-    CTL_HIP(c, hipMemcpyAsync(c->d_s2[b], c->h_s2[b], n1 * 2 * sizeof(float), hipMemcpyHostToDevice, s));
-    CTL_HIP(c, hipEventRecord(c->ev[b], s));
+    XorwowDev base;
+    ctl::sampler_pass_state(pass_index, c->nseq, c->len, base.v, &base.d);
+    hipLaunchKernelGGL(sampler_kernel, dim3((c->nseq + 255) / 256), dim3(256), 0, s, c->d_powers, base, c->nseq,
+                       c->len, c->d_s1[b], c->d_s2[b]);
+    CTL_HIP(c, hipGetLastError());
     c->active = b;
     c->next_buf = 1 - b;
     return CTL_OK;

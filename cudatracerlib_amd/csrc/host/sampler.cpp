@@ -91,6 +91,18 @@ inline float next_uniform(XorwowState& s) {
 
 }  // namespace
 
+// First XORWOW state of pass `pass` (for the device generator) and the
+// GF(2) powers M^(2^k), k < kmax, as kmax x 160 columns x 5 words.
+void sampler_pass_state(uint64_t pass, uint32_t nseq, uint32_t len, uint32_t v[5], uint32_t* d) {
+    XorwowState s = xorwow_at(1234, 7539414, pass * ((uint64_t)nseq * len * 3));
+    memcpy(v, s.v, sizeof(s.v));
+    *d = s.d;
+}
+void sampler_step_powers(uint32_t* out, int kmax) {
+    const auto& P = step_powers();
+    for (int k = 0; k < kmax; k++) memcpy(out + (size_t)k * 800, P[k].col, 800 * sizeof(uint32_t));
+}
+
 void sampler_tables(uint64_t pass, uint32_t nseq, uint32_t len, float* seq1d, float* seq2d) {
     const uint64_t per_pass = (uint64_t)nseq * len * 3;
     XorwowState s = xorwow_at(1234, 7539414, pass * per_pass);
