@@ -23,10 +23,10 @@ import ctypes as C
 
 from . import _abi
 from ._abi import (PTParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK,
-                   CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION)
+                   CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL)
 
 __all__ = ["HostScene", "Tracer", "PathTracer", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
-           "CTL_SCENE_HALF_HOST_QUIRK", "lib", "diffuse_material"]
+           "CTL_SCENE_HALF_HOST_QUIRK", "CTL_PT_MEGAKERNEL", "lib", "diffuse_material"]
 
 
 def lib():
@@ -178,10 +178,10 @@ class PathTracer(Tracer):
     Defaults: Direct=1, MaxPathLength=50, RRStartDepth=5 (PathTracer.h:16-19)."""
 
     def __init__(self, device=0, max_path_length=50, rr_start_depth=5, shadow_any_hit=True, tile_size=64,
-                 num_ranks=1, rank=0):
+                 num_ranks=1, rank=0, megakernel=False):
         super().__init__(device)
         self.params = PTParams(1, max_path_length, rr_start_depth, 1 if shadow_any_hit else 0, tile_size,
-                               num_ranks, rank, 0)
+                               num_ranks, rank, CTL_PT_MEGAKERNEL if megakernel else 0)
 
     def do_pass(self, fb_ptr, pass_index, stream=0):
         """UpdateKernel's sampler regeneration + one render pass into fb (device PixelData[w*h])."""

@@ -14,6 +14,7 @@ CTL_SCENE_HALF_HOST_QUIRK = 1
 CTL_BSDF_DIFFUSE = 1
 CTL_EDIFFUSE_REFLECTION = 0x2
 CTL_MAX_NUM_LIGHTS = 16
+CTL_PT_MEGAKERNEL = 1
 
 
 class BVHNode(C.Structure):          # BVHNodeData, 64 B

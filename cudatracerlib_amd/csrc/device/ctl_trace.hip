@@ -16,7 +16,7 @@
 #include <vector>
 
 #include "../../../include/ctl_trace.h"
-#include "traverse.h"
+#include "common.h"
 
 namespace ctl {
 void sampler_tables(uint64_t pass, uint32_t nseq, uint32_t len, float* seq1d, float* seq2d);
@@ -37,56 +37,6 @@ static_assert(sizeof(ctl_pixel) == 28, "PixelData is 28 B");
 static_assert(sizeof(ctl_light_tri) == 64, "ShapeSet::triData is 64 B");
 
 namespace {
-
-constexpr int kBlock = 256;
-
-struct PathParams {
-    uint32_t width, height;
-    int32_t max_path_length, rr_start_depth;
-    uint32_t tile_size, tiles_x, num_tiles, num_ranks, rank;
-    uint32_t nseq, len;
-    int32_t shadow_any_hit;
-    bool half_quirk;
-};
-
-struct SamplerDev {   // SequenceSampler (Kernel/Sampler_device.h:59-113)
-    const float* s1;
-    const float2* s2;
-    uint32_t nseq, len, a, b;   // a = idx % nseq, b = (idx / nseq) % nseq
-    uint32_t d1, d2;
-    __device__ __forceinline__ float next1() {
-        uint32_t k = d1 % len;
-        float val = 0.0f;
-        val += s1[k * nseq + a];
-        val += s1[k * nseq + b];
-        d1++;
-        return fracf_ref(val);
-    }
-    __device__ __forceinline__ f2 next2() {
-        uint32_t k = d2 % len;
-        float2 p = s2[k * nseq + a], q = s2[k * nseq + b];
-        float x = 0.0f, y = 0.0f;
-        x += p.x; y += p.y;
-        x += q.x; y += q.y;
-        d2++;
-        return mk2(fracf_ref(x), fracf_ref(y));
-    }
-};
-
-struct LutDecode {
-    const float4* lut;
-    __device__ __forceinline__ f3 operator()(uint32_t c) const { float4 q = lut[c]; return mk3(q.x, q.y, q.z); }
-};
-
-__device__ __forceinline__ m44 load_m44(const float4* M) {
-    float4 r0 = M[0], r1 = M[1], r2 = M[2], r3 = M[3];
-    m44 m;
-    m.d[0] = r0.x; m.d[1] = r0.y; m.d[2] = r0.z; m.d[3] = r0.w;
-    m.d[4] = r1.x; m.d[5] = r1.y; m.d[6] = r1.z; m.d[7] = r1.w;
-    m.d[8] = r2.x; m.d[9] = r2.y; m.d[10] = r2.z; m.d[11] = r2.w;
-    m.d[12] = r3.x; m.d[13] = r3.y; m.d[14] = r3.z; m.d[15] = r3.w;
-    return m;
-}
 
 template <bool STATS>
 struct PathCtx {
@@ -274,19 +224,10 @@ __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict
     }
 }
 
-__device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint64_t v) {
-    // one atomic per wave: reduce across the active lanes
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
-}
-
 template <bool STATS>
 __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
                                                       ctl_pixel* fb, unsigned long long* counters) {
-    __shared__ int s_stack[kLdsStack * kBlock];
-    LaneStack st;
-    st.lds = &s_stack[threadIdx.x];
-    st.stride = kBlock;
+    CTL_LANE_STACK(st);
     const uint32_t perTile = P.tile_size * P.tile_size;
     const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const uint32_t j = (uint32_t)(g / perTile), w = (uint32_t)(g % perTile);
@@ -341,10 +282,7 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
 template <bool ANY, bool STATS>
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            unsigned long long* counters) {
-    __shared__ int s_stack[kLdsStack * kBlock];
-    LaneStack st;
-    st.lds = &s_stack[threadIdx.x];
-    st.stride = kBlock;
+    CTL_LANE_STACK(st);
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     TraceStats ts{0, 0, 0};
     bool ok = true;
@@ -376,25 +314,6 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, int64_t n
 // ===========================================================================
 // Context + C ABI
 // ===========================================================================
-struct ctl_ctx {
-    int device = 0;
-    std::string err;
-    std::vector<void*> scene_allocs;
-    DevScene scene{};
-    bool has_scene = false;
-    bool half_quirk = false;
-    uint32_t nseq = 4096, len = 30;
-    float* d_s1[2] = {nullptr, nullptr};
-    float2* d_s2[2] = {nullptr, nullptr};
-    float* h_s1[2] = {nullptr, nullptr};
-    float* h_s2[2] = {nullptr, nullptr};
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    int next_buf = 0, active = -1;
-    unsigned long long* d_counters = nullptr;   // [0] rays [1] overflow [2..4] stats
-    uint32_t* d_powers = nullptr;               // XORWOW step powers for sampler_kernel
-    int active_dev = -1;                        // device-generated table buffer in use
-};
-
 static std::mutex g_err_mtx;
 static std::string g_create_err;
 
@@ -454,6 +373,7 @@ CTL_API ctl_ctx* ctl_create(int32_t device) {
         return fail(std::string("ctl_create: device is ") + prop.gcnArchName + ", kernels are built for gfx950 only");
     ctl_ctx* c = new ctl_ctx();
     c->device = device;
+    c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemset(c->d_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
         delete c;
@@ -487,6 +407,7 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     free_scene(c);
+    ctl::wavefront_free(c);
     for (int i = 0; i < 2; i++) {
         if (c->d_s1[i]) (void)hipFree(c->d_s1[i]);
         if (c->d_s2[i]) (void)hipFree(c->d_s2[i]);
@@ -547,6 +468,17 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     S.ray_eps = d->ray_eps;
     for (int i = 0; i < CTL_MAX_NUM_LIGHTS; i++) S.light_cdf[i] = d->light_cdf[i];
     S.camera = d->camera;
+    S.single = 0;
+    if (d->n_nodes > 0 && d->scene_start_node < 0) {
+        uint32_t node = ~(uint32_t)d->scene_start_node;
+        if (node >= d->n_nodes) { free_scene(c); c->err = "scene_upload: start node out of range"; return CTL_ERR_INVALID; }
+        const ctl_kernel_mesh& M = d->meshes[d->nodes[node].mesh_index];
+        S.single = 1;
+        S.s_node_base = M.bvh_node_offset;
+        S.s_tri_base = M.bvh_triangle_offset;
+        S.s_idx_base = M.bvh_indices_offset;
+        S.s_tri_offset = M.triangle_offset;
+    }
     c->scene = S;
     c->half_quirk = (d->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
     c->has_scene = true;
@@ -598,11 +530,11 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
     if (stats) {
-        if (any_hit) hipLaunchKernelGGL((intersect_kernel<true, true>), grid, dim3(kBlock), 0, s, c->scene, n, rays, hits, c->d_counters);
-        else hipLaunchKernelGGL((intersect_kernel<false, true>), grid, dim3(kBlock), 0, s, c->scene, n, rays, hits, c->d_counters);
+        if (any_hit) hipLaunchKernelGGL((intersect_kernel<true, true>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, c->d_counters);
+        else hipLaunchKernelGGL((intersect_kernel<false, true>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, c->d_counters);
     } else {
-        if (any_hit) hipLaunchKernelGGL((intersect_kernel<true, false>), grid, dim3(kBlock), 0, s, c->scene, n, rays, hits, c->d_counters);
-        else hipLaunchKernelGGL((intersect_kernel<false, false>), grid, dim3(kBlock), 0, s, c->scene, n, rays, hits, c->d_counters);
+        if (any_hit) hipLaunchKernelGGL((intersect_kernel<true, false>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, c->d_counters);
+        else hipLaunchKernelGGL((intersect_kernel<false, false>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, c->d_counters);
     }
     CTL_HIP(c, hipGetLastError());
     return CTL_OK;
@@ -655,8 +587,12 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
     dim3 grid((unsigned)((threads + kBlock - 1) / kBlock));
     const float* s1 = c->d_s1[c->active];
     const float2* s2 = c->d_s2[c->active];
-    if (stats) hipLaunchKernelGGL((path_kernel<true>), grid, dim3(kBlock), 0, s, c->scene, P, s1, s2, fb, c->d_counters);
-    else hipLaunchKernelGGL((path_kernel<false>), grid, dim3(kBlock), 0, s, c->scene, P, s1, s2, fb, c->d_counters);
+    if (!(p->flags & CTL_PT_MEGAKERNEL)) {
+        int r2 = ctl::wavefront_pass(c, P, fb, stats, s);
+        return r2;
+    }
+    if (stats) hipLaunchKernelGGL((path_kernel<true>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, fb, c->d_counters);
+    else hipLaunchKernelGGL((path_kernel<false>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, fb, c->d_counters);
     CTL_HIP(c, hipGetLastError());
     return CTL_OK;
 }

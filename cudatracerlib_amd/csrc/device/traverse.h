@@ -11,12 +11,18 @@
 // bit patterns (kepler_math, Math/MathFunc.h:402-445 -> v_min3/v_max3_i32).
 //
 // MI355X-specific structure:
+//  * the traversal is a resumable per-lane state machine (Traverser): one
+//    round() = inner nodes until every active lane holds a leaf, then the
+//    postponed leaves.  Persistent kernels refill lanes whose ray finished
+//    between rounds, so waves stay full on incoherent secondary rays;
 //  * one traversal stack per lane for BOTH levels; the 16 most recent entries
 //    live in LDS ([entry][thread] layout: consecutive lanes hit consecutive
 //    banks), deeper entries spill to a private scratch array;
 //  * level switch without a second stack: entering an instance pushes the
 //    pending top-level node and a sentinel; the mesh level ends when that
 //    sentinel (or a sentinel child, as in the reference) comes up;
+//  * SINGLE specialisation for one-instance scenes (startNode < 0): the ray is
+//    transformed once and only the mesh level runs (fewer live VGPRs);
 //  * node = 4 x 16-B loads, Woop triangle = 3 x 16-B loads (dwordx4);
 //  * no FMA contraction (-ffp-contract=off) => bit-identical to the CPU oracle.
 #pragma once
@@ -52,6 +58,9 @@ struct DevScene {
     float ray_eps;
     float light_cdf[CTL_MAX_NUM_LIGHTS];
     ctl_camera camera;
+    // single-instance fast path (start_node < 0): mesh of node ~start_node
+    uint32_t single;
+    uint32_t s_node_base, s_tri_base, s_idx_base, s_tri_offset;
 };
 
 struct TraceStats { uint32_t nodes, tris, inst; };
@@ -73,14 +82,19 @@ __device__ __forceinline__ float span_end(float a0, float a1, float b0, float b1
                                 min(max(__float_as_int(c0), __float_as_int(c1)), __float_as_int(d))));
 }
 
+// LDS part of the per-lane stacks: [entry][thread] (dynamic shared memory,
+// kLdsStack * blockDim ints).  Indexed through this address-space-3 array so
+// every push/pop is a ds_read/ds_write, never a generic (flat) access.
+extern __shared__ int ctl_lds_stack[];
+constexpr int kStackBlock = 256;   // every kernel using LaneStack runs 256-thread blocks
+
 struct LaneStack {
-    int* lds;       // &s_stack[0][tid], stride = block size
-    int stride;
-    int spill[kStackMax - kLdsStack];
+    int* spill;     // private array of kStackMax - kLdsStack entries (scratch, deep stacks only)
     int sp;
+    int tid;
     bool overflow;
     __device__ __forceinline__ void push(int v) {
-        if (sp < kLdsStack) lds[sp * stride] = v;
+        if (sp < kLdsStack) ctl_lds_stack[sp * kStackBlock + tid] = v;
         else if (sp < kStackMax) spill[sp - kLdsStack] = v;
         else overflow = true;
         sp++;
@@ -88,11 +102,19 @@ struct LaneStack {
     __device__ __forceinline__ int pop() {
         --sp;
         if (sp < 0) { sp = 0; return CTL_SENTINEL; }
-        if (sp < kLdsStack) return lds[sp * stride];
+        if (sp < kLdsStack) return ctl_lds_stack[sp * kStackBlock + tid];
         if (sp < kStackMax) return spill[sp - kLdsStack];
         return CTL_SENTINEL;
     }
 };
+#define CTL_LANE_STACK(name)                       \
+    int name##_spill[kStackMax - kLdsStack];       \
+    LaneStack name;                                \
+    name.spill = name##_spill;                     \
+    name.sp = 0;                                   \
+    name.tid = (int)threadIdx.x;                   \
+    name.overflow = false
+constexpr size_t kStackLdsBytes = sizeof(int) * kLdsStack * kStackBlock;
 
 struct RayLocal {
     float ox, oy, oz, dx, dy, dz;
@@ -119,31 +141,90 @@ __device__ __forceinline__ void xform_rows(const float4* M, f3 p, f3 d, f3& po, 
     po = xform_point(m, p);
 }
 
-// Closest (ANY=false) or any (ANY=true) hit with tmin_tri < t < h.t.  Box
-// spans start at span_tmin.  h must be initialised by the caller (t = tmax,
-// tri = node = UINT_MAX).  Returns false if the lane overflowed its stack.
-template <bool ANY, bool STATS>
-__device__ bool trace_ray_dev(const DevScene& S, f3 ori, f3 dir, float span_tmin, float tri_tmin, HitRec& h,
-                              LaneStack& st, TraceStats* stats) {
-    if (S.n_nodes == 0) return true;
-    RayLocal world, cur;
-    world.set(ori.x, ori.y, ori.z, dir.x, dir.y, dir.z);
-    cur = world;
-    st.sp = 0;
-    st.overflow = false;
-    st.push(CTL_SENTINEL);
-    int level = 0;
-    int meshSent = 0;
-    int nodeAddr, leafAddr;
-    if (S.start_node < 0) { leafAddr = S.start_node; nodeAddr = CTL_SENTINEL; }
-    else { leafAddr = 0; nodeAddr = S.start_node; }
-    const float4* nodes = S.scene_bvh;
-    uint32_t nodeBase = 0, triBase = 0, idxBase = 0, triOffset = 0, instIdx = 0;
-    bool done = false;
-    bool resumeLeaves = false;   // back from an instance with a second postponed top-level leaf
+// Closest (ANY=false) or any (ANY=true) hit with tri_tmin < t < h.t; box spans
+// start at span_tmin.
+template <bool ANY, bool STATS, bool SINGLE>
+struct Traverser {
+    RayLocal cur;
+    RayLocal world;   // unused when SINGLE
+    HitRec h;
+    float span_tmin, tri_tmin;
+    int nodeAddr, leafAddr, level, meshSent;
+    uint32_t nodeBase, triBase, idxBase, triOffset, instIdx;
+    bool done, resumeLeaves;
 
-    while (!done) {
-        // ---- inner nodes until every active lane holds a postponed leaf
+    __device__ __forceinline__ void enter_instance(const DevScene& S, uint32_t inst, f3 o, f3 d) {
+        instIdx = inst;
+        f3 o2, d2;
+        xform_rows(S.inv_xf + 4 * inst, o, d, o2, d2);
+        cur.set(o2.x, o2.y, o2.z, d2.x, d2.y, d2.z);
+    }
+
+    __device__ __forceinline__ void init(const DevScene& S, f3 o, f3 d, float smin, float tmn, float tmaxv,
+                                         LaneStack& st, TraceStats* stats) {
+        h.t = tmaxv; h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
+        span_tmin = smin; tri_tmin = tmn;
+        st.sp = 0;
+        st.overflow = false;
+        st.push(CTL_SENTINEL);
+        done = (S.n_nodes == 0);
+        resumeLeaves = false;
+        meshSent = 0;
+        if (SINGLE) {
+            // start_node < 0: TracerayTemplate calls the instance callback directly (BVHTraversal.h:130-131)
+            if (STATS) stats->inst++;
+            enter_instance(S, ~(uint32_t)S.start_node, o, d);
+            nodeBase = S.s_node_base; triBase = S.s_tri_base; idxBase = S.s_idx_base; triOffset = S.s_tri_offset;
+            level = 1;
+            nodeAddr = 0;
+            leafAddr = 0;
+        } else {
+            world.set(o.x, o.y, o.z, d.x, d.y, d.z);
+            cur = world;
+            level = 0;
+            nodeBase = triBase = idxBase = triOffset = instIdx = 0;
+            if (S.start_node < 0) { leafAddr = S.start_node; nodeAddr = CTL_SENTINEL; }
+            else { leafAddr = 0; nodeAddr = S.start_node; }
+        }
+    }
+
+    __device__ __forceinline__ void leaf_tris(const DevScene& S, TraceStats* stats) {
+        for (int triAddr = ~leafAddr;; triAddr++) {
+            const float4* tv = S.woop + triBase + (uint32_t)triAddr * 3u;
+            const float4 v00 = tv[0];
+            const float4 v11 = tv[1];
+            const float4 v22 = tv[2];
+            const uint32_t index = S.tri_idx[idxBase + (uint32_t)triAddr];
+            if (STATS) stats->tris++;
+            float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
+            float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
+            float t = Oz * invDz;
+            if (t > tri_tmin && t < h.t) {
+                float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
+                float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
+                float u = Ox + t * Dx;
+                if (u >= 0.0f) {
+                    float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
+                    float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
+                    float v = Oy + t * Dy;
+                    if (v >= 0.0f && u + v <= 1.0f) {
+                        h.node = instIdx;
+                        h.tri = (index >> 1) + triOffset;
+                        h.u = u;
+                        h.v = v;
+                        h.t = t;
+                        if (ANY) { done = true; break; }
+                    }
+                }
+            }
+            if (index & 1) break;
+        }
+    }
+
+    // One round: inner nodes until every active lane holds a postponed leaf,
+    // then the postponed leaves (and the level transitions).
+    __device__ __forceinline__ void round(const DevScene& S, LaneStack& st, TraceStats* stats) {
+        const float4* nodes = (SINGLE || level) ? S.bvh : S.scene_bvh;
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
             const float4* n = nodes + nodeBase + nodeAddr;
             const float4 n0xy = n[0];
@@ -186,84 +267,45 @@ __device__ bool trace_ray_dev(const DevScene& S, f3 ori, f3 dir, float span_tmin
             }
             if (!__any(leafAddr >= 0)) break;
         }
-        // ---- postponed leaves
         resumeLeaves = false;
-        bool entered = false;
         while (leafAddr < 0) {
-            if (level == 1) {
+            if (SINGLE || level == 1) {
                 if (leafAddr != -214783648) {
-                    for (int triAddr = ~leafAddr;; triAddr++) {
-                        const float4* tv = S.woop + triBase + (uint32_t)triAddr * 3u;
-                        const float4 v00 = tv[0];
-                        const float4 v11 = tv[1];
-                        const float4 v22 = tv[2];
-                        const uint32_t index = S.tri_idx[idxBase + (uint32_t)triAddr];
-                        if (STATS) stats->tris++;
-                        float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
-                        float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
-                        float t = Oz * invDz;
-                        if (t > tri_tmin && t < h.t) {
-                            float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
-                            float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
-                            float u = Ox + t * Dx;
-                            if (u >= 0.0f) {
-                                float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
-                                float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
-                                float v = Oy + t * Dy;
-                                if (v >= 0.0f && u + v <= 1.0f) {
-                                    h.node = instIdx;
-                                    h.tri = (index >> 1) + triOffset;
-                                    h.u = u;
-                                    h.v = v;
-                                    h.t = t;
-                                    if (ANY) { done = true; break; }
-                                }
-                            }
-                        }
-                        if (index & 1) break;
-                    }
-                    if (done) break;
+                    leaf_tris(S, stats);
+                    if (done) return;
                 }
                 leafAddr = nodeAddr;
                 if (nodeAddr < 0) nodeAddr = st.pop();
             } else {
                 if (leafAddr != -214783648) {
                     // enter instance ~leafAddr (TraceHelper.cu:91-100, 528-561)
-                    instIdx = (uint32_t)(~leafAddr);
+                    const uint32_t inst = (uint32_t)(~leafAddr);
                     if (STATS) stats->inst++;
-                    const ctl_node& N = S.nodes[instIdx];
+                    const ctl_node& N = S.nodes[inst];
                     const ctl_kernel_mesh& M = S.meshes[N.mesh_index];
                     nodeBase = M.bvh_node_offset;
                     triBase = M.bvh_triangle_offset;
                     idxBase = M.bvh_indices_offset;
                     triOffset = M.triangle_offset;
-                    f3 o2, d2;
-                    xform_rows(S.inv_xf + 4 * instIdx, mk3(world.ox, world.oy, world.oz),
-                               mk3(world.dx, world.dy, world.dz), o2, d2);
-                    cur.set(o2.x, o2.y, o2.z, d2.x, d2.y, d2.z);
+                    enter_instance(S, inst, mk3(world.ox, world.oy, world.oz), mk3(world.dx, world.dy, world.dz));
                     st.push(nodeAddr);        // pending top-level work
                     meshSent = st.sp;
                     st.push(CTL_SENTINEL);    // bottom of the mesh-level stack
-                    nodes = S.bvh;
                     level = 1;
                     nodeAddr = 0;             // mesh root (TraceHelper.cu:170)
                     leafAddr = 0;
-                    entered = true;
-                    break;
+                    return;
                 }
                 leafAddr = nodeAddr;
                 if (nodeAddr < 0) nodeAddr = st.pop();
             }
         }
-        if (done) break;
-        if (entered) continue;
         if (nodeAddr == CTL_SENTINEL) {
-            if (level == 1) {
+            if (!SINGLE && level == 1) {
                 // mesh traversal finished (bottom sentinel or a sentinel child)
                 st.sp = meshSent;
                 int saved = st.pop();
                 level = 0;
-                nodes = S.scene_bvh;
                 nodeBase = 0;
                 cur = world;
                 leafAddr = saved;
@@ -271,11 +313,28 @@ __device__ bool trace_ray_dev(const DevScene& S, f3 ori, f3 dir, float span_tmin
                 if (saved < 0) nodeAddr = st.pop();
                 resumeLeaves = leafAddr < 0;   // the reference's leaf loop continues right away
             } else {
-                break;
+                done = true;
             }
         }
     }
+};
+
+// Whole traversal of one ray (megakernel, batch kernel).
+template <bool ANY, bool STATS, bool SINGLE>
+__device__ __forceinline__ bool trace_one(const DevScene& S, f3 ori, f3 dir, float span_tmin, float tri_tmin,
+                                          HitRec& h, LaneStack& st, TraceStats* stats) {
+    Traverser<ANY, STATS, SINGLE> T;
+    T.init(S, ori, dir, span_tmin, tri_tmin, h.t, st, stats);
+    while (!T.done) T.round(S, st, stats);
+    h = T.h;
     return !st.overflow;
+}
+
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool trace_ray_dev(const DevScene& S, f3 ori, f3 dir, float span_tmin, float tri_tmin,
+                                              HitRec& h, LaneStack& st, TraceStats* stats) {
+    if (S.single) return trace_one<ANY, STATS, true>(S, ori, dir, span_tmin, tri_tmin, h, st, stats);
+    return trace_one<ANY, STATS, false>(S, ori, dir, span_tmin, tri_tmin, h, st, stats);
 }
 
 }  // namespace ctl

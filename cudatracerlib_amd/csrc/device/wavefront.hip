@@ -1,0 +1,390 @@
+// wavefront.hip — the PathTracer pass as a wavefront pipeline on gfx950.
+//
+// Same per-path arithmetic and random-number order as the megakernel restatement
+// of PathTrace<true> (Integrators/PathTracer.cu:10-113), reorganised per bounce:
+//
+//   gen      sensor ray per owned pixel               (pathKernel2, PathTracer.cu:182-194)
+//   trace    closest hit over the extension queue     (traceRay, TraceHelper.cu:174-180)
+//   shade    emission + MIS, BSDF sample, NEE light sample, Russian roulette;
+//            pushes the shadow ray (Occluded, KernelDynamicScene.cu:70-80) and the
+//            next extension ray into compacted queues
+//   trace    any-hit over the shadow queue
+//   resolve  cl += NEE contribution if unoccluded; AddSample of finished paths
+//
+// The NEE term of bounce k is added to cl after bounce k's emission and before
+// bounce k+1's, so every fp32 addition happens in the reference order and the
+// framebuffer is bit-identical to the megakernel and to the CPU oracle.
+// Why: the traversal kernel stays lean (no shading state -> high occupancy) and
+// always runs on compacted, full waves of live rays instead of idling lanes whose
+// paths already ended.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "common.h"
+
+namespace ctl {
+namespace {
+
+constexpr int kMaxBounces = 64;   // count slots per pass (MaxPathLength is clamped to this)
+
+__device__ __forceinline__ uint32_t queue_push(uint32_t* count, bool want) {
+    // wave-aggregated append: one atomic per wave
+    const uint64_t mask = __ballot(want);
+    if (!mask) return 0xffffffffu;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    return want ? base + rank : 0xffffffffu;
+}
+
+__global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
+                                                        WfState W, uint64_t n_items, ctl_pixel* fb) {
+    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;; g += (uint64_t)gridDim.x * kBlock) {
+        // keep whole waves in the loop so the ballot in queue_push sees every lane
+        const bool inRange = g < n_items;
+        if (!__any(inRange)) break;
+        uint32_t px = 0, py = 0;
+        const bool valid = inRange && work_pixel(P, g, px, py);
+        f2 pX = mk2(0, 0);
+        f3 o = mk3s(0), d = mk3s(0);
+        uint32_t idx = py * P.width + px;
+        if (valid) {
+            SamplerDev rng;
+            rng.init(s1, s2, P, idx, 0, 0);
+            pX = mk2((float)px, (float)py) + rng.next2();
+            (void)rng.next2();   // aperture sample
+            sensor_ray(S, pX, o, d);
+        }
+        const bool live = valid && P.max_path_length > 0;
+        if (valid && !live) add_sample(fb, P, pX, mk3s(0.0f) + (mk3s(1.0f) * 1.0f) * mk3s(0.0f));
+        const uint32_t slot = queue_push(&W.counts[0], live);
+        if (live) {
+            const uint32_t i = (uint32_t)g;
+            W.q[0][slot] = i;
+            W.o[i] = make_float4(o.x, o.y, o.z, 0.0f);
+            W.d[i] = make_float4(d.x, d.y, d.z, 0.0f);
+            W.cl[i] = make_float4(0.0f, 0.0f, 0.0f, pX.x);
+            W.cf[i] = make_float4(1.0f, 1.0f, 1.0f, pX.y);
+            W.wo[i] = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+            W.ln[i] = make_float2(0.0f, 0.0f);
+            W.meta[i] = make_uint4(idx, 0u | (2u << 16), 1u, 0u);   // d1=0, d2=2, depth=1 (while(depth++ < max))
+        }
+    }
+}
+
+// Persistent trace over a queue: MODE 0 = extension rays (closest hit),
+// 1 = shadow rays any-hit over (eps, dist - eps), 2 = shadow rays as the
+// reference's closest-hit Occluded().  Lanes whose ray finished fetch the next
+// queue entry between traversal rounds (one atomic per wave), so waves stay
+// full while long rays finish (dynamic fetch, cf. intersectKernel's warp
+// fetch at TraceHelper.cu:379-399, here per round instead of per batch).
+template <int MODE, bool STATS, bool SINGLE>
+__global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S, WfState W, const uint32_t* queue,
+                                                          const uint32_t* countp, uint32_t* cursor,
+                                                          unsigned long long* counters) {
+    CTL_LANE_STACK(st);
+    const uint32_t count = *countp;
+    if (count == 0) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&counters[0], (unsigned long long)count);
+    TraceStats ts{0, 0, 0};
+    Traverser<MODE == 1, STATS, SINGLE> T;
+    T.done = true;
+    bool haveRay = false, exhausted = false, ovf = false;
+    uint32_t ray = 0;
+    const int lane = threadIdx.x & 63;
+    while (true) {
+        if (haveRay && T.done) {
+            if (MODE == 0) {
+                W.hit[ray] = make_float4(T.h.t, T.h.u, T.h.v, __int_as_float((int)T.h.tri));
+                W.hit_node[ray] = T.h.node;
+            } else if (MODE == 1) {
+                W.sh_occ[ray] = T.h.tri != 0xffffffffu ? 1u : 0u;
+            } else {
+                const float dist = W.sh_d[ray].w;
+                bool end = T.h.t < dist - S.ray_eps;
+                W.sh_occ[ray] = (T.h.t > 0 + S.ray_eps && end) ? 1u : 0u;
+            }
+            ovf |= st.overflow;
+            haveRay = false;
+        }
+        const bool need = !haveRay && !exhausted;
+        const uint64_t mask = __ballot(need);
+        if (mask) {
+            const int leader = __ffsll((unsigned long long)mask) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(cursor, (uint32_t)__popcll(mask));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t k = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                if (k < count) {
+                    ray = queue[k];
+                    haveRay = true;
+                    if (MODE == 0) {
+                        const float4 o = W.o[ray], d = W.d[ray];
+                        T.init(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), 0.0f, S.ray_eps, FLT_MAX, st, &ts);
+                    } else {
+                        const float4 o = W.sh_o[ray], d = W.sh_d[ray];
+                        T.init(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), 0.0f, S.ray_eps,
+                               MODE == 1 ? o.w : FLT_MAX, st, &ts);
+                    }
+                } else {
+                    exhausted = true;
+                }
+            }
+        }
+        if (!__any(haveRay)) break;
+        if (haveRay && !T.done) T.round(S, st, &ts);
+    }
+    if (ovf) atomicAdd(&counters[1], 1ull);
+    if (STATS) {
+        wave_add_u64(&counters[2], ts.nodes);
+        wave_add_u64(&counters[3], ts.tris);
+        wave_add_u64(&counters[4], ts.inst);
+    }
+}
+
+// Persistent grid = exactly the blocks that are co-resident (occupancy from
+// the compiled register/LDS footprint x CU count), so no block waits for a
+// slot and the refill loop drains the queue evenly across all CUs.
+template <class K>
+int resident_blocks(ctl_ctx* c, K kernel, size_t lds) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess || per_cu <= 0)
+        per_cu = 4;
+    return per_cu * c->cu_count;
+}
+
+template <int MODE>
+void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32_t* cnt, uint32_t* cursor, bool stats) {
+    WfState& W = c->wf;
+    const bool single = c->scene.single != 0;
+#define LT(ST, SG)                                                                                              \
+    do {                                                                                                        \
+        static int blocks = 0;                                                                                  \
+        if (!blocks) blocks = resident_blocks(c, wf_trace_kernel<MODE, ST, SG>, kStackLdsBytes);                \
+        hipLaunchKernelGGL((wf_trace_kernel<MODE, ST, SG>), dim3(blocks), dim3(kBlock), kStackLdsBytes, s,       \
+                           c->scene, W, queue, cnt, cursor, c->d_counters);                                     \
+    } while (0)
+    if (stats) { if (single) LT(true, true); else LT(true, false); }
+    else { if (single) LT(false, true); else LT(false, false); }
+#undef LT
+}
+
+__global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
+                                                          WfState W, int bounce, ctl_pixel* fb) {
+    const uint32_t count = W.counts[2 * bounce];
+    const uint32_t* qin = W.q[bounce & 1];
+    uint32_t* qout = W.q[(bounce + 1) & 1];
+    uint32_t* nextCount = &W.counts[2 * (bounce + 1)];
+    uint32_t* shCount = &W.counts[2 * bounce + 1];
+    const uint32_t stride = gridDim.x * kBlock;
+    const uint32_t rounds = (count + stride - 1) / stride;
+    for (uint32_t r = 0; r < rounds; r++) {
+        const uint32_t k = r * stride + blockIdx.x * kBlock + threadIdx.x;
+        const bool act = k < count;
+        const uint32_t i = act ? qin[k] : 0u;
+        bool pushShadow = false, pushNext = false;
+        float4 shO, shD, shV;
+        if (act) {
+            float4 o4 = W.o[i], d4 = W.d[i], cl4 = W.cl[i], cf4 = W.cf[i], wo4 = W.wo[i];
+            float2 ln2 = W.ln[i];
+            uint4 meta = W.meta[i];
+            float4 hit = W.hit[i];
+            const uint32_t node = W.hit_node[i];
+            f3 rori = mk3(o4.x, o4.y, o4.z), rdir = mk3(d4.x, d4.y, d4.z);
+            spec cl = mk3(cl4.x, cl4.y, cl4.z), cf = mk3(cf4.x, cf4.y, cf4.z);
+            const f2 pX = mk2(cl4.w, cf4.w);
+            float brdf_pdf = o4.w;
+            f3 last_nor = mk3(wo4.w, ln2.x, ln2.y);
+            int depth = (int)(meta.z & 0xffffu);
+            bool specularBounce = (meta.z >> 16) & 1u;
+            SamplerDev rng;
+            rng.init(s1, s2, P, meta.x, meta.y & 0xffffu, meta.y >> 16);
+            const uint32_t tri = (uint32_t)__float_as_int(hit.w);
+            bool terminated = false;
+            if (tri != 0xffffffffu) {
+                bsdf_rec b;
+                b.wo = mk3(wo4.x, wo4.y, wo4.z);
+                b.sampled_type = 0;
+                b.type_mask = kEAll;
+                dgeom dg;
+                dg.P = rori + hit.x * rdir;
+                const ctl_triangle_data td = S.tri_data[tri];
+                const ctl_node N = S.nodes[node];
+                fill_dg(td, load_m44(S.xf + 4 * node), mk2(hit.y, hit.z), P.half_quirk, LutDecode{S.normal_lut}, dg);
+                b.wi = to_local(dg.sys, -rdir);
+                const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N.material_offset];
+                if (mat.two_sided && b.wi.z < 0) {
+                    dg.n = -dg.n;
+                    dg.sys.n = -dg.sys.n;
+                    b.wi.z *= -1.0f;
+                }
+                if (mat.node_light_index != 0xffffffffu) {
+                    const uint32_t li = N.lights[mat.node_light_index];
+                    const ctl_light L = S.lights[li];
+                    float misWeight = 1.0f;
+                    if (!(depth == 1 || specularBounce)) {
+                        direct_rec dRec;
+                        dRec.ref = rori; dRec.refN = last_nor; dRec.p = dg.P; dRec.n = dg.n;
+                        dRec.d = rdir; dRec.dist = hit.x; dRec.measure = kESolidAngle;
+                        float direct_pdf = light_pdf_direct(L, dRec) * (S.light_cdf[li] - (li == 0 ? 0.0f : S.light_cdf[li - 1]));
+                        misWeight = power_heuristic(brdf_pdf, direct_pdf);
+                    }
+                    f3 w = -rdir;
+                    spec Le = (dot(dg.sys.n, w) <= 0) ? mk3s(0.0f) : mk3(L.radiance[0], L.radiance[1], L.radiance[2]);
+                    cl = cl + (cf * misWeight) * Le;
+                }
+                spec f = diffuse_sample(mat, b, brdf_pdf, rng.next2());
+                last_nor = dg.sys.n;
+                if ((mat.combined_type & kESmooth) != 0 && S.n_lights) {
+                    // UniformSampleOneLight up to the occlusion test (TraceAlgorithms.cu:44-73,92-101)
+                    f2 sample = rng.next2();
+                    uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
+                    uint32_t first = 0, cnt = nl;
+                    while (cnt > 0) {
+                        uint32_t c2 = cnt / 2, mid = first + c2;
+                        if (!(sample.x < S.light_cdf[mid])) { first = mid + 1; cnt -= c2 + 1; }
+                        else cnt = c2;
+                    }
+                    uint32_t lidx = first < nl ? first : nl - 1;
+                    float fU = S.light_cdf[lidx], fL = lidx > 0 ? S.light_cdf[lidx - 1] : 0.0f;
+                    sample.x = (sample.x - fL) / (fU - fL);
+                    const float lpdf = fU - fL;
+                    direct_rec dRec;
+                    dRec.p = dg.P; dRec.n = dg.sys.n; dRec.measure = kEArea;
+                    dRec.ref = dg.P; dRec.refN = dg.sys.n;
+                    spec value = light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, rng.next2());
+                    if (!spec_zero(value)) {
+                        bsdf_rec b2 = b;
+                        b2.wo = to_local(dg.sys, dRec.d);
+                        b2.type_mask = kEAll & ~kEDelta;
+                        spec bsdfVal = diffuse_f(mat, b2);
+                        if (!spec_zero(bsdfVal)) {
+                            float weight = 1.0f;
+                            if (dRec.measure != kEDiscrete)
+                                weight = power_heuristic(dRec.pdf * lpdf, diffuse_pdf(mat, b2));
+                            spec ret = value * bsdfVal * weight;
+                            ret = ret * mk3s(1.0f);
+                            spec add = cf * spec_div(ret, lpdf);
+                            pushShadow = true;
+                            shO = make_float4(dRec.ref.x, dRec.ref.y, dRec.ref.z, dRec.dist - S.ray_eps);
+                            shD = make_float4(dRec.d.x, dRec.d.y, dRec.d.z, dRec.dist);
+                            shV = make_float4(add.x, add.y, add.z, 0.0f);
+                        }
+                    }
+                }
+                specularBounce = (b.sampled_type & kEDelta) != 0;
+                cf = cf * f;
+                rori = dg.P;
+                rdir = to_world(dg.sys, b.wo);
+                if (depth > P.rr_start_depth && !specularBounce) {
+                    if (rng.next1() >= spec_max(cf)) terminated = true;
+                    else cf = spec_div(cf, spec_max(cf));
+                }
+                if (!terminated) {
+                    if (depth < P.max_path_length) { depth++; pushNext = true; }
+                    else terminated = true;
+                }
+                W.o[i] = make_float4(rori.x, rori.y, rori.z, brdf_pdf);
+                W.d[i] = make_float4(rdir.x, rdir.y, rdir.z, 0.0f);
+                W.cf[i] = make_float4(cf.x, cf.y, cf.z, pX.y);
+                W.wo[i] = make_float4(b.wo.x, b.wo.y, b.wo.z, last_nor.x);
+                W.ln[i] = make_float2(last_nor.y, last_nor.z);
+                W.meta[i] = make_uint4(meta.x, rng.d1 | (rng.d2 << 16), (uint32_t)depth | ((specularBounce ? 1u : 0u) << 16), 0u);
+                if (terminated && pushShadow) shV.w = 1.0f;   // resolve adds NEE, then AddSample
+                if (terminated && !pushShadow) add_sample(fb, P, pX, mk3s(1.0f) * cl);
+            } else {
+                // miss: loop ends; environment term of PathTracer.cu:98-111 (no env map -> 0)
+                cl = cl + (cf * 1.0f) * mk3s(0.0f);
+                add_sample(fb, P, pX, mk3s(1.0f) * cl);
+            }
+            W.cl[i] = make_float4(cl.x, cl.y, cl.z, pX.x);
+        }
+        const uint32_t ns = queue_push(shCount, pushShadow);
+        if (pushShadow) {
+            W.sq[ns] = i;
+            W.sh_o[i] = shO;
+            W.sh_d[i] = shD;
+            W.sh_val[i] = shV;
+        }
+        const uint32_t nn = queue_push(nextCount, pushNext);
+        if (pushNext) qout[nn] = i;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void wf_resolve_kernel(PathParams P, WfState W, int bounce, ctl_pixel* fb) {
+    const uint32_t count = W.counts[2 * bounce + 1];
+    for (uint32_t k = blockIdx.x * kBlock + threadIdx.x; k < count; k += gridDim.x * kBlock) {
+        const uint32_t i = W.sq[k];
+        const float4 v = W.sh_val[i];
+        float4 cl4 = W.cl[i];
+        spec cl = mk3(cl4.x, cl4.y, cl4.z);
+        if (!W.sh_occ[i]) cl = cl + mk3(v.x, v.y, v.z);
+        W.cl[i] = make_float4(cl.x, cl.y, cl.z, cl4.w);
+        if (v.w != 0.0f) add_sample(fb, P, mk2(cl4.w, W.cf[i].w), mk3s(1.0f) * cl);
+    }
+}
+
+template <class T>
+bool wf_alloc(ctl_ctx* c, T** p, size_t n) {
+    if (hipMalloc((void**)p, n * sizeof(T) + 16) != hipSuccess) return false;
+    c->wf_allocs.push_back((void*)*p);
+    return true;
+}
+
+}  // namespace
+
+void wavefront_free(ctl_ctx* c) {
+    for (void* p : c->wf_allocs) (void)hipFree(p);
+    c->wf_allocs.clear();
+    c->wf = WfState{};
+}
+
+int wavefront_pass(ctl_ctx* c, const PathParams& P, ctl_pixel* fb, bool stats, hipStream_t s) {
+    const uint32_t owned = (P.num_tiles > P.rank) ? (P.num_tiles - P.rank + P.num_ranks - 1) / P.num_ranks : 0;
+    const uint64_t items = (uint64_t)owned * P.tile_size * P.tile_size;
+    if (items == 0) return 0;
+    if (items > 0xffffffffull) { c->err = "wavefront: too many paths per pass"; return CTL_ERR_INVALID; }
+    WfState& W = c->wf;
+    if (W.capacity < items) {
+        (void)hipStreamSynchronize(s);
+        wavefront_free(c);
+        size_t n = items;
+        bool ok = wf_alloc(c, &W.o, n) && wf_alloc(c, &W.d, n) && wf_alloc(c, &W.cl, n) && wf_alloc(c, &W.cf, n) &&
+                  wf_alloc(c, &W.wo, n) && wf_alloc(c, &W.ln, n) && wf_alloc(c, &W.meta, n) &&
+                  wf_alloc(c, &W.hit, n) && wf_alloc(c, &W.hit_node, n) && wf_alloc(c, &W.q[0], n) &&
+                  wf_alloc(c, &W.q[1], n) && wf_alloc(c, &W.sq, n) && wf_alloc(c, &W.sh_o, n) &&
+                  wf_alloc(c, &W.sh_d, n) && wf_alloc(c, &W.sh_val, n) && wf_alloc(c, &W.sh_occ, n) &&
+                  wf_alloc(c, &W.counts, 4 * (kMaxBounces + 2));
+        if (!ok) { wavefront_free(c); c->err = "wavefront: state allocation failed"; return CTL_ERR_NOMEM; }
+        W.capacity = items;
+    }
+    if (hipMemsetAsync(W.counts, 0, 4 * (kMaxBounces + 2) * sizeof(uint32_t), s) != hipSuccess) {
+        c->err = "wavefront: memset failed";
+        return CTL_ERR_HIP;
+    }
+    const float* s1 = c->d_s1[c->active];
+    const float2* s2 = c->d_s2[c->active];
+    const int persist = c->cu_count * 8;
+    const unsigned genBlocks = (unsigned)std::min<uint64_t>((items + kBlock - 1) / kBlock, (uint64_t)persist);
+    hipLaunchKernelGGL(wf_gen_kernel, dim3(genBlocks), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, items, fb);
+    const int maxB = std::min(P.max_path_length, kMaxBounces);
+    uint32_t* cursors = W.counts + 2 * (kMaxBounces + 2);
+    for (int b = 0; b < maxB; b++) {
+        const uint32_t* cnt = &W.counts[2 * b];
+        launch_trace<0>(c, s, W.q[b & 1], cnt, &cursors[2 * b], stats);
+        hipLaunchKernelGGL(wf_shade_kernel, dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, fb);
+        const uint32_t* scnt = &W.counts[2 * b + 1];
+        if (P.shadow_any_hit) launch_trace<1>(c, s, W.sq, scnt, &cursors[2 * b + 1], stats);
+        else launch_trace<2>(c, s, W.sq, scnt, &cursors[2 * b + 1], stats);
+        hipLaunchKernelGGL(wf_resolve_kernel, dim3(persist), dim3(kBlock), 0, s, P, W, b, fb);
+    }
+    if (hipGetLastError() != hipSuccess) { c->err = "wavefront: launch failed"; return CTL_ERR_HIP; }
+    return 0;
+}
+
+}  // namespace ctl

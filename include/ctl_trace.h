@@ -223,8 +223,14 @@ typedef struct {
     uint32_t tile_size;        /* image tile edge (64 = BLOCK_SAMPLER_BlockSize) */
     uint32_t num_ranks;        /* tiles with (tile_id % num_ranks) == rank are */
     uint32_t rank;             /*   rendered by this call                      */
-    uint32_t flags;            /* reserved, 0                                  */
+    uint32_t flags;            /* CTL_PT_*                                     */
 } ctl_pt_params;
+
+enum {
+    /* run the pass as one per-pixel megakernel (pathKernel2's structure)
+     * instead of the default wavefront pipeline; identical results */
+    CTL_PT_MEGAKERNEL = 1u << 0
+};
 
 /* ------------------------------------------------------------------------ */
 /* Device API (needs a gfx950 GPU)                                           */

@@ -93,9 +93,10 @@ def render_gpu(ctl, tracer, desc, params, passes, w, h, dev, first_pass=0):
 
 @pytest.mark.parametrize("config,scale,w,h,passes", [(1, 1.0, 64, 64, 4), (2, 0.25, 96, 64, 2), (3, 0.003, 64, 48, 2)])
 @pytest.mark.parametrize("any_hit", [1, 0])
-def test_render_pass_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, passes, any_hit):
+@pytest.mark.parametrize("mode", ["wavefront", "megakernel"])
+def test_render_pass_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, passes, any_hit, mode):
     d = scene(ctl, config, scale, w, h)
-    p = ctl.PTParams(1, 50, 5, any_hit, 64, 1, 0, 0)
+    p = ctl.PTParams(1, 50, 5, any_hit, 64, 1, 0, ctl.CTL_PT_MEGAKERNEL if mode == "megakernel" else 0)
     want, wrays = oracle_render(orc, d, p, passes, w, h)
     got, grays = render_gpu(ctl, tracer, d, p, passes, w, h, dev)
     assert grays == wrays
@@ -103,6 +104,17 @@ def test_render_pass_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, passe
     assert np.isfinite(got).all()
     bad = np.nonzero((want.view(np.uint32) != got.view(np.uint32)).any(axis=1))[0]
     assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
+
+
+@pytest.mark.parametrize("mpl,rr", [(1, 5), (3, 1), (8, 2)])
+def test_render_short_paths_and_rr(ctl, orc, tracer, dev, mpl, rr):
+    """MaxPathLength / RRStartDepth edge values (PathTracer.h:16-19)."""
+    d = scene(ctl, 1, 1.0, 64, 64)
+    p = ctl.PTParams(1, mpl, rr, 1, 64, 1, 0, 0)
+    want, wrays = oracle_render(orc, d, p, 2, 64, 64)
+    got, grays = render_gpu(ctl, tracer, d, p, 2, 64, 64, dev)
+    assert grays == wrays
+    assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
 
 
 def test_render_half_quirk_mode(ctl, orc, tracer, dev):
