@@ -28,6 +28,13 @@ import time
 import numpy as np
 
 
+KERNEL_NAME = {
+    "persistent": "path_kernel_persistent<false,true> (traversal + shading, path regeneration)",
+    "megakernel": "path_kernel<false,true> (one thread per pixel path)",
+    "wavefront": "wavefront pass (gen/trace/shade/shadow/resolve kernels; timed as one unit)",
+}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -47,6 +54,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl")
+    ap.add_argument("--schedule", default="persistent", choices=["persistent", "megakernel", "wavefront"])
     return ap.parse_args()
 
 
@@ -109,7 +117,8 @@ def main():
         f"built in {t_build:.1f}s with {threads} threads")
 
     pt = ctl.PathTracer(local, max_path_length=a.max_path_length, rr_start_depth=a.rr_start,
-                        shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, num_ranks=world, rank=rank)
+                        shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, num_ranks=world, rank=rank,
+                        schedule=a.schedule)
     pt.upload_scene(desc)
     W, H = a.width, a.height
     fb = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
@@ -126,9 +135,22 @@ def main():
     pass_base = 0
     steps_done = 0
 
-    def step(s):
+    # HIP events bracket every path-kernel launch (on the stream it runs on) so
+    # the roofline uses that kernel's own average duration; the sampler-table
+    # kernel of each pass stays outside the brackets but inside the step time.
+    kev = []
+
+    def step(s, timed=False):
         for k in range(world):
-            pt.do_pass(fb.data_ptr(), pass_base + s * world + k, sptr)
+            pt.generate_samples(pass_base + s * world + k, sptr)
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            pt.render_pass(fb.data_ptr(), sptr)
+            if timed:
+                e1.record(stream)
+                kev.append((e0, e1))
 
     for s in range(a.warmup):
         step(s)
@@ -146,7 +168,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for s in range(a.steps):
-        step(s)
+        step(s, timed=True)
     ev1.record(stream)
     if world > 1:
         dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)   # RCCL over xGMI
@@ -155,7 +177,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1)
+    step_ms = ev0.elapsed_time(ev1)
+    kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in kev)
 
     rays = pt.rays_traced()
     tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -170,7 +193,7 @@ def main():
         passes = a.steps * world
         img = fb.view(H, W, 7)
         wsum = float(img[..., 6].sum().item())
-        launches = a.steps * world   # path_kernel launches on this rank in the timed region
+        launches = len(kev)   # path-kernel launches on this rank in the timed region
         per_launch_ms = kernel_ms / launches
         achieved = alg_bytes_per_pass / (per_launch_ms * 1e-3) / 1e9
         traffic = None
@@ -215,7 +238,9 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / 8000.0, 4),
                 "traffic": traffic,
-                "kernel": "path_kernel<false> (megakernel: traversal + shading)",
+                "kernel": KERNEL_NAME[a.schedule],
+                "launches_timed": launches,
+                "gpu_step_ms": round(step_ms / a.steps, 3),
                 "alg_bytes_per_launch": int(alg_bytes_per_pass),
                 "per_launch_ms": round(per_launch_ms, 3),
                 "visits_per_launch": {"inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3]),

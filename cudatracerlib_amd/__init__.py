@@ -23,10 +23,10 @@ import ctypes as C
 
 from . import _abi
 from ._abi import (PTParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK,
-                   CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL)
+                   CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT)
 
 __all__ = ["HostScene", "Tracer", "PathTracer", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
-           "CTL_SCENE_HALF_HOST_QUIRK", "CTL_PT_MEGAKERNEL", "lib", "diffuse_material"]
+           "CTL_SCENE_HALF_HOST_QUIRK", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "lib", "diffuse_material"]
 
 
 def lib():
@@ -178,14 +178,22 @@ class PathTracer(Tracer):
     Defaults: Direct=1, MaxPathLength=50, RRStartDepth=5 (PathTracer.h:16-19)."""
 
     def __init__(self, device=0, max_path_length=50, rr_start_depth=5, shadow_any_hit=True, tile_size=64,
-                 num_ranks=1, rank=0, megakernel=False):
+                 num_ranks=1, rank=0, schedule="persistent"):
+        """schedule: "persistent" (regenerating path kernel, default), "megakernel"
+        (one thread per pixel path) or "wavefront"; all bit-identical."""
         super().__init__(device)
+        flags = {"persistent": 0, "megakernel": CTL_PT_MEGAKERNEL, "wavefront": CTL_PT_WAVEFRONT}[schedule]
         self.params = PTParams(1, max_path_length, rr_start_depth, 1 if shadow_any_hit else 0, tile_size,
-                               num_ranks, rank, CTL_PT_MEGAKERNEL if megakernel else 0)
+                               num_ranks, rank, flags)
 
     def do_pass(self, fb_ptr, pass_index, stream=0):
         """UpdateKernel's sampler regeneration + one render pass into fb (device PixelData[w*h])."""
         self.generate_samples(pass_index, stream)
+        _check(self._L.ctl_render_pass(self._ctx, C.byref(self.params), fb_ptr, stream), self._ctx,
+               "ctl_render_pass")
+
+    def render_pass(self, fb_ptr, stream=0):
+        """One pass with the sampler tables already generated (generate_samples)."""
         _check(self._L.ctl_render_pass(self._ctx, C.byref(self.params), fb_ptr, stream), self._ctx,
                "ctl_render_pass")
 

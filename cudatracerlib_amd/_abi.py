@@ -15,6 +15,7 @@ CTL_BSDF_DIFFUSE = 1
 CTL_EDIFFUSE_REFLECTION = 0x2
 CTL_MAX_NUM_LIGHTS = 16
 CTL_PT_MEGAKERNEL = 1
+CTL_PT_WAVEFRONT = 2
 
 
 class BVHNode(C.Structure):          # BVHNodeData, 64 B

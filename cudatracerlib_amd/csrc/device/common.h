@@ -110,6 +110,145 @@ __device__ __forceinline__ void add_sample(ctl_pixel* fb, const PathParams& P, f
     }
 }
 
+// Loop-carried variables of PathTrace<true> (PathTracer.cu:10-33).  wo and
+// brdf_pdf persist: diffuse_sample leaves them untouched when it rejects a
+// sample, and the reference then continues with the previous values.
+struct PathVars {
+    spec cl, cf;
+    f3 rori, rdir, last_nor, wo;
+    f2 pX;
+    float brdf_pdf;
+    int depth;
+    bool specular;
+    __device__ __forceinline__ void begin(f2 px, f3 o, f3 d) {
+        cl = mk3s(0.0f); cf = mk3s(1.0f);
+        rori = o; rdir = d;
+        last_nor = mk3s(0.0f);
+        wo = mk3(0.0f, 0.0f, 1.0f);
+        pX = px;
+        brdf_pdf = 0.0f;
+        depth = 0;
+        specular = false;
+    }
+};
+
+// NEE shadow ray of one bounce: origin = the new rori, unoccluded -> cl += add.
+// Skipping the add for occluded / absent shadow rays is exact: the reference
+// adds cf * (0 / lightPdf) = +0 there (cf is finite and >= 0).
+struct ShadowReq {
+    f3 d;
+    float dist;
+    spec add;
+    bool valid;
+};
+
+// Sensor sample + primary ray of pixel (px, py) (pathKernel2, PathTracer.cu:182-194;
+// PerspectiveSensor::sampleRayDifferential, Sensor.cu:130-144).
+__device__ __forceinline__ f2 primary_ray(const DevScene& S, SamplerDev& rng, uint32_t px, uint32_t py, f3& o,
+                                          f3& dw) {
+    f2 pX = mk2((float)px, (float)py) + rng.next2();
+    (void)rng.next2();   // aperture sample (unused by PerspectiveSensor)
+    sensor_ray(S, pX, o, dw);
+    return pX;
+}
+
+// One closest hit of PathTrace<true> (PathTracer.cu:35-96): emission with MIS,
+// BSDF sample, UniformSampleOneLight up to its occlusion test
+// (TraceAlgorithms.cu:44-73, 92-101; sampleEmitter KernelDynamicScene.cu:25-39),
+// throughput update and Russian roulette.  Returns false when RR ends the path.
+// Sampler draws are in the reference order: BSDF 2D, light choice 2D, light
+// position 2D, RR 1D.
+__device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P, SamplerDev& rng, PathVars& v,
+                                          const HitRec& r, ShadowReq& sh) {
+    sh.valid = false;
+    bsdf_rec b;
+    b.wo = v.wo;
+    b.sampled_type = 0;
+    b.type_mask = kEAll;
+    dgeom dg;
+    dg.P = v.rori + r.t * v.rdir;
+    const ctl_triangle_data td = S.tri_data[r.tri];
+    const ctl_node N = S.nodes[r.node];
+    fill_dg(td, load_m44(S.xf + 4 * r.node), mk2(r.u, r.v), P.half_quirk, LutDecode{S.normal_lut}, dg);
+    b.wi = to_local(dg.sys, -v.rdir);
+    const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N.material_offset];
+    if (mat.two_sided && b.wi.z < 0) {
+        dg.n = -dg.n;
+        dg.sys.n = -dg.sys.n;
+        b.wi.z *= -1.0f;
+    }
+    if (mat.node_light_index != 0xffffffffu) {
+        const uint32_t li = N.lights[mat.node_light_index];
+        const ctl_light L = S.lights[li];
+        float misWeight = 1.0f;
+        if (!(v.depth == 1 || v.specular)) {
+            direct_rec dRec;
+            dRec.ref = v.rori; dRec.refN = v.last_nor; dRec.p = dg.P; dRec.n = dg.n;
+            dRec.d = v.rdir; dRec.dist = r.t; dRec.measure = kESolidAngle;
+            float direct_pdf = light_pdf_direct(L, dRec) * (S.light_cdf[li] - (li == 0 ? 0.0f : S.light_cdf[li - 1]));
+            misWeight = power_heuristic(v.brdf_pdf, direct_pdf);
+        }
+        f3 w = -v.rdir;
+        spec Le = (dot(dg.sys.n, w) <= 0) ? mk3s(0.0f) : mk3(L.radiance[0], L.radiance[1], L.radiance[2]);
+        v.cl = v.cl + (v.cf * misWeight) * Le;
+    }
+    spec f = diffuse_sample(mat, b, v.brdf_pdf, rng.next2());
+    v.last_nor = dg.sys.n;
+    if ((mat.combined_type & kESmooth) != 0 && S.n_lights) {
+        f2 sample = rng.next2();
+        const uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
+        uint32_t first = 0, cnt = nl;   // STL_upper_bound
+        while (cnt > 0) {
+            uint32_t c2 = cnt / 2, mid = first + c2;
+            if (!(sample.x < S.light_cdf[mid])) { first = mid + 1; cnt -= c2 + 1; }
+            else cnt = c2;
+        }
+        const uint32_t lidx = first < nl ? first : nl - 1;
+        const float fU = S.light_cdf[lidx], fL = lidx > 0 ? S.light_cdf[lidx - 1] : 0.0f;
+        sample.x = (sample.x - fL) / (fU - fL);
+        const float lpdf = fU - fL;
+        direct_rec dRec;
+        dRec.p = dg.P; dRec.n = dg.sys.n; dRec.measure = kEArea;
+        dRec.ref = dg.P; dRec.refN = dg.sys.n;
+        spec value = light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, rng.next2());
+        if (!spec_zero(value)) {
+            bsdf_rec b2 = b;
+            b2.wo = to_local(dg.sys, dRec.d);
+            b2.type_mask = kEAll & ~kEDelta;
+            spec bsdfVal = diffuse_f(mat, b2);
+            if (!spec_zero(bsdfVal)) {
+                float weight = 1.0f;
+                if (dRec.measure != kEDiscrete) weight = power_heuristic(dRec.pdf * lpdf, diffuse_pdf(mat, b2));
+                spec ret = value * bsdfVal * weight;
+                ret = ret * mk3s(1.0f);
+                sh.valid = true;
+                sh.d = dRec.d;
+                sh.dist = dRec.dist;
+                sh.add = v.cf * spec_div(ret, lpdf);
+            }
+        }
+    }
+    v.specular = (b.sampled_type & kEDelta) != 0;
+    v.cf = v.cf * f;
+    v.rori = dg.P;
+    v.rdir = to_world(dg.sys, b.wo);
+    v.wo = b.wo;
+    if (v.depth > P.rr_start_depth && !v.specular) {
+        if (rng.next1() >= spec_max(v.cf)) return false;
+        v.cf = spec_div(v.cf, spec_max(v.cf));
+    }
+    return true;
+}
+
+// KernelDynamicScene::Occluded(ray, 0, dist) decided from a finished shadow
+// traversal (KernelDynamicScene.cu:70-80): any-hit over (eps, dist - eps), or
+// the reference's closest hit tested against (eps, dist - eps).
+__device__ __forceinline__ bool shadow_occluded(const DevScene& S, bool any_hit, const HitRec& h, float dist) {
+    if (any_hit) return h.tri != 0xffffffffu;
+    bool end = h.t < dist - S.ray_eps;
+    return h.t > 0 + S.ray_eps && end;
+}
+
 // Wavefront path state, structure of arrays (capacity = paths per pass).
 struct WfState {
     float4* o;        // ray origin xyz | w: brdf_pdf
@@ -155,6 +294,17 @@ struct ctl_ctx {
 };
 
 namespace ctl {
+// Persistent grids = exactly the co-resident blocks (occupancy from the
+// compiled register/LDS footprint x CU count): no block waits for a slot and
+// the atomic work cursor spreads the pass evenly over all CUs.
+template <class K>
+int resident_blocks(ctl_ctx* c, K kernel, size_t lds) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess || per_cu <= 0)
+        per_cu = 2;
+    return per_cu * c->cu_count;
+}
+
 // wavefront.hip
 int wavefront_pass(ctl_ctx* c, const PathParams& P, ctl_pixel* fb, bool stats, hipStream_t s);
 void wavefront_free(ctl_ctx* c);

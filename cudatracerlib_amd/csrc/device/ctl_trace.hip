@@ -4,12 +4,18 @@
 //   intersect_kernel   batch closest/any hit over ctl_ray -> ctl_hit
 //                      (intersectKernel<ANY_HIT> + __internal__IntersectBuffers,
 //                       Kernel/TraceHelper.cu:326-746)
-//   path_kernel        one PathTracer pass: sensor ray + PathTrace<true> + AddSample
-//                      (pathKernel2 / PathTrace, Integrators/PathTracer.cu:10-113,182-194;
+//   path_kernel_persistent  one PathTracer pass (default schedule): resident
+//                      grid, path regeneration from an atomic pixel cursor
+//   path_kernel        one PathTracer pass, one thread per pixel path
+//                      (both: sensor ray + PathTrace<true> + AddSample;
+//                       pathKernel2 / PathTrace, Integrators/PathTracer.cu:10-113,182-194;
 //                       Image::AddSample, Engine/Image.cu:22-44)
+//   sampler_kernel     SequenceSamplerData tables of a pass (Sampler.cu, CudaRandom.cu)
+// The wavefront schedule lives in wavefront.hip.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -38,7 +44,9 @@ static_assert(sizeof(ctl_light_tri) == 64, "ShapeSet::triData is 64 B");
 
 namespace {
 
-template <bool STATS>
+// Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
+// traversals inline in the bounce, as the reference's pathKernel2 runs it.
+template <bool STATS, bool SINGLE>
 struct PathCtx {
     const DevScene& S;
     const PathParams& P;
@@ -47,134 +55,31 @@ struct PathCtx {
     uint32_t rays;
     TraceStats ts;
     bool ok;
+    PathVars v;
 
-    __device__ void trace_closest(f3 o, f3 d, HitRec& h) {   // traceRay (TraceHelper.cu:174-180)
+    // one iteration of `while (depth++ < MaxPathLength)`; false = path done
+    __device__ __forceinline__ bool bounce() {
+        if (!(v.depth++ < P.max_path_length)) return false;
+        HitRec r2;   // traceRay (TraceHelper.cu:174-180)
+        r2.t = FLT_MAX; r2.tri = 0xffffffffu; r2.node = 0xffffffffu; r2.u = r2.v = 0.0f;
         rays++;
-        h.t = FLT_MAX; h.tri = 0xffffffffu; h.node = 0xffffffffu; h.u = h.v = 0.0f;
-        ok &= trace_ray_dev<false, STATS>(S, o, d, 0.0f, S.ray_eps, h, st, &ts);
-    }
-    // KernelDynamicScene::Occluded(ray, 0, tmax) (KernelDynamicScene.cu:70-80)
-    __device__ bool occluded(f3 o, f3 d, float tmax) {
-        if (P.shadow_any_hit) {
-            rays++;
+        ok &= trace_one<0, STATS, SINGLE>(S, v.rori, v.rdir, 0.0f, S.ray_eps, r2, st, &ts);
+        if (r2.tri == 0xffffffffu) {
+            v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);   // no environment map
+            return false;
+        }
+        ShadowReq sh;
+        const bool cont = shade_hit(S, P, rng, v, r2, sh);
+        if (sh.valid) {
+            const bool any = P.shadow_any_hit != 0;
             HitRec h;
-            h.t = tmax - S.ray_eps; h.tri = 0xffffffffu; h.node = 0xffffffffu; h.u = h.v = 0.0f;
-            ok &= trace_ray_dev<true, STATS>(S, o, d, 0.0f, S.ray_eps, h, st, &ts);
-            return h.tri != 0xffffffffu;
+            h.t = any ? sh.dist - S.ray_eps : FLT_MAX; h.tri = 0xffffffffu; h.node = 0xffffffffu; h.u = h.v = 0.0f;
+            rays++;
+            if (any) ok &= trace_one<1, STATS, SINGLE>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            else ok &= trace_one<0, STATS, SINGLE>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            if (!shadow_occluded(S, any, h, sh.dist)) v.cl = v.cl + sh.add;
         }
-        HitRec h;
-        trace_closest(o, d, h);
-        bool end = h.t < tmax - S.ray_eps;
-        return h.t > 0 + S.ray_eps && end;
-    }
-
-    // EstimateDirect (Kernel/TraceAlgorithms.cu:44-73): flags EAll & ~EDelta, attenuated, MIS
-    __device__ spec estimate_direct(bsdf_rec b, const dgeom& dg, const ctl_material& mat, const ctl_light& L,
-                                    float light_pdf) {
-        direct_rec dRec;
-        dRec.p = dg.P; dRec.n = dg.sys.n; dRec.measure = kEArea;
-        dRec.ref = dg.P; dRec.refN = dg.sys.n;
-        spec value = light_sample_direct(L, S.light_tris, S.light_tri_cdf, dRec, rng.next2());
-        spec ret = mk3s(0.0f);
-        if (!spec_zero(value)) {
-            b.wo = to_local(dg.sys, dRec.d);
-            b.type_mask = kEAll & ~kEDelta;
-            spec bsdfVal = diffuse_f(mat, b);
-            if (!spec_zero(bsdfVal) && !occluded(dRec.ref, dRec.d, dRec.dist)) {
-                float weight = 1.0f;
-                if (dRec.measure != kEDiscrete) {
-                    const float bsdfPdf = diffuse_pdf(mat, b);
-                    const float directPdf = dRec.pdf * light_pdf;
-                    weight = power_heuristic(directPdf, bsdfPdf);
-                }
-                ret = value * bsdfVal * weight;
-                ret = ret * mk3s(1.0f);
-            }
-        }
-        return ret;
-    }
-
-    // UniformSampleOneLight (TraceAlgorithms.cu:92-101) + sampleEmitter (KernelDynamicScene.cu:25-39)
-    __device__ spec sample_one_light(const bsdf_rec& b, const dgeom& dg, const ctl_material& mat) {
-        if (!S.n_lights) return mk3s(0.0f);
-        f2 sample = rng.next2();
-        uint32_t n = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
-        uint32_t first = 0, count = n;   // STL_upper_bound
-        while (count > 0) {
-            uint32_t c2 = count / 2, mid = first + c2;
-            if (!(sample.x < S.light_cdf[mid])) { first = mid + 1; count -= c2 + 1; }
-            else count = c2;
-        }
-        uint32_t idx = first;
-        if (idx >= n) idx = n - 1;
-        float fU = S.light_cdf[idx], fL = idx > 0 ? S.light_cdf[idx - 1] : 0.0f;
-        sample.x = (sample.x - fL) / (fU - fL);
-        float pdf = fU - fL;
-        return spec_div(estimate_direct(b, dg, mat, S.lights[idx], pdf), pdf);
-    }
-
-    // PathTrace<true> without media / environment (PathTracer.cu:10-113)
-    __device__ spec path_trace(f3 rori, f3 rdir) {
-        spec cl = mk3s(0.0f), cf = mk3s(1.0f);
-        int depth = 0;
-        bool specularBounce = false;
-        bsdf_rec b;
-        b.wo = mk3(0.0f, 0.0f, 1.0f);
-        b.wi = mk3(0.0f, 0.0f, 1.0f);
-        b.sampled_type = 0;
-        b.type_mask = kEAll;
-        float brdf_pdf = 0.0f;
-        f3 last_nor = mk3s(0.0f);
-        HitRec r2;
-        r2.tri = 0xffffffffu;
-        while (depth++ < P.max_path_length) {
-            trace_closest(rori, rdir, r2);
-            if (r2.tri != 0xffffffffu) {
-                b.sampled_type = 0;
-                b.type_mask = kEAll;
-                dgeom dg;
-                dg.P = rori + r2.t * rdir;
-                const ctl_triangle_data td = S.tri_data[r2.tri];
-                const ctl_node N = S.nodes[r2.node];
-                fill_dg(td, load_m44(S.xf + 4 * r2.node), mk2(r2.u, r2.v), P.half_quirk, LutDecode{S.normal_lut}, dg);
-                b.wi = to_local(dg.sys, -rdir);
-                const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N.material_offset];
-                if (mat.two_sided && b.wi.z < 0) {
-                    dg.n = -dg.n;
-                    dg.sys.n = -dg.sys.n;
-                    b.wi.z *= -1.0f;
-                }
-                if (mat.node_light_index != 0xffffffffu) {
-                    uint32_t li = N.lights[mat.node_light_index];
-                    const ctl_light L = S.lights[li];
-                    float misWeight = 1.0f;
-                    if (!(depth == 1 || specularBounce)) {
-                        direct_rec dRec;
-                        dRec.ref = rori; dRec.refN = last_nor; dRec.p = dg.P; dRec.n = dg.n;
-                        dRec.d = rdir; dRec.dist = r2.t; dRec.measure = kESolidAngle;
-                        float direct_pdf = light_pdf_direct(L, dRec) * (S.light_cdf[li] - (li == 0 ? 0.0f : S.light_cdf[li - 1]));
-                        misWeight = power_heuristic(brdf_pdf, direct_pdf);
-                    }
-                    f3 w = -rdir;
-                    spec Le = (dot(dg.sys.n, w) <= 0) ? mk3s(0.0f) : mk3(L.radiance[0], L.radiance[1], L.radiance[2]);
-                    cl = cl + (cf * misWeight) * Le;
-                }
-                spec f = diffuse_sample(mat, b, brdf_pdf, rng.next2());
-                last_nor = dg.sys.n;
-                if ((mat.combined_type & kESmooth) != 0) cl = cl + cf * sample_one_light(b, dg, mat);
-                specularBounce = (b.sampled_type & kEDelta) != 0;
-                cf = cf * f;
-                rori = dg.P;
-                rdir = to_world(dg.sys, b.wo);
-            }
-            if (r2.tri == 0xffffffffu) break;
-            if (depth > P.rr_start_depth && !specularBounce) {
-                if (rng.next1() >= spec_max(cf)) break;
-                cf = spec_div(cf, spec_max(cf));
-            }
-        }
-        if (r2.tri == 0xffffffffu) cl = cl + (cf * 1.0f) * mk3s(0.0f);
-        return cl;
+        return cont;
     }
 };
 
@@ -224,50 +129,143 @@ __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict
     }
 }
 
-template <bool STATS>
+// One path per thread (the reference's pathKernel2 launch shape).
+template <bool STATS, bool SINGLE>
 __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
                                                       ctl_pixel* fb, unsigned long long* counters) {
     CTL_LANE_STACK(st);
-    const uint32_t perTile = P.tile_size * P.tile_size;
     const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t j = (uint32_t)(g / perTile), w = (uint32_t)(g % perTile);
-    const uint32_t tile = j * P.num_ranks + P.rank;
     uint32_t rays = 0;
     TraceStats ts{0, 0, 0};
     bool ok = true;
-    if (tile < P.num_tiles) {
-        const uint32_t groupsPerRow = P.tile_size / 8;
-        const uint32_t grp = w / 64, lane = w % 64;
-        const uint32_t px = (tile % P.tiles_x) * P.tile_size + (grp % groupsPerRow) * 8 + lane % 8;
-        const uint32_t py = (tile / P.tiles_x) * P.tile_size + (grp / groupsPerRow) * 8 + lane / 8;
+    uint32_t px, py;
+    if (work_pixel(P, g, px, py)) {
         const uint32_t idx = py * P.width + px;   // TracerBase::getPixelIndex (Tracer.h:89-97)
-        if (px < P.width && py < P.height) {
-            SamplerDev rng{s1, s2, P.nseq, P.len, idx % P.nseq, (idx / P.nseq) % P.nseq, 0, 0};
-            PathCtx<STATS> C{S, P, rng, st, 0, TraceStats{0, 0, 0}, true};
-            f2 pX = mk2((float)px, (float)py) + rng.next2();
-            (void)rng.next2();   // aperture sample (unused by PerspectiveSensor)
-            // PerspectiveSensor::sampleRayDifferential (Sensor.cu:130-144)
-            m44 s2c = to_m44(S.camera.sample_to_camera), tw = to_m44(S.camera.to_world);
-            f3 nearP = xform_point(s2c, mk3(pX.x * S.camera.inv_resolution[0], pX.y * S.camera.inv_resolution[1], 0.0f));
-            f3 d = normalize(nearP);
-            f3 o = xform_point(tw, mk3s(0.0f));
-            f3 dw = xform_dir(tw, d);
-            spec col = mk3s(1.0f) * C.path_trace(o, dw);
-            // Image::AddSample: single owner per pixel per pass -> plain read-modify-write
-            col.x = tmax(0.0f, col.x); col.y = tmax(0.0f, col.y); col.z = tmax(0.0f, col.z);
-            int x = (int)floorf(pX.x), y = (int)floorf(pX.y);
-            bool valid = !(isnan(col.x) || isnan(col.y) || isnan(col.z)) && isfinite(col.x) && isfinite(col.y) &&
-                         isfinite(col.z) && col.x >= 0.0f && col.y >= 0.0f && col.z >= 0.0f;
-            if (x >= 0 && x < (int)P.width && y >= 0 && y < (int)P.height && valid) {
-                ctl_pixel* pp = fb + (size_t)y * P.width + x;
-                pp->rgb[0] += col.x;
-                pp->rgb[1] += col.y;
-                pp->rgb[2] += col.z;
-                pp->weight_sum += 1.0f;
+        SamplerDev rng{s1, s2, P.nseq, P.len, idx % P.nseq, (idx / P.nseq) % P.nseq, 0, 0};
+        PathCtx<STATS, SINGLE> C{S, P, rng, st, 0, TraceStats{0, 0, 0}, true, PathVars{}};
+        f3 o, dw;
+        const f2 pX = primary_ray(S, rng, px, py, o, dw);
+        C.v.begin(pX, o, dw);
+        while (C.bounce()) {}
+        add_sample(fb, P, pX, mk3s(1.0f) * C.v.cl);
+        rays = C.rays;
+        ts = C.ts;
+        ok = C.ok;
+    }
+    wave_add_u64(&counters[0], rays);
+    if (!ok) atomicAdd(&counters[1], 1ull);
+    if (STATS) {
+        wave_add_u64(&counters[2], ts.nodes);
+        wave_add_u64(&counters[3], ts.tris);
+        wave_add_u64(&counters[4], ts.inst);
+    }
+}
+
+// Persistent path kernel (default schedule).  A resident grid of lanes, each
+// owning one path at a time and one resumable traversal (Traverser::round):
+//  * a lane alternates extension ray -> shade_hit -> shadow ray -> ... ; the
+//    NEE shadow ray is traced right after the bounce that made it, so the
+//    radiance sums happen in the reference's order;
+//  * a lane whose traversal finished shades and starts its next ray before
+//    the next traversal round, and a lane whose path ended does AddSample and
+//    takes the next pixel of the pass from a wave-aggregated atomic cursor;
+//    waves therefore stay full through long rays and the RR tail;
+//  * exactly one traversal and one shading site in the kernel (one I-cache
+//    footprint, lower VGPR peak).
+// Pixels are independent (own sampler index, single owner in the framebuffer)
+// so the framebuffer is bit-identical to path_kernel's.
+// Persistent path kernel with path regeneration (default schedule).  A
+// resident grid of lanes, each owning one path at a time:
+//  * every iteration a lane traces its pending ray to completion (extension
+//    ray, or the NEE shadow ray of its last bounce) with one traversal call
+//    site in the kernel, then shades / resolves it; the shadow ray is traced
+//    right after the bounce that made it, so radiance sums happen in the
+//    reference's order;
+//  * a lane whose path ended does AddSample and takes the next pixel of the
+//    pass from a wave-aggregated atomic cursor, so waves stay full through
+//    the Russian-roulette tail instead of idling until their longest path
+//    ends;
+//  * the traverser is local to an iteration: only the path variables and the
+//    pending ray are loop-carried, keeping the register peak low.
+// Pixels are independent (own sampler index, single owner in the framebuffer)
+// so the framebuffer is bit-identical to path_kernel's.
+template <bool STATS, bool SINGLE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? 4 : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
+                                                                 const float2* s2, ctl_pixel* fb, uint64_t items,
+                                                                 uint32_t* cursor, unsigned long long* counters) {
+    CTL_LANE_STACK(st);
+    SamplerDev rng{s1, s2, P.nseq, P.len, 0, 0, 0, 0};
+    PathVars v;
+    ShadowReq sh;
+    sh.valid = false;
+    sh.dist = 0.0f;
+    TraceStats ts{0, 0, 0};
+    uint32_t rays = 0;
+    bool active = false, exhausted = false, shadowPhase = false, ending = false, ok = true;
+    const bool shadowAny = P.shadow_any_hit != 0;
+    const int lane = threadIdx.x & 63;
+    while (true) {
+        const bool need = !active && !exhausted;
+        const uint64_t mask = __ballot(need);
+        if (mask) {
+            const int leader = __ffsll((unsigned long long)mask) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(cursor, (uint32_t)__popcll(mask));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t k = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                uint32_t px, py;
+                if (k >= items) {
+                    exhausted = true;
+                } else if (work_pixel(P, k, px, py)) {
+                    const uint32_t idx = py * P.width + px;
+                    rng.a = idx % P.nseq; rng.b = (idx / P.nseq) % P.nseq; rng.d1 = 0; rng.d2 = 0;
+                    f3 o, dw;
+                    const f2 pX = primary_ray(S, rng, px, py, o, dw);
+                    v.begin(pX, o, dw);
+                    shadowPhase = false;
+                    ending = false;
+                    // loop head of PathTrace: `while (depth++ < MaxPathLength)`
+                    if (v.depth++ < P.max_path_length) active = true;
+                    else add_sample(fb, P, v.pX, mk3s(1.0f) * v.cl);
+                }
             }
-            rays = C.rays;
-            ts = C.ts;
-            ok = C.ok;
+        }
+        if (!__any(active)) {
+            if (__all(exhausted)) break;
+            continue;
+        }
+        if (active) {
+            HitRec h;
+            h.t = (shadowPhase && shadowAny) ? sh.dist - S.ray_eps : FLT_MAX;
+            h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
+            const f3 d = shadowPhase ? sh.d : v.rdir;
+            rays++;
+            if (S.n_nodes != 0) {
+                Traverser<2, STATS, SINGLE> T;
+                T.anyhit = shadowPhase && shadowAny;
+                T.init(S, v.rori, d, 0.0f, S.ray_eps, h.t, st, &ts);
+                while (!T.done) T.round(S, st, &ts);
+                h = T.h;
+                ok &= !st.overflow;
+            }
+            bool cont;
+            if (shadowPhase) {
+                if (!shadow_occluded(S, shadowAny, h, sh.dist)) v.cl = v.cl + sh.add;
+                shadowPhase = false;
+                cont = !ending && v.depth++ < P.max_path_length;
+            } else if (h.tri == 0xffffffffu) {
+                v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);   // no environment map
+                cont = false;
+            } else {
+                ending = !shade_hit(S, P, rng, v, h, sh);
+                shadowPhase = sh.valid;
+                cont = sh.valid || (!ending && v.depth++ < P.max_path_length);
+            }
+            if (!cont) {
+                add_sample(fb, P, v.pX, mk3s(1.0f) * v.cl);
+                active = false;
+            }
         }
     }
     wave_add_u64(&counters[0], rays);
@@ -587,12 +585,30 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
     dim3 grid((unsigned)((threads + kBlock - 1) / kBlock));
     const float* s1 = c->d_s1[c->active];
     const float2* s2 = c->d_s2[c->active];
+    if (p->flags & CTL_PT_WAVEFRONT) return (ctl_status)ctl::wavefront_pass(c, P, fb, stats, s);
+    const bool single = c->scene.single != 0;
     if (!(p->flags & CTL_PT_MEGAKERNEL)) {
-        int r2 = ctl::wavefront_pass(c, P, fb, stats, s);
-        return r2;
+        uint32_t* cursor = reinterpret_cast<uint32_t*>(c->d_counters + 7);
+        CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(uint32_t), s));
+        const uint64_t want = (threads + kBlock - 1) / kBlock;
+#define PK(ST, SG)                                                                                               \
+        do {                                                                                                     \
+            static int nb = 0;                                                                                   \
+            if (!nb) nb = resident_blocks(c, path_kernel_persistent<ST, SG>, kStackLdsBytes);                    \
+            hipLaunchKernelGGL((path_kernel_persistent<ST, SG>), dim3((unsigned)std::min<uint64_t>(nb, want)),   \
+                               dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, fb, threads, cursor,        \
+                               c->d_counters);                                                                   \
+        } while (0)
+        if (stats) { if (single) PK(true, true); else PK(true, false); }
+        else { if (single) PK(false, true); else PK(false, false); }
+#undef PK
+    } else {
+#define MK(ST, SG) hipLaunchKernelGGL((path_kernel<ST, SG>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, \
+                                      fb, c->d_counters)
+        if (stats) { if (single) MK(true, true); else MK(true, false); }
+        else { if (single) MK(false, true); else MK(false, false); }
+#undef MK
     }
-    if (stats) hipLaunchKernelGGL((path_kernel<true>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, fb, c->d_counters);
-    else hipLaunchKernelGGL((path_kernel<false>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, fb, c->d_counters);
     CTL_HIP(c, hipGetLastError());
     return CTL_OK;
 }

@@ -141,9 +141,9 @@ __device__ __forceinline__ void xform_rows(const float4* M, f3 p, f3 d, f3& po, 
     po = xform_point(m, p);
 }
 
-// Closest (ANY=false) or any (ANY=true) hit with tri_tmin < t < h.t; box spans
-// start at span_tmin.
-template <bool ANY, bool STATS, bool SINGLE>
+// Closest (ANY=0) or any (ANY=1) hit with tri_tmin < t < h.t, or chosen per
+// ray by the `anyhit` member (ANY=2); box spans start at span_tmin.
+template <int ANY, bool STATS, bool SINGLE>
 struct Traverser {
     RayLocal cur;
     RayLocal world;   // unused when SINGLE
@@ -152,6 +152,7 @@ struct Traverser {
     int nodeAddr, leafAddr, level, meshSent;
     uint32_t nodeBase, triBase, idxBase, triOffset, instIdx;
     bool done, resumeLeaves;
+    bool anyhit;   // ANY == 2 only
 
     __device__ __forceinline__ void enter_instance(const DevScene& S, uint32_t inst, f3 o, f3 d) {
         instIdx = inst;
@@ -213,7 +214,7 @@ struct Traverser {
                         h.u = u;
                         h.v = v;
                         h.t = t;
-                        if (ANY) { done = true; break; }
+                        if (ANY == 1 || (ANY == 2 && anyhit)) { done = true; break; }
                     }
                 }
             }
@@ -320,7 +321,7 @@ struct Traverser {
 };
 
 // Whole traversal of one ray (megakernel, batch kernel).
-template <bool ANY, bool STATS, bool SINGLE>
+template <int ANY, bool STATS, bool SINGLE>
 __device__ __forceinline__ bool trace_one(const DevScene& S, f3 ori, f3 dir, float span_tmin, float tri_tmin,
                                           HitRec& h, LaneStack& st, TraceStats* stats) {
     Traverser<ANY, STATS, SINGLE> T;

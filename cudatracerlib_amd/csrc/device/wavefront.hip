@@ -147,17 +147,6 @@ __global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S, WfState W,
     }
 }
 
-// Persistent grid = exactly the blocks that are co-resident (occupancy from
-// the compiled register/LDS footprint x CU count), so no block waits for a
-// slot and the refill loop drains the queue evenly across all CUs.
-template <class K>
-int resident_blocks(ctl_ctx* c, K kernel, size_t lds) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess || per_cu <= 0)
-        per_cu = 4;
-    return per_cu * c->cu_count;
-}
-
 template <int MODE>
 void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32_t* cnt, uint32_t* cursor, bool stats) {
     WfState& W = c->wf;
@@ -188,129 +177,55 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams
         const bool act = k < count;
         const uint32_t i = act ? qin[k] : 0u;
         bool pushShadow = false, pushNext = false;
-        float4 shO, shD, shV;
+        ShadowReq sh;
         if (act) {
-            float4 o4 = W.o[i], d4 = W.d[i], cl4 = W.cl[i], cf4 = W.cf[i], wo4 = W.wo[i];
-            float2 ln2 = W.ln[i];
-            uint4 meta = W.meta[i];
-            float4 hit = W.hit[i];
-            const uint32_t node = W.hit_node[i];
-            f3 rori = mk3(o4.x, o4.y, o4.z), rdir = mk3(d4.x, d4.y, d4.z);
-            spec cl = mk3(cl4.x, cl4.y, cl4.z), cf = mk3(cf4.x, cf4.y, cf4.z);
-            const f2 pX = mk2(cl4.w, cf4.w);
-            float brdf_pdf = o4.w;
-            f3 last_nor = mk3(wo4.w, ln2.x, ln2.y);
-            int depth = (int)(meta.z & 0xffffu);
-            bool specularBounce = (meta.z >> 16) & 1u;
+            const float4 o4 = W.o[i], d4 = W.d[i], cl4 = W.cl[i], cf4 = W.cf[i], wo4 = W.wo[i];
+            const float2 ln2 = W.ln[i];
+            const uint4 meta = W.meta[i];
+            const float4 hit = W.hit[i];
+            PathVars v;
+            v.rori = mk3(o4.x, o4.y, o4.z); v.rdir = mk3(d4.x, d4.y, d4.z);
+            v.cl = mk3(cl4.x, cl4.y, cl4.z); v.cf = mk3(cf4.x, cf4.y, cf4.z);
+            v.pX = mk2(cl4.w, cf4.w);
+            v.brdf_pdf = o4.w;
+            v.wo = mk3(wo4.x, wo4.y, wo4.z);
+            v.last_nor = mk3(wo4.w, ln2.x, ln2.y);
+            v.depth = (int)(meta.z & 0xffffu);
+            v.specular = (meta.z >> 16) & 1u;
             SamplerDev rng;
             rng.init(s1, s2, P, meta.x, meta.y & 0xffffu, meta.y >> 16);
-            const uint32_t tri = (uint32_t)__float_as_int(hit.w);
-            bool terminated = false;
-            if (tri != 0xffffffffu) {
-                bsdf_rec b;
-                b.wo = mk3(wo4.x, wo4.y, wo4.z);
-                b.sampled_type = 0;
-                b.type_mask = kEAll;
-                dgeom dg;
-                dg.P = rori + hit.x * rdir;
-                const ctl_triangle_data td = S.tri_data[tri];
-                const ctl_node N = S.nodes[node];
-                fill_dg(td, load_m44(S.xf + 4 * node), mk2(hit.y, hit.z), P.half_quirk, LutDecode{S.normal_lut}, dg);
-                b.wi = to_local(dg.sys, -rdir);
-                const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N.material_offset];
-                if (mat.two_sided && b.wi.z < 0) {
-                    dg.n = -dg.n;
-                    dg.sys.n = -dg.sys.n;
-                    b.wi.z *= -1.0f;
-                }
-                if (mat.node_light_index != 0xffffffffu) {
-                    const uint32_t li = N.lights[mat.node_light_index];
-                    const ctl_light L = S.lights[li];
-                    float misWeight = 1.0f;
-                    if (!(depth == 1 || specularBounce)) {
-                        direct_rec dRec;
-                        dRec.ref = rori; dRec.refN = last_nor; dRec.p = dg.P; dRec.n = dg.n;
-                        dRec.d = rdir; dRec.dist = hit.x; dRec.measure = kESolidAngle;
-                        float direct_pdf = light_pdf_direct(L, dRec) * (S.light_cdf[li] - (li == 0 ? 0.0f : S.light_cdf[li - 1]));
-                        misWeight = power_heuristic(brdf_pdf, direct_pdf);
-                    }
-                    f3 w = -rdir;
-                    spec Le = (dot(dg.sys.n, w) <= 0) ? mk3s(0.0f) : mk3(L.radiance[0], L.radiance[1], L.radiance[2]);
-                    cl = cl + (cf * misWeight) * Le;
-                }
-                spec f = diffuse_sample(mat, b, brdf_pdf, rng.next2());
-                last_nor = dg.sys.n;
-                if ((mat.combined_type & kESmooth) != 0 && S.n_lights) {
-                    // UniformSampleOneLight up to the occlusion test (TraceAlgorithms.cu:44-73,92-101)
-                    f2 sample = rng.next2();
-                    uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
-                    uint32_t first = 0, cnt = nl;
-                    while (cnt > 0) {
-                        uint32_t c2 = cnt / 2, mid = first + c2;
-                        if (!(sample.x < S.light_cdf[mid])) { first = mid + 1; cnt -= c2 + 1; }
-                        else cnt = c2;
-                    }
-                    uint32_t lidx = first < nl ? first : nl - 1;
-                    float fU = S.light_cdf[lidx], fL = lidx > 0 ? S.light_cdf[lidx - 1] : 0.0f;
-                    sample.x = (sample.x - fL) / (fU - fL);
-                    const float lpdf = fU - fL;
-                    direct_rec dRec;
-                    dRec.p = dg.P; dRec.n = dg.sys.n; dRec.measure = kEArea;
-                    dRec.ref = dg.P; dRec.refN = dg.sys.n;
-                    spec value = light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, rng.next2());
-                    if (!spec_zero(value)) {
-                        bsdf_rec b2 = b;
-                        b2.wo = to_local(dg.sys, dRec.d);
-                        b2.type_mask = kEAll & ~kEDelta;
-                        spec bsdfVal = diffuse_f(mat, b2);
-                        if (!spec_zero(bsdfVal)) {
-                            float weight = 1.0f;
-                            if (dRec.measure != kEDiscrete)
-                                weight = power_heuristic(dRec.pdf * lpdf, diffuse_pdf(mat, b2));
-                            spec ret = value * bsdfVal * weight;
-                            ret = ret * mk3s(1.0f);
-                            spec add = cf * spec_div(ret, lpdf);
-                            pushShadow = true;
-                            shO = make_float4(dRec.ref.x, dRec.ref.y, dRec.ref.z, dRec.dist - S.ray_eps);
-                            shD = make_float4(dRec.d.x, dRec.d.y, dRec.d.z, dRec.dist);
-                            shV = make_float4(add.x, add.y, add.z, 0.0f);
-                        }
-                    }
-                }
-                specularBounce = (b.sampled_type & kEDelta) != 0;
-                cf = cf * f;
-                rori = dg.P;
-                rdir = to_world(dg.sys, b.wo);
-                if (depth > P.rr_start_depth && !specularBounce) {
-                    if (rng.next1() >= spec_max(cf)) terminated = true;
-                    else cf = spec_div(cf, spec_max(cf));
-                }
+            HitRec h;
+            h.t = hit.x; h.u = hit.y; h.v = hit.z; h.tri = (uint32_t)__float_as_int(hit.w); h.node = W.hit_node[i];
+            if (h.tri != 0xffffffffu) {
+                bool terminated = !shade_hit(S, P, rng, v, h, sh);
+                pushShadow = sh.valid;
                 if (!terminated) {
-                    if (depth < P.max_path_length) { depth++; pushNext = true; }
+                    // loop head of the next bounce: `while (depth++ < MaxPathLength)`
+                    if (v.depth < P.max_path_length) { v.depth++; pushNext = true; }
                     else terminated = true;
                 }
-                W.o[i] = make_float4(rori.x, rori.y, rori.z, brdf_pdf);
-                W.d[i] = make_float4(rdir.x, rdir.y, rdir.z, 0.0f);
-                W.cf[i] = make_float4(cf.x, cf.y, cf.z, pX.y);
-                W.wo[i] = make_float4(b.wo.x, b.wo.y, b.wo.z, last_nor.x);
-                W.ln[i] = make_float2(last_nor.y, last_nor.z);
-                W.meta[i] = make_uint4(meta.x, rng.d1 | (rng.d2 << 16), (uint32_t)depth | ((specularBounce ? 1u : 0u) << 16), 0u);
-                if (terminated && pushShadow) shV.w = 1.0f;   // resolve adds NEE, then AddSample
-                if (terminated && !pushShadow) add_sample(fb, P, pX, mk3s(1.0f) * cl);
+                W.o[i] = make_float4(v.rori.x, v.rori.y, v.rori.z, v.brdf_pdf);
+                W.d[i] = make_float4(v.rdir.x, v.rdir.y, v.rdir.z, 0.0f);
+                W.cf[i] = make_float4(v.cf.x, v.cf.y, v.cf.z, v.pX.y);
+                W.wo[i] = make_float4(v.wo.x, v.wo.y, v.wo.z, v.last_nor.x);
+                W.ln[i] = make_float2(v.last_nor.y, v.last_nor.z);
+                W.meta[i] = make_uint4(meta.x, rng.d1 | (rng.d2 << 16), (uint32_t)v.depth | ((v.specular ? 1u : 0u) << 16), 0u);
+                if (terminated && !pushShadow) add_sample(fb, P, v.pX, mk3s(1.0f) * v.cl);
+                if (pushShadow) {
+                    W.sh_o[i] = make_float4(v.rori.x, v.rori.y, v.rori.z, sh.dist - S.ray_eps);
+                    W.sh_d[i] = make_float4(sh.d.x, sh.d.y, sh.d.z, sh.dist);
+                    // w: the path ended here -> resolve adds NEE, then AddSample
+                    W.sh_val[i] = make_float4(sh.add.x, sh.add.y, sh.add.z, terminated ? 1.0f : 0.0f);
+                }
             } else {
                 // miss: loop ends; environment term of PathTracer.cu:98-111 (no env map -> 0)
-                cl = cl + (cf * 1.0f) * mk3s(0.0f);
-                add_sample(fb, P, pX, mk3s(1.0f) * cl);
+                v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);
+                add_sample(fb, P, v.pX, mk3s(1.0f) * v.cl);
             }
-            W.cl[i] = make_float4(cl.x, cl.y, cl.z, pX.x);
+            W.cl[i] = make_float4(v.cl.x, v.cl.y, v.cl.z, v.pX.x);
         }
         const uint32_t ns = queue_push(shCount, pushShadow);
-        if (pushShadow) {
-            W.sq[ns] = i;
-            W.sh_o[i] = shO;
-            W.sh_d[i] = shD;
-            W.sh_val[i] = shV;
-        }
+        if (pushShadow) W.sq[ns] = i;
         const uint32_t nn = queue_push(nextCount, pushNext);
         if (pushNext) qout[nn] = i;
     }

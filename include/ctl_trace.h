@@ -227,9 +227,13 @@ typedef struct {
 } ctl_pt_params;
 
 enum {
-    /* run the pass as one per-pixel megakernel (pathKernel2's structure)
-     * instead of the default wavefront pipeline; identical results */
-    CTL_PT_MEGAKERNEL = 1u << 0
+    /* Pass schedules; all three give bit-identical framebuffers.
+     * default (0): persistent path kernel with path regeneration
+     * CTL_PT_MEGAKERNEL: one thread per pixel path (pathKernel2's launch shape)
+     * CTL_PT_WAVEFRONT: wavefront pipeline (gen / trace / shade / shadow /
+     *                   resolve kernels per bounce over compacted queues)   */
+    CTL_PT_MEGAKERNEL = 1u << 0,
+    CTL_PT_WAVEFRONT = 1u << 1
 };
 
 /* ------------------------------------------------------------------------ */

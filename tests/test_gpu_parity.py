@@ -93,10 +93,11 @@ def render_gpu(ctl, tracer, desc, params, passes, w, h, dev, first_pass=0):
 
 @pytest.mark.parametrize("config,scale,w,h,passes", [(1, 1.0, 64, 64, 4), (2, 0.25, 96, 64, 2), (3, 0.003, 64, 48, 2)])
 @pytest.mark.parametrize("any_hit", [1, 0])
-@pytest.mark.parametrize("mode", ["wavefront", "megakernel"])
+@pytest.mark.parametrize("mode", ["persistent", "wavefront", "megakernel"])
 def test_render_pass_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, passes, any_hit, mode):
     d = scene(ctl, config, scale, w, h)
-    p = ctl.PTParams(1, 50, 5, any_hit, 64, 1, 0, ctl.CTL_PT_MEGAKERNEL if mode == "megakernel" else 0)
+    p = ctl.PTParams(1, 50, 5, any_hit, 64, 1, 0, {"persistent": 0, "megakernel": ctl.CTL_PT_MEGAKERNEL,
+                                                 "wavefront": ctl.CTL_PT_WAVEFRONT}[mode])
     want, wrays = oracle_render(orc, d, p, passes, w, h)
     got, grays = render_gpu(ctl, tracer, d, p, passes, w, h, dev)
     assert grays == wrays
