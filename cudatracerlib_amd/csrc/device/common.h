@@ -168,17 +168,19 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
     dgeom dg;
     dg.P = v.rori + r.t * v.rdir;
     const ctl_triangle_data td = S.tri_data[r.tri];
-    const ctl_node N = S.nodes[r.node];
+    // Node fields read in place: a local copy of the struct would be indexed
+    // dynamically (lights[]) and so live in scratch.
+    const ctl_node* N = S.nodes + r.node;
     fill_dg(td, load_m44(S.xf + 4 * r.node), mk2(r.u, r.v), P.half_quirk, LutDecode{S.normal_lut}, dg);
     b.wi = to_local(dg.sys, -v.rdir);
-    const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N.material_offset];
+    const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N->material_offset];
     if (mat.two_sided && b.wi.z < 0) {
         dg.n = -dg.n;
         dg.sys.n = -dg.sys.n;
         b.wi.z *= -1.0f;
     }
     if (mat.node_light_index != 0xffffffffu) {
-        const uint32_t li = N.lights[mat.node_light_index];
+        const uint32_t li = N->lights[mat.node_light_index];
         const ctl_light L = S.lights[li];
         float misWeight = 1.0f;
         if (!(v.depth == 1 || v.specular)) {

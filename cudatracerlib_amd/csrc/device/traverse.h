@@ -93,18 +93,23 @@ struct LaneStack {
     int sp;
     int tid;
     bool overflow;
+    // sp never drops below 0: every pop is matched by an earlier push (the
+    // bottom entry is the sentinel), so the common case is one ds op and one
+    // rarely-taken branch for the deep part.
     __device__ __forceinline__ void push(int v) {
-        if (sp < kLdsStack) ctl_lds_stack[sp * kStackBlock + tid] = v;
-        else if (sp < kStackMax) spill[sp - kLdsStack] = v;
-        else overflow = true;
+        if (sp < kLdsStack) {
+            ctl_lds_stack[sp * kStackBlock + tid] = v;
+        } else {
+            if (sp < kStackMax) spill[sp - kLdsStack] = v;
+            else overflow = true;
+        }
         sp++;
     }
     __device__ __forceinline__ int pop() {
         --sp;
-        if (sp < 0) { sp = 0; return CTL_SENTINEL; }
-        if (sp < kLdsStack) return ctl_lds_stack[sp * kStackBlock + tid];
-        if (sp < kStackMax) return spill[sp - kLdsStack];
-        return CTL_SENTINEL;
+        int v = ctl_lds_stack[min(sp, kLdsStack - 1) * kStackBlock + tid];
+        if (sp >= kLdsStack) v = sp < kStackMax ? spill[sp - kLdsStack] : CTL_SENTINEL;
+        return v;
     }
 };
 #define CTL_LANE_STACK(name)                       \
@@ -234,6 +239,9 @@ struct Traverser {
             const float4 tmp = n[3];
             if (STATS) stats->nodes++;
             int c0i = __float_as_int(tmp.x), c1i = __float_as_int(tmp.y);
+            // keep the child-index load beside the box loads: left to itself the
+            // compiler sinks it behind the box test, a second dependent L2 trip
+            asm volatile("" : "+v"(c0i), "+v"(c1i));
             const float c0lox = n0xy.x * cur.idx - cur.oodx;
             const float c0hix = n0xy.y * cur.idx - cur.oodx;
             const float c0loy = n0xy.z * cur.idy - cur.oody;
