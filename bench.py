@@ -89,6 +89,42 @@ def cpu_baseline(desc, params, seconds, threads):
     }
 
 
+def primary_ray_leg(pt, dev, stream, sptr, torch, pass_index, launches=10):
+    """Primary-ray traversal through the batch C-ABI (ctl_camera_rays ->
+    ctl_intersect): SURVEY §8(d)'s "C3 primary rays" roofline.  Algorithmic
+    bytes per launch = 64*inner visits + 52*tri tests + 108*instance entries
+    + 48 per ray (32-B ray in, 16-B hit out)."""
+    pt.generate_samples(pass_index, sptr)
+    n = pt.camera_rays(None, 0, sptr)
+    rays = torch.empty((n, 8), dtype=torch.float32, device=dev)
+    hits = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    pt.camera_rays(rays.data_ptr(), n, sptr)
+    st = pt.intersect_stats(n, rays.data_ptr(), hits.data_ptr(), False, sptr)
+    alg = 64 * st[1] + 52 * st[2] + 108 * st[3] + 48 * n
+    for _ in range(2):
+        pt.intersect_buffers(n, rays.data_ptr(), hits.data_ptr(), False, sptr)
+    ev = []
+    for _ in range(launches):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        pt.intersect_buffers(n, rays.data_ptr(), hits.data_ptr(), False, sptr)
+        e1.record(stream)
+        ev.append((e0, e1))
+    torch.cuda.synchronize(dev)
+    ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / launches
+    achieved = alg / (ms * 1e-3) / 1e9
+    return {
+        "kernel": "intersect_kernel<closest,single> (ctl_intersect over ctl_camera_rays)",
+        "rays_per_launch": int(n),
+        "ms_per_launch": round(ms, 4),
+        "mrays_s": round(n / ms / 1e3, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(achieved / 8000.0, 4), "alg_bytes_per_launch": int(alg),
+                     "inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3])},
+    }
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -181,6 +217,7 @@ def main():
     kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in kev)
 
     rays = pt.rays_traced()
+    prim = primary_ray_leg(pt, dev, stream, sptr, torch, pass_base + a.steps * world) if rank == 0 else None
     tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     rr = torch.tensor([rays], dtype=torch.int64, device=dev)
     if world > 1:
@@ -246,6 +283,7 @@ def main():
                 "visits_per_launch": {"inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3]),
                                       "rays": int(st[0])},
             },
+            "primary_rays": prim,
             "image_weight_sum": wsum,
             "scene_build_s": round(t_build, 2),
         }

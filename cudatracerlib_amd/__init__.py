@@ -197,6 +197,20 @@ class PathTracer(Tracer):
         _check(self._L.ctl_render_pass(self._ctx, C.byref(self.params), fb_ptr, stream), self._ctx,
                "ctl_render_pass")
 
+    def last_pass_ms(self):
+        """Device time of the last render pass (Tracer::getLastTimeSpentRenderingSec)."""
+        ms = C.c_float()
+        _check(self._L.ctl_last_pass_ms(self._ctx, C.byref(ms)), self._ctx, "ctl_last_pass_ms")
+        return ms.value
+
+    def camera_rays(self, rays_ptr=None, capacity=0, stream=0):
+        """Primary rays of the current pass (sampler tables from generate_samples) as a
+        ctl_ray batch; returns the ray count (call with rays_ptr=None to query it)."""
+        n = C.c_int64()
+        _check(self._L.ctl_camera_rays(self._ctx, C.byref(self.params), rays_ptr, int(capacity), C.byref(n), stream),
+               self._ctx, "ctl_camera_rays")
+        return n.value
+
     def pass_stats(self, fb_ptr, pass_index, stream=0):
         self.generate_samples(pass_index, stream)
         out = (C.c_uint64 * 4)()

@@ -126,6 +126,8 @@ SYMBOLS = [
     ("ctl_sync", C.c_int32, [_vp, _vp]),
     ("ctl_intersect_stats", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, C.POINTER(C.c_uint64), _vp]),
     ("ctl_render_pass_stats", C.c_int32, [_vp, C.POINTER(PTParams), _vp, C.POINTER(C.c_uint64), _vp]),
+    ("ctl_last_pass_ms", C.c_int32, [_vp, C.POINTER(C.c_float)]),
+    ("ctl_camera_rays", C.c_int32, [_vp, C.POINTER(PTParams), _vp, C.c_int64, C.POINTER(C.c_int64), _vp]),
     ("ctl_woop_set", None, [_vp, _vp, _vp, C.POINTER(WoopTri)]),
     ("ctl_host_sampler_tables", C.c_int32, [C.c_uint64, C.c_uint32, C.c_uint32, _vp, _vp]),
     ("ctl_host_scene_create", _vp, []),

@@ -289,6 +289,9 @@ struct ctl_ctx {
     hipEvent_t ev[2] = {nullptr, nullptr};
     int next_buf = 0, active = -1;
     unsigned long long* d_counters = nullptr;   // [0] rays [1] overflow [2..4] stats
+    uint32_t* d_cursors = nullptr;              // work cursors: [0] batch intersect [1] path pass
+    hipEvent_t pass_ev[2] = {nullptr, nullptr}; // bracket the last render pass (ctl_last_pass_ms)
+    bool pass_timed = false;
     uint32_t* d_powers = nullptr;               // XORWOW step powers for sampler_kernel
     ctl::WfState wf{};
     std::vector<void*> wf_allocs;

@@ -277,34 +277,86 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
     }
 }
 
-template <bool ANY, bool STATS>
+// Batch closest/any hit (intersectKernel<ANY_HIT>, TraceHelper.cu:326-734):
+// ray tmin bounds both the node spans and the triangle test (:650).  Resident
+// grid; lanes whose ray finished take the next ray from a wave-aggregated
+// atomic cursor between traversal rounds (the reference fetches per warp per
+// batch of 32 rays, :379-399), so waves stay full on incoherent rays.
+template <bool ANY, bool STATS, bool SINGLE>
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
-                                                           unsigned long long* counters) {
+                                                           uint32_t* cursor, unsigned long long* counters) {
     CTL_LANE_STACK(st);
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     TraceStats ts{0, 0, 0};
-    bool ok = true;
-    if (i < n) {
-        const float4* r4 = reinterpret_cast<const float4*>(rays + i);
-        const float4 o = r4[0], d = r4[1];
-        HitRec h;
-        h.t = d.w; h.tri = 0xffffffffu; h.node = 0xffffffffu; h.u = h.v = 0.0f;
-        if (S.n_nodes != 0) ok = trace_ray_dev<ANY, STATS>(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), o.w, o.w, h, st, &ts);
-        uint4 res = make_uint4((uint32_t)__float_as_int(h.t), 0xffffffffu, 0xffffffffu, 0u);
-        if (h.tri != 0xffffffffu) {   // TraceHelper.cu:722-731
-            res.y = h.node;
-            res.z = h.tri;
-            uint16_t xd = (uint16_t)(h.u * 65535), yd = (uint16_t)(h.v * 65535);
-            res.w = ((uint32_t)yd << 16) | (uint32_t)xd;
+    Traverser<ANY ? 1 : 0, STATS, SINGLE> T;
+    T.done = true;
+    bool haveRay = false, exhausted = false, ovf = false;
+    int64_t ray = 0;
+    const int lane = threadIdx.x & 63;
+    while (true) {
+        if (haveRay && T.done) {
+            uint4 res = make_uint4((uint32_t)__float_as_int(T.h.t), 0xffffffffu, 0xffffffffu, 0u);
+            if (T.h.tri != 0xffffffffu) {   // TraceHelper.cu:722-731
+                res.y = T.h.node;
+                res.z = T.h.tri;
+                uint16_t xd = (uint16_t)(T.h.u * 65535), yd = (uint16_t)(T.h.v * 65535);
+                res.w = ((uint32_t)yd << 16) | (uint32_t)xd;
+            }
+            reinterpret_cast<uint4*>(hits)[ray] = res;
+            ovf |= st.overflow;
+            haveRay = false;
         }
-        reinterpret_cast<uint4*>(hits)[i] = res;
+        const bool need = !haveRay && !exhausted;
+        const uint64_t mask = __ballot(need);
+        if (mask) {
+            const int leader = __ffsll((unsigned long long)mask) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(cursor, (uint32_t)__popcll(mask));
+            base = __shfl(base, leader);
+            if (need) {
+                const int64_t k = (int64_t)base + __popcll(mask & ((1ull << lane) - 1ull));
+                if (k < n) {
+                    ray = k;
+                    haveRay = true;
+                    const float4* r4 = reinterpret_cast<const float4*>(rays + k);
+                    const float4 o = r4[0], d = r4[1];
+                    T.init(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), o.w, o.w, d.w, st, &ts);
+                } else {
+                    exhausted = true;
+                }
+            }
+        }
+        if (!__any(haveRay)) break;
+        if (haveRay && !T.done) T.round(S, st, &ts);
     }
-    if (!ok) atomicAdd(&counters[1], 1ull);
+    if (ovf) atomicAdd(&counters[1], 1ull);
     if (STATS) {
         wave_add_u64(&counters[2], ts.nodes);
         wave_add_u64(&counters[3], ts.tris);
         wave_add_u64(&counters[4], ts.inst);
     }
+}
+
+// Primary rays of one pass in work order (the path kernels' first ray: pixel
+// jitter + aperture draw + PerspectiveSensor, Sensor.cu:130-144), as a
+// traversalRay batch: tmin = scene eps, tmax = FLT_MAX.  Work items outside
+// the image get an empty interval (tmax = 0).
+__global__ __launch_bounds__(kBlock) void camera_ray_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
+                                                            uint64_t items, ctl_ray* rays) {
+    const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= items) return;
+    uint32_t px, py;
+    float4 o4 = make_float4(0.0f, 0.0f, 0.0f, S.ray_eps), d4 = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+    if (work_pixel(P, g, px, py)) {
+        const uint32_t idx = py * P.width + px;
+        SamplerDev rng{s1, s2, P.nseq, P.len, idx % P.nseq, (idx / P.nseq) % P.nseq, 0, 0};
+        f3 o, d;
+        (void)primary_ray(S, rng, px, py, o, d);
+        o4 = make_float4(o.x, o.y, o.z, S.ray_eps);
+        d4 = make_float4(d.x, d.y, d.z, FLT_MAX);
+    }
+    float4* r4 = reinterpret_cast<float4*>(rays + g);
+    r4[0] = o4;
+    r4[1] = d4;
 }
 
 }  // namespace
@@ -377,6 +429,12 @@ CTL_API ctl_ctx* ctl_create(int32_t device) {
         delete c;
         return fail("ctl_create: counter allocation failed");
     }
+    if (hipMalloc(&c->d_cursors, 16 * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(c->d_cursors, 0, 16 * sizeof(uint32_t)) != hipSuccess ||
+        hipEventCreate(&c->pass_ev[0]) != hipSuccess || hipEventCreate(&c->pass_ev[1]) != hipSuccess) {
+        ctl_destroy(c);
+        return fail("ctl_create: cursor/event allocation failed");
+    }
     {
         std::vector<uint32_t> pw((size_t)kJumpBits * 800);
         ctl::sampler_step_powers(pw.data(), kJumpBits);
@@ -414,6 +472,9 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     }
     if (c->d_counters) (void)hipFree(c->d_counters);
+    if (c->d_cursors) (void)hipFree(c->d_cursors);
+    for (int i = 0; i < 2; i++)
+        if (c->pass_ev[i]) (void)hipEventDestroy(c->pass_ev[i]);
     if (c->d_powers) (void)hipFree(c->d_powers);
     delete c;
 }
@@ -523,17 +584,26 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
                                    bool stats, void* stream) {
     if (!c || n < 0 || (n > 0 && (!rays || !hits))) return CTL_ERR_INVALID;
     if (!c->has_scene) { c->err = "intersect: no scene uploaded"; return CTL_ERR_STATE; }
+    if (n > 0xffffffffll) { c->err = "intersect: more than 2^32-1 rays per call"; return CTL_ERR_INVALID; }
     CTL_HIP(c, hipSetDevice(c->device));
     if (n == 0) return CTL_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
-    if (stats) {
-        if (any_hit) hipLaunchKernelGGL((intersect_kernel<true, true>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, c->d_counters);
-        else hipLaunchKernelGGL((intersect_kernel<false, true>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, c->d_counters);
-    } else {
-        if (any_hit) hipLaunchKernelGGL((intersect_kernel<true, false>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, c->d_counters);
-        else hipLaunchKernelGGL((intersect_kernel<false, false>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, c->d_counters);
-    }
+    uint32_t* cursor = c->d_cursors;
+    CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(uint32_t), s));
+    const bool single = c->scene.single != 0;
+    const uint64_t want = ((uint64_t)n + kBlock - 1) / kBlock;
+#define IK(AN, ST, SG)                                                                                           \
+    do {                                                                                                         \
+        static int nb = 0;                                                                                       \
+        if (!nb) nb = resident_blocks(c, intersect_kernel<AN, ST, SG>, kStackLdsBytes);                          \
+        hipLaunchKernelGGL((intersect_kernel<AN, ST, SG>), dim3((unsigned)std::min<uint64_t>(nb, want)),         \
+                           dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, cursor, c->d_counters);     \
+    } while (0)
+#define IK2(AN, ST) do { if (single) IK(AN, ST, true); else IK(AN, ST, false); } while (0)
+    if (stats) { if (any_hit) IK2(true, true); else IK2(false, true); }
+    else { if (any_hit) IK2(true, false); else IK2(false, false); }
+#undef IK2
+#undef IK
     CTL_HIP(c, hipGetLastError());
     return CTL_OK;
 }
@@ -573,6 +643,9 @@ static ctl_status prepare_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb
     return CTL_OK;
 }
 
+static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const PathParams& P, ctl_pixel* fb, bool stats,
+                                  hipStream_t s, uint64_t threads, dim3 grid, const float* s1, const float2* s2);
+
 static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb, bool stats, void* stream) {
     PathParams P;
     ctl_status r = prepare_pass(c, p, fb, P);
@@ -585,10 +658,20 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
     dim3 grid((unsigned)((threads + kBlock - 1) / kBlock));
     const float* s1 = c->d_s1[c->active];
     const float2* s2 = c->d_s2[c->active];
+    CTL_HIP(c, hipEventRecord(c->pass_ev[0], s));
+    ctl_status r2 = launch_schedule(c, p, P, fb, stats, s, threads, grid, s1, s2);
+    if (r2 != CTL_OK) return r2;
+    CTL_HIP(c, hipEventRecord(c->pass_ev[1], s));
+    c->pass_timed = true;
+    return CTL_OK;
+}
+
+static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const PathParams& P, ctl_pixel* fb, bool stats,
+                                  hipStream_t s, uint64_t threads, dim3 grid, const float* s1, const float2* s2) {
     if (p->flags & CTL_PT_WAVEFRONT) return (ctl_status)ctl::wavefront_pass(c, P, fb, stats, s);
     const bool single = c->scene.single != 0;
     if (!(p->flags & CTL_PT_MEGAKERNEL)) {
-        uint32_t* cursor = reinterpret_cast<uint32_t*>(c->d_counters + 7);
+        uint32_t* cursor = c->d_cursors + 1;
         CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(uint32_t), s));
         const uint64_t want = (threads + kBlock - 1) / kBlock;
 #define PK(ST, SG)                                                                                               \
@@ -615,6 +698,35 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
 
 CTL_API ctl_status ctl_render_pass(ctl_ctx* c, const ctl_pt_params* params, ctl_pixel* d_fb, void* stream) {
     return launch_pass(c, params, d_fb, false, stream);
+}
+
+CTL_API ctl_status ctl_last_pass_ms(ctl_ctx* c, float* ms) {
+    if (!c || !ms) return CTL_ERR_INVALID;
+    if (!c->pass_timed) { c->err = "last_pass_ms: no render pass yet"; return CTL_ERR_STATE; }
+    CTL_HIP(c, hipSetDevice(c->device));
+    CTL_HIP(c, hipEventSynchronize(c->pass_ev[1]));
+    CTL_HIP(c, hipEventElapsedTime(ms, c->pass_ev[0], c->pass_ev[1]));
+    return CTL_OK;
+}
+
+CTL_API ctl_status ctl_camera_rays(ctl_ctx* c, const ctl_pt_params* params, ctl_ray* d_rays, int64_t capacity,
+                                   int64_t* n_out, void* stream) {
+    if (!c || !params || !n_out) return CTL_ERR_INVALID;
+    PathParams P;
+    ctl_pixel dummy;
+    ctl_status r = prepare_pass(c, params, &dummy, P);
+    if (r != CTL_OK) return r;
+    const uint32_t owned = (P.num_tiles > P.rank) ? (P.num_tiles - P.rank + P.num_ranks - 1) / P.num_ranks : 0;
+    const uint64_t items = (uint64_t)owned * P.tile_size * P.tile_size;
+    *n_out = (int64_t)items;
+    if (items == 0 || !d_rays) return CTL_OK;   // d_rays == NULL: size query
+    if (capacity < (int64_t)items) { c->err = "camera_rays: ray buffer too small"; return CTL_ERR_INVALID; }
+    CTL_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(camera_ray_kernel, dim3((unsigned)((items + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, c->scene,
+                       P, c->d_s1[c->active], c->d_s2[c->active], items, d_rays);
+    CTL_HIP(c, hipGetLastError());
+    return CTL_OK;
 }
 
 __global__ void add_kernel(unsigned long long* ctr, unsigned long long k) { ctr[0] += k; }

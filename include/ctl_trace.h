@@ -254,10 +254,11 @@ CTL_API const char* ctl_last_error(const ctl_ctx* ctx);
 CTL_API ctl_status ctl_scene_upload(ctl_ctx* ctx, const ctl_scene_desc* desc);
 
 /* Generates the SequenceSamplerData tables of render pass `pass_index` (the
- * pass-th UpdateKernel call, Kernel/Sampler.h:36-55 + 63-85) on the host and
- * copies them asynchronously on `stream` (double-buffered; safe to call while
- * the previous pass still renders).  num_sequences=4096, length=30 as
- * InitializeKernel (TraceHelper.cu:253-257). */
+ * pass-th UpdateKernel call, Kernel/Sampler.h:36-55 + 63-85) on the device,
+ * asynchronously on `stream` (double-buffered; safe to call while the
+ * previous pass still renders).  num_sequences=4096, length=30 as
+ * InitializeKernel (TraceHelper.cu:253-257).  Replaces the host generation in
+ * UpdateKernel (TraceHelper.cu:182-217). */
 CTL_API ctl_status ctl_sampler_generate(ctl_ctx* ctx, uint64_t pass_index, void* stream);
 /* Uploads caller-provided tables instead (element-major: [k*num_seq + s]). */
 CTL_API ctl_status ctl_sampler_upload(ctl_ctx* ctx, const float* seq1d, const float* seq2d,
@@ -275,6 +276,20 @@ CTL_API ctl_status ctl_intersect(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays,
  * ctl_sampler_upload on the same stream.  Asynchronous on `stream`. */
 CTL_API ctl_status ctl_render_pass(ctl_ctx* ctx, const ctl_pt_params* params, ctl_pixel* d_fb,
                                    void* stream);
+
+/* Device time of the last ctl_render_pass on its stream, in milliseconds
+ * (Tracer::getLastTimeSpentRenderingSec, Kernel/Tracer.h:133-140, which times
+ * DoPass with cudaEvents, Tracer.h:213,239-244).  Waits for that pass. */
+CTL_API ctl_status ctl_last_pass_ms(ctl_ctx* ctx, float* ms);
+
+/* The primary rays of a pass (what ctl_render_pass traces first: pixel jitter,
+ * aperture draw, PerspectiveSensor::sampleRayDifferential, Sensor.cu:130-144)
+ * as a traversalRay batch in work order, for ctl_intersect - the camera stage
+ * of the reference's batch tracers (DoubleRayBuffer callers).  Work items
+ * outside the image get tmax = 0.  *n_out = number of rays (owned tiles x
+ * tile_size^2); d_rays must hold that many (query with capacity 0). */
+CTL_API ctl_status ctl_camera_rays(ctl_ctx* ctx, const ctl_pt_params* params, ctl_ray* d_rays, int64_t capacity,
+                                   int64_t* n_out, void* stream);
 
 /* Number of traceRay-equivalent queries (camera + bounce + shadow rays +
  * batched rays) since the last reset; 64-bit (the reference's counter is a

@@ -44,6 +44,7 @@ def load():
         "oracle_brute_force": (None, [C.POINTER(SceneDesc), C.c_int64, vp, vp, vp, C.c_int32]),
         "oracle_render_pass": (C.c_uint64, [C.POINTER(SceneDesc), C.POINTER(PTParams), C.c_uint64, vp, C.c_int32,
                                             C.c_int32, C.c_uint32, vp]),
+        "oracle_camera_rays": (None, [C.POINTER(SceneDesc), C.c_uint64, vp]),
         "oracle_triangle_data_set": (None, [vp, C.c_uint8, vp, vp, vp]),
         "oracle_light_tri": (None, [vp, vp, vp, vp, vp, vp]),
         "oracle_matrix_inverse": (None, [vp, vp]),

@@ -892,6 +892,27 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
     return totalRays;
 }
 
+// Primary rays of pass `pass_index` in image order (pixel y*W+x): the first
+// ray path_trace gets in oracle_render_pass (pathKernel2, PathTracer.cu:182-194),
+// as traversalRay {o, eps; d, FLT_MAX}.
+void oracle_camera_rays(const ctl_scene_desc* desc, uint64_t pass_index, ctl_ray* out) {
+    const uint32_t nseq = 4096, len = 30;
+    std::vector<float> s1((size_t)nseq * len), s2((size_t)nseq * len * 2);
+    sampler_tables(pass_index, nseq, len, s1.data(), s2.data());
+    const ctl_camera& cam = desc->camera;
+    for (uint32_t y = 0; y < cam.height; y++)
+        for (uint32_t x = 0; x < cam.width; x++) {
+            Sampler rng{s1.data(), s2.data(), nseq, len, y * cam.width + x};
+            V2 pX = v2((float)x, (float)y) + rng.randomFloat2();
+            (void)rng.randomFloat2();
+            V3 o, d;
+            sensor_ray(cam, pX, o, d);
+            ctl_ray& r = out[(size_t)y * cam.width + x];
+            r.o[0] = o.x; r.o[1] = o.y; r.o[2] = o.z; r.tmin = desc->ray_eps;
+            r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z; r.tmax = FLT_MAX;
+        }
+}
+
 // Host-side compile pieces, for checking the product's scene compiler.
 void oracle_triangle_data_set(const float* P9, uint8_t mat, const float* T6, const float* N9, uint32_t* out8) {
     // TriangleData::TriangleData + setUvSetData + setData (TriangleData.cu:10-68), EXT_TRI

@@ -170,3 +170,72 @@ def test_full_size_c2_pass_properties(ctl, orc, tracer, dev):
     sel = np.arange(0, w * h, 97)
     assert np.array_equal(want[sel].view(np.uint32), got[sel].view(np.uint32))
     assert grays > w * h
+
+
+def work_order_pixels(w, h, ts=64, num_ranks=1, rank=0):
+    """numpy restatement of work_pixel(): work item -> (px, py, valid)."""
+    tiles_x, tiles_y = -(-w // ts), -(-h // ts)
+    num_tiles = tiles_x * tiles_y
+    owned = (num_tiles - rank + num_ranks - 1) // num_ranks
+    g = np.arange(owned * ts * ts, dtype=np.int64)
+    j, wi = g // (ts * ts), g % (ts * ts)
+    tile = j * num_ranks + rank
+    grp, lane = wi // 64, wi % 64
+    gpr = ts // 8
+    px = (tile % tiles_x) * ts + (grp % gpr) * 8 + lane % 8
+    py = (tile // tiles_x) * ts + (grp // gpr) * 8 + lane // 8
+    return px, py, (px < w) & (py < h)
+
+
+def test_camera_rays_and_batch_trace_bit_exact(ctl, orc, dev):
+    """ctl_camera_rays == the oracle's first path ray per pixel (bit-exact), and
+    ctl_intersect over them == the oracle's batch intersect."""
+    w, h = 200, 136                        # partial tiles on both axes
+    d = scene(ctl, 2, 0.25, w, h)
+    pt = ctl.PathTracer(0)
+    pt.upload_scene(d)
+    pt.generate_samples(3)
+    n = pt.camera_rays()
+    px, py, valid = work_order_pixels(w, h)
+    assert n == px.size
+    rays = torch.zeros((n, 8), dtype=torch.float32, device=dev)
+    assert pt.camera_rays(rays.data_ptr(), n) == n
+    hits = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+    pt.intersect_buffers(n, rays.data_ptr(), hits.data_ptr())
+    torch.cuda.synchronize()
+    got = rays.cpu().numpy()
+    want = np.zeros((w * h, 8), np.float32)
+    orc.oracle_camera_rays(C.byref(d), 3, oracle.ptr(want))
+    lin = py[valid] * w + px[valid]
+    assert np.array_equal(got[valid].view(np.uint32), want[lin].view(np.uint32))
+    assert np.all(got[~valid][:, 7] == 0.0)
+    wh = oracle_intersect(orc, d, want, any_hit=False)
+    gh = hits.cpu().numpy()
+    assert (wh[:, 2] >= 0).sum() > 1000
+    assert np.array_equal(gh[valid], wh[lin])
+    pt.close()
+
+
+def test_intersect_large_batch_refill(ctl, orc, tracer, dev):
+    """More rays than resident lanes: every lane refills from the work cursor."""
+    d = scene(ctl, 2, 0.05, 64, 64)
+    rays = random_rays(d, 1_500_000, seed=11)
+    rays[::7, 3] = np.float32(d.ray_eps)
+    for any_hit in (False, True):
+        want = oracle_intersect(orc, d, rays, any_hit=any_hit)
+        got = gpu_intersect(tracer, d, rays, any_hit, dev)
+        if any_hit:
+            assert np.array_equal(got[:, 2] >= 0, want[:, 2] >= 0)
+        else:
+            assert np.array_equal(got, want)
+
+
+def test_last_pass_ms(ctl, dev):
+    d = scene(ctl, 2, 0.05, 128, 128)
+    pt = ctl.PathTracer(0)
+    pt.upload_scene(d)
+    fb = torch.zeros((128 * 128, 7), dtype=torch.float32, device=dev)
+    pt.do_pass(fb.data_ptr(), 0)
+    ms = pt.last_pass_ms()
+    assert 0.0 < ms < 10_000.0
+    pt.close()
