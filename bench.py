@@ -136,6 +136,7 @@ def main():
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import cudatracerlib_amd as ctl
+    from cudatracerlib_amd import shard
 
     if world > 1:
         dist.init_process_group(a.backend)
@@ -177,8 +178,8 @@ def main():
     kev = []
 
     def step(s, timed=False):
-        for k in range(world):
-            pt.generate_samples(pass_base + s * world + k, sptr)
+        for pidx in shard.step_pass_indices(s, world, pass_base):
+            pt.generate_samples(pidx, sptr)
             if timed:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
@@ -207,7 +208,7 @@ def main():
         step(s, timed=True)
     ev1.record(stream)
     if world > 1:
-        dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)   # RCCL over xGMI
+        shard.reduce_framebuffer(fb, dist)   # RCCL over xGMI
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

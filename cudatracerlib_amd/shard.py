@@ -1,0 +1,33 @@
+"""Image-tile sharding across GPUs.
+
+Rank r of N owns the 64x64 tiles with ``tile_id % N == r`` (interleaved for
+load balance; tile space of IBlockSampler.h:100-108).  A *step* renders N
+progressive passes on every rank, so per-GPU work is fixed (weak scaling) and
+after K steps the job holds the N*K-pass image.  Pixel i always uses sampler
+index y*w+x and the same pass index, so summing the disjoint per-rank
+PixelData framebuffers with one reduce gives exactly the 1-GPU image.
+"""
+
+
+def shard_params(params, world, rank):
+    """Point a ctl_pt_params (PTParams) at this rank's tiles."""
+    params.num_ranks = int(world)
+    params.rank = int(rank)
+    return params
+
+
+def step_pass_indices(step, world, base=0):
+    """Sampler pass indices rendered by every rank in `step`."""
+    return [base + step * world + k for k in range(world)]
+
+
+def owned_tiles(width, height, tile, world, rank):
+    tiles = (-(-width // tile)) * (-(-height // tile))
+    return [t for t in range(tiles) if t % world == rank]
+
+
+def reduce_framebuffer(fb, dist, dst=0):
+    """Sum the per-rank PixelData framebuffers to `dst` (RCCL over xGMI on GPUs,
+    gloo on CPU).  Ownership is disjoint, so the fp32 sum is exact."""
+    dist.reduce(fb, dst=dst, op=dist.ReduceOp.SUM)
+    return fb

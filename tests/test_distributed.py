@@ -1,0 +1,77 @@
+"""world_size-2 gloo run of the tile-shard + framebuffer-reduce path on CPU.
+Each rank renders its tiles (oracle as the renderer: no GPU here) for the
+pass indices shard.step_pass_indices gives it; the reduced image must equal
+the single-rank render of the same passes bit for bit."""
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+W, H, STEPS = 160, 96, 2
+
+
+def _render(desc, params, passes):
+    import oracle
+    O = oracle.load()
+    fb = np.zeros((W * H, 7), np.float32)
+    for p in passes:
+        O.oracle_render_pass(C.byref(desc), C.byref(params), p, oracle.ptr(fb), 0, 2, 1, None)
+    return fb
+
+
+def _scene():
+    import cudatracerlib_amd as ctl
+    hs = ctl.HostScene().generate(2, 0.05, W, H)
+    return hs, hs.compile(threads=2)
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import cudatracerlib_amd as ctl
+        from cudatracerlib_amd import shard
+        hs, desc = _scene()
+        params = shard.shard_params(ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0), world, rank)
+        passes = [p for s in range(STEPS) for p in shard.step_pass_indices(s, world)]
+        fb = torch.from_numpy(_render(desc, params, passes))
+        shard.reduce_framebuffer(fb, dist)
+        if rank == 0:
+            np.save(out, fb.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_shard_reduce_equals_single_rank(tmp_path):
+    import cudatracerlib_amd as ctl
+    from cudatracerlib_amd import shard
+    world = 2
+    out = str(tmp_path / "fb.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    hs, desc = _scene()
+    params = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
+    want = _render(desc, params, [p for s in range(STEPS) for p in shard.step_pass_indices(s, world)])
+    assert want[:, 6].sum() > 0.9 * W * H * STEPS * world
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_owned_tiles_partition():
+    from cudatracerlib_amd import shard
+    tiles = [shard.owned_tiles(1920, 1080, 64, 8, r) for r in range(8)]
+    flat = sorted(t for ts in tiles for t in ts)
+    assert flat == list(range(30 * 17))
+    assert max(map(len, tiles)) - min(map(len, tiles)) <= 1
