@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libctl_trace.so")
+# CTL_LIB overrides the library path (variant builds for measurements).
+LIB_PATH = os.environ.get("CTL_LIB") or os.path.join(_HERE, "_lib", "libctl_trace.so")
 
 CTL_OK = 0
 CTL_SCENE_HALF_HOST_QUIRK = 1

@@ -42,6 +42,12 @@ static_assert(sizeof(ctl_hit) == 16, "traversalResult is 16 B");
 static_assert(sizeof(ctl_pixel) == 28, "PixelData is 28 B");
 static_assert(sizeof(ctl_light_tri) == 64, "ShapeSet::triData is 64 B");
 
+#ifndef CTL_PERSIST_WAVES
+#define CTL_PERSIST_WAVES 6   // waves/SIMD for the persistent path kernel: measured best on C3
+                              // (4: 732, 5: 758, 6: 789, 7: 781, 8: 768 Mrays/s); its spills
+                              // save path state around the traversal, outside the traversal loops
+#endif
+
 namespace {
 
 // Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
@@ -190,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
 // Pixels are independent (own sampler index, single owner in the framebuffer)
 // so the framebuffer is bit-identical to path_kernel's.
 template <bool STATS, bool SINGLE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? 4 : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? CTL_PERSIST_WAVES : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
                                                                  const float2* s2, ctl_pixel* fb, uint64_t items,
                                                                  uint32_t* cursor, unsigned long long* counters) {
     CTL_LANE_STACK(st);
