@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--schedule", default="persistent", choices=["persistent", "megakernel", "wavefront"])
+    ap.add_argument("--split-alpha", type=float, default=None, help="BVH reference splitting (default: library's)")
+    ap.add_argument("--split-depth", type=int, default=8)
+    ap.add_argument("--bvh", default="wide", choices=["wide", "binary"],
+                    help="device traversal: 4-wide collapsed BVH, or the reference's binary order")
     return ap.parse_args()
 
 
@@ -148,7 +152,11 @@ def main():
 
     t0 = time.perf_counter()
     hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
+    if a.split_alpha is not None:
+        hs.set_bvh_params(a.split_alpha, a.split_depth)
     desc = hs.compile(threads=threads)
+    if a.bvh == "binary":
+        desc.flags |= ctl.CTL_SCENE_BINARY_BVH
     t_build = time.perf_counter() - t0
     log(f"[rank {rank}] scene config {a.config}: {desc.n_tri_data} tris, {desc.n_bvh_nodes} BVH nodes, "
         f"built in {t_build:.1f}s with {threads} threads")
@@ -263,6 +271,8 @@ def main():
                             f"{a.shadow_any_hit}",
                 "triangles": int(desc.n_tri_data),
                 "bvh_inner_nodes": int(desc.n_bvh_nodes),
+                "bvh_refs": int(desc.n_tri_indices),
+                "bvh": a.bvh,
                 "resolution": [W, H],
                 "spp": passes,
                 "tile": 64,

@@ -22,11 +22,11 @@ missing or fails.
 import ctypes as C
 
 from . import _abi
-from ._abi import (PTParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK,
+from ._abi import (PTParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK, CTL_SCENE_BINARY_BVH,
                    CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT)
 
 __all__ = ["HostScene", "Tracer", "PathTracer", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
-           "CTL_SCENE_HALF_HOST_QUIRK", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "lib", "diffuse_material"]
+           "CTL_SCENE_HALF_HOST_QUIRK", "CTL_SCENE_BINARY_BVH", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "lib", "diffuse_material"]
 
 
 def lib():
@@ -118,6 +118,12 @@ class HostScene:
 
     def set_flags(self, flags):
         _check(self._L.ctl_host_scene_set_flags(self._h, flags), None, "set_flags")
+
+    def set_bvh_params(self, split_alpha=0.5, split_depth=8):
+        """Reference splitting of large triangles before the BVH build (0 disables)."""
+        _check(self._L.ctl_host_scene_set_bvh_params(self._h, float(split_alpha), int(split_depth)), None,
+               "set_bvh_params")
+        return self
 
     def compile(self, threads=0):
         d = SceneDesc()

@@ -12,6 +12,7 @@ LIB_PATH = os.environ.get("CTL_LIB") or os.path.join(_HERE, "_lib", "libctl_trac
 
 CTL_OK = 0
 CTL_SCENE_HALF_HOST_QUIRK = 1
+CTL_SCENE_BINARY_BVH = 2
 CTL_BSDF_DIFFUSE = 1
 CTL_EDIFFUSE_REFLECTION = 0x2
 CTL_MAX_NUM_LIGHTS = 16
@@ -140,6 +141,7 @@ SYMBOLS = [
     ("ctl_host_scene_set_camera", C.c_int32, [_vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
                                               C.c_uint32, C.c_uint32]),
     ("ctl_host_scene_set_flags", C.c_int32, [_vp, C.c_uint32]),
+    ("ctl_host_scene_set_bvh_params", C.c_int32, [_vp, C.c_float, C.c_uint32]),
     ("ctl_host_scene_compile", C.c_int32, [_vp, C.c_uint32, C.POINTER(SceneDesc)]),
     ("ctl_host_last_error", C.c_char_p, []),
     ("ctl_host_scene_generate", C.c_int32, [_vp, C.c_int32, C.c_double, C.c_uint32, C.c_uint32]),

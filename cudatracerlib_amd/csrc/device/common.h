@@ -292,6 +292,7 @@ struct ctl_ctx {
     uint32_t* d_cursors = nullptr;              // work cursors: [0] batch intersect [1] path pass
     hipEvent_t pass_ev[2] = {nullptr, nullptr}; // bracket the last render pass (ctl_last_pass_ms)
     bool pass_timed = false;
+    size_t wide_nodes = 0;
     uint32_t* d_powers = nullptr;               // XORWOW step powers for sampler_kernel
     ctl::WfState wf{};
     std::vector<void*> wf_allocs;

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../../include/ctl_trace.h"
+#include "../host/bvh_wide.h"
 #include "common.h"
 
 namespace ctl {
@@ -52,7 +53,7 @@ namespace {
 
 // Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
 // traversals inline in the bounce, as the reference's pathKernel2 runs it.
-template <bool STATS, bool SINGLE>
+template <bool STATS, bool SINGLE, bool WIDE>
 struct PathCtx {
     const DevScene& S;
     const PathParams& P;
@@ -69,7 +70,7 @@ struct PathCtx {
         HitRec r2;   // traceRay (TraceHelper.cu:174-180)
         r2.t = FLT_MAX; r2.tri = 0xffffffffu; r2.node = 0xffffffffu; r2.u = r2.v = 0.0f;
         rays++;
-        ok &= trace_one<0, STATS, SINGLE>(S, v.rori, v.rdir, 0.0f, S.ray_eps, r2, st, &ts);
+        ok &= trace_one<0, STATS, SINGLE, WIDE>(S, v.rori, v.rdir, 0.0f, S.ray_eps, r2, st, &ts);
         if (r2.tri == 0xffffffffu) {
             v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);   // no environment map
             return false;
@@ -81,8 +82,8 @@ struct PathCtx {
             HitRec h;
             h.t = any ? sh.dist - S.ray_eps : FLT_MAX; h.tri = 0xffffffffu; h.node = 0xffffffffu; h.u = h.v = 0.0f;
             rays++;
-            if (any) ok &= trace_one<1, STATS, SINGLE>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
-            else ok &= trace_one<0, STATS, SINGLE>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            if (any) ok &= trace_one<1, STATS, SINGLE, WIDE>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            else ok &= trace_one<0, STATS, SINGLE, WIDE>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
             if (!shadow_occluded(S, any, h, sh.dist)) v.cl = v.cl + sh.add;
         }
         return cont;
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict
 }
 
 // One path per thread (the reference's pathKernel2 launch shape).
-template <bool STATS, bool SINGLE>
+template <bool STATS, bool SINGLE, bool WIDE>
 __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
                                                       ctl_pixel* fb, unsigned long long* counters) {
     CTL_LANE_STACK(st);
@@ -148,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
     if (work_pixel(P, g, px, py)) {
         const uint32_t idx = py * P.width + px;   // TracerBase::getPixelIndex (Tracer.h:89-97)
         SamplerDev rng{s1, s2, P.nseq, P.len, idx % P.nseq, (idx / P.nseq) % P.nseq, 0, 0};
-        PathCtx<STATS, SINGLE> C{S, P, rng, st, 0, TraceStats{0, 0, 0}, true, PathVars{}};
+        PathCtx<STATS, SINGLE, WIDE> C{S, P, rng, st, 0, TraceStats{0, 0, 0}, true, PathVars{}};
         f3 o, dw;
         const f2 pX = primary_ray(S, rng, px, py, o, dw);
         C.v.begin(pX, o, dw);
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
 //    pending ray are loop-carried, keeping the register peak low.
 // Pixels are independent (own sampler index, single owner in the framebuffer)
 // so the framebuffer is bit-identical to path_kernel's.
-template <bool STATS, bool SINGLE>
+template <bool STATS, bool SINGLE, bool WIDE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? CTL_PERSIST_WAVES : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
                                                                  const float2* s2, ctl_pixel* fb, uint64_t items,
                                                                  uint32_t* cursor, unsigned long long* counters) {
@@ -248,7 +249,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             const f3 d = shadowPhase ? sh.d : v.rdir;
             rays++;
             if (S.n_nodes != 0) {
-                Traverser<2, STATS, SINGLE> T;
+                Traverser<2, STATS, SINGLE, WIDE> T;
                 T.anyhit = shadowPhase && shadowAny;
                 T.init(S, v.rori, d, 0.0f, S.ray_eps, h.t, st, &ts);
                 while (!T.done) T.round(S, st, &ts);
@@ -288,12 +289,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
 // grid; lanes whose ray finished take the next ray from a wave-aggregated
 // atomic cursor between traversal rounds (the reference fetches per warp per
 // batch of 32 rays, :379-399), so waves stay full on incoherent rays.
-template <bool ANY, bool STATS, bool SINGLE>
+template <bool ANY, bool STATS, bool SINGLE, bool WIDE>
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            uint32_t* cursor, unsigned long long* counters) {
     CTL_LANE_STACK(st);
     TraceStats ts{0, 0, 0};
-    Traverser<ANY ? 1 : 0, STATS, SINGLE> T;
+    Traverser<ANY ? 1 : 0, STATS, SINGLE, WIDE> T;
     T.done = true;
     bool haveRay = false, exhausted = false, ovf = false;
     int64_t ray = 0;
@@ -520,6 +521,35 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
         lut[code] = make_float4(v.x, v.y, v.z, 0.0f);
     }
     UP(lut.data(), lut.size(), &S.normal_lut);
+    // 4-wide trees for the device traversal (host/bvh_wide.h), unless the
+    // caller asks for the reference's binary visit order
+    const bool wide = (d->flags & CTL_SCENE_BINARY_BVH) == 0 && d->n_bvh_nodes > 0;
+    if (wide) {
+        std::vector<WideNode> wn, sw;
+        std::vector<uint32_t> wbase(d->n_meshes, 0);
+        try {
+            for (uint32_t m = 0; m < d->n_meshes; m++) {
+                const size_t first = d->meshes[m].bvh_node_offset / 4;
+                if (first >= d->n_bvh_nodes) throw std::runtime_error("mesh BVH offset out of range");
+                wbase[m] = (uint32_t)wn.size();
+                collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn);
+            }
+            if (d->n_nodes > 0 && d->scene_start_node >= 0)
+                collapse_wide(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, sw);
+        } catch (const std::exception& e) {
+            free_scene(c);
+            c->err = std::string("scene_upload: ") + e.what();
+            return CTL_ERR_INVALID;
+        }
+        const WideNode* wd; UP(wn.data(), wn.size(), &wd);
+        const WideNode* swd; UP(sw.data(), sw.size(), &swd);
+        UP(wbase.data(), wbase.size(), &S.mesh_wbase);
+        S.wbvh = reinterpret_cast<const float4*>(wd);
+        S.scene_wbvh = reinterpret_cast<const float4*>(swd);
+        S.wide = 1;
+        S.tie_min = 1;
+        c->wide_nodes = wn.size();
+    }
 #undef UP
     S.bvh = reinterpret_cast<const float4*>(bvh);
     S.woop = reinterpret_cast<const float4*>(woop);
@@ -543,6 +573,12 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
         S.s_tri_base = M.bvh_triangle_offset;
         S.s_idx_base = M.bvh_indices_offset;
         S.s_tri_offset = M.triangle_offset;
+        if (S.wide) {
+            // host copy of the wide base of that mesh
+            uint32_t mi = d->nodes[node].mesh_index, base = 0;
+            CTL_HIP(c, hipMemcpy(&base, S.mesh_wbase + mi, 4, hipMemcpyDeviceToHost));
+            S.s_wnode_base = base;
+        }
     }
     c->scene = S;
     c->half_quirk = (d->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
@@ -598,14 +634,21 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
     CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(uint32_t), s));
     const bool single = c->scene.single != 0;
     const uint64_t want = ((uint64_t)n + kBlock - 1) / kBlock;
-#define IK(AN, ST, SG)                                                                                           \
+#define IK(AN, ST, SG, WD)                                                                                       \
     do {                                                                                                         \
         static int nb = 0;                                                                                       \
-        if (!nb) nb = resident_blocks(c, intersect_kernel<AN, ST, SG>, kStackLdsBytes);                          \
-        hipLaunchKernelGGL((intersect_kernel<AN, ST, SG>), dim3((unsigned)std::min<uint64_t>(nb, want)),         \
+        if (!nb) nb = resident_blocks(c, intersect_kernel<AN, ST, SG, WD>, kStackLdsBytes);                      \
+        hipLaunchKernelGGL((intersect_kernel<AN, ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)),     \
                            dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, cursor, c->d_counters);     \
     } while (0)
-#define IK2(AN, ST) do { if (single) IK(AN, ST, true); else IK(AN, ST, false); } while (0)
+    // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
+    const bool wide = c->scene.wide != 0 && !stats;
+#define IK2(AN, ST)                                                       \
+    do {                                                                  \
+        if (ST) { if (single) IK(AN, true, true, false); else IK(AN, true, false, false); } \
+        else if (wide) { if (single) IK(AN, false, true, true); else IK(AN, false, false, true); } \
+        else { if (single) IK(AN, false, true, false); else IK(AN, false, false, false); } \
+    } while (0)
     if (stats) { if (any_hit) IK2(true, true); else IK2(false, true); }
     else { if (any_hit) IK2(true, false); else IK2(false, false); }
 #undef IK2
@@ -676,26 +719,30 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
                                   hipStream_t s, uint64_t threads, dim3 grid, const float* s1, const float2* s2) {
     if (p->flags & CTL_PT_WAVEFRONT) return (ctl_status)ctl::wavefront_pass(c, P, fb, stats, s);
     const bool single = c->scene.single != 0;
+    // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
+    const bool wide = c->scene.wide != 0 && !stats;
     if (!(p->flags & CTL_PT_MEGAKERNEL)) {
         uint32_t* cursor = c->d_cursors + 1;
         CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(uint32_t), s));
         const uint64_t want = (threads + kBlock - 1) / kBlock;
-#define PK(ST, SG)                                                                                               \
+#define PK(ST, SG, WD)                                                                                           \
         do {                                                                                                     \
             static int nb = 0;                                                                                   \
-            if (!nb) nb = resident_blocks(c, path_kernel_persistent<ST, SG>, kStackLdsBytes);                    \
-            hipLaunchKernelGGL((path_kernel_persistent<ST, SG>), dim3((unsigned)std::min<uint64_t>(nb, want)),   \
+            if (!nb) nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD>, kStackLdsBytes);                \
+            hipLaunchKernelGGL((path_kernel_persistent<ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)), \
                                dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, fb, threads, cursor,        \
                                c->d_counters);                                                                   \
         } while (0)
-        if (stats) { if (single) PK(true, true); else PK(true, false); }
-        else { if (single) PK(false, true); else PK(false, false); }
+        if (stats) { if (single) PK(true, true, false); else PK(true, false, false); }
+        else if (wide) { if (single) PK(false, true, true); else PK(false, false, true); }
+        else { if (single) PK(false, true, false); else PK(false, false, false); }
 #undef PK
     } else {
-#define MK(ST, SG) hipLaunchKernelGGL((path_kernel<ST, SG>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, \
-                                      fb, c->d_counters)
-        if (stats) { if (single) MK(true, true); else MK(true, false); }
-        else { if (single) MK(false, true); else MK(false, false); }
+#define MK(ST, SG, WD) hipLaunchKernelGGL((path_kernel<ST, SG, WD>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, \
+                                          s2, fb, c->d_counters)
+        if (stats) { if (single) MK(true, true, false); else MK(true, false, false); }
+        else if (wide) { if (single) MK(false, true, true); else MK(false, false, true); }
+        else { if (single) MK(false, true, false); else MK(false, false, false); }
 #undef MK
     }
     CTL_HIP(c, hipGetLastError());

@@ -61,6 +61,13 @@ struct DevScene {
     // single-instance fast path (start_node < 0): mesh of node ~start_node
     uint32_t single;
     uint32_t s_node_base, s_tri_base, s_idx_base, s_tri_offset;
+    // 4-wide BVH collapsed on upload (host/bvh_wide.h), traversed when WIDE
+    const float4* wbvh;          // mesh wide nodes, 8 float4 (128 B) each
+    const float4* scene_wbvh;    // instance-level wide nodes
+    const uint32_t* mesh_wbase;  // first wide node of each mesh
+    uint32_t wide;               // wide trees present (scene flag CTL_SCENE_BINARY_BVH clear)
+    uint32_t tie_min;            // exact-t ties -> lowest (triangle, node) instead of first found
+    uint32_t s_wnode_base;
 };
 
 struct TraceStats { uint32_t nodes, tris, inst; };
@@ -148,7 +155,7 @@ __device__ __forceinline__ void xform_rows(const float4* M, f3 p, f3 d, f3& po, 
 
 // Closest (ANY=0) or any (ANY=1) hit with tri_tmin < t < h.t, or chosen per
 // ray by the `anyhit` member (ANY=2); box spans start at span_tmin.
-template <int ANY, bool STATS, bool SINGLE>
+template <int ANY, bool STATS, bool SINGLE, bool WIDE = false>
 struct Traverser {
     RayLocal cur;
     RayLocal world;   // unused when SINGLE
@@ -180,7 +187,8 @@ struct Traverser {
             // start_node < 0: TracerayTemplate calls the instance callback directly (BVHTraversal.h:130-131)
             if (STATS) stats->inst++;
             enter_instance(S, ~(uint32_t)S.start_node, o, d);
-            nodeBase = S.s_node_base; triBase = S.s_tri_base; idxBase = S.s_idx_base; triOffset = S.s_tri_offset;
+            nodeBase = WIDE ? S.s_wnode_base : S.s_node_base;
+            triBase = S.s_tri_base; idxBase = S.s_idx_base; triOffset = S.s_tri_offset;
             level = 1;
             nodeAddr = 0;
             leafAddr = 0;
@@ -190,7 +198,7 @@ struct Traverser {
             level = 0;
             nodeBase = triBase = idxBase = triOffset = instIdx = 0;
             if (S.start_node < 0) { leafAddr = S.start_node; nodeAddr = CTL_SENTINEL; }
-            else { leafAddr = 0; nodeAddr = S.start_node; }
+            else { leafAddr = 0; nodeAddr = WIDE ? 0 : S.start_node; }
         }
     }
 
@@ -205,7 +213,9 @@ struct Traverser {
             float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
             float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
             float t = Oz * invDz;
-            if (t > tri_tmin && t < h.t) {
+            // exact-t tie under tie_min: lower (triangle, node) wins, in any
+            // visit order; a hit at exactly the initial tmax stays rejected
+            if (t > tri_tmin && (t < h.t || (S.tie_min && t == h.t && h.tri != 0xffffffffu))) {
                 float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
                 float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
                 float u = Ox + t * Dx;
@@ -213,9 +223,11 @@ struct Traverser {
                     float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
                     float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
                     float v = Oy + t * Dy;
-                    if (v >= 0.0f && u + v <= 1.0f) {
+                    const uint32_t gtri = (index >> 1) + triOffset;
+                    if (v >= 0.0f && u + v <= 1.0f &&
+                        (t < h.t || gtri < h.tri || (gtri == h.tri && instIdx < h.node))) {
                         h.node = instIdx;
-                        h.tri = (index >> 1) + triOffset;
+                        h.tri = gtri;
                         h.u = u;
                         h.v = v;
                         h.t = t;
@@ -227,9 +239,59 @@ struct Traverser {
         }
     }
 
-    // One round: inner nodes until every active lane holds a postponed leaf,
-    // then the postponed leaves (and the level transitions).
-    __device__ __forceinline__ void round(const DevScene& S, LaneStack& st, TraceStats* stats) {
+    // 4-wide inner-node loop: the four child slabs of a 128-B node, hit
+    // children ordered near-first by a 5-comparator sorting network on their
+    // entry distance (non-negative floats compare as ints), the nearest taken,
+    // the others pushed far-to-near.  Same postponed-leaf / wave-exit rule.
+    __device__ __forceinline__ void inner_wide(const DevScene& S, LaneStack& st, TraceStats* stats) {
+        const float4* nodes = (SINGLE || level) ? S.wbvh : S.scene_wbvh;
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
+            const float4* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 8u;
+            const float4 lox = n[0], hix = n[1], loy = n[2], hiy = n[3], loz = n[4], hiz = n[5];
+            int4 ch = reinterpret_cast<const int4*>(n)[6];
+            asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
+            if (STATS) stats->nodes++;
+            int k0, k1, k2, k3, c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+#define CTL_WIDE_CHILD(K, C, comp)                                                                   \
+            {                                                                                        \
+                const float ax = lox.comp * cur.idx - cur.oodx, bx = hix.comp * cur.idx - cur.oodx;   \
+                const float ay = loy.comp * cur.idy - cur.oody, by = hiy.comp * cur.idy - cur.oody;   \
+                const float az = loz.comp * cur.idz - cur.oodz, bz = hiz.comp * cur.idz - cur.oodz;   \
+                const float cmin = span_begin(ax, bx, ay, by, az, bz, span_tmin);                    \
+                const float cmax = span_end(ax, bx, ay, by, az, bz, h.t);                            \
+                K = (cmax >= cmin && C != CTL_SENTINEL) ? __float_as_int(cmin) : 0x7fffffff;          \
+            }
+            CTL_WIDE_CHILD(k0, c0, x)
+            CTL_WIDE_CHILD(k1, c1, y)
+            CTL_WIDE_CHILD(k2, c2, z)
+            CTL_WIDE_CHILD(k3, c3, w)
+#undef CTL_WIDE_CHILD
+#define CTL_CX(KA, CA, KB, CB)                      \
+            {                                       \
+                const bool sw = KB < KA;            \
+                const int tk = sw ? KB : KA, tc = sw ? CB : CA; \
+                KB = sw ? KA : KB; CB = sw ? CA : CB; \
+                KA = tk; CA = tc;                   \
+            }
+            CTL_CX(k0, c0, k1, c1)
+            CTL_CX(k2, c2, k3, c3)
+            CTL_CX(k0, c0, k2, c2)
+            CTL_CX(k1, c1, k3, c3)
+            CTL_CX(k1, c1, k2, c2)
+#undef CTL_CX
+            if (k3 != 0x7fffffff) st.push(c3);
+            if (k2 != 0x7fffffff) st.push(c2);
+            if (k1 != 0x7fffffff) st.push(c1);
+            nodeAddr = (k0 != 0x7fffffff) ? c0 : st.pop();
+            if (nodeAddr < 0 && leafAddr >= 0) {
+                leafAddr = nodeAddr;
+                nodeAddr = st.pop();
+            }
+            if (!__any(leafAddr >= 0)) break;
+        }
+    }
+
+    __device__ __forceinline__ void inner_binary(const DevScene& S, LaneStack& st, TraceStats* stats) {
         const float4* nodes = (SINGLE || level) ? S.bvh : S.scene_bvh;
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
             const float4* n = nodes + nodeBase + nodeAddr;
@@ -276,6 +338,13 @@ struct Traverser {
             }
             if (!__any(leafAddr >= 0)) break;
         }
+    }
+
+    // One round: inner nodes until every active lane holds a postponed leaf,
+    // then the postponed leaves (and the level transitions).
+    __device__ __forceinline__ void round(const DevScene& S, LaneStack& st, TraceStats* stats) {
+        if (WIDE) inner_wide(S, st, stats);
+        else inner_binary(S, st, stats);
         resumeLeaves = false;
         while (leafAddr < 0) {
             if (SINGLE || level == 1) {
@@ -292,7 +361,7 @@ struct Traverser {
                     if (STATS) stats->inst++;
                     const ctl_node& N = S.nodes[inst];
                     const ctl_kernel_mesh& M = S.meshes[N.mesh_index];
-                    nodeBase = M.bvh_node_offset;
+                    nodeBase = WIDE ? S.mesh_wbase[N.mesh_index] : M.bvh_node_offset;
                     triBase = M.bvh_triangle_offset;
                     idxBase = M.bvh_indices_offset;
                     triOffset = M.triangle_offset;
@@ -329,10 +398,10 @@ struct Traverser {
 };
 
 // Whole traversal of one ray (megakernel, batch kernel).
-template <int ANY, bool STATS, bool SINGLE>
+template <int ANY, bool STATS, bool SINGLE, bool WIDE = false>
 __device__ __forceinline__ bool trace_one(const DevScene& S, f3 ori, f3 dir, float span_tmin, float tri_tmin,
                                           HitRec& h, LaneStack& st, TraceStats* stats) {
-    Traverser<ANY, STATS, SINGLE> T;
+    Traverser<ANY, STATS, SINGLE, WIDE> T;
     T.init(S, ori, dir, span_tmin, tri_tmin, h.t, st, stats);
     while (!T.done) T.round(S, st, stats);
     h = T.h;

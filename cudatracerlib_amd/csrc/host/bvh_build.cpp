@@ -251,7 +251,7 @@ struct Emitter {
 
 }  // namespace
 
-void build_bvh(const Box* boxes, uint32_t n, const BvhBuildParams& p, BvhOutput& out) {
+void build_bvh(const Box* boxes, uint32_t n, const BvhBuildParams& p, BvhOutput& out, const uint32_t* ids) {
     out = BvhOutput{};
     Builder B(p);
     B.max_threads = (int)(p.threads ? p.threads : std::max(1u, std::thread::hardware_concurrency()));
@@ -264,7 +264,7 @@ void build_bvh(const Box* boxes, uint32_t n, const BvhBuildParams& p, BvhOutput&
         Ref r;
         std::memcpy(r.lo, bx.lo, 12);
         std::memcpy(r.hi, bx.hi, 12);
-        r.id = i;
+        r.id = ids ? ids[i] : i;
         B.refs.push_back(r);
     }
     uint32_t m = (uint32_t)B.refs.size();

@@ -31,9 +31,11 @@ struct BvhOutput {
     Box root_box;
 };
 
-// Builds over object boxes (`boxes[i]`), `n` objects.  Degenerate boxes
-// (min extent < 0 or a line/point: sum(size)==max(size)) are dropped like the
-// reference's "Remove degenerates" step (SplitBVHBuilder.cpp:296-303).
-void build_bvh(const Box* boxes, uint32_t n, const BvhBuildParams& p, BvhOutput& out);
+// Builds over `n` references: box `boxes[i]` of object `ids[i]` (ids == NULL:
+// object i).  An object may have several references (split triangles); leaf
+// entries carry the object id.  Degenerate boxes (min extent < 0 or a
+// line/point: sum(size)==max(size)) are dropped like the reference's "Remove
+// degenerates" step (SplitBVHBuilder.cpp:296-303).
+void build_bvh(const Box* boxes, uint32_t n, const BvhBuildParams& p, BvhOutput& out, const uint32_t* ids = nullptr);
 
 }  // namespace ctl

@@ -1,0 +1,88 @@
+// bvh_wide.cpp — see bvh_wide.h.
+#include "bvh_wide.h"
+
+#include <cstring>
+#include <stdexcept>
+
+namespace ctl {
+namespace {
+
+const int32_t kSentinel = 0x76543210;
+
+struct Kid {
+    float lo[3], hi[3];
+    int32_t v;
+};
+
+inline bool is_inner(int32_t v) { return v >= 0 && v != kSentinel; }
+
+inline float kid_area(const Kid& k) {
+    float ax = k.hi[0] - k.lo[0], ay = k.hi[1] - k.lo[1], az = k.hi[2] - k.lo[2];
+    return 2.0f * (ax * ay + ax * az + ay * az);
+}
+
+// Children of binary node `idx` with the boxes stored in it (BVHNodeData::getLeft/getRight).
+void binary_kids(const ctl_bvh_node& n, Kid& a, Kid& b) {
+    a.lo[0] = n.v[0]; a.hi[0] = n.v[1]; a.lo[1] = n.v[2]; a.hi[1] = n.v[3]; a.lo[2] = n.v[8]; a.hi[2] = n.v[9];
+    b.lo[0] = n.v[4]; b.hi[0] = n.v[5]; b.lo[1] = n.v[6]; b.hi[1] = n.v[7]; b.lo[2] = n.v[10]; b.hi[2] = n.v[11];
+    std::memcpy(&a.v, &n.v[12], 4);
+    std::memcpy(&b.v, &n.v[13], 4);
+}
+
+struct Collapser {
+    const ctl_bvh_node* nodes;
+    size_t n_nodes;
+    std::vector<WideNode>& out;
+    size_t base;
+
+    const ctl_bvh_node& node_of(int32_t v) const {
+        size_t i = (size_t)v / 4;
+        if ((v & 3) != 0 || i >= n_nodes) throw std::runtime_error("wide BVH: bad child offset");
+        return nodes[i];
+    }
+
+    int32_t emit(int32_t v, int depth) {
+        if (depth > 256) throw std::runtime_error("wide BVH: tree too deep");
+        Kid k[4];
+        int nk = 2;
+        binary_kids(node_of(v), k[0], k[1]);
+        while (nk < 4) {
+            int best = -1;
+            float bestArea = -1.0f;
+            for (int i = 0; i < nk; i++)
+                if (is_inner(k[i].v) && kid_area(k[i]) > bestArea) { bestArea = kid_area(k[i]); best = i; }
+            if (best < 0) break;
+            Kid a, b;
+            binary_kids(node_of(k[best].v), a, b);
+            k[best] = a;
+            k[nk++] = b;
+        }
+        const size_t me = out.size();
+        out.push_back(WideNode{});
+        int32_t child[4];
+        for (int i = 0; i < 4; i++) {
+            if (i >= nk) { child[i] = kSentinel; continue; }
+            child[i] = is_inner(k[i].v) ? emit(k[i].v, depth + 1) : k[i].v;
+        }
+        WideNode& w = out[me];
+        for (int i = 0; i < 4; i++) {
+            const bool used = i < nk;
+            w.lo_x[i] = used ? k[i].lo[0] : 0.0f; w.hi_x[i] = used ? k[i].hi[0] : 0.0f;
+            w.lo_y[i] = used ? k[i].lo[1] : 0.0f; w.hi_y[i] = used ? k[i].hi[1] : 0.0f;
+            w.lo_z[i] = used ? k[i].lo[2] : 0.0f; w.hi_z[i] = used ? k[i].hi[2] : 0.0f;
+            w.child[i] = child[i];
+            w.pad[i] = 0;
+        }
+        return (int32_t)(me - base);
+    }
+};
+
+}  // namespace
+
+int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out) {
+    if (!is_inner(root_value) || n_nodes == 0) throw std::runtime_error("wide BVH: root is not an inner node");
+    Collapser c{nodes, n_nodes, out, out.size()};
+    return c.emit(root_value, 0);
+}
+
+}  // namespace ctl

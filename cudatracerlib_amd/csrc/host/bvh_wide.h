@@ -1,0 +1,37 @@
+// bvh_wide.h — 4-wide BVH collapsed from the reference's binary BVHNodeData.
+//
+// The boundary takes the reference layout (two children per 64-B node,
+// SplitBVHBuilder.cpp:163-203); on upload each binary tree is collapsed into
+// 128-B four-child nodes for the device traversal:
+//
+//   float4 lo_x, hi_x, lo_y, hi_y, lo_z, hi_z   child boxes, one child per lane of the float4
+//   int4   child                                >= 0: node index in this tree,
+//                                               < 0: ~first leaf entry (unchanged reference
+//                                                    TriIntersectorData2 ranges),
+//                                               0x76543210: empty slot / reference sentinel
+//   int4   pad
+//
+// A binary node becomes a wide node by repeatedly opening the inner child of
+// largest surface area until four children are reached (or only leaves are
+// left).  Leaves, leaf entries and Woop data are shared with the binary tree.
+#pragma once
+#include <cstdint>
+#include <vector>
+#include "../../../include/ctl_trace.h"
+
+namespace ctl {
+
+struct alignas(16) WideNode {
+    float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
+    int32_t child[4];
+    int32_t pad[4];
+};
+static_assert(sizeof(WideNode) == 128, "wide node is 128 B");
+
+// Collapses the binary tree rooted at `root_value` (a BVHNodeData child value:
+// >= 0 inner node float4 offset, i.e. 4 x node index) of `nodes` and appends
+// the wide nodes to `out`.  Returns the root's index relative to the first
+// node appended; child indices are relative to that first node as well.
+int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out);
+
+}  // namespace ctl

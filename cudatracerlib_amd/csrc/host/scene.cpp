@@ -8,6 +8,7 @@
 //   getKernelSceneData eps            (Engine/DynamicScene.cpp:587)
 #include "scene.h"
 #include "bvh_build.h"
+#include "ref_split.h"
 #include "../ctl_shade.h"
 
 #include <algorithm>
@@ -237,6 +238,13 @@ CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags) {
     return CTL_OK;
 }
 
+CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth) {
+    if (!s || !(split_alpha >= 0.0f) || split_depth > 16) { set_host_error("set_bvh_params: invalid argument"); return CTL_ERR_INVALID; }
+    s->split_alpha = split_alpha;
+    s->split_depth = split_depth;
+    return CTL_OK;
+}
+
 CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, ctl_scene_desc* out) {
     if (!s || !out) return CTL_ERR_INVALID;
     if (!s->has_camera) { set_host_error("compile: no camera"); return CTL_ERR_INVALID; }
@@ -267,7 +275,28 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         BvhBuildParams bp;
         bp.threads = threads;
         BvhOutput bo;
-        build_bvh(boxes.data(), ntri, bp, bo);
+        if (s->split_alpha > 0.0f && s->split_depth > 0) {
+            // references of large triangles split in space (ref_split.h)
+            std::vector<float> tv((size_t)ntri * 9);
+            parallel_for(ntri, threads, [&](uint64_t b, uint64_t e) {
+                for (uint64_t t = b; t < e; t++)
+                    for (int c = 0; c < 3; c++) {
+                        f3 p = V(M.idx[3 * t + c]);
+                        tv[9 * t + 3 * c] = p.x; tv[9 * t + 3 * c + 1] = p.y; tv[9 * t + 3 * c + 2] = p.z;
+                    }
+            });
+            RefSplitParams rp;
+            rp.alpha = s->split_alpha;
+            rp.max_depth = s->split_depth;
+            rp.threads = threads;
+            std::vector<Box> rb;
+            std::vector<uint32_t> rid;
+            split_refs(tv.data(), boxes.data(), ntri, rp, rb, rid);
+            if (rb.size() >= 0x7fffffffull) { set_host_error("compile: too many BVH references"); return CTL_ERR_INVALID; }
+            build_bvh(rb.data(), (uint32_t)rb.size(), bp, bo, rid.data());
+        } else {
+            build_bvh(boxes.data(), ntri, bp, bo);
+        }
         s->max_mesh_depth = std::max(s->max_mesh_depth, bo.max_depth);
         meshBox[mi] = bo.root_box;
 

@@ -27,6 +27,9 @@ struct ctl_host_scene {
     float cam_pos[3], cam_tar[3], cam_up[3], cam_fov, cam_near, cam_far;
     uint32_t cam_w = 0, cam_h = 0;
     uint32_t flags = 0;
+    // reference splitting of large triangles before the BVH build (ref_split.h)
+    float split_alpha = CTL_DEFAULT_SPLIT_ALPHA;
+    uint32_t split_depth = CTL_DEFAULT_SPLIT_DEPTH;
 
     // compiled arrays (owned)
     std::vector<ctl_triangle_data> tri_data;

@@ -182,7 +182,13 @@ enum {
     /* decode half floats like the reference's HOST path (Math/half.h:72-84,
      * ((h & 0x7fff) << 13) + 0x38000000, i.e. +0 -> 2^-15); off = IEEE decode
      * like its CUDA path (__half2float).  The oracle supports both.          */
-    CTL_SCENE_HALF_HOST_QUIRK = 1u << 0
+    CTL_SCENE_HALF_HOST_QUIRK = 1u << 0,
+    /* traverse the uploaded binary BVH in the reference's visit order, so an
+     * exact-t tie goes to the first triangle found (TraceHelper.cu:121,650).
+     * Off (default): the backend collapses each tree into 4-wide 128-B nodes
+     * on upload and resolves exact-t ties to the lowest (triangle, node);
+     * every other hit is identical.                                          */
+    CTL_SCENE_BINARY_BVH = 1u << 1
 };
 
 /* Everything KernelDynamicScene (Engine/KernelDynamicScene.h:28-57) holds that
@@ -346,6 +352,13 @@ CTL_API ctl_status ctl_host_scene_set_camera(ctl_host_scene* s, const float pos[
 CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags);
 /* Builds BVHs (threads=0: all hardware threads) and fills *out; the arrays
  * stay owned by `s` until it is destroyed or compiled again. */
+/* BVH build quality knobs of the compile (SplitBVHBuilder's splitAlpha /
+ * MaxSpatialDepth play this role in the reference, SplitBVHBuilder.hpp:62-67):
+ * triangles whose box area exceeds split_alpha x the mesh mean get up to
+ * 2^split_depth references with clipped boxes.  split_alpha = 0 disables. */
+#define CTL_DEFAULT_SPLIT_ALPHA 0.5f
+#define CTL_DEFAULT_SPLIT_DEPTH 8u
+CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth);
 CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, ctl_scene_desc* out);
 CTL_API const char* ctl_host_last_error(void);
 

@@ -200,7 +200,11 @@ bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float t
                 float invDz = 1.0f / (dl.x * v[0] + dl.y * v[1] + dl.z * v[2]);
                 float t = Oz * invDz;
                 unsigned int gtri = (index >> 1) + mesh.triangle_offset;
-                bool closer = t < h.t || (tie == TIE_MIN_INDEX && t == h.t && gtri < h.tri);
+                // TIE_MIN_INDEX: an exact-t tie goes to the lower (triangle, node)
+                // whatever the visit order (the rule of the wide-BVH device path);
+                // a hit at exactly the initial tmax is still rejected.
+                bool closer = t < h.t || (tie == TIE_MIN_INDEX && t == h.t && h.tri != UINT_MAX &&
+                                          (gtri < h.tri || (gtri == h.tri && (uint32_t)nodeIdx < h.node)));
                 if (t > triTmin && closer) {
                     float Ox = v[7] + ol.x * v[4] + ol.y * v[5] + ol.z * v[6];
                     float Dx = dl.x * v[4] + dl.y * v[5] + dl.z * v[6];

@@ -42,7 +42,8 @@ def camera_rays(desc, w, h, seed=0):
     return r
 
 
-def oracle_intersect(orc, desc, rays, any_hit=False, tie=0, threads=0):
+def oracle_intersect(orc, desc, rays, any_hit=False, tie=None, threads=0):
+    tie = tie_rule(desc) if tie is None else tie
     n = rays.shape[0]
     hits = np.zeros((n, 4), np.int32)
     orc.oracle_intersect(C.byref(desc), n, oracle.ptr(rays), oracle.ptr(hits), 1 if any_hit else 0, tie, threads)
@@ -62,10 +63,25 @@ def oracle_trace(orc, desc, rays, mode=0, tie=0, threads=0):
     return t, u, v, tri, node, st
 
 
+def tie_rule(desc):
+    """Oracle tie rule matching the device traversal the scene selects: the
+    reference's first-found order for CTL_SCENE_BINARY_BVH, else the wide
+    BVH's lowest-(triangle, node) rule (oracle TIE_MIN_INDEX = 1)."""
+    return 0 if desc.flags & 2 else 1
+
+
+def binary_bvh(desc):
+    """Copy of a compiled scene desc that selects the reference's binary visit order."""
+    d = type(desc).from_buffer_copy(desc)
+    d.flags |= 2
+    return d
+
+
 def oracle_render(orc, desc, params, passes, w, h, threads=0, fb=None, first_pass=0):
     if fb is None:
         fb = np.zeros((w * h, 7), np.float32)
     rays = 0
     for p in range(first_pass, first_pass + passes):
-        rays += orc.oracle_render_pass(C.byref(desc), C.byref(params), p, oracle.ptr(fb), 0, threads, 1, None)
+        rays += orc.oracle_render_pass(C.byref(desc), C.byref(params), p, oracle.ptr(fb), tie_rule(desc), threads, 1,
+                                       None)
     return fb, rays

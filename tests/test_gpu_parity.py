@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
-from helpers import camera_rays, oracle_intersect, oracle_render, random_rays
+from helpers import binary_bvh, camera_rays, oracle_intersect, oracle_render, random_rays, tie_rule
 
 pytestmark = pytest.mark.gpu
 
@@ -49,8 +49,11 @@ def gpu_intersect(tracer, desc, rays, any_hit, dev):
 
 @pytest.mark.parametrize("config,scale", [(1, 1.0), (2, 0.25), (3, 0.004)])
 @pytest.mark.parametrize("kind", ["random", "camera"])
-def test_intersect_closest_bit_exact(ctl, orc, tracer, dev, config, scale, kind):
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_intersect_closest_bit_exact(ctl, orc, tracer, dev, config, scale, kind, bvh):
     d = scene(ctl, config, scale, 96, 64)
+    if bvh == "binary":
+        d = binary_bvh(d)
     rays = random_rays(d, 50000, seed=config) if kind == "random" else camera_rays(d, 96, 64, seed=config)
     if kind == "random":
         rays[::3, 3] = np.float32(d.ray_eps)      # some rays with tmin > 0
@@ -63,11 +66,14 @@ def test_intersect_closest_bit_exact(ctl, orc, tracer, dev, config, scale, kind)
 
 
 @pytest.mark.parametrize("config,scale", [(1, 1.0), (2, 0.25)])
-def test_intersect_any_hit(ctl, orc, tracer, dev, config, scale):
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_intersect_any_hit(ctl, orc, tracer, dev, config, scale, bvh):
     """Any-hit returns *a* hit (order dependent, TraceHelper.cu:675-679): the
     hit/miss decision must equal the oracle's, and the reported triangle must
     really be hit inside (tmin, tmax) at the reported t."""
     d = scene(ctl, config, scale, 96, 64)
+    if bvh == "binary":
+        d = binary_bvh(d)
     rays = random_rays(d, 30000, seed=5)
     rays[:, 7] = np.float32(np.linalg.norm(np.array(d.box_max[:]) - np.array(d.box_min[:])) * 0.3)
     want = oracle_intersect(orc, d, rays, any_hit=True)
@@ -94,8 +100,11 @@ def render_gpu(ctl, tracer, desc, params, passes, w, h, dev, first_pass=0):
 @pytest.mark.parametrize("config,scale,w,h,passes", [(1, 1.0, 64, 64, 4), (2, 0.25, 96, 64, 2), (3, 0.003, 64, 48, 2)])
 @pytest.mark.parametrize("any_hit", [1, 0])
 @pytest.mark.parametrize("mode", ["persistent", "wavefront", "megakernel"])
-def test_render_pass_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, passes, any_hit, mode):
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_render_pass_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, passes, any_hit, mode, bvh):
     d = scene(ctl, config, scale, w, h)
+    if bvh == "binary":
+        d = binary_bvh(d)
     p = ctl.PTParams(1, 50, 5, any_hit, 64, 1, 0, {"persistent": 0, "megakernel": ctl.CTL_PT_MEGAKERNEL,
                                                  "wavefront": ctl.CTL_PT_WAVEFRONT}[mode])
     want, wrays = oracle_render(orc, d, p, passes, w, h)
@@ -166,7 +175,7 @@ def test_full_size_c2_pass_properties(ctl, orc, tracer, dev):
     # AddSample drops NaN/inf/negative samples (Image.cu:26-28); that must stay rare
     assert (got[:, 6] == 0).sum() < w * h * 1e-3
     want = np.zeros((w * h, 7), np.float32)
-    orc.oracle_render_pass(C.byref(d), C.byref(p), 0, oracle.ptr(want), 0, 0, 97, None)
+    orc.oracle_render_pass(C.byref(d), C.byref(p), 0, oracle.ptr(want), tie_rule(d), 0, 97, None)
     sel = np.arange(0, w * h, 97)
     assert np.array_equal(want[sel].view(np.uint32), got[sel].view(np.uint32))
     assert grays > w * h

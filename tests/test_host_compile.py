@@ -102,11 +102,14 @@ def test_triangle_data_and_lights_bit_exact(ctl, orc):
 
 
 @pytest.mark.parametrize("config,scale", [(1, 1.0), (2, 1.0), (3, 0.01)])
-def test_bvh_layout_contract(ctl, config, scale):
+@pytest.mark.parametrize("split", [False, True])
+def test_bvh_layout_contract(ctl, config, scale, split):
     """Reference layout contract (SplitBVHBuilder.cpp:163-203): DFS inner nodes
-    (child = index*4), leaves = ~first entry, every triangle referenced once,
-    leaf <= 8, last-in-leaf flags, depth bounded for the 64-entry stacks."""
+    (child = index*4), leaves = ~first entry, every triangle referenced (exactly
+    once without reference splitting; at least once with it, as the reference's
+    SBVH), leaf <= 8, last-in-leaf flags, depth bounded for the 64-entry stacks."""
     s = ctl.HostScene().generate(config, scale, 64, 64)
+    s.set_bvh_params(1.0 if split else 0.0, 4 if split else 0)
     d = s.compile()
     for m in range(d.n_meshes):
         km = d.meshes[m]
@@ -119,7 +122,11 @@ def test_bvh_layout_contract(ctl, config, scale):
         idx = np.ctypeslib.as_array(C.cast(d.tri_indices, C.POINTER(C.c_uint32)), shape=(d.n_tri_indices,))[e0:e1]
         t0 = km.triangle_offset
         t1 = d.meshes[m + 1].triangle_offset if m + 1 < d.n_meshes else d.n_tri_data
-        assert sorted((idx >> 1).tolist()) == list(range(t1 - t0))   # each triangle exactly once
+        if split:
+            assert set((idx >> 1).tolist()) == set(range(t1 - t0))   # each triangle at least once
+            assert idx.size <= 16 * (t1 - t0)
+        else:
+            assert sorted((idx >> 1).tolist()) == list(range(t1 - t0))   # each triangle exactly once
         seen_inner = set()
         stack = [(0, 0)]
         maxdepth = 0
@@ -144,3 +151,8 @@ def test_bvh_layout_contract(ctl, config, scale):
                     leaves += 1
         assert len(seen_inner) == nxt - nb
         assert maxdepth <= 62
+
+
+def test_wide_bvh_collapse_is_exercised_by_upload_contract(ctl):
+    """The scene flag that keeps the reference's binary order is part of the ABI."""
+    assert ctl.CTL_SCENE_BINARY_BVH == 2
