@@ -21,11 +21,14 @@ missing or fails.
 """
 import ctypes as C
 
+import numpy as np
+
 from . import _abi
 from ._abi import (PTParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK, CTL_SCENE_BINARY_BVH,
                    CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT)
 
 __all__ = ["HostScene", "Tracer", "PathTracer", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
+           "roughdielectric_material",
            "CTL_SCENE_HALF_HOST_QUIRK", "CTL_SCENE_BINARY_BVH", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "lib", "diffuse_material"]
 
 
@@ -44,13 +47,37 @@ def _check(status, ctx=None, what=""):
         raise CTLError(f"{what} failed (status {status}): {msg.decode() if msg else ''}")
 
 
-def diffuse_material(r, g, b, two_sided=True):
+def diffuse_material(r, g, b, two_sided=True, texture=None):
+    """diffuse BSDF (BSDF_Simple.cu:7-75); `texture` = ImageTexture index of
+    m_reflectance (HostScene.add_texture), else the constant (r, g, b)."""
     m = Material()
     m.bsdf_type = CTL_BSDF_DIFFUSE
     m.combined_type = CTL_EDIFFUSE_REFLECTION
     m.two_sided = 1 if two_sided else 0
     m.node_light_index = 0xFFFFFFFF
     m.reflectance[:] = [r, g, b]
+    m.texture = 0xFFFFFFFF if texture is None else int(texture)
+    return m
+
+
+def roughdielectric_material(distribution, eta, alpha_u, alpha_v=None, reflectance=(1.0, 1.0, 1.0),
+                             transmittance=(1.0, 1.0, 1.0)):
+    """roughdielectric BSDF (BSDF_Simple.cu:373-615) with constant textures;
+    distribution = _abi.CTL_MICROFACET_BECKMANN or _abi.CTL_MICROFACET_GGX."""
+    m = Material()
+    m.bsdf_type = _abi.CTL_BSDF_ROUGHDIELECTRIC
+    m.combined_type = _abi.CTL_EGLOSSY_REFLECTION | _abi.CTL_EGLOSSY_TRANSMISSION
+    m.two_sided = 0
+    m.node_light_index = 0xFFFFFFFF
+    m.reflectance[:] = list(reflectance)
+    m.texture = 0xFFFFFFFF
+    m.transmittance[:] = list(transmittance)
+    m.distribution = int(distribution)
+    m.eta = float(eta)
+    m.inv_eta = float(np.float32(1.0) / np.float32(eta))      # roughdielectric::Update
+    m.alpha_u = float(alpha_u)
+    m.alpha_v = float(alpha_u if alpha_v is None else alpha_v)
+    m.sample_visible = 1                                         # getSampleVisible(Beckmann/GGX, true)
     return m
 
 
@@ -93,6 +120,18 @@ class HostScene:
             None if mi is None else mi.ctypes.data, mats, len(materials))
         if r < 0:
             _check(1, None, "add_mesh")
+        return r
+
+    def add_texture(self, rgba, filter=_abi.CTL_TEX_TRILINEAR, wrap=_abi.CTL_WRAP_REPEAT,
+                    mapping=(1.0, 0.0, 0.0, 0.0, 1.0, 0.0), scale=(1.0, 1.0, 1.0)):
+        """ImageTexture over an (h, w) uint32 RGBA8 image (r in the low byte); returns its index."""
+        img = np.ascontiguousarray(rgba, dtype=np.uint32)
+        h, w = img.shape
+        self._keep = getattr(self, "_keep", []) + [img]
+        r = self._L.ctl_host_scene_add_texture(self._h, img.ctypes.data, w, h, int(filter), int(wrap),
+                                               (C.c_float * 6)(*mapping), (C.c_float * 3)(*scale))
+        if r < 0:
+            _check(1, None, "add_texture")
         return r
 
     def add_node(self, mesh, xf16=None):

@@ -15,6 +15,13 @@ CTL_SCENE_HALF_HOST_QUIRK = 1
 CTL_SCENE_BINARY_BVH = 2
 CTL_BSDF_DIFFUSE = 1
 CTL_EDIFFUSE_REFLECTION = 0x2
+CTL_EGLOSSY_REFLECTION = 0x8
+CTL_EGLOSSY_TRANSMISSION = 0x10
+CTL_BSDF_ROUGHDIELECTRIC = 5
+CTL_MICROFACET_BECKMANN = 0
+CTL_MICROFACET_GGX = 1
+CTL_TEX_POINT, CTL_TEX_BILINEAR, CTL_TEX_EWA, CTL_TEX_TRILINEAR = 0, 1, 2, 3
+CTL_WRAP_REPEAT, CTL_WRAP_CLAMP, CTL_WRAP_MIRROR, CTL_WRAP_BLACK = 0, 1, 2, 3
 CTL_MAX_NUM_LIGHTS = 16
 CTL_PT_MEGAKERNEL = 1
 CTL_PT_WAVEFRONT = 2
@@ -59,9 +66,18 @@ class Pixel(C.Structure):            # PixelData, 28 B
     _fields_ = [("rgb", C.c_float * 3), ("rgb_splat", C.c_float * 3), ("weight_sum", C.c_float)]
 
 
-class Material(C.Structure):
+class Material(C.Structure):        # 80 B
     _fields_ = [("bsdf_type", C.c_uint32), ("combined_type", C.c_uint32), ("two_sided", C.c_uint32),
-                ("node_light_index", C.c_uint32), ("reflectance", C.c_float * 3), ("pad", C.c_float)]
+                ("node_light_index", C.c_uint32), ("reflectance", C.c_float * 3), ("texture", C.c_uint32),
+                ("transmittance", C.c_float * 3), ("distribution", C.c_uint32), ("eta", C.c_float),
+                ("inv_eta", C.c_float), ("alpha_u", C.c_float), ("alpha_v", C.c_float),
+                ("sample_visible", C.c_uint32), ("pad", C.c_uint32 * 3)]
+
+
+class Texture(C.Structure):
+    _fields_ = [("mapping", C.c_float * 6), ("set_id", C.c_uint32), ("scale", C.c_float * 3),
+                ("width", C.c_uint32), ("height", C.c_uint32), ("levels", C.c_uint32), ("filter", C.c_uint32),
+                ("wrap", C.c_uint32), ("offsets", C.c_uint32 * 16), ("weight_lut", C.c_float * 64)]
 
 
 class LightTri(C.Structure):         # ShapeSet::triData, 64 B
@@ -97,6 +113,8 @@ class SceneDesc(C.Structure):
         ("light_tris", C.POINTER(LightTri)), ("n_light_tris", C.c_uint32),
         ("light_tri_cdf", C.POINTER(C.c_float)), ("n_light_tri_cdf", C.c_uint32),
         ("light_cdf", C.c_float * CTL_MAX_NUM_LIGHTS),
+        ("textures", C.POINTER(Texture)), ("n_textures", C.c_uint32),
+        ("tex_data", C.POINTER(C.c_uint32)), ("n_tex_data", C.c_uint64),
         ("env_map_index", C.c_uint32),
         ("box_min", C.c_float * 3), ("box_max", C.c_float * 3),
         ("ray_eps", C.c_float),
@@ -136,6 +154,7 @@ SYMBOLS = [
     ("ctl_host_scene_destroy", None, [_vp]),
     ("ctl_host_scene_add_mesh", C.c_int32, [_vp, _vp, C.c_uint32, _vp, C.c_uint32, _vp, _vp, _vp,
                                             C.POINTER(Material), C.c_uint32]),
+    ("ctl_host_scene_add_texture", C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _vp, _vp]),
     ("ctl_host_scene_add_node", C.c_int32, [_vp, C.c_uint32, _vp]),
     ("ctl_host_scene_add_area_light", C.c_int32, [_vp, C.c_uint32, C.c_uint32, _vp]),
     ("ctl_host_scene_set_camera", C.c_int32, [_vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,

@@ -41,6 +41,11 @@ CTL_HD float cr_cos(float x) { return (float)cos((double)x); }
 CTL_HD float cr_tan(float x) { return (float)tan((double)x); }
 CTL_HD float cr_acos(float x) { return (float)acos((double)x); }
 CTL_HD float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+CTL_HD float cr_atan(float x) { return (float)atan((double)x); }
+CTL_HD float cr_exp(float x) { return (float)exp((double)x); }
+CTL_HD float cr_log(float x) { return (float)log((double)x); }
+CTL_HD float cr_log2(float x) { return (float)log2((double)x); }
+CTL_HD float cr_pow(float a, float b) { return (float)pow((double)a, (double)b); }
 
 struct f2 { float x, y; };
 struct f3 { float x, y, z; };

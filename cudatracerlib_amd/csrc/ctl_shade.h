@@ -20,10 +20,14 @@ CTL_HD float spec_max(spec s) { float r = s.x; r = tmax(r, s.y); r = tmax(r, s.z
 CTL_HD bool spec_zero(spec s) { return s.x == 0.0f && s.y == 0.0f && s.z == 0.0f; }
 CTL_HD spec spec_div(spec s, float f) { float recip = 1.0f / f; return s * recip; }   // Spectrum.h:122-128
 
-struct dgeom {   // DifferentialGeometry subset used by the path
+struct dgeom {   // DifferentialGeometry subset used by the path (Engine/DifferentialGeometry.h)
     f3 P;
     frame sys;
     f3 n;
+    f3 dpdu, dpdv;                   // world space
+    f2 uv;                           // uv[0] (TriangleData holds one UV set)
+    float dudx, dudy, dvdx, dvdy;    // computePartials; live for the whole path
+    bool has_partials;
 };
 
 // NDEC: callable uint32 (16-bit code) -> f3 normal (the device passes a LUT).
@@ -45,9 +49,60 @@ CTL_HD void fill_dg(const ctl_triangle_data& td, const m44& L2W, f2 bary, bool h
     dg.sys.s = normalize(s);
     dg.sys.t = normalize(t);
     dg.sys.n = normalize(cross(t, s));
-    f3 ddu = xform_dir(L2W, dpdu), ddv = xform_dir(L2W, dpdv);
-    dg.n = normalize(cross(ddu, ddv));
+    dg.dpdu = xform_dir(L2W, dpdu);
+    dg.dpdv = xform_dir(L2W, dpdv);
+    dg.n = normalize(cross(dg.dpdu, dg.dpdv));
+    {   // UV set 0: three half2 (TriangleData.cu:91-98)
+        f2 ta = mk2(half_to_float(w[5] & 0xffffu, half_quirk), half_to_float(w[5] >> 16, half_quirk));
+        f2 tb = mk2(half_to_float(w[6] & 0xffffu, half_quirk), half_to_float(w[6] >> 16, half_quirk));
+        f2 tc = mk2(half_to_float(w[7] & 0xffffu, half_quirk), half_to_float(w[7] >> 16, half_quirk));
+        dg.uv = u * ta + v * tb + ww * tc;
+    }
     if (dot(dg.n, dg.sys.n) < 0.0f) dg.n = -dg.n;
+}
+
+// DifferentialGeometry::computePartials (Engine/DifferentialGeometry.cu:5-84)
+// with AlgebraHelper::solveLinearSystem2x2 (Math/AlgebraHelper.h:11-24).
+CTL_HD bool solve2x2_ref(const float a[2][2], const float b[2], float x[2]) {
+    const float det = a[0][0] * a[1][1] - a[0][1] * a[1][0];
+    if (fabsf(det) <= 2.93873587705571876e-39f) return false;   // RCPOVERFLOW
+    const float inverse = (float)1.0f / det;
+    x[0] = (a[1][1] * b[0] - a[0][1] * b[1]) * inverse;
+    x[1] = (a[0][0] * b[1] - a[1][0] * b[0]) * inverse;
+    return true;
+}
+CTL_HD void compute_partials(dgeom& dg, f3 rxo, f3 rxd, f3 ryo, f3 ryd) {
+    float A[2][2], Bx[2], By[2], x[2];
+    int axes[2];
+    dg.has_partials = true;
+    if (dot(dg.dpdu, dg.dpdu) == 0 && dot(dg.dpdv, dg.dpdv) == 0) {
+        dg.dudx = dg.dvdx = dg.dudy = dg.dvdy = 0.0f;
+        return;
+    }
+    const float pp = dot(dg.n, dg.P), pox = dot(dg.n, rxo), poy = dot(dg.n, ryo), prx = dot(dg.n, rxd),
+                pry = dot(dg.n, ryd);
+    if (prx == 0 || pry == 0) {
+        dg.dudx = dg.dvdx = dg.dudy = dg.dvdy = 0.0f;
+        return;
+    }
+    const float tx = (pp - pox) / prx, ty = (pp - poy) / pry;
+    const float absX = fabsf(dg.n.x), absY = fabsf(dg.n.y), absZ = fabsf(dg.n.z);
+    if (absX > absY && absX > absZ) { axes[0] = 1; axes[1] = 2; }
+    else if (absY > absZ) { axes[0] = 0; axes[1] = 2; }
+    else { axes[0] = 0; axes[1] = 1; }
+    A[0][0] = comp(dg.dpdu, axes[0]);
+    A[0][1] = comp(dg.dpdv, axes[0]);
+    A[1][0] = comp(dg.dpdu, axes[1]);
+    A[1][1] = comp(dg.dpdv, axes[1]);
+    const f3 px = rxo + rxd * tx, py = ryo + ryd * ty;
+    Bx[0] = comp(px, axes[0]) - comp(dg.P, axes[0]);
+    Bx[1] = comp(px, axes[1]) - comp(dg.P, axes[1]);
+    By[0] = comp(py, axes[0]) - comp(dg.P, axes[0]);
+    By[1] = comp(py, axes[1]) - comp(dg.P, axes[1]);
+    if (solve2x2_ref(A, Bx, x)) { dg.dudx = x[0]; dg.dvdx = x[1]; }
+    else { dg.dudx = 1; dg.dvdx = 0; }
+    if (solve2x2_ref(A, By, x)) { dg.dudy = x[0]; dg.dvdy = x[1]; }
+    else { dg.dudy = 0; dg.dvdy = 1; }
 }
 
 struct bsdf_rec { f3 wi, wo; uint32_t sampled_type, type_mask; };
@@ -56,12 +111,14 @@ enum : uint32_t { kEAll = 0x1ffu, kEDelta = 0x61u, kESmooth = 0x1eu };
 
 CTL_HD spec refl(const ctl_material& m) { return mk3(m.reflectance[0], m.reflectance[1], m.reflectance[2]); }
 
-CTL_HD spec diffuse_sample(const ctl_material& m, bsdf_rec& b, float& pdf, f2 sample) {
+// diffuse::sample up to its return value (BSDF_Simple.cu:7-24, pure
+// EDiffuseReflection): false = the reference returns 0.
+CTL_HD bool diffuse_sample_dir(const ctl_material& m, bsdf_rec& b, float& pdf, f2 sample) {
     bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
-    spec res;
+    bool ok;
     if (!(b.type_mask & m.combined_type) || (m.combined_type == CTL_EDIFFUSE_REFLECTION && b.wi.z <= 0)) {
-        res = mk3s(0.0f);
+        ok = false;
     } else {
         b.sampled_type = m.combined_type;
         // Warp::squareToCosineHemisphere + squareToUniformDiskConcentric (Math/Warp.h:61-125)
@@ -75,26 +132,33 @@ CTL_HD spec diffuse_sample(const ctl_material& m, bsdf_rec& b, float& pdf, f2 sa
         float z = sqrtf(1.0f - p.x * p.x - p.y * p.y);
         b.wo = mk3(p.x, p.y, z);
         pdf = fabsf(CTL_INV_PI * b.wo.z) * 1.0f;
-        res = refl(m) * 1.0f;
+        ok = true;
     }
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
-    return res;
+    return ok;
 }
 
-CTL_HD spec diffuse_f(const ctl_material& m, bsdf_rec& b) {
+CTL_HD spec diffuse_sample(const ctl_material& m, bsdf_rec& b, float& pdf, f2 sample) {
+    return diffuse_sample_dir(m, b, pdf, sample) ? refl(m) * 1.0f : mk3s(0.0f);
+}
+
+// diffuse::f (BSDF_Simple.cu:31-43) with the evaluated reflectance R
+CTL_HD spec diffuse_f_refl(const ctl_material& m, bsdf_rec& b, spec R) {
     bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
     spec res = mk3s(0.0f);
     if (b.type_mask & m.combined_type) {
         bool validRefl = m.combined_type == CTL_EDIFFUSE_REFLECTION && b.wi.z > 0 && b.wo.z > 0;
         bool validTrans = m.combined_type == CTL_EDIFFUSE_TRANSMISSION && b.wi.z * b.wo.z < 0;
-        spec s = refl(m) * (CTL_INV_PI * fabsf(b.wo.z));
+        spec s = R * (CTL_INV_PI * fabsf(b.wo.z));
         if (validRefl || validTrans) res = s;
         else if (m.combined_type == (CTL_EDIFFUSE_REFLECTION | CTL_EDIFFUSE_TRANSMISSION)) res = s * 0.5f;
     }
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
     return res;
 }
+
+CTL_HD spec diffuse_f(const ctl_material& m, bsdf_rec& b) { return diffuse_f_refl(m, b, refl(m)); }
 
 CTL_HD float diffuse_pdf(const ctl_material& m, bsdf_rec& b) {
     bool flip = b.wi.z < 0 && m.two_sided;

@@ -120,7 +120,13 @@ struct PathVars {
     float brdf_pdf;
     int depth;
     bool specular;
+    // DifferentialGeometry partials: computed at the first hit and kept for the
+    // rest of the path (PathTrace's bRec lives across bounces, PathTracer.cu:16,60-61)
+    float dudx, dudy, dvdx, dvdy;
+    bool has_partials;
     __device__ __forceinline__ void begin(f2 px, f3 o, f3 d) {
+        dudx = dudy = dvdx = dvdy = 0.0f;
+        has_partials = false;
         cl = mk3s(0.0f); cf = mk3s(1.0f);
         rori = o; rdir = d;
         last_nor = mk3s(0.0f);
@@ -141,6 +147,16 @@ struct ShadowReq {
     spec add;
     bool valid;
 };
+
+// Ray-differential directions of PerspectiveSensor::sampleRayDifferential
+// (Sensor.cu:130-144): rX/rY start at the camera and point through nearP + m_dx / m_dy.
+__device__ __forceinline__ void sensor_diff(const DevScene& S, f2 pX, f3& o, f3& dX, f3& dY) {
+    m44 s2c = to_m44(S.camera.sample_to_camera), tw = to_m44(S.camera.to_world);
+    f3 nearP = xform_point(s2c, mk3(pX.x * S.camera.inv_resolution[0], pX.y * S.camera.inv_resolution[1], 0.0f));
+    o = xform_point(tw, mk3s(0.0f));
+    dX = xform_dir(tw, normalize(nearP + mk3(S.camera.dx[0], S.camera.dx[1], S.camera.dx[2])));
+    dY = xform_dir(tw, normalize(nearP + mk3(S.camera.dy[0], S.camera.dy[1], S.camera.dy[2])));
+}
 
 // Sensor sample + primary ray of pixel (px, py) (pathKernel2, PathTracer.cu:182-194;
 // PerspectiveSensor::sampleRayDifferential, Sensor.cu:130-144).
@@ -179,6 +195,17 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
         dg.sys.n = -dg.sys.n;
         b.wi.z *= -1.0f;
     }
+    if (v.depth == 1) {   // bRec.dg.computePartials(r, rX, rY) (PathTracer.cu:60-61)
+        f3 co, dX, dY;
+        sensor_diff(S, v.pX, co, dX, dY);
+        compute_partials(dg, co, dX, co, dY);
+        v.dudx = dg.dudx; v.dudy = dg.dudy; v.dvdx = dg.dvdx; v.dvdy = dg.dvdy;
+        v.has_partials = true;
+    } else {
+        dg.dudx = v.dudx; dg.dudy = v.dudy; dg.dvdx = v.dvdx; dg.dvdy = v.dvdy;
+        dg.has_partials = v.has_partials;
+    }
+    const TexView tex{S.textures, S.tex_data};
     if (mat.node_light_index != 0xffffffffu) {
         const uint32_t li = N->lights[mat.node_light_index];
         const ctl_light L = S.lights[li];
@@ -194,7 +221,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
         spec Le = (dot(dg.sys.n, w) <= 0) ? mk3s(0.0f) : mk3(L.radiance[0], L.radiance[1], L.radiance[2]);
         v.cl = v.cl + (v.cf * misWeight) * Le;
     }
-    spec f = diffuse_sample(mat, b, v.brdf_pdf, rng.next2());
+    spec f = bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex);
     v.last_nor = dg.sys.n;
     if ((mat.combined_type & kESmooth) != 0 && S.n_lights) {
         f2 sample = rng.next2();
@@ -217,10 +244,10 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
             bsdf_rec b2 = b;
             b2.wo = to_local(dg.sys, dRec.d);
             b2.type_mask = kEAll & ~kEDelta;
-            spec bsdfVal = diffuse_f(mat, b2);
+            spec bsdfVal = bsdf_f(mat, b2, dg, &tex);
             if (!spec_zero(bsdfVal)) {
                 float weight = 1.0f;
-                if (dRec.measure != kEDiscrete) weight = power_heuristic(dRec.pdf * lpdf, diffuse_pdf(mat, b2));
+                if (dRec.measure != kEDiscrete) weight = power_heuristic(dRec.pdf * lpdf, bsdf_pdf(mat, b2));
                 spec ret = value * bsdfVal * weight;
                 ret = ret * mk3s(1.0f);
                 sh.valid = true;
@@ -259,7 +286,8 @@ struct WfState {
     float4* cf;       // throughput xyz | w: pX.y
     float4* wo;       // persistent BSDF wo xyz | w: last_nor.x
     float2* ln;       // last_nor.yz
-    uint4* meta;      // x: pixel idx, y: d1 | d2 << 16, z: depth | specular << 16
+    uint4* meta;      // x: pixel idx, y: d1 | d2 << 16, z: depth | specular << 16, w: has_partials
+    float4* part;     // dudx, dudy, dvdx, dvdy (first-hit partials, kept for the path)
     float4* hit;      // t, u, v, tri bits
     uint32_t* hit_node;
     uint32_t* q[2];   // extension-ray queues (path indices), ping-pong

@@ -42,6 +42,8 @@ static_assert(sizeof(ctl_ray) == 32, "traversalRay is 32 B");
 static_assert(sizeof(ctl_hit) == 16, "traversalResult is 16 B");
 static_assert(sizeof(ctl_pixel) == 28, "PixelData is 28 B");
 static_assert(sizeof(ctl_light_tri) == 64, "ShapeSet::triData is 64 B");
+static_assert(sizeof(ctl_material) == 80, "ctl_material is 80 B");
+static_assert(sizeof(ctl_texture) == 380, "ctl_texture is 380 B");
 
 #ifndef CTL_PERSIST_WAVES
 #define CTL_PERSIST_WAVES 6   // waves/SIMD for the persistent path kernel: measured best on C3
@@ -493,8 +495,29 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     if (d->n_lights > CTL_MAX_NUM_LIGHTS) { c->err = "scene_upload: more than 16 lights"; return CTL_ERR_INVALID; }
     for (uint32_t i = 0; i < d->n_lights; i++)
         if (d->lights[i].orthogonal) { c->err = "scene_upload: orthogonal DiffuseLight unsupported"; return CTL_ERR_INVALID; }
-    for (uint32_t i = 0; i < d->n_materials; i++)
-        if (d->materials[i].bsdf_type != CTL_BSDF_DIFFUSE) { c->err = "scene_upload: only diffuse BSDFs are supported"; return CTL_ERR_INVALID; }
+    for (uint32_t i = 0; i < d->n_materials; i++) {
+        const ctl_material& m = d->materials[i];
+        if (m.bsdf_type != CTL_BSDF_DIFFUSE && m.bsdf_type != CTL_BSDF_ROUGHDIELECTRIC) {
+            c->err = "scene_upload: only diffuse and roughdielectric BSDFs are supported";
+            return CTL_ERR_INVALID;
+        }
+        if (m.bsdf_type == CTL_BSDF_ROUGHDIELECTRIC && (m.distribution > CTL_MICROFACET_GGX || !m.sample_visible)) {
+            c->err = "scene_upload: roughdielectric needs a Beckmann/GGX distribution with visible-normal sampling";
+            return CTL_ERR_INVALID;
+        }
+        if (m.bsdf_type == CTL_BSDF_DIFFUSE && m.texture != 0xffffffffu && m.texture >= d->n_textures) {
+            c->err = "scene_upload: material texture index out of range";
+            return CTL_ERR_INVALID;
+        }
+    }
+    for (uint32_t i = 0; i < d->n_textures; i++) {
+        const ctl_texture& t = d->textures[i];
+        if (t.levels == 0 || t.levels > 16 || t.width < 2 || t.height < 2 || t.set_id != 0 ||
+            (uint64_t)t.offsets[t.levels - 1] + (uint64_t)(t.width >> (t.levels - 1)) * (t.height >> (t.levels - 1)) > d->n_tex_data) {
+            c->err = "scene_upload: invalid texture record";
+            return CTL_ERR_INVALID;
+        }
+    }
     CTL_HIP(c, hipDeviceSynchronize());
     free_scene(c);
     DevScene S{};
@@ -521,6 +544,8 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
         lut[code] = make_float4(v.x, v.y, v.z, 0.0f);
     }
     UP(lut.data(), lut.size(), &S.normal_lut);
+    UP(d->textures, d->n_textures, &S.textures);
+    UP(d->tex_data, d->n_tex_data, &S.tex_data);
     // 4-wide trees for the device traversal (host/bvh_wide.h), unless the
     // caller asks for the reference's binary visit order
     const bool wide = (d->flags & CTL_SCENE_BINARY_BVH) == 0 && d->n_bvh_nodes > 0;

@@ -27,13 +27,16 @@
 //  * no FMA contraction (-ffp-contract=off) => bit-identical to the CPU oracle.
 #pragma once
 #include <hip/hip_runtime.h>
-#include "../ctl_shade.h"
+#include "../ctl_bsdf.h"
 
 namespace ctl {
 
 #define CTL_SENTINEL 0x76543210
 
-constexpr int kLdsStack = 16;
+#ifndef CTL_LDS_STACK
+#define CTL_LDS_STACK 16
+#endif
+constexpr int kLdsStack = CTL_LDS_STACK;   // stack entries per lane held in LDS
 constexpr int kStackMax = 128;
 
 struct DevScene {
@@ -51,6 +54,8 @@ struct DevScene {
     const ctl_light_tri* light_tris;
     const float* light_tri_cdf;
     const float4* normal_lut;   // 65536 decoded spherical normals (Compression.h:20-31)
+    const ctl_texture* textures;   // ImageTexture + KernelMIPMap records
+    const uint32_t* tex_data;      // RGBCOL texels of all MIP levels
     uint32_t n_nodes;
     int32_t start_node;
     uint32_t n_lights;

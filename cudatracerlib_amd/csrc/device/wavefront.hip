@@ -194,6 +194,11 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams
             v.last_nor = mk3(wo4.w, ln2.x, ln2.y);
             v.depth = (int)(meta.z & 0xffffu);
             v.specular = (meta.z >> 16) & 1u;
+            v.has_partials = meta.w != 0u;
+            if (v.has_partials) {
+                const float4 pt = W.part[i];
+                v.dudx = pt.x; v.dudy = pt.y; v.dvdx = pt.z; v.dvdy = pt.w;
+            }
             SamplerDev rng;
             rng.init(s1, s2, P, meta.x, meta.y & 0xffffu, meta.y >> 16);
             HitRec h;
@@ -211,7 +216,9 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams
                 W.cf[i] = make_float4(v.cf.x, v.cf.y, v.cf.z, v.pX.y);
                 W.wo[i] = make_float4(v.wo.x, v.wo.y, v.wo.z, v.last_nor.x);
                 W.ln[i] = make_float2(v.last_nor.y, v.last_nor.z);
-                W.meta[i] = make_uint4(meta.x, rng.d1 | (rng.d2 << 16), (uint32_t)v.depth | ((v.specular ? 1u : 0u) << 16), 0u);
+                W.meta[i] = make_uint4(meta.x, rng.d1 | (rng.d2 << 16), (uint32_t)v.depth | ((v.specular ? 1u : 0u) << 16),
+                                       v.has_partials ? 1u : 0u);
+                if (v.has_partials && !meta.w) W.part[i] = make_float4(v.dudx, v.dudy, v.dvdx, v.dvdy);
                 if (terminated && !pushShadow) add_sample(fb, P, v.pX, mk3s(1.0f) * v.cl);
                 if (pushShadow) {
                     W.sh_o[i] = make_float4(v.rori.x, v.rori.y, v.rori.z, sh.dist - S.ray_eps);
@@ -272,7 +279,7 @@ int wavefront_pass(ctl_ctx* c, const PathParams& P, ctl_pixel* fb, bool stats, h
         wavefront_free(c);
         size_t n = items;
         bool ok = wf_alloc(c, &W.o, n) && wf_alloc(c, &W.d, n) && wf_alloc(c, &W.cl, n) && wf_alloc(c, &W.cf, n) &&
-                  wf_alloc(c, &W.wo, n) && wf_alloc(c, &W.ln, n) && wf_alloc(c, &W.meta, n) &&
+                  wf_alloc(c, &W.wo, n) && wf_alloc(c, &W.ln, n) && wf_alloc(c, &W.meta, n) && wf_alloc(c, &W.part, n) &&
                   wf_alloc(c, &W.hit, n) && wf_alloc(c, &W.hit_node, n) && wf_alloc(c, &W.q[0], n) &&
                   wf_alloc(c, &W.q[1], n) && wf_alloc(c, &W.sq, n) && wf_alloc(c, &W.sh_o, n) &&
                   wf_alloc(c, &W.sh_d, n) && wf_alloc(c, &W.sh_val, n) && wf_alloc(c, &W.sh_occ, n) &&

@@ -238,6 +238,60 @@ CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags) {
     return CTL_OK;
 }
 
+// ImageTexture + KernelMIPMap of an RGBA8 image.  The pyramid is our own
+// 2x2 box filter (the reference resamples with FreeImage, MIPMap.cpp:40-86,
+// which this build does not have); the weight LUT is MIPMap.cpp:88-93.
+CTL_API int32_t ctl_host_scene_add_texture(ctl_host_scene* s, const uint32_t* rgba, uint32_t w, uint32_t h,
+                                           uint32_t filter, uint32_t wrap, const float mapping[6],
+                                           const float scale[3]) {
+    auto pow2 = [](uint32_t v) { return v && !(v & (v - 1)); };
+    if (!s || !rgba || !mapping || !scale || !pow2(w) || !pow2(h) || filter > CTL_TEX_TRILINEAR || wrap > CTL_WRAP_BLACK) {
+        set_host_error("add_texture: invalid argument (width and height must be powers of two)");
+        return -1;
+    }
+    ctl_texture t{};
+    t.m11 = mapping[0]; t.m12 = mapping[1]; t.m13 = mapping[2];
+    t.m21 = mapping[3]; t.m22 = mapping[4]; t.m23 = mapping[5];
+    t.set_id = 0;
+    t.scale[0] = scale[0]; t.scale[1] = scale[1]; t.scale[2] = scale[2];
+    t.width = w; t.height = h;
+    t.filter = filter;
+    t.wrap = wrap;
+    uint32_t levels = 1;
+    while (levels < 16 && (w >> levels) >= 1 && (h >> levels) >= 1) levels++;
+    t.levels = levels;
+    std::vector<uint32_t> cur(rgba, rgba + (size_t)w * h);
+    uint64_t off = s->tex_data.size();
+    for (uint32_t l = 0; l < levels; l++) {
+        const uint32_t lw = w >> l, lh = h >> l;
+        if (off + (uint64_t)lw * lh > 0xffffffffull) { set_host_error("add_texture: texel storage exceeds 2^32"); return -1; }
+        t.offsets[l] = (uint32_t)off;
+        s->tex_data.insert(s->tex_data.end(), cur.begin(), cur.end());
+        off += (uint64_t)lw * lh;
+        if (l + 1 == levels) break;
+        std::vector<uint32_t> nxt((size_t)(lw / 2) * (lh / 2));
+        for (uint32_t y = 0; y < lh / 2; y++)
+            for (uint32_t x = 0; x < lw / 2; x++) {
+                uint32_t px[4] = {cur[(2 * y) * lw + 2 * x], cur[(2 * y) * lw + 2 * x + 1], cur[(2 * y + 1) * lw + 2 * x],
+                                  cur[(2 * y + 1) * lw + 2 * x + 1]};
+                uint32_t o = 0;
+                for (int c = 0; c < 4; c++) {
+                    uint32_t sum = 2;
+                    for (int k = 0; k < 4; k++) sum += (px[k] >> (8 * c)) & 0xffu;
+                    o |= ((sum / 4) & 0xffu) << (8 * c);
+                }
+                nxt[(size_t)y * (lw / 2) + x] = o;
+            }
+        cur.swap(nxt);
+    }
+    for (int i = 0; i < 64; i++) {
+        float r2 = (float)i / (float)(64 - 1);
+        t.weight_lut[i] = cr_exp(-2.0f * r2) - cr_exp(-2.0f);
+    }
+    s->textures.push_back(t);
+    return (int32_t)s->textures.size() - 1;
+}
+
 CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth) {
     if (!s || !(split_alpha >= 0.0f) || split_depth > 16) { set_host_error("set_bvh_params: invalid argument"); return CTL_ERR_INVALID; }
     s->split_alpha = split_alpha;
@@ -474,6 +528,15 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         }
     }
     d.env_map_index = 0xffffffffu;
+    d.textures = s->textures.data();
+    d.n_textures = (uint32_t)s->textures.size();
+    d.tex_data = s->tex_data.data();
+    d.n_tex_data = s->tex_data.size();
+    for (const ctl_material& m : s->materials)
+        if (m.bsdf_type == CTL_BSDF_DIFFUSE && m.texture != 0xffffffffu && m.texture >= s->textures.size()) {
+            set_host_error("compile: material texture index out of range");
+            return CTL_ERR_INVALID;
+        }
     for (int k = 0; k < 3; k++) { d.box_min[k] = sceneBox.lo[k]; d.box_max[k] = sceneBox.hi[k]; }
     f3 size = mk3(sceneBox.hi[0] - sceneBox.lo[0], sceneBox.hi[1] - sceneBox.lo[1], sceneBox.hi[2] - sceneBox.lo[2]);
     d.ray_eps = 1e-4f * length(size);   // MIN_RAYTRACE_DISTANCE_RELATIVE * |box|

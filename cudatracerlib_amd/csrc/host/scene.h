@@ -44,6 +44,8 @@ struct ctl_host_scene {
     std::vector<ctl_light> klights;
     std::vector<ctl_light_tri> light_tris;
     std::vector<float> light_tri_cdf;
+    std::vector<ctl_texture> textures;   // added by ctl_host_scene_add_texture (kept across compiles)
+    std::vector<uint32_t> tex_data;
     ctl_scene_desc desc{};
     uint32_t max_mesh_depth = 0;
 };

@@ -115,6 +115,7 @@ ctl_material diffuse_mat(float r, float g, float b) {
     m.two_sided = 1;
     m.node_light_index = 0xffffffffu;
     m.reflectance[0] = r; m.reflectance[1] = g; m.reflectance[2] = b;
+    m.texture = 0xffffffffu;
     return m;
 }
 
@@ -125,10 +126,64 @@ double hf_c3(double x, double z) {
            0.15 * std::sin(0.53 * x - 0.41 * z);
 }
 
-int add_mesh(ctl_host_scene* s, MeshB& M, const std::vector<ctl_material>& mats) {
+int add_mesh(ctl_host_scene* s, MeshB& M, const std::vector<ctl_material>& mats, const float* uvs = nullptr) {
     return ctl_host_scene_add_mesh(s, M.v.data(), (uint32_t)(M.v.size() / 3), M.idx.data(),
-                                   (uint32_t)(M.idx.size() / 3), nullptr, nullptr, M.mat.data(), mats.data(),
+                                   (uint32_t)(M.idx.size() / 3), nullptr, uvs, M.mat.data(), mats.data(),
                                    (uint32_t)mats.size());
+}
+
+// C5 textures: 1024^2 RGBA8 procedural images (row 0 = top).
+std::vector<uint32_t> tex_checker(uint32_t n) {
+    std::vector<uint32_t> img((size_t)n * n);
+    for (uint32_t y = 0; y < n; y++)
+        for (uint32_t x = 0; x < n; x++) {
+            bool c = ((x / 32) + (y / 32)) & 1;
+            uint32_t r = c ? 230 : 40, g = c ? 220 : 70, b = c ? 200 : 120;
+            img[(size_t)y * n + x] = r | (g << 8) | (b << 16) | (255u << 24);
+        }
+    return img;
+}
+std::vector<uint32_t> tex_noise(uint32_t n, SplitMix64& R) {
+    // value noise: 4 octaves of bilinearly interpolated lattice values
+    std::vector<float> acc((size_t)n * n, 0.0f);
+    float amp = 0.5f;
+    for (uint32_t cell = 128; cell >= 16; cell /= 2, amp *= 0.5f) {
+        uint32_t m = n / cell + 1;
+        std::vector<float> lat((size_t)m * m);
+        for (auto& v : lat) v = (float)R.range(0.0, 1.0);
+        for (uint32_t y = 0; y < n; y++)
+            for (uint32_t x = 0; x < n; x++) {
+                float fx = (float)x / cell, fy = (float)y / cell;
+                uint32_t ix = (uint32_t)fx, iy = (uint32_t)fy;
+                float tx = fx - ix, ty = fy - iy;
+                float a = lat[iy * m + ix], b = lat[iy * m + ix + 1], c = lat[(iy + 1) * m + ix], d = lat[(iy + 1) * m + ix + 1];
+                acc[(size_t)y * n + x] += amp * ((a * (1 - tx) + b * tx) * (1 - ty) + (c * (1 - tx) + d * tx) * ty);
+            }
+    }
+    std::vector<uint32_t> img((size_t)n * n);
+    for (size_t i = 0; i < img.size(); i++) {
+        float v = std::min(1.0f, std::max(0.0f, acc[i] * 1.1f));
+        uint32_t r = (uint32_t)(60 + 150 * v), g = (uint32_t)(90 + 140 * v), b = (uint32_t)(30 + 60 * v);
+        img[i] = r | (g << 8) | (b << 16) | (255u << 24);
+    }
+    return img;
+}
+
+ctl_material rough_mat(uint32_t dist, float eta, float alpha) {
+    ctl_material m{};
+    m.bsdf_type = CTL_BSDF_ROUGHDIELECTRIC;
+    m.combined_type = CTL_EGLOSSY_REFLECTION | CTL_EGLOSSY_TRANSMISSION;
+    m.two_sided = 0;
+    m.node_light_index = 0xffffffffu;
+    m.reflectance[0] = m.reflectance[1] = m.reflectance[2] = 1.0f;
+    m.texture = 0xffffffffu;
+    m.transmittance[0] = m.transmittance[1] = m.transmittance[2] = 1.0f;
+    m.distribution = dist;
+    m.eta = eta;
+    m.inv_eta = 1.0f / eta;   // roughdielectric::Update
+    m.alpha_u = m.alpha_v = alpha;
+    m.sample_visible = 1;     // getSampleVisible(Beckmann/GGX, true)
+    return m;
 }
 
 ctl_status gen_cornell(ctl_host_scene* s, uint32_t W, uint32_t H) {
@@ -197,12 +252,29 @@ ctl_status gen_c2(ctl_host_scene* s, double scale, uint32_t W, uint32_t H) {
     return ctl_host_scene_set_camera(s, pos, tar, up, 60.0f, 1.0f, 100000.0f, W, H);
 }
 
-ctl_status gen_c3(ctl_host_scene* s, double scale, uint32_t W, uint32_t H) {
+ctl_status gen_c3(ctl_host_scene* s, double scale, uint32_t W, uint32_t H, bool c5) {
     SplitMix64 R{0x5EED};
     std::vector<ctl_material> mats;
     for (int i = 0; i < 16; i++)
         mats.push_back(diffuse_mat((float)R.range(0.3, 0.8), (float)R.range(0.3, 0.8), (float)R.range(0.3, 0.8)));
     mats.push_back(diffuse_mat(0.8f, 0.8f, 0.8f));   // 16: lights
+    if (c5) {
+        // C5 materials (a separate stream, so the geometry stays C3's): 5 of the
+        // 16 roughdielectric (Beckmann / GGX alternating, eta 1.5, alpha in
+        // [0.05, 0.5]), 5 diffuse with an image texture (checker: trilinear,
+        // noise: EWA), the rest constant diffuse.
+        SplitMix64 Q{0x5EED ^ 0xC5C5ull};
+        const float ident[6] = {1, 0, 0, 0, 1, 0}, one[3] = {1, 1, 1};
+        std::vector<uint32_t> chk = tex_checker(1024), noi = tex_noise(1024, Q);
+        int tc = ctl_host_scene_add_texture(s, chk.data(), 1024, 1024, CTL_TEX_TRILINEAR, CTL_WRAP_REPEAT, ident, one);
+        int tn = ctl_host_scene_add_texture(s, noi.data(), 1024, 1024, CTL_TEX_EWA, CTL_WRAP_REPEAT, ident, one);
+        if (tc < 0 || tn < 0) return CTL_ERR_INVALID;
+        const int rough[5] = {0, 3, 6, 10, 13}, texd[5] = {1, 4, 7, 11, 14};
+        for (int k = 0; k < 5; k++)
+            mats[rough[k]] = rough_mat(k % 2 ? CTL_MICROFACET_GGX : CTL_MICROFACET_BECKMANN, 1.5f,
+                                       (float)Q.range(0.05, 0.5));
+        for (int k = 0; k < 5; k++) mats[texd[k]].texture = (uint32_t)(k % 2 ? tn : tc);
+    }
     MeshB M;
     const double half = 100.0;
     // terrain: 2M triangles
@@ -250,7 +322,15 @@ ctl_status gen_c3(ctl_host_scene* s, double scale, uint32_t W, uint32_t H) {
     // two 24 x 24 m quad lights at y = 60, facing down
     M.quad({-28, 60, -40}, {-28, 60, -16}, {-52, 60, -16}, {-52, 60, -40}, 16);
     M.quad({52, 60, 16}, {52, 60, 40}, {28, 60, 40}, {28, 60, 16}, 16);
-    int mi = add_mesh(s, M, mats);
+    std::vector<float> uv;
+    if (c5) {   // planar world-space UVs: the textures repeat every 50 m
+        uv.resize(M.v.size() / 3 * 2);
+        for (size_t i = 0; i < M.v.size() / 3; i++) {
+            uv[2 * i] = (M.v[3 * i] + 100.0f) / 50.0f;
+            uv[2 * i + 1] = (M.v[3 * i + 2] + 100.0f) / 50.0f;
+        }
+    }
+    int mi = add_mesh(s, M, mats, c5 ? uv.data() : nullptr);
     if (mi < 0) return CTL_ERR_INVALID;
     int ni = ctl_host_scene_add_node(s, (uint32_t)mi, nullptr);
     if (ni < 0) return CTL_ERR_INVALID;
@@ -269,7 +349,8 @@ extern "C" CTL_API ctl_status ctl_host_scene_generate(ctl_host_scene* s, int32_t
     switch (config) {
         case 1: return gen_cornell(s, width, height);
         case 2: return gen_c2(s, scale, width, height);
-        case 3: return gen_c3(s, scale, width, height);
-        default: ctl::set_host_error("generate: config must be 1, 2 or 3"); return CTL_ERR_INVALID;
+        case 3: return gen_c3(s, scale, width, height, false);
+        case 5: return gen_c3(s, scale, width, height, true);
+        default: ctl::set_host_error("generate: config must be 1, 2, 3 or 5"); return CTL_ERR_INVALID;
     }
 }

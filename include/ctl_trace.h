@@ -122,24 +122,58 @@ typedef struct { float rgb[3]; float rgb_splat[3]; float weight_sum; } ctl_pixel
 /* ------------------------------------------------------------------------ */
 
 enum {                        /* BSDF TYPE_FUNC ids (SceneTypes/BSDF_Simple.h) */
-    CTL_BSDF_DIFFUSE = 1,         /* diffuse, BSDF_Simple.cu:7-75             */
-    CTL_BSDF_ROUGHDIELECTRIC = 5  /* reserved (config C5, not yet supported) */
+    CTL_BSDF_DIFFUSE = 1,         /* diffuse, BSDF_Simple.cu:7-75                  */
+    CTL_BSDF_ROUGHDIELECTRIC = 5  /* roughdielectric, BSDF_Simple.cu:373-615        */
 };
 
 /* EBSDFType bits used by the path (SceneTypes/Samples.h:32-60). */
 enum {
     CTL_EDIFFUSE_REFLECTION = 0x00002,
-    CTL_EDIFFUSE_TRANSMISSION = 0x00004
+    CTL_EDIFFUSE_TRANSMISSION = 0x00004,
+    CTL_EGLOSSY_REFLECTION = 0x00008,
+    CTL_EGLOSSY_TRANSMISSION = 0x00010
 };
 
+/* MicrofacetDistribution::EType (Engine/MicrofacetDistribution.h:14-21). */
+enum { CTL_MICROFACET_BECKMANN = 0, CTL_MICROFACET_GGX = 1 };
+
+/* Material + the parameters of its BSDF (the reference keeps them in the
+ * BSDFALL CudaVirtualAggregate, SceneTypes/BSDF.h:140), 80 B.  Textures other
+ * than ConstantTexture are supported for diffuse::m_reflectance only. */
 typedef struct {
     uint32_t bsdf_type;          /* CTL_BSDF_*                                   */
-    uint32_t combined_type;      /* BSDF::m_combinedType (EDiffuseReflection)    */
+    uint32_t combined_type;      /* BSDF::m_combinedType (EBSDFType bits)        */
     uint32_t two_sided;          /* BSDF::m_enableTwoSided                       */
     uint32_t node_light_index;   /* Material::NodeLightIndex, 0xFFFFFFFF = none  */
-    float reflectance[3];        /* ConstantTexture value of diffuse::m_reflectance */
-    float pad;
+    float reflectance[3];        /* diffuse: ConstantTexture value of m_reflectance;
+                                    roughdielectric: m_specularReflectance       */
+    uint32_t texture;            /* diffuse: ImageTexture index of m_reflectance
+                                    (0xFFFFFFFF: the constant above)             */
+    float transmittance[3];      /* roughdielectric: m_specularTransmittance     */
+    uint32_t distribution;       /* roughdielectric: CTL_MICROFACET_*            */
+    float eta, inv_eta;          /* roughdielectric: m_eta, m_invEta = 1/m_eta   */
+    float alpha_u, alpha_v;      /* ConstantTexture values of m_alphaU / m_alphaV */
+    uint32_t sample_visible;     /* m_sampleVisible                              */
+    uint32_t pad[3];
 } ctl_material;
+
+/* ImageTexture (SceneTypes/Texture.h:159-183) with its TextureMapping2D and
+ * the KernelMIPMap it samples (Engine/MIPMap_device.h:59-80).  Texels are
+ * RGBCOL (r, g, b, a bytes, little-endian uint32) in the scene's tex_data
+ * array; level l starts at tex_data[offsets[l]] and is (width >> l) x
+ * (height >> l). */
+enum { CTL_TEX_POINT = 0, CTL_TEX_BILINEAR = 1, CTL_TEX_EWA = 2, CTL_TEX_TRILINEAR = 3 };   /* ImageFilter */
+enum { CTL_WRAP_REPEAT = 0, CTL_WRAP_CLAMP = 1, CTL_WRAP_MIRROR = 2, CTL_WRAP_BLACK = 3 };  /* ImageWrap */
+typedef struct {
+    float m11, m12, m13, m21, m22, m23;   /* TextureMapping2D                     */
+    uint32_t set_id;                      /* must be 0 (one UV set in TriangleData) */
+    float scale[3];                       /* ImageTexture::m_scale                */
+    uint32_t width, height, levels;       /* KernelMIPMap m_uWidth/m_uHeight/m_uLevels */
+    uint32_t filter;                      /* CTL_TEX_*                            */
+    uint32_t wrap;                        /* CTL_WRAP_*                           */
+    uint32_t offsets[16];                 /* m_sOffsets (MAX_MIPS 16)             */
+    float weight_lut[64];                 /* m_weightLut (MTS_MIPMAP_LUT_SIZE 64) */
+} ctl_texture;
 
 /* ShapeSet::triData, 64 B (Engine/ShapeSet.h:17-27), world space. */
 typedef struct {
@@ -211,6 +245,9 @@ typedef struct {
     const ctl_light_tri* light_tris;    uint32_t n_light_tris;
     const float* light_tri_cdf;         uint32_t n_light_tri_cdf;
     float light_cdf[CTL_MAX_NUM_LIGHTS];/* m_pLightCDF (lights are active, identity index map) */
+    /* m_sTexData: image textures and their texel data */
+    const ctl_texture* textures;        uint32_t n_textures;
+    const uint32_t* tex_data;           uint64_t n_tex_data;
     uint32_t env_map_index;             /* must be 0xFFFFFFFF (no environment)  */
     float box_min[3], box_max[3];       /* m_sBox                               */
     float ray_eps;                      /* m_rayTraceEps, DynamicScene.cpp:587  */
@@ -340,6 +377,14 @@ CTL_API int32_t ctl_host_scene_add_mesh(ctl_host_scene* s, const float* vertices
                                         const ctl_material* materials, uint32_t n_materials);
 /* Adds a node (instance) of a mesh with an object->world transform (row-major
  * 4x4, NULL = identity); returns the node index or -1. */
+/* Adds an ImageTexture over the RGBA8 image `rgba` (width x height, both
+ * powers of two, row 0 = top as loaded images are): builds the MIP pyramid
+ * (2x2 box filter) and the EWA weight table (MIPMap.cpp:88-93).  mapping =
+ * TextureMapping2D {m11, m12, m13, m21, m22, m23}, scale = m_scale.  Returns
+ * the texture index for ctl_material.texture, or -1. */
+CTL_API int32_t ctl_host_scene_add_texture(ctl_host_scene* s, const uint32_t* rgba, uint32_t width, uint32_t height,
+                                           uint32_t filter, uint32_t wrap, const float mapping[6],
+                                           const float scale[3]);
 CTL_API int32_t ctl_host_scene_add_node(ctl_host_scene* s, uint32_t mesh, const float* xf16);
 /* Marks material `local_material` of `node` as a DiffuseLight with constant
  * radiance (DynamicScene::CreateLight on a mesh part). Returns the light index. */
@@ -363,7 +408,10 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
 CTL_API const char* ctl_host_last_error(void);
 
 /* Synthetic workloads of BASELINE.json (seed 0x5EED): 1 = C1 Cornell box
- * (32 tris), 2 = C2 100k-tri field, 3 = C3 ~10M-tri "San-Miguel-scale".
+ * (32 tris), 2 = C2 100k-tri field, 3 = C3 ~10M-tri "San-Miguel-scale",
+ * 5 = C5: C3 geometry with 30 % roughdielectric (Beckmann / GGX, eta 1.5,
+ * alpha 0.05-0.5) and 30 % image-textured diffuse materials (procedural
+ * 1024^2 checker/noise MIP maps, trilinear and EWA filtering).
  * `scale` multiplies the triangle budget (1.0 = the named size).  The camera
  * resolution is width x height. */
 CTL_API ctl_status ctl_host_scene_generate(ctl_host_scene* s, int32_t config, double scale,

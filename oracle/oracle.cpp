@@ -357,6 +357,9 @@ inline Spec spec_div(Spec s, float f) { float recip = 1.0f / f; return s * recip
 
 struct DG {   // DifferentialGeometry subset
     V3 P; Frame sys; V3 n; V3 dpdu, dpdv; V2 bary;
+    V2 uv;                                   // uv[0]
+    float dudx = 0, dudy = 0, dvdx = 0, dvdy = 0;
+    bool hasUVPartials = false;              // set by computePartials, never reset (PathTracer.cu:16,60)
 };
 
 void fill_dg(const SceneView& S, V2 bary, uint32_t triIdx, uint32_t nodeIdx, DG& dg, bool quirk) {
@@ -378,6 +381,9 @@ void fill_dg(const SceneView& S, V2 bary, uint32_t triIdx, uint32_t nodeIdx, DG&
     dg.dpdu = transformDirection(L2W, dpdu);
     dg.dpdv = transformDirection(L2W, dpdv);
     dg.n = normalize(cross(dg.dpdu, dg.dpdv));
+    V2 ta = v2(hf(w[5] & 0xffff), hf(w[5] >> 16)), tb = v2(hf(w[6] & 0xffff), hf(w[6] >> 16)),
+       tc = v2(hf(w[7] & 0xffff), hf(w[7] >> 16));
+    dg.uv = u * ta + v * tb + ww * tc;
     if (dot(dg.n, dg.sys.n) < 0.0f) dg.n = -dg.n;
 }
 
@@ -396,8 +402,18 @@ uint32_t light_index(const SceneView& S, uint32_t tri, uint32_t node) {  // Trac
     return S.d->nodes[node].lights[m.node_light_index];
 }
 
+}  // namespace
+#include "oracle_c5.h"
+namespace {
+
+// diffuse::m_reflectance.Evaluate(bRec.dg): ConstantTexture or ImageTexture
+Spec diffuse_R(const ctl_scene_desc* d, const ctl_material& m, const DG& dg) {
+    if (m.texture != UINT_MAX) return c5::image_eval(d->textures + m.texture, d->tex_data, dg);
+    return v3(m.reflectance[0], m.reflectance[1], m.reflectance[2]);
+}
+
 // diffuse (BSDF_Simple.cu:7-75) under BSDFALL two-sided wrapper (BSDF.h:147-208)
-Spec diffuse_sample(const ctl_material& m, BRec& b, float& pdf, V2 sample) {
+Spec diffuse_sample(const ctl_scene_desc* d, const ctl_material& m, BRec& b, float& pdf, V2 sample) {
     bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
     Spec res;
@@ -416,19 +432,19 @@ Spec diffuse_sample(const ctl_material& m, BRec& b, float& pdf, V2 sample) {
         float z = sqrtf(1.0f - p.x * p.x - p.y * p.y);
         b.wo = v3(p.x, p.y, z);
         pdf = fabsf(O_INV_PI * b.wo.z) * 1.0f;
-        res = v3(m.reflectance[0], m.reflectance[1], m.reflectance[2]) * 1.0f;
+        res = diffuse_R(d, m, b.dg) * 1.0f;
     }
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
     return res;
 }
-Spec diffuse_f(const ctl_material& m, BRec& b) {
+Spec diffuse_f(const ctl_scene_desc* d, const ctl_material& m, BRec& b) {
     bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
     Spec res = v3s(0.0f);
     if (b.typeMask & m.combined_type) {
         bool validRefl = m.combined_type == CTL_EDIFFUSE_REFLECTION && b.wi.z > 0 && b.wo.z > 0;
         bool validTrans = m.combined_type == CTL_EDIFFUSE_TRANSMISSION && b.wi.z * b.wo.z < 0;
-        Spec s = v3(m.reflectance[0], m.reflectance[1], m.reflectance[2]) * (O_INV_PI * fabsf(b.wo.z));
+        Spec s = diffuse_R(d, m, b.dg) * (O_INV_PI * fabsf(b.wo.z));
         if (validRefl || validTrans) res = s;
         else if (m.combined_type == (CTL_EDIFFUSE_REFLECTION | CTL_EDIFFUSE_TRANSMISSION)) res = s * 0.5f;
     }
@@ -448,6 +464,33 @@ float diffuse_pdf(const ctl_material& m, BRec& b) {
     }
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
     return res;
+}
+
+// BSDFALL::sample / f / pdf (BSDF.h:140-208): the type switch; diffuse does its
+// own two-sided flip above, roughdielectric gets the wrapper here.
+Spec bsdf_sample(const ctl_scene_desc* d, const ctl_material& m, BRec& b, float& pdf, V2 sample) {
+    if (m.bsdf_type == CTL_BSDF_DIFFUSE) return diffuse_sample(d, m, b, pdf, sample);
+    bool flip = b.wi.z < 0 && m.two_sided;
+    if (flip) b.wi.z *= -1.0f;
+    Spec r = c5::rough_sample(m, b, pdf, sample);
+    if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
+    return r;
+}
+Spec bsdf_f(const ctl_scene_desc* d, const ctl_material& m, BRec& b) {
+    if (m.bsdf_type == CTL_BSDF_DIFFUSE) return diffuse_f(d, m, b);
+    bool flip = b.wi.z < 0 && m.two_sided;
+    if (flip) b.wi.z *= -1.0f;
+    Spec r = c5::rough_f(m, b);
+    if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
+    return r;
+}
+float bsdf_pdf(const ctl_scene_desc*, const ctl_material& m, BRec& b) {
+    if (m.bsdf_type == CTL_BSDF_DIFFUSE) return diffuse_pdf(m, b);
+    bool flip = b.wi.z < 0 && m.two_sided;
+    if (flip) b.wi.z *= -1.0f;
+    float r = c5::rough_pdf(m, b);
+    if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
+    return r;
 }
 
 struct DRec {   // DirectSamplingRecord
@@ -553,11 +596,11 @@ Spec estimate_direct(RenderCtx& C, BRec bRec, const ctl_material& mat, const ctl
     if (!spec_zero(value)) {
         bRec.wo = toLocal(bRec.dg.sys, dRec.d);
         bRec.typeMask = EAll & ~EDelta;
-        Spec bsdfVal = diffuse_f(mat, bRec);
+        Spec bsdfVal = bsdf_f(C.S.d, mat, bRec);
         if (!spec_zero(bsdfVal) && !occluded(C, dRec.ref, dRec.d, dRec.dist)) {
             float weight = 1.0f;
             if (dRec.measure != EDiscrete) {
-                const float bsdfPdf = diffuse_pdf(mat, bRec);
+                const float bsdfPdf = bsdf_pdf(C.S.d, mat, bRec);
                 const float directPdf = dRec.pdf * light_pdf;   // measure is ESolidAngle
                 weight = power_heuristic(directPdf, bsdfPdf);
             }
@@ -589,7 +632,7 @@ Spec uniform_sample_one_light(RenderCtx& C, const BRec& bRec, const ctl_material
 }
 
 // PathTrace<true> restricted to surfaces without media / env map (PathTracer.cu:10-113)
-Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, int maxPathLength, int rrStartDepth) {
+Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, V3 rXo, V3 rXd, V3 rYo, V3 rYd, int maxPathLength, int rrStartDepth) {
     const ctl_scene_desc* d = C.S.d;
     Spec cl = v3s(0.0f), cf = v3s(1.0f);
     int depth = 0;
@@ -615,6 +658,7 @@ Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, int maxPathLength, int rrStartDe
                 bRec.dg.sys.n = -bRec.dg.sys.n;
                 bRec.wi.z *= -1.0f;
             }
+            if (depth == 1) c5::compute_partials(bRec.dg, rXo, rXd, rYo, rYd);   // PathTracer.cu:60-61
             uint32_t li = light_index(C.S, r2.tri, r2.node);
             if (li != UINT_MAX) {
                 float misWeight = 1.0f;
@@ -631,7 +675,7 @@ Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, int maxPathLength, int rrStartDe
                 Spec Le = (dot(bRec.dg.sys.n, w) <= 0) ? v3s(0.0f) : v3(L.radiance[0], L.radiance[1], L.radiance[2]);
                 cl = cl + (cf * misWeight) * Le;
             }
-            Spec f = diffuse_sample(mat, bRec, brdf_scattering_pdf, C.rng->randomFloat2());
+            Spec f = bsdf_sample(d, mat, bRec, brdf_scattering_pdf, C.rng->randomFloat2());
             last_nor = bRec.dg.sys.n;
             if ((mat.combined_type & ESmooth) != 0) cl = cl + cf * uniform_sample_one_light(C, bRec, mat);
             specularBounce = (bRec.sampledType & EDelta) != 0;
@@ -647,6 +691,17 @@ Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, int maxPathLength, int rrStartDe
     }
     if (r2.tri == UINT_MAX) cl = cl + (cf * 1.0f) * v3s(0.0f);   // EvalEnvironment without env map
     return cl;
+}
+
+// PerspectiveSensor::sampleRayDifferential's rayX / rayY (Sensor.cu:138-141)
+void sensor_ray_diff(const ctl_camera& cam, V2 pixelSample, V3& ori, V3& dX, V3& dY) {
+    M44 s2c, tw;
+    std::memcpy(s2c.d, cam.sample_to_camera.m, 64);
+    std::memcpy(tw.d, cam.to_world.m, 64);
+    V3 nearP = transformPoint(s2c, v3(pixelSample.x * cam.inv_resolution[0], pixelSample.y * cam.inv_resolution[1], 0.0f));
+    ori = transformPoint(tw, v3s(0.0f));
+    dX = transformDirection(tw, normalize(nearP + v3(cam.dx[0], cam.dx[1], cam.dx[2])));
+    dY = transformDirection(tw, normalize(nearP + v3(cam.dy[0], cam.dy[1], cam.dy[2])));
 }
 
 void sensor_ray(const ctl_camera& cam, V2 pixelSample, V3& ori, V3& dir) {
@@ -879,9 +934,10 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
                 V2 pX = v2((float)x, (float)y) + rng.randomFloat2();
                 V2 aperture = rng.randomFloat2();
                 (void)aperture;
-                V3 o, dd;
+                V3 o, dd, xo, dX, dY;
                 sensor_ray(cam, pX, o, dd);
-                Spec col = v3s(1.0f) * path_trace(C, o, dd, prm->max_path_length, prm->rr_start_depth);
+                sensor_ray_diff(cam, pX, xo, dX, dY);
+                Spec col = v3s(1.0f) * path_trace(C, o, dd, xo, dX, xo, dY, prm->max_path_length, prm->rr_start_depth);
                 add_sample(fb, W, H, pX.x, pX.y, col);
             }
         }

@@ -41,6 +41,11 @@ static inline float cr_cos(float x) { return (float)std::cos((double)x); }
 static inline float cr_tan(float x) { return (float)std::tan((double)x); }
 static inline float cr_acos(float x) { return (float)std::acos((double)x); }
 static inline float cr_atan2(float y, float x) { return (float)std::atan2((double)y, (double)x); }
+static inline float cr_atan(float x) { return (float)std::atan((double)x); }
+static inline float cr_exp(float x) { return (float)std::exp((double)x); }
+static inline float cr_log(float x) { return (float)std::log((double)x); }
+static inline float cr_log2(float x) { return (float)std::log2((double)x); }
+static inline float cr_pow(float a, float b) { return (float)std::pow((double)a, (double)b); }
 
 // --- vectors (Vector.h VectorBase: component-wise ops, dot/lenSqr start at 0)
 struct V2 { float x, y; };

@@ -37,6 +37,8 @@ def test_reference_layout_sizes():
     assert C.sizeof(abi.Hit) == 16            # traversalResult
     assert C.sizeof(abi.Pixel) == 28          # PixelData
     assert C.sizeof(abi.LightTri) == 64       # ShapeSet::triData
+    assert C.sizeof(abi.Material) == 80       # flattened Material + BSDF parameters
+    assert C.sizeof(abi.Texture) == 380       # ImageTexture + KernelMIPMap
 
 
 def test_create_without_gpu_fails_cleanly():
