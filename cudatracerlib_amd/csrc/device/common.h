@@ -174,6 +174,11 @@ __device__ __forceinline__ f2 primary_ray(const DevScene& S, SamplerDev& rng, ui
 // throughput update and Russian roulette.  Returns false when RR ends the path.
 // Sampler draws are in the reference order: BSDF 2D, light choice 2D, light
 // position 2D, RR 1D.
+// FULL = the scene has C5 materials (roughdielectric or image textures): ray
+// differentials, partials and the BSDF type switch.  Scenes with constant
+// diffuse materials only take the lean instantiation — the partials are only
+// observable through textures, so both give identical results there.
+template <bool FULL>
 __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P, SamplerDev& rng, PathVars& v,
                                           const HitRec& r, ShadowReq& sh) {
     sh.valid = false;
@@ -195,15 +200,17 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
         dg.sys.n = -dg.sys.n;
         b.wi.z *= -1.0f;
     }
-    if (v.depth == 1) {   // bRec.dg.computePartials(r, rX, rY) (PathTracer.cu:60-61)
-        f3 co, dX, dY;
-        sensor_diff(S, v.pX, co, dX, dY);
-        compute_partials(dg, co, dX, co, dY);
-        v.dudx = dg.dudx; v.dudy = dg.dudy; v.dvdx = dg.dvdx; v.dvdy = dg.dvdy;
-        v.has_partials = true;
-    } else {
-        dg.dudx = v.dudx; dg.dudy = v.dudy; dg.dvdx = v.dvdx; dg.dvdy = v.dvdy;
-        dg.has_partials = v.has_partials;
+    if (FULL) {
+        if (v.depth == 1) {   // bRec.dg.computePartials(r, rX, rY) (PathTracer.cu:60-61)
+            f3 co, dX, dY;
+            sensor_diff(S, v.pX, co, dX, dY);
+            compute_partials(dg, co, dX, co, dY);
+            v.dudx = dg.dudx; v.dudy = dg.dudy; v.dvdx = dg.dvdx; v.dvdy = dg.dvdy;
+            v.has_partials = true;
+        } else {
+            dg.dudx = v.dudx; dg.dudy = v.dudy; dg.dvdx = v.dvdx; dg.dvdy = v.dvdy;
+            dg.has_partials = v.has_partials;
+        }
     }
     const TexView tex{S.textures, S.tex_data};
     if (mat.node_light_index != 0xffffffffu) {
@@ -221,7 +228,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
         spec Le = (dot(dg.sys.n, w) <= 0) ? mk3s(0.0f) : mk3(L.radiance[0], L.radiance[1], L.radiance[2]);
         v.cl = v.cl + (v.cf * misWeight) * Le;
     }
-    spec f = bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex);
+    spec f = FULL ? bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex) : diffuse_sample(mat, b, v.brdf_pdf, rng.next2());
     v.last_nor = dg.sys.n;
     if ((mat.combined_type & kESmooth) != 0 && S.n_lights) {
         f2 sample = rng.next2();
@@ -244,10 +251,11 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
             bsdf_rec b2 = b;
             b2.wo = to_local(dg.sys, dRec.d);
             b2.type_mask = kEAll & ~kEDelta;
-            spec bsdfVal = bsdf_f(mat, b2, dg, &tex);
+            spec bsdfVal = FULL ? bsdf_f(mat, b2, dg, &tex) : diffuse_f(mat, b2);
             if (!spec_zero(bsdfVal)) {
                 float weight = 1.0f;
-                if (dRec.measure != kEDiscrete) weight = power_heuristic(dRec.pdf * lpdf, bsdf_pdf(mat, b2));
+                if (dRec.measure != kEDiscrete)
+                    weight = power_heuristic(dRec.pdf * lpdf, FULL ? bsdf_pdf(mat, b2) : diffuse_pdf(mat, b2));
                 spec ret = value * bsdfVal * weight;
                 ret = ret * mk3s(1.0f);
                 sh.valid = true;

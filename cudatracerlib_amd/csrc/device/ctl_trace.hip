@@ -45,6 +45,9 @@ static_assert(sizeof(ctl_light_tri) == 64, "ShapeSet::triData is 64 B");
 static_assert(sizeof(ctl_material) == 80, "ctl_material is 80 B");
 static_assert(sizeof(ctl_texture) == 380, "ctl_texture is 380 B");
 
+#ifndef CTL_PERSIST_WAVES_FULL
+#define CTL_PERSIST_WAVES_FULL 4   // ... with the C5 shading (textures, microfacets)
+#endif
 #ifndef CTL_PERSIST_WAVES
 #define CTL_PERSIST_WAVES 6   // waves/SIMD for the persistent path kernel: measured best on C3
                               // (4: 732, 5: 758, 6: 789, 7: 781, 8: 768 Mrays/s); its spills
@@ -55,7 +58,7 @@ namespace {
 
 // Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
 // traversals inline in the bounce, as the reference's pathKernel2 runs it.
-template <bool STATS, bool SINGLE, bool WIDE>
+template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
 struct PathCtx {
     const DevScene& S;
     const PathParams& P;
@@ -78,7 +81,7 @@ struct PathCtx {
             return false;
         }
         ShadowReq sh;
-        const bool cont = shade_hit(S, P, rng, v, r2, sh);
+        const bool cont = shade_hit<FULL>(S, P, rng, v, r2, sh);
         if (sh.valid) {
             const bool any = P.shadow_any_hit != 0;
             HitRec h;
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict
 }
 
 // One path per thread (the reference's pathKernel2 launch shape).
-template <bool STATS, bool SINGLE, bool WIDE>
+template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
 __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
                                                       ctl_pixel* fb, unsigned long long* counters) {
     CTL_LANE_STACK(st);
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
     if (work_pixel(P, g, px, py)) {
         const uint32_t idx = py * P.width + px;   // TracerBase::getPixelIndex (Tracer.h:89-97)
         SamplerDev rng{s1, s2, P.nseq, P.len, idx % P.nseq, (idx / P.nseq) % P.nseq, 0, 0};
-        PathCtx<STATS, SINGLE, WIDE> C{S, P, rng, st, 0, TraceStats{0, 0, 0}, true, PathVars{}};
+        PathCtx<STATS, SINGLE, WIDE, FULL> C{S, P, rng, st, 0, TraceStats{0, 0, 0}, true, PathVars{}};
         f3 o, dw;
         const f2 pX = primary_ray(S, rng, px, py, o, dw);
         C.v.begin(pX, o, dw);
@@ -198,8 +201,8 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
 //    pending ray are loop-carried, keeping the register peak low.
 // Pixels are independent (own sampler index, single owner in the framebuffer)
 // so the framebuffer is bit-identical to path_kernel's.
-template <bool STATS, bool SINGLE, bool WIDE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? CTL_PERSIST_WAVES : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
+template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? (FULL ? CTL_PERSIST_WAVES_FULL : CTL_PERSIST_WAVES) : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
                                                                  const float2* s2, ctl_pixel* fb, uint64_t items,
                                                                  uint32_t* cursor, unsigned long long* counters) {
     CTL_LANE_STACK(st);
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                 v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);   // no environment map
                 cont = false;
             } else {
-                ending = !shade_hit(S, P, rng, v, h, sh);
+                ending = !shade_hit<FULL>(S, P, rng, v, h, sh);
                 shadowPhase = sh.valid;
                 cont = sh.valid || (!ending && v.depth++ < P.max_path_length);
             }
@@ -588,6 +591,9 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     S.ray_eps = d->ray_eps;
     for (int i = 0; i < CTL_MAX_NUM_LIGHTS; i++) S.light_cdf[i] = d->light_cdf[i];
     S.camera = d->camera;
+    S.full_shading = 0;
+    for (uint32_t i = 0; i < d->n_materials; i++)
+        if (d->materials[i].bsdf_type != CTL_BSDF_DIFFUSE || d->materials[i].texture != 0xffffffffu) S.full_shading = 1;
     S.single = 0;
     if (d->n_nodes > 0 && d->scene_start_node < 0) {
         uint32_t node = ~(uint32_t)d->scene_start_node;
@@ -746,28 +752,33 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
     const bool single = c->scene.single != 0;
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;
+    const bool full = c->scene.full_shading != 0;
     if (!(p->flags & CTL_PT_MEGAKERNEL)) {
         uint32_t* cursor = c->d_cursors + 1;
         CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(uint32_t), s));
         const uint64_t want = (threads + kBlock - 1) / kBlock;
-#define PK(ST, SG, WD)                                                                                           \
+#define PK(ST, SG, WD, FU)                                                                                       \
         do {                                                                                                     \
             static int nb = 0;                                                                                   \
-            if (!nb) nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD>, kStackLdsBytes);                \
-            hipLaunchKernelGGL((path_kernel_persistent<ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)), \
+            if (!nb) nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD, FU>, kStackLdsBytes);            \
+            hipLaunchKernelGGL((path_kernel_persistent<ST, SG, WD, FU>), dim3((unsigned)std::min<uint64_t>(nb, want)), \
                                dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, fb, threads, cursor,        \
                                c->d_counters);                                                                   \
         } while (0)
-        if (stats) { if (single) PK(true, true, false); else PK(true, false, false); }
-        else if (wide) { if (single) PK(false, true, true); else PK(false, false, true); }
-        else { if (single) PK(false, true, false); else PK(false, false, false); }
+#define PK2(ST, SG, WD) do { if (full) PK(ST, SG, WD, true); else PK(ST, SG, WD, false); } while (0)
+        if (stats) { if (single) PK2(true, true, false); else PK2(true, false, false); }
+        else if (wide) { if (single) PK2(false, true, true); else PK2(false, false, true); }
+        else { if (single) PK2(false, true, false); else PK2(false, false, false); }
+#undef PK2
 #undef PK
     } else {
-#define MK(ST, SG, WD) hipLaunchKernelGGL((path_kernel<ST, SG, WD>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, \
-                                          s2, fb, c->d_counters)
-        if (stats) { if (single) MK(true, true, false); else MK(true, false, false); }
-        else if (wide) { if (single) MK(false, true, true); else MK(false, false, true); }
-        else { if (single) MK(false, true, false); else MK(false, false, false); }
+#define MK(ST, SG, WD, FU) hipLaunchKernelGGL((path_kernel<ST, SG, WD, FU>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, \
+                                              P, s1, s2, fb, c->d_counters)
+#define MK2(ST, SG, WD) do { if (full) MK(ST, SG, WD, true); else MK(ST, SG, WD, false); } while (0)
+        if (stats) { if (single) MK2(true, true, false); else MK2(true, false, false); }
+        else if (wide) { if (single) MK2(false, true, true); else MK2(false, false, true); }
+        else { if (single) MK2(false, true, false); else MK2(false, false, false); }
+#undef MK2
 #undef MK
     }
     CTL_HIP(c, hipGetLastError());

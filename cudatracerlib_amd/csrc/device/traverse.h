@@ -71,6 +71,7 @@ struct DevScene {
     const float4* scene_wbvh;    // instance-level wide nodes
     const uint32_t* mesh_wbase;  // first wide node of each mesh
     uint32_t wide;               // wide trees present (scene flag CTL_SCENE_BINARY_BVH clear)
+    uint32_t full_shading;       // C5 materials present (shade_hit<true>)
     uint32_t tie_min;            // exact-t ties -> lowest (triangle, node) instead of first found
     uint32_t s_wnode_base;
 };

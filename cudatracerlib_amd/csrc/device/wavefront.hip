@@ -165,6 +165,7 @@ void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32
 #undef LT
 }
 
+template <bool FULL>
 __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
                                                           WfState W, int bounce, ctl_pixel* fb) {
     const uint32_t count = W.counts[2 * bounce];
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams
             HitRec h;
             h.t = hit.x; h.u = hit.y; h.v = hit.z; h.tri = (uint32_t)__float_as_int(hit.w); h.node = W.hit_node[i];
             if (h.tri != 0xffffffffu) {
-                bool terminated = !shade_hit(S, P, rng, v, h, sh);
+                bool terminated = !shade_hit<FULL>(S, P, rng, v, h, sh);
                 pushShadow = sh.valid;
                 if (!terminated) {
                     // loop head of the next bounce: `while (depth++ < MaxPathLength)`
@@ -301,7 +302,10 @@ int wavefront_pass(ctl_ctx* c, const PathParams& P, ctl_pixel* fb, bool stats, h
     for (int b = 0; b < maxB; b++) {
         const uint32_t* cnt = &W.counts[2 * b];
         launch_trace<0>(c, s, W.q[b & 1], cnt, &cursors[2 * b], stats);
-        hipLaunchKernelGGL(wf_shade_kernel, dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, fb);
+        if (c->scene.full_shading)
+            hipLaunchKernelGGL((wf_shade_kernel<true>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, fb);
+        else
+            hipLaunchKernelGGL((wf_shade_kernel<false>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, fb);
         const uint32_t* scnt = &W.counts[2 * b + 1];
         if (P.shadow_any_hit) launch_trace<1>(c, s, W.sq, scnt, &cursors[2 * b + 1], stats);
         else launch_trace<2>(c, s, W.sq, scnt, &cursors[2 * b + 1], stats);
