@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--schedule", default="persistent", choices=["persistent", "megakernel", "wavefront"])
     ap.add_argument("--split-alpha", type=float, default=None, help="BVH reference splitting (default: library's)")
     ap.add_argument("--split-depth", type=int, default=8)
+    ap.add_argument("--bins", type=int, default=0, help="SAH bins (0: library default)")
+    ap.add_argument("--max-leaf", type=int, default=0, help="max leaf size (0: library default)")
     ap.add_argument("--bvh", default="wide", choices=["wide", "binary"],
                     help="device traversal: 4-wide collapsed BVH, or the reference's binary order")
     return ap.parse_args()
@@ -152,8 +154,8 @@ def main():
 
     t0 = time.perf_counter()
     hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
-    if a.split_alpha is not None:
-        hs.set_bvh_params(a.split_alpha, a.split_depth)
+    if a.split_alpha is not None or a.bins or a.max_leaf:
+        hs.set_bvh_params(0.5 if a.split_alpha is None else a.split_alpha, a.split_depth, a.bins, a.max_leaf)
     desc = hs.compile(threads=threads)
     if a.bvh == "binary":
         desc.flags |= ctl.CTL_SCENE_BINARY_BVH

@@ -158,10 +158,11 @@ class HostScene:
     def set_flags(self, flags):
         _check(self._L.ctl_host_scene_set_flags(self._h, flags), None, "set_flags")
 
-    def set_bvh_params(self, split_alpha=0.5, split_depth=8):
-        """Reference splitting of large triangles before the BVH build (0 disables)."""
-        _check(self._L.ctl_host_scene_set_bvh_params(self._h, float(split_alpha), int(split_depth)), None,
-               "set_bvh_params")
+    def set_bvh_params(self, split_alpha=0.5, split_depth=8, bins=0, max_leaf=0):
+        """BVH build knobs: reference splitting of large triangles (split_alpha = 0
+        disables), SAH bins per axis and max leaf size (0 = library default)."""
+        _check(self._L.ctl_host_scene_set_bvh_params(self._h, float(split_alpha), int(split_depth), int(bins),
+                                                      int(max_leaf)), None, "set_bvh_params")
         return self
 
     def compile(self, threads=0):

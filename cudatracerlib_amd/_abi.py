@@ -160,7 +160,7 @@ SYMBOLS = [
     ("ctl_host_scene_set_camera", C.c_int32, [_vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
                                               C.c_uint32, C.c_uint32]),
     ("ctl_host_scene_set_flags", C.c_int32, [_vp, C.c_uint32]),
-    ("ctl_host_scene_set_bvh_params", C.c_int32, [_vp, C.c_float, C.c_uint32]),
+    ("ctl_host_scene_set_bvh_params", C.c_int32, [_vp, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("ctl_host_scene_compile", C.c_int32, [_vp, C.c_uint32, C.POINTER(SceneDesc)]),
     ("ctl_host_last_error", C.c_char_p, []),
     ("ctl_host_scene_generate", C.c_int32, [_vp, C.c_int32, C.c_double, C.c_uint32, C.c_uint32]),

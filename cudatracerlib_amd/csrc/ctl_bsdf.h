@@ -75,7 +75,15 @@ CTL_HD float erf_ref(float x) {                                                 
 }
 
 // ---------------------------------------------------------------------------
-// Image textures (KernelMIPMap, RGBCOL texels)
+// Image textures (KernelMIPMap, RGBCOL texels).  The bilinear, EWA and
+// texture entry points are out of line on the device: the MIP/EWA filter is
+// large and would otherwise be inlined at every call site (instruction-cache
+// footprint of the path kernel).
+#if defined(__HIP__)
+#define CTL_TEX_FN static __host__ __device__ __noinline__
+#else
+#define CTL_TEX_FN static inline
+#endif
 struct TexView {
     const ctl_texture* tex;
     const uint32_t* data;
@@ -115,7 +123,7 @@ CTL_HD spec tex_texel(const TexView& T, uint32_t level, f2 uv) {                
     return mk3(float(c & 0xffu) / 255.0f, float((c >> 8) & 0xffu) / 255.0f, float((c >> 16) & 0xffu) / 255.0f);
 }
 
-CTL_HD spec tex_triangle(const TexView& T, uint32_t level, f2 uv) {                  // MIPMap.cu:37-48
+CTL_TEX_FN spec tex_triangle(const TexView& T, uint32_t level, f2 uv) {                  // MIPMap.cu:37-48
     const ctl_texture& t = *T.tex;
     level = clampu_ref(level, 0u, t.levels - 1);
     const f2 s = mk2((float)(t.width >> level), (float)(t.height >> level));
@@ -126,7 +134,7 @@ CTL_HD spec tex_triangle(const TexView& T, uint32_t level, f2 uv) {             
            ds * (1.f - dt) * tex_texel(T, level, uv + mk2(is.x, 0)) + ds * dt * tex_texel(T, level, uv + mk2(is.x, is.y));
 }
 
-CTL_HD spec tex_ewa(const TexView& T, uint32_t level, f2 uv, float A, float B, float C) {   // MIPMap.cu:50-111
+CTL_TEX_FN spec tex_ewa(const TexView& T, uint32_t level, f2 uv, float A, float B, float C) {   // MIPMap.cu:50-111
     const ctl_texture& t = *T.tex;
     if (level >= t.levels) return tex_texel(T, t.levels - 1, mk2(0.0f, 0.0f));
     const f2 size = mk2((float)(t.width >> level), (float)(t.height >> level));
@@ -215,8 +223,10 @@ CTL_HD spec tex_eval(const TexView& T, f2 uv, f2 d0, f2 d1) {
     return tex_ewa(T, (uint32_t)ilevel, uv, A, B, C) * (1.0f - a) + tex_ewa(T, (uint32_t)ilevel + 1, uv, A, B, C) * a;
 }
 
-// ImageTexture::Evaluate(const DifferentialGeometry&) (Texture.cu:16-31)
-CTL_HD spec image_texture_eval(const TexView& T, const dgeom& dg) {
+// ImageTexture::Evaluate(const DifferentialGeometry&) (Texture.cu:16-31).
+// Out of line on the device: the MIP/EWA filter is large and would otherwise
+// be inlined at every BSDF call site (instruction-cache footprint).
+CTL_TEX_FN spec image_texture_eval(const TexView& T, const dgeom& dg) {
     const ctl_texture& t = *T.tex;
     spec r;
     if (dg.has_partials) {
@@ -421,7 +431,7 @@ CTL_HD Microfacet rough_distr(const ctl_material& m) {
     return d;
 }
 
-CTL_HD float rough_pdf(const ctl_material& mat, const bsdf_rec& b) {
+CTL_TEX_FN float rough_pdf(const ctl_material& mat, const bsdf_rec& b) {
     const bool hasReflection = (b.type_mask & CTL_EGLOSSY_REFLECTION) != 0,
                hasTransmission = (b.type_mask & CTL_EGLOSSY_TRANSMISSION) != 0,
                reflect = b.wi.z * b.wo.z > 0;
@@ -455,7 +465,7 @@ CTL_HD float rough_pdf(const ctl_material& mat, const bsdf_rec& b) {
     return fabsf(prob * dwh_dwo);
 }
 
-CTL_HD spec rough_f(const ctl_material& mat, const bsdf_rec& b) {
+CTL_TEX_FN spec rough_f(const ctl_material& mat, const bsdf_rec& b) {
     const bool reflect = b.wi.z * b.wo.z > 0;
     f3 H;
     if (reflect) {
@@ -483,7 +493,7 @@ CTL_HD spec rough_f(const ctl_material& mat, const bsdf_rec& b) {
     return mk3(mat.transmittance[0], mat.transmittance[1], mat.transmittance[2]) * fabsf(value * factor * factor);
 }
 
-CTL_HD spec rough_sample(const ctl_material& mat, bsdf_rec& b, float& pdf, f2 sample) {
+CTL_TEX_FN spec rough_sample(const ctl_material& mat, bsdf_rec& b, float& pdf, f2 sample) {
     const bool hasReflection = (b.type_mask & CTL_EGLOSSY_REFLECTION) != 0,
                hasTransmission = (b.type_mask & CTL_EGLOSSY_TRANSMISSION) != 0;
     bool sampleReflection = hasReflection;

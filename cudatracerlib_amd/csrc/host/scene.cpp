@@ -292,10 +292,16 @@ CTL_API int32_t ctl_host_scene_add_texture(ctl_host_scene* s, const uint32_t* rg
     return (int32_t)s->textures.size() - 1;
 }
 
-CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth) {
-    if (!s || !(split_alpha >= 0.0f) || split_depth > 16) { set_host_error("set_bvh_params: invalid argument"); return CTL_ERR_INVALID; }
+CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth,
+                                                 uint32_t bins, uint32_t max_leaf) {
+    if (!s || !(split_alpha >= 0.0f) || split_depth > 16 || bins == 1 || bins > 1024 || max_leaf > 64) {
+        set_host_error("set_bvh_params: invalid argument");
+        return CTL_ERR_INVALID;
+    }
     s->split_alpha = split_alpha;
     s->split_depth = split_depth;
+    s->sah_bins = bins ? bins : CTL_DEFAULT_SAH_BINS;
+    s->max_leaf = max_leaf ? max_leaf : CTL_DEFAULT_MAX_LEAF;
     return CTL_OK;
 }
 
@@ -328,6 +334,8 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         });
         BvhBuildParams bp;
         bp.threads = threads;
+        bp.bins = s->sah_bins;
+        bp.max_leaf = s->max_leaf;
         BvhOutput bo;
         if (s->split_alpha > 0.0f && s->split_depth > 0) {
             // references of large triangles split in space (ref_split.h)

@@ -30,6 +30,8 @@ struct ctl_host_scene {
     // reference splitting of large triangles before the BVH build (ref_split.h)
     float split_alpha = CTL_DEFAULT_SPLIT_ALPHA;
     uint32_t split_depth = CTL_DEFAULT_SPLIT_DEPTH;
+    uint32_t sah_bins = CTL_DEFAULT_SAH_BINS;
+    uint32_t max_leaf = CTL_DEFAULT_MAX_LEAF;
 
     // compiled arrays (owned)
     std::vector<ctl_triangle_data> tri_data;

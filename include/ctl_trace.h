@@ -400,10 +400,15 @@ CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags);
 /* BVH build quality knobs of the compile (SplitBVHBuilder's splitAlpha /
  * MaxSpatialDepth play this role in the reference, SplitBVHBuilder.hpp:62-67):
  * triangles whose box area exceeds split_alpha x the mesh mean get up to
- * 2^split_depth references with clipped boxes.  split_alpha = 0 disables. */
+ * 2^split_depth references with clipped boxes (split_alpha = 0 disables);
+ * `bins` SAH bins per axis and leaves of at most `max_leaf` references
+ * (Platform::m_maxLeafSize = 8, BVHBuilderHelper.cpp:119).  0 = default. */
 #define CTL_DEFAULT_SPLIT_ALPHA 0.5f
 #define CTL_DEFAULT_SPLIT_DEPTH 8u
-CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth);
+#define CTL_DEFAULT_SAH_BINS 32u
+#define CTL_DEFAULT_MAX_LEAF 8u
+CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth,
+                                                 uint32_t bins, uint32_t max_leaf);
 CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, ctl_scene_desc* out);
 CTL_API const char* ctl_host_last_error(void);
 

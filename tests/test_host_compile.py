@@ -109,7 +109,7 @@ def test_bvh_layout_contract(ctl, config, scale, split):
     once without reference splitting; at least once with it, as the reference's
     SBVH), leaf <= 8, last-in-leaf flags, depth bounded for the 64-entry stacks."""
     s = ctl.HostScene().generate(config, scale, 64, 64)
-    s.set_bvh_params(1.0 if split else 0.0, 4 if split else 0)
+    s.set_bvh_params(1.0 if split else 0.0, 4 if split else 0, 0, 0)
     d = s.compile()
     for m in range(d.n_meshes):
         km = d.meshes[m]
