@@ -215,6 +215,22 @@ class Tracer:
     def reset_rays(self, stream=0):
         _check(self._L.ctl_reset_rays(self._ctx, stream), self._ctx, "ctl_reset_rays")
 
+    def image_resolve(self, fb_ptr, width, height, out_ptr, splat_scale=0.0, stream=0):
+        """applyImagePipeline without filter/post-process: RGBA8 sRGB output (ImagePipeline.cu)."""
+        _check(self._L.ctl_image_resolve(self._ctx, fb_ptr, width, height, float(splat_scale), out_ptr, stream),
+               self._ctx, "ctl_image_resolve")
+
+    def variance_add_pass(self, fb_ptr, width, height, tile_samples, var_ptr, splat_scale=0.0, tile_size=64,
+                          stream=0):
+        """PixelVarianceBuffer::AddPass; tile_samples = uint8 samples per tile this pass."""
+        flags = np.ascontiguousarray(tile_samples, dtype=np.uint8)
+        _check(self._L.ctl_variance_add_pass(self._ctx, fb_ptr, width, height, float(splat_scale), int(tile_size),
+                                             flags.ctypes.data, var_ptr, stream), self._ctx, "ctl_variance_add_pass")
+
+    def variance_stats(self, var_ptr, n, err_ptr=None, variance_ptr=None, average_ptr=None, stream=0):
+        _check(self._L.ctl_variance_stats(self._ctx, var_ptr, int(n), err_ptr, variance_ptr, average_ptr, stream),
+               self._ctx, "ctl_variance_stats")
+
     def sync(self, stream=0):
         _check(self._L.ctl_sync(self._ctx, stream), self._ctx, "ctl_sync")
 

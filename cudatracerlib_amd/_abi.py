@@ -123,6 +123,11 @@ class SceneDesc(C.Structure):
     ]
 
 
+class PixelVariance(C.Structure):    # PixelVarianceInfo, 44 B
+    _fields_ = [("prev_I", C.c_float * 3), ("half_buffer", C.c_float * 3), ("iterations_done", C.c_int32),
+                ("weight", C.c_float), ("sum_x", C.c_float), ("sum_x2", C.c_float), ("num_samples_var", C.c_int32)]
+
+
 class PTParams(C.Structure):
     _fields_ = [("direct", C.c_int32), ("max_path_length", C.c_int32), ("rr_start_depth", C.c_int32),
                 ("shadow_any_hit", C.c_int32), ("tile_size", C.c_uint32), ("num_ranks", C.c_uint32),
@@ -148,6 +153,9 @@ SYMBOLS = [
     ("ctl_render_pass_stats", C.c_int32, [_vp, C.POINTER(PTParams), _vp, C.POINTER(C.c_uint64), _vp]),
     ("ctl_last_pass_ms", C.c_int32, [_vp, C.POINTER(C.c_float)]),
     ("ctl_camera_rays", C.c_int32, [_vp, C.POINTER(PTParams), _vp, C.c_int64, C.POINTER(C.c_int64), _vp]),
+    ("ctl_image_resolve", C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, C.c_float, _vp, _vp]),
+    ("ctl_variance_add_pass", C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, C.c_float, C.c_uint32, _vp, _vp, _vp]),
+    ("ctl_variance_stats", C.c_int32, [_vp, _vp, C.c_uint64, _vp, _vp, _vp, _vp]),
     ("ctl_woop_set", None, [_vp, _vp, _vp, C.POINTER(WoopTri)]),
     ("ctl_host_sampler_tables", C.c_int32, [C.c_uint64, C.c_uint32, C.c_uint32, _vp, _vp]),
     ("ctl_host_scene_create", _vp, []),

@@ -329,6 +329,8 @@ struct ctl_ctx {
     hipEvent_t pass_ev[2] = {nullptr, nullptr}; // bracket the last render pass (ctl_last_pass_ms)
     bool pass_timed = false;
     size_t wide_nodes = 0;
+    uint8_t* d_tile_flags = nullptr;            // PixelVarianceBuffer block flags
+    size_t tile_flags_cap = 0;
     uint32_t* d_powers = nullptr;               // XORWOW step powers for sampler_kernel
     ctl::WfState wf{};
     std::vector<void*> wf_allocs;

@@ -44,9 +44,10 @@ static_assert(sizeof(ctl_pixel) == 28, "PixelData is 28 B");
 static_assert(sizeof(ctl_light_tri) == 64, "ShapeSet::triData is 64 B");
 static_assert(sizeof(ctl_material) == 80, "ctl_material is 80 B");
 static_assert(sizeof(ctl_texture) == 380, "ctl_texture is 380 B");
+static_assert(sizeof(ctl_pixel_variance) == 44, "PixelVarianceInfo is 44 B");
 
 #ifndef CTL_PERSIST_WAVES_FULL
-#define CTL_PERSIST_WAVES_FULL 4   // ... with the C5 shading (textures, microfacets)
+#define CTL_PERSIST_WAVES_FULL 3   // ... with the C5 shading (out-of-line texture / microfacet calls)
 #endif
 #ifndef CTL_PERSIST_WAVES
 #define CTL_PERSIST_WAVES 6   // waves/SIMD for the persistent path kernel: measured best on C3
@@ -485,6 +486,7 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
     }
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_cursors) (void)hipFree(c->d_cursors);
+    if (c->d_tile_flags) (void)hipFree(c->d_tile_flags);
     for (int i = 0; i < 2; i++)
         if (c->pass_ev[i]) (void)hipEventDestroy(c->pass_ev[i]);
     if (c->d_powers) (void)hipFree(c->d_powers);

@@ -334,6 +334,41 @@ CTL_API ctl_status ctl_last_pass_ms(ctl_ctx* ctx, float* ms);
 CTL_API ctl_status ctl_camera_rays(ctl_ctx* ctx, const ctl_pt_params* params, ctl_ray* d_rays, int64_t capacity,
                                    int64_t* n_out, void* stream);
 
+/* ---- final-image stage -------------------------------------- */
+
+/* PixelVarianceInfo (Kernel/PixelVarianceBuffer.h:10-63), 44 B. */
+typedef struct {
+    float prev_I[3];          /* Spectrum prev_I                                */
+    float half_buffer[3];     /* Spectrum half_buffer                           */
+    int32_t iterations_done;
+    float weight;
+    float sum_x, sum_x2;      /* VarAccumulator<float> I                        */
+    int32_t num_samples_var;
+} ctl_pixel_variance;
+
+/* applyImagePipeline without filter or post-process (ImagePipeline.cu:57-65):
+ * copySamplesToOutput, d_rgba[y*w+x] = gammaCorrecture(PixelData::toSpectrum(
+ * splat_scale)) as RGBCOL (r in the low byte, a = 255).  Asynchronous. */
+CTL_API ctl_status ctl_image_resolve(ctl_ctx* ctx, const ctl_pixel* d_fb, uint32_t width, uint32_t height,
+                                     float splat_scale, uint32_t* d_rgba, void* stream);
+
+/* PixelVarianceBuffer::AddPass (PixelVarianceBuffer.cu:10-37): updates the
+ * moments of every pixel of the tiles sampled in this pass.  tile_samples
+ * (host, one byte per tile_size^2 block, row-major over ceil(w/tile_size) x
+ * ceil(h/tile_size); the reference's BLOCK_SAMPLER_BlockSize is 64 or 128,
+ * IBlockSampler_device.h:6-19) is the block-flag array: how many samples the
+ * pass put into each block (0 = not rendered, its pixels untouched).  d_var
+ * holds width*height records, zero-initialised by the caller before the first
+ * pass.  Asynchronous. */
+CTL_API ctl_status ctl_variance_add_pass(ctl_ctx* ctx, const ctl_pixel* d_fb, uint32_t width, uint32_t height,
+                                         float splat_scale, uint32_t tile_size, const uint8_t* tile_samples,
+                                         ctl_pixel_variance* d_var, void* stream);
+
+/* PixelVarianceInfo::computeError / computeVariance / computeAverage
+ * (PixelVarianceBuffer.h:43-62) for n records; any output may be NULL. */
+CTL_API ctl_status ctl_variance_stats(ctl_ctx* ctx, const ctl_pixel_variance* d_var, uint64_t n, float* d_error,
+                                      float* d_variance, float* d_average, void* stream);
+
 /* Number of traceRay-equivalent queries (camera + bounce + shadow rays +
  * batched rays) since the last reset; 64-bit (the reference's counter is a
  * 32-bit atomicInc, Base/Platform.cu:12-21).  Synchronises the device. */

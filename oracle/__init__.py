@@ -45,6 +45,9 @@ def load():
         "oracle_render_pass": (C.c_uint64, [C.POINTER(SceneDesc), C.POINTER(PTParams), C.c_uint64, vp, C.c_int32,
                                             C.c_int32, C.c_uint32, vp]),
         "oracle_camera_rays": (None, [C.POINTER(SceneDesc), C.c_uint64, vp]),
+        "oracle_image_resolve": (None, [vp, C.c_uint32, C.c_uint32, C.c_float, vp]),
+        "oracle_variance_add_pass": (None, [vp, C.c_uint32, C.c_uint32, C.c_float, C.c_uint32, vp, vp]),
+        "oracle_variance_stats": (None, [vp, C.c_uint64, vp, vp, vp]),
         "oracle_triangle_data_set": (None, [vp, C.c_uint8, vp, vp, vp]),
         "oracle_light_tri": (None, [vp, vp, vp, vp, vp, vp]),
         "oracle_matrix_inverse": (None, [vp, vp]),

@@ -1040,4 +1040,74 @@ void oracle_matrix_inverse(const float* in16, float* out16) {
     std::memcpy(out16, r.d, 64);
 }
 
+// ---- final-image stage: ImagePipeline.cu copySamplesToOutput + PixelVarianceBuffer ----
+static float o_to_srgb(float v) {   // toSRGBComponent (Math/Spectrum.cu:229-234)
+    if (v <= (float)0.0031308) return (float)12.92 * v;
+    return (float)1.055 * cr_pow(v, (float)(1.0 / 2.4)) - (float)0.055;
+}
+static unsigned o_to_u8(float x) {  // Float3ToCOLORREF: (unsigned char)(clamp01(x) * 255.0f)
+    return (unsigned)(unsigned char)(omin(omax(x, 0.0f), 1.0f) * 255.0f);
+}
+
+void oracle_image_resolve(const ctl_pixel* fb, uint32_t w, uint32_t h, float splat, uint32_t* out) {
+    for (uint64_t i = 0; i < (uint64_t)w * h; i++) {
+        const ctl_pixel& p = fb[i];
+        // PixelData::toSpectrum (Engine/Image.h:21-28): s / weight + s2 * splatScale
+        float weight = p.weight_sum != 0 ? p.weight_sum : 1;
+        Spec s = spec_div(v3(p.rgb[0], p.rgb[1], p.rgb[2]), weight) + v3(p.rgb_splat[0], p.rgb_splat[1], p.rgb_splat[2]) * splat;
+        out[i] = o_to_u8(o_to_srgb(s.x)) | (o_to_u8(o_to_srgb(s.y)) << 8) | (o_to_u8(o_to_srgb(s.z)) << 16) | (255u << 24);
+    }
+}
+
+void oracle_variance_add_pass(const ctl_pixel* fb, uint32_t w, uint32_t h, float splat, uint32_t tile,
+                              const uint8_t* flags, ctl_pixel_variance* var) {
+    const uint32_t tx = (w + tile - 1) / tile;
+    for (uint32_t y = 0; y < h; y++)
+        for (uint32_t x = 0; x < w; x++) {
+            char f = (char)flags[(y / tile) * tx + x / tile];
+            if (!f) continue;   // updateVarianceBuffer: g_BlockFlags[bIdx] (PixelVarianceBuffer.cu:15-19)
+            const ctl_pixel& p = fb[(size_t)y * w + x];
+            ctl_pixel_variance& v = var[(size_t)y * w + x];
+            float samplerPerformed = (float)f;
+            // PixelVarianceInfo::updateMoments (PixelVarianceBuffer.h:22-41)
+            Spec nps = v3(p.rgb[0], p.rgb[1], p.rgb[2]) + v3(p.rgb_splat[0], p.rgb_splat[1], p.rgb_splat[2]) * splat;
+            Spec est = spec_div(nps - v3(v.prev_I[0], v.prev_I[1], v.prev_I[2]), samplerPerformed);
+            v.prev_I[0] = nps.x; v.prev_I[1] = nps.y; v.prev_I[2] = nps.z;
+            v.weight = p.weight_sum;
+            if (v.iterations_done++ % 2 == 1) {
+                v.half_buffer[0] += est.x; v.half_buffer[1] += est.y; v.half_buffer[2] += est.z;
+            }
+            if (samplerPerformed != 0) {
+                float L = est.x * 0.212671f + est.y * 0.715160f + est.z * 0.072169f;   // getLuminance (RGB)
+                v.sum_x += L;
+                v.sum_x2 += L * L;   // math::sqr
+                v.num_samples_var++;
+            }
+        }
+}
+
+void oracle_variance_stats(const ctl_pixel_variance* var, uint64_t n, float* err, float* variance, float* average) {
+    for (uint64_t i = 0; i < n; i++) {
+        const ctl_pixel_variance& v = var[i];
+        if (err) {   // computeError (PixelVarianceBuffer.h:55-62)
+            Spec I = spec_div(v3(v.prev_I[0], v.prev_I[1], v.prev_I[2]), v.weight);
+            Spec A = spec_div(v3(v.half_buffer[0], v.half_buffer[1], v.half_buffer[2]), float(v.iterations_done / 2));
+            Spec dd = I - A;
+            float sa = 0.0f; sa += fabsf(dd.x); sa += fabsf(dd.y); sa += fabsf(dd.z);
+            float si = 0.0f; si += I.x; si += I.y; si += I.z;
+            float e_p = sa / sqrtf(si);
+            bool zero = I.x == 0.0f && I.y == 0.0f && I.z == 0.0f;
+            bool nan = std::isnan(I.x) || std::isnan(I.y) || std::isnan(I.z) || std::isnan(A.x) || std::isnan(A.y) ||
+                       std::isnan(A.z);
+            err[i] = zero || nan ? 0.0f : omax(e_p, 1e-2f);
+        }
+        float N = (float)v.num_samples_var;
+        if (variance) {   // VarAccumulator::Var -> VarianceFromMoments
+            float invN = 1.0f / N;
+            variance[i] = (v.sum_x2 - (v.sum_x * v.sum_x) * invN) * invN;
+        }
+        if (average) average[i] = v.sum_x / N;   // VarAccumulator::E
+    }
+}
+
 }  // extern "C"

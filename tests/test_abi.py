@@ -39,6 +39,7 @@ def test_reference_layout_sizes():
     assert C.sizeof(abi.LightTri) == 64       # ShapeSet::triData
     assert C.sizeof(abi.Material) == 80       # flattened Material + BSDF parameters
     assert C.sizeof(abi.Texture) == 380       # ImageTexture + KernelMIPMap
+    assert C.sizeof(abi.PixelVariance) == 44  # PixelVarianceInfo
 
 
 def test_create_without_gpu_fails_cleanly():

@@ -308,3 +308,39 @@ def test_render_c5_textured_quad(ctl, orc, tracer, dev):
     assert grays == wrays
     assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
     assert want[:, 0].std() > 0.01                 # the textures show up
+
+
+def test_image_resolve_and_variance_buffer(ctl, orc, dev):
+    """Final-image stage: ctl_image_resolve and the
+    PixelVarianceBuffer passes/statistics, bit-exact against the oracle over a
+    few real render passes, with one tile skipped in a pass."""
+    w, h = 160, 96
+    d = scene(ctl, 2, 0.05, w, h)
+    pt = ctl.PathTracer(0)
+    pt.upload_scene(d)
+    fb = torch.zeros((w * h, 7), dtype=torch.float32, device=dev)
+    var = torch.zeros((w * h, 11), dtype=torch.float32, device=dev)   # 44-B records
+    tiles = ((w + 63) // 64) * ((h + 63) // 64)
+    var_o = np.zeros((w * h, 11), np.float32)
+    for p in range(4):
+        pt.do_pass(fb.data_ptr(), p)
+        flags = np.ones(tiles, np.uint8)
+        if p == 2:
+            flags[1] = 0
+        pt.variance_add_pass(fb.data_ptr(), w, h, flags, var.data_ptr(), splat_scale=0.5)
+        torch.cuda.synchronize()
+        orc.oracle_variance_add_pass(oracle.ptr(fb.cpu().numpy()), w, h, np.float32(0.5), 64, oracle.ptr(flags),
+                                     oracle.ptr(var_o))
+    assert np.array_equal(var.cpu().numpy().view(np.uint32), var_o.view(np.uint32))
+    out = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    pt.image_resolve(fb.data_ptr(), w, h, out.data_ptr(), splat_scale=0.5)
+    stats = torch.zeros((3, w * h), dtype=torch.float32, device=dev)
+    pt.variance_stats(var.data_ptr(), w * h, stats[0].data_ptr(), stats[1].data_ptr(), stats[2].data_ptr())
+    torch.cuda.synchronize()
+    want = np.zeros(w * h, np.uint32)
+    orc.oracle_image_resolve(oracle.ptr(fb.cpu().numpy()), w, h, np.float32(0.5), oracle.ptr(want))
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    so = np.zeros((3, w * h), np.float32)
+    orc.oracle_variance_stats(oracle.ptr(var_o), w * h, oracle.ptr(so[0]), oracle.ptr(so[1]), oracle.ptr(so[2]))
+    assert np.array_equal(stats.cpu().numpy().view(np.uint32), so.view(np.uint32))
+    pt.close()

@@ -87,3 +87,25 @@ def test_bvh_traversal_equals_brute_force(ctl, orc, config, scale):
     assert (tri != 0xFFFFFFFF).sum() > n // 10
     assert np.array_equal(t, bt)
     assert np.array_equal(tri, btri)
+
+
+def test_image_resolve_oracle_matches_numpy(orc):
+    """copySamplesToOutput: weight-normalised RGB (+ splat), sRGB curve, clamp,
+    truncation to 8 bit (ImagePipeline.cu:8-21, Spectrum.cu:229-234,
+    Spectrum.h:521-526) - the oracle against an independent numpy restatement."""
+    rng = np.random.default_rng(7)
+    n = 5000
+    fb = np.zeros((n, 7), np.float32)
+    fb[:, 0:3] = rng.random((n, 3), dtype=np.float32) * 3
+    fb[:, 3:6] = rng.random((n, 3), dtype=np.float32) * 0.1
+    fb[:, 6] = rng.integers(0, 5, n).astype(np.float32)
+    out = np.zeros(n, np.uint32)
+    orc.oracle_image_resolve(oracle.ptr(fb), n, 1, np.float32(0.25), oracle.ptr(out))
+    w = np.where(fb[:, 6] != 0, fb[:, 6], np.float32(1)).astype(np.float32)
+    s = fb[:, 0:3] * (np.float32(1) / w)[:, None] + fb[:, 3:6] * np.float32(0.25)
+    lin = s <= np.float32(0.0031308)
+    srgb = np.where(lin, np.float32(12.92) * s,
+                    np.float32(1.055) * np.power(s.astype(np.float64), 1 / 2.4).astype(np.float32) - np.float32(0.055))
+    c = (np.clip(srgb, 0, 1).astype(np.float32) * np.float32(255)).astype(np.uint32)
+    want = c[:, 0] | (c[:, 1] << 8) | (c[:, 2] << 16) | (255 << 24)
+    assert np.array_equal(out, want.astype(np.uint32))
