@@ -28,7 +28,7 @@ from ._abi import (PTParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HAL
                    CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT)
 
 __all__ = ["HostScene", "Tracer", "PathTracer", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
-           "roughdielectric_material",
+           "roughdielectric_material", "set_alpha_map",
            "CTL_SCENE_HALF_HOST_QUIRK", "CTL_SCENE_BINARY_BVH", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "lib", "diffuse_material"]
 
 
@@ -47,10 +47,20 @@ def _check(status, ctx=None, what=""):
         raise CTLError(f"{what} failed (status {status}): {msg.decode() if msg else ''}")
 
 
+def set_alpha_map(m, state, threshold, alpha_texture=None):
+    """Material::AlphaMap (Engine/Material.h:14-36): state 1/2 = luminance/alpha of
+    `alpha_texture`, 5/6 = luminance/alpha of the diffuse reflectance texture."""
+    m.alpha_state = int(state)
+    m.alpha_texture = 0xFFFFFFFF if alpha_texture is None else int(alpha_texture)
+    m.alpha_threshold = float(threshold)
+    return m
+
+
 def diffuse_material(r, g, b, two_sided=True, texture=None):
     """diffuse BSDF (BSDF_Simple.cu:7-75); `texture` = ImageTexture index of
     m_reflectance (HostScene.add_texture), else the constant (r, g, b)."""
     m = Material()
+    m.alpha_texture = 0xFFFFFFFF
     m.bsdf_type = CTL_BSDF_DIFFUSE
     m.combined_type = CTL_EDIFFUSE_REFLECTION
     m.two_sided = 1 if two_sided else 0
@@ -65,6 +75,7 @@ def roughdielectric_material(distribution, eta, alpha_u, alpha_v=None, reflectan
     """roughdielectric BSDF (BSDF_Simple.cu:373-615) with constant textures;
     distribution = _abi.CTL_MICROFACET_BECKMANN or _abi.CTL_MICROFACET_GGX."""
     m = Material()
+    m.alpha_texture = 0xFFFFFFFF
     m.bsdf_type = _abi.CTL_BSDF_ROUGHDIELECTRIC
     m.combined_type = _abi.CTL_EGLOSSY_REFLECTION | _abi.CTL_EGLOSSY_TRANSMISSION
     m.two_sided = 0

@@ -71,7 +71,8 @@ class Material(C.Structure):        # 80 B
                 ("node_light_index", C.c_uint32), ("reflectance", C.c_float * 3), ("texture", C.c_uint32),
                 ("transmittance", C.c_float * 3), ("distribution", C.c_uint32), ("eta", C.c_float),
                 ("inv_eta", C.c_float), ("alpha_u", C.c_float), ("alpha_v", C.c_float),
-                ("sample_visible", C.c_uint32), ("pad", C.c_uint32 * 3)]
+                ("sample_visible", C.c_uint32), ("alpha_state", C.c_uint32), ("alpha_texture", C.c_uint32),
+                ("alpha_threshold", C.c_float)]
 
 
 class Texture(C.Structure):

@@ -241,6 +241,48 @@ CTL_TEX_FN spec image_texture_eval(const TexView& T, const dgeom& dg) {
     return r * mk3(t.scale[0], t.scale[1], t.scale[2]);
 }
 
+// KernelMIPMap::SampleAlpha (MIPMap.cu:123-139): level-0 texel alpha, no
+// filtering.  The reference indexes without clamping; the index is clamped
+// here (it can only differ where the reference would read out of bounds).
+CTL_HD float tex_sample_alpha(const TexView& T, f2 uv) {
+    const ctl_texture& t = *T.tex;
+    f2 l;
+    if (!tex_wrap(uv, mk2((float)t.width, (float)t.height), t.wrap, l)) return 0.0f;
+    const uint32_t x = tmin((uint32_t)l.x, t.width - 1), y = tmin((uint32_t)l.y, t.height - 1);
+    const uint32_t c = T.data[t.offsets[0] + y * t.width + x];
+    return float(c >> 24) / 255.0f;
+}
+
+CTL_HD f2 tex_map(const ctl_texture& t, f2 uv) {   // TextureMapping2D::TransformPoint
+    return mk2(t.m11 * uv.x + t.m12 * uv.y, t.m21 * uv.x + t.m22 * uv.y) + mk2(t.m13, t.m23);
+}
+
+// Material::AlphaTest (Engine/Material.cu:160-189) for image / constant
+// textures (sample_fast, :140-158), states without the Color compare.
+CTL_HD bool material_alpha_test(const ctl_material& m, const TexView& tex, f2 uv) {
+    if (!m.alpha_state) return true;
+    const bool reflImg = m.texture != 0xffffffffu;
+    const bool alphaImg = m.alpha_texture != 0xffffffffu;
+    if ((m.alpha_state == 2 && alphaImg) || (m.alpha_state == 6 && reflImg)) {
+        const ctl_texture& t = tex.tex[m.alpha_state == 2 ? m.alpha_texture : m.texture];
+        const TexView T{&t, tex.data};
+        return tex_sample_alpha(T, tex_map(t, uv)) >= m.alpha_threshold;
+    }
+    spec val;
+    const uint32_t src = (m.alpha_state & 4) ? m.texture : m.alpha_texture;
+    if (src != 0xffffffffu) {   // ImageTexture::Evaluate(uv) -> Sample
+        const ctl_texture& t = tex.tex[src];
+        const TexView T{&t, tex.data};
+        const f2 u2 = tex_map(t, uv);
+        val = (t.filter == CTL_TEX_POINT ? tex_texel(T, 0, u2) : tex_triangle(T, 0, u2)) *
+              mk3(t.scale[0], t.scale[1], t.scale[2]);
+    } else {                    // ConstantTexture (the diffuse reflectance)
+        val = refl(m);
+    }
+    if ((m.alpha_state & 3) == 1) return val.x * 0.212671f + val.y * 0.715160f + val.z * 0.072169f >= m.alpha_threshold;
+    return true;
+}
+
 // ---------------------------------------------------------------------------
 // MicrofacetDistribution (Beckmann / GGX; isotropic or anisotropic alpha)
 struct Microfacet {

@@ -76,7 +76,7 @@ struct PathCtx {
         HitRec r2;   // traceRay (TraceHelper.cu:174-180)
         r2.t = FLT_MAX; r2.tri = 0xffffffffu; r2.node = 0xffffffffu; r2.u = r2.v = 0.0f;
         rays++;
-        ok &= trace_one<0, STATS, SINGLE, WIDE>(S, v.rori, v.rdir, 0.0f, S.ray_eps, r2, st, &ts);
+        ok &= trace_one<0, STATS, SINGLE, WIDE, FULL>(S, v.rori, v.rdir, 0.0f, S.ray_eps, r2, st, &ts);
         if (r2.tri == 0xffffffffu) {
             v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);   // no environment map
             return false;
@@ -88,8 +88,8 @@ struct PathCtx {
             HitRec h;
             h.t = any ? sh.dist - S.ray_eps : FLT_MAX; h.tri = 0xffffffffu; h.node = 0xffffffffu; h.u = h.v = 0.0f;
             rays++;
-            if (any) ok &= trace_one<1, STATS, SINGLE, WIDE>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
-            else ok &= trace_one<0, STATS, SINGLE, WIDE>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            if (any) ok &= trace_one<1, STATS, SINGLE, WIDE, FULL>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            else ok &= trace_one<0, STATS, SINGLE, WIDE, FULL>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
             if (!shadow_occluded(S, any, h, sh.dist)) v.cl = v.cl + sh.add;
         }
         return cont;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             const f3 d = shadowPhase ? sh.d : v.rdir;
             rays++;
             if (S.n_nodes != 0) {
-                Traverser<2, STATS, SINGLE, WIDE> T;
+                Traverser<2, STATS, SINGLE, WIDE, FULL> T;
                 T.anyhit = shadowPhase && shadowAny;
                 T.init(S, v.rori, d, 0.0f, S.ray_eps, h.t, st, &ts);
                 while (!T.done) T.round(S, st, &ts);
@@ -514,6 +514,21 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
             c->err = "scene_upload: material texture index out of range";
             return CTL_ERR_INVALID;
         }
+        if (m.alpha_state) {
+            const uint32_t st = m.alpha_state;
+            if (st != 1 && st != 2 && st != 5 && st != 6) {
+                c->err = "scene_upload: alpha state must be 0, 1, 2, 5 or 6 (color compare unsupported)";
+                return CTL_ERR_INVALID;
+            }
+            if (st < 4 && (m.alpha_texture == 0xffffffffu || m.alpha_texture >= d->n_textures)) {
+                c->err = "scene_upload: alpha map texture index out of range";
+                return CTL_ERR_INVALID;
+            }
+            if (m.bsdf_type != CTL_BSDF_DIFFUSE && st >= 4) {
+                c->err = "scene_upload: reflectance-map alpha needs a diffuse material";
+                return CTL_ERR_INVALID;
+            }
+        }
     }
     for (uint32_t i = 0; i < d->n_textures; i++) {
         const ctl_texture& t = d->textures[i];
@@ -594,8 +609,12 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     for (int i = 0; i < CTL_MAX_NUM_LIGHTS; i++) S.light_cdf[i] = d->light_cdf[i];
     S.camera = d->camera;
     S.full_shading = 0;
-    for (uint32_t i = 0; i < d->n_materials; i++)
-        if (d->materials[i].bsdf_type != CTL_BSDF_DIFFUSE || d->materials[i].texture != 0xffffffffu) S.full_shading = 1;
+    S.alpha = 0;
+    for (uint32_t i = 0; i < d->n_materials; i++) {
+        const ctl_material& m = d->materials[i];
+        if (m.bsdf_type != CTL_BSDF_DIFFUSE || m.texture != 0xffffffffu || m.alpha_state) S.full_shading = 1;
+        if (m.alpha_state) S.alpha = 1;   // DynamicScene.cpp:586 doAlphaMapping
+    }
     S.single = 0;
     if (d->n_nodes > 0 && d->scene_start_node < 0) {
         uint32_t node = ~(uint32_t)d->scene_start_node;

@@ -72,6 +72,7 @@ struct DevScene {
     const uint32_t* mesh_wbase;  // first wide node of each mesh
     uint32_t wide;               // wide trees present (scene flag CTL_SCENE_BINARY_BVH clear)
     uint32_t full_shading;       // C5 materials present (shade_hit<true>)
+    uint32_t alpha;              // KernelDynamicScene::doAlphaMapping (some material has an alpha map)
     uint32_t tie_min;            // exact-t ties -> lowest (triangle, node) instead of first found
     uint32_t s_wnode_base;
 };
@@ -161,7 +162,10 @@ __device__ __forceinline__ void xform_rows(const float4* M, f3 p, f3 d, f3& po, 
 
 // Closest (ANY=0) or any (ANY=1) hit with tri_tmin < t < h.t, or chosen per
 // ray by the `anyhit` member (ANY=2); box spans start at span_tmin.
-template <int ANY, bool STATS, bool SINGLE, bool WIDE = false>
+// ALPHA: the traceRay flavour with Material::AlphaTest on candidate hits
+// (__traceRay_internal__<true>, TraceHelper.cu:136-154), active when the scene
+// has alpha maps; the batch intersectKernel never alpha-tests.
+template <int ANY, bool STATS, bool SINGLE, bool WIDE = false, bool ALPHA = false>
 struct Traverser {
     RayLocal cur;
     RayLocal world;   // unused when SINGLE
@@ -208,6 +212,19 @@ struct Traverser {
         }
     }
 
+    // TriangleData UV set 0 at (u, v) -> Material::AlphaTest (TraceHelper.cu:140-152)
+    __device__ __forceinline__ bool alpha_survives(const DevScene& S, uint32_t gtri, float u, float v) const {
+        const ctl_triangle_data td = S.tri_data[gtri];
+        const ctl_material& m = S.mats[((td.w[1] >> 16) & 0xffu) + S.nodes[instIdx].material_offset];
+        if (!m.alpha_state) return true;
+        const bool q = (S.flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
+        const f2 a = mk2(half_to_float(td.w[5] & 0xffffu, q), half_to_float(td.w[5] >> 16, q));
+        const f2 b = mk2(half_to_float(td.w[6] & 0xffffu, q), half_to_float(td.w[6] >> 16, q));
+        const f2 c = mk2(half_to_float(td.w[7] & 0xffffu, q), half_to_float(td.w[7] >> 16, q));
+        const f2 uv = u * a + v * b + (1 - u - v) * c;
+        return material_alpha_test(m, TexView{S.textures, S.tex_data}, uv);
+    }
+
     __device__ __forceinline__ void leaf_tris(const DevScene& S, TraceStats* stats) {
         for (int triAddr = ~leafAddr;; triAddr++) {
             const float4* tv = S.woop + triBase + (uint32_t)triAddr * 3u;
@@ -231,7 +248,8 @@ struct Traverser {
                     float v = Oy + t * Dy;
                     const uint32_t gtri = (index >> 1) + triOffset;
                     if (v >= 0.0f && u + v <= 1.0f &&
-                        (t < h.t || gtri < h.tri || (gtri == h.tri && instIdx < h.node))) {
+                        (t < h.t || gtri < h.tri || (gtri == h.tri && instIdx < h.node)) &&
+                        (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v))) {
                         h.node = instIdx;
                         h.tri = gtri;
                         h.u = u;
@@ -404,10 +422,10 @@ struct Traverser {
 };
 
 // Whole traversal of one ray (megakernel, batch kernel).
-template <int ANY, bool STATS, bool SINGLE, bool WIDE = false>
+template <int ANY, bool STATS, bool SINGLE, bool WIDE = false, bool ALPHA = false>
 __device__ __forceinline__ bool trace_one(const DevScene& S, f3 ori, f3 dir, float span_tmin, float tri_tmin,
                                           HitRec& h, LaneStack& st, TraceStats* stats) {
-    Traverser<ANY, STATS, SINGLE, WIDE> T;
+    Traverser<ANY, STATS, SINGLE, WIDE, ALPHA> T;
     T.init(S, ori, dir, span_tmin, tri_tmin, h.t, st, stats);
     while (!T.done) T.round(S, st, stats);
     h = T.h;

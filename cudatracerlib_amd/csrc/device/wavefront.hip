@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S, PathParams P
 // queue entry between traversal rounds (one atomic per wave), so waves stay
 // full while long rays finish (dynamic fetch, cf. intersectKernel's warp
 // fetch at TraceHelper.cu:379-399, here per round instead of per batch).
-template <int MODE, bool STATS, bool SINGLE, bool WIDE>
+template <int MODE, bool STATS, bool SINGLE, bool WIDE, bool ALPHA>
 __global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S, WfState W, const uint32_t* queue,
                                                           const uint32_t* countp, uint32_t* cursor,
                                                           unsigned long long* counters) {
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S, WfState W,
     if (count == 0) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&counters[0], (unsigned long long)count);
     TraceStats ts{0, 0, 0};
-    Traverser<MODE == 1, STATS, SINGLE, WIDE> T;
+    Traverser<MODE == 1, STATS, SINGLE, WIDE, ALPHA> T;
     T.done = true;
     bool haveRay = false, exhausted = false, ovf = false;
     uint32_t ray = 0;
@@ -151,17 +151,20 @@ template <int MODE>
 void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32_t* cnt, uint32_t* cursor, bool stats) {
     WfState& W = c->wf;
     const bool single = c->scene.single != 0;
-#define LT(ST, SG, WD)                                                                                          \
+#define LT(ST, SG, WD, AL)                                                                                      \
     do {                                                                                                        \
         static int blocks = 0;                                                                                  \
-        if (!blocks) blocks = resident_blocks(c, wf_trace_kernel<MODE, ST, SG, WD>, kStackLdsBytes);            \
-        hipLaunchKernelGGL((wf_trace_kernel<MODE, ST, SG, WD>), dim3(blocks), dim3(kBlock), kStackLdsBytes, s,   \
+        if (!blocks) blocks = resident_blocks(c, wf_trace_kernel<MODE, ST, SG, WD, AL>, kStackLdsBytes);        \
+        hipLaunchKernelGGL((wf_trace_kernel<MODE, ST, SG, WD, AL>), dim3(blocks), dim3(kBlock), kStackLdsBytes, s, \
                            c->scene, W, queue, cnt, cursor, c->d_counters);                                     \
     } while (0)
+#define LT2(SG, WD) do { if (alpha) LT(false, SG, WD, true); else LT(false, SG, WD, false); } while (0)
     const bool wide = c->scene.wide != 0 && !stats;   // stats: the reference's binary traversal
-    if (stats) { if (single) LT(true, true, false); else LT(true, false, false); }
-    else if (wide) { if (single) LT(false, true, true); else LT(false, false, true); }
-    else { if (single) LT(false, true, false); else LT(false, false, false); }
+    const bool alpha = c->scene.alpha != 0;
+    if (stats) { if (single) LT(true, true, false, false); else LT(true, false, false, false); }
+    else if (wide) { if (single) LT2(true, true); else LT2(false, true); }
+    else { if (single) LT2(true, false); else LT2(false, false); }
+#undef LT2
 #undef LT
 }
 

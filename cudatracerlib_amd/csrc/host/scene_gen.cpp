@@ -116,6 +116,7 @@ ctl_material diffuse_mat(float r, float g, float b) {
     m.node_light_index = 0xffffffffu;
     m.reflectance[0] = r; m.reflectance[1] = g; m.reflectance[2] = b;
     m.texture = 0xffffffffu;
+    m.alpha_texture = 0xffffffffu;
     return m;
 }
 

@@ -154,7 +154,12 @@ typedef struct {
     float eta, inv_eta;          /* roughdielectric: m_eta, m_invEta = 1/m_eta   */
     float alpha_u, alpha_v;      /* ConstantTexture values of m_alphaU / m_alphaV */
     uint32_t sample_visible;     /* m_sampleVisible                              */
-    uint32_t pad[3];
+    uint32_t alpha_state;        /* Material::AlphaMap.state (AlphaBlendState,
+                                    Engine/Material.h:14-22): 0 disabled, 1/2 =
+                                    alpha texture luminance/alpha, 5/6 = the
+                                    reflectance texture's luminance/alpha    */
+    uint32_t alpha_texture;      /* ImageTexture of AlphaMap.tex (states 1, 2)    */
+    float alpha_threshold;       /* AlphaMap.test_val_scalar                     */
 } ctl_material;
 
 /* ImageTexture (SceneTypes/Texture.h:159-183) with its TextureMapping2D and

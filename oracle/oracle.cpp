@@ -174,8 +174,17 @@ struct Hit {
 // Generic two-level closest/any hit.  traceRay (TraceHelper.cu:88-180):
 // spanTmin=0, triTmin=rayEps, t0=FLT_MAX.  Batch (TraceHelper.cu:326-734):
 // spanTmin=triTmin=ray.tmin, t0=ray.tmax.
+// Material::AlphaTest of a candidate hit (TraceHelper.cu:136-154), defined
+// after oracle_c5.h; used by the traceRay flavour only (alpha = true).
+bool alpha_survives(const ctl_scene_desc* d, uint32_t gtri, uint32_t nodeIdx, float u, float v);
+bool scene_has_alpha(const ctl_scene_desc* d) {   // DynamicScene.cpp:586 doAlphaMapping
+    for (uint32_t i = 0; i < d->n_materials; i++)
+        if (d->materials[i].alpha_state) return true;
+    return false;
+}
+
 bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
-                     int tie, Stats* st) {
+                     int tie, Stats* st, bool alpha = false) {
     const ctl_scene_desc* d = S.d;
     if (d->n_nodes == 0) return false;
     const float* sceneNodes = reinterpret_cast<const float*>(d->scene_bvh_nodes);
@@ -213,7 +222,7 @@ bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float t
                         float Oy = v[11] + ol.x * v[8] + ol.y * v[9] + ol.z * v[10];
                         float Dy = dl.x * v[8] + dl.y * v[9] + dl.z * v[10];
                         float vv = Oy + t * Dy;
-                        if (vv >= 0.0f && u + vv <= 1.0f) {
+                        if (vv >= 0.0f && u + vv <= 1.0f && (!alpha || alpha_survives(d, gtri, (uint32_t)nodeIdx, u, vv))) {
                             h.node = (uint32_t)nodeIdx;
                             h.tri = gtri;
                             h.u = u; h.v = vv;
@@ -235,7 +244,7 @@ bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float t
 // traceRay(dir, ori, TraceResult*) (TraceHelper.cu:174-180) on an Init()'ed result
 bool trace_ray(const SceneView& S, V3 ori, V3 dir, Hit& h, int tie, Stats* st) {
     h.t = FLT_MAX; h.tri = UINT_MAX; h.node = UINT_MAX; h.u = h.v = 0;
-    trace_two_level(S, ori, dir, 0.0f, S.d->ray_eps, h, false, tie, st);
+    trace_two_level(S, ori, dir, 0.0f, S.d->ray_eps, h, false, tie, st, scene_has_alpha(S.d));
     return h.tri != UINT_MAX;
 }
 
@@ -405,6 +414,44 @@ uint32_t light_index(const SceneView& S, uint32_t tri, uint32_t node) {  // Trac
 }  // namespace
 #include "oracle_c5.h"
 namespace {
+
+// Material::AlphaTest (Engine/Material.cu:160-189) with sample_fast (:140-158)
+// and KernelMIPMap::SampleAlpha (MIPMap.cu:123-139, index clamped).
+bool alpha_survives(const ctl_scene_desc* d, uint32_t gtri, uint32_t nodeIdx, float u, float v) {
+    const uint32_t* w = d->tri_data[gtri].w;
+    const ctl_material& m = d->materials[((w[1] >> 16) & 0xff) + d->nodes[nodeIdx].material_offset];
+    if (!m.alpha_state) return true;
+    const bool q = (d->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
+    auto hf = [&](uint16_t x) { return q ? half_to_float_host(x) : half_to_float_ieee(x); };
+    V2 a = v2(hf(w[5] & 0xffff), hf(w[5] >> 16)), b = v2(hf(w[6] & 0xffff), hf(w[6] >> 16)),
+       c = v2(hf(w[7] & 0xffff), hf(w[7] >> 16));
+    V2 uv = u * a + v * b + (1 - u - v) * c;
+    auto mapped = [&](const ctl_texture* t) {
+        return v2(t->m11 * uv.x + t->m12 * uv.y, t->m21 * uv.x + t->m22 * uv.y) + v2(t->m13, t->m23);
+    };
+    const ctl_texture* refl_img = m.texture != UINT_MAX ? d->textures + m.texture : nullptr;
+    const ctl_texture* alpha_img = m.alpha_texture != UINT_MAX ? d->textures + m.alpha_texture : nullptr;
+    if ((m.alpha_state == 2 && alpha_img) || (m.alpha_state == 6 && refl_img)) {
+        const ctl_texture* t = m.alpha_state == 2 ? alpha_img : refl_img;
+        V2 l;
+        if (!c5::wrap_coords(mapped(t), v2((float)t->width, (float)t->height), t->wrap, &l)) return 0.0f >= m.alpha_threshold;
+        uint32_t x = omin((uint32_t)l.x, t->width - 1), y = omin((uint32_t)l.y, t->height - 1);
+        float alpha = float(d->tex_data[t->offsets[0] + y * t->width + x] >> 24) / 255.0f;
+        return alpha >= m.alpha_threshold;
+    }
+    const ctl_texture* src = (m.alpha_state & 4) ? refl_img : alpha_img;
+    Spec val;
+    if (src) {
+        c5::Mip M{src, d->tex_data};
+        V2 u2 = mapped(src);
+        val = (src->filter == CTL_TEX_POINT ? c5::texel(M, 0, u2) : c5::triangle(M, 0, u2)) *
+              v3(src->scale[0], src->scale[1], src->scale[2]);
+    } else {
+        val = v3(m.reflectance[0], m.reflectance[1], m.reflectance[2]);
+    }
+    if ((m.alpha_state & 3) == 1) return val.x * 0.212671f + val.y * 0.715160f + val.z * 0.072169f >= m.alpha_threshold;
+    return true;
+}
 
 // diffuse::m_reflectance.Evaluate(bRec.dg): ConstantTexture or ImageTexture
 Spec diffuse_R(const ctl_scene_desc* d, const ctl_material& m, const DG& dg) {
@@ -578,7 +625,7 @@ bool occluded(RenderCtx& C, V3 ori, V3 dir, float tmax) {   // KernelDynamicScen
     if (C.anyHitShadow) {
         h.t = tmax - eps; h.tri = UINT_MAX; h.node = UINT_MAX;
         if (C.S.d->n_nodes == 0) return false;
-        trace_two_level(C.S, ori, dir, 0.0f, eps, h, true, C.tie, &C.st);
+        trace_two_level(C.S, ori, dir, 0.0f, eps, h, true, C.tie, &C.st, scene_has_alpha(C.S.d));
         return h.tri != UINT_MAX;
     }
     trace_ray(C.S, ori, dir, h, C.tie, &C.st);
