@@ -20,6 +20,7 @@ fallback: every compute call goes through the HIP library and raises if it is
 missing or fails.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -144,6 +145,33 @@ class HostScene:
         if r < 0:
             _check(1, None, "add_texture")
         return r
+
+    def add_xmsh(self, data, materials=None, material_record_size=_abi.CTL_XMSH_MATERIAL_RECORD_SIZE):
+        """Compiled mesh from an .xmsh stream (bytes or a path) — Mesh::Mesh(path, IInStream&)
+        (Engine/Mesh.cpp:46-98).  Reference files: pass sizeof(Material) of the writing build as
+        material_record_size and the kernel materials in file order."""
+        if isinstance(data, (str, os.PathLike)):
+            with open(data, "rb") as f:
+                data = f.read()
+        buf = C.create_string_buffer(bytes(data), len(data))
+        mats = None if materials is None else (Material * len(materials))(*materials)
+        r = self._L.ctl_host_scene_add_xmsh(self._h, buf, len(data), int(material_record_size), mats,
+                                            0 if materials is None else len(materials))
+        if r < 0:
+            _check(1, None, "add_xmsh")
+        return r
+
+    def write_xmsh(self, mesh, path=None):
+        """Mesh `mesh` of the last compile as .xmsh bytes (written to `path` when given)."""
+        n = C.c_uint64(0)
+        _check(self._L.ctl_host_scene_write_xmsh(self._h, int(mesh), None, 0, C.byref(n)), None, "write_xmsh")
+        buf = C.create_string_buffer(n.value)
+        _check(self._L.ctl_host_scene_write_xmsh(self._h, int(mesh), buf, n.value, C.byref(n)), None, "write_xmsh")
+        data = buf.raw[:n.value]
+        if path is not None:
+            with open(path, "wb") as f:
+                f.write(data)
+        return data
 
     def add_node(self, mesh, xf16=None):
         arr = None

@@ -157,6 +157,21 @@ struct NormalDecodeHost {
 };
 
 }  // namespace
+bool scene_add_light(ctl_host_scene* s, uint32_t node, uint32_t local_mat, const float L[3]) {
+    uint32_t perNode = 0;
+    for (auto& l : s->lights) {
+        if (l.node == node && l.local_mat == local_mat) {   // NodeLightIndex != -1: SetData on the old light
+            l.L[0] = L[0]; l.L[1] = L[1]; l.L[2] = L[2];
+            return true;
+        }
+        perNode += l.node == node;
+    }
+    if (perNode >= 2) { set_host_error("area light: MAX_AREALIGHT_NUM (2) lights per node"); return false; }
+    if (s->lights.size() >= CTL_MAX_NUM_LIGHTS) { set_host_error("area light: MAX_NUM_LIGHTS (16)"); return false; }
+    s->lights.push_back(ctl_host_scene::Light{node, local_mat, {L[0], L[1], L[2]}});
+    return true;
+}
+
 }  // namespace ctl
 
 using namespace ctl;
@@ -204,7 +219,17 @@ CTL_API int32_t ctl_host_scene_add_node(ctl_host_scene* s, uint32_t mesh, const 
     n.xf = m44_identity();
     if (xf16) memcpy(n.xf.d, xf16, 64);
     s->nodes.push_back(n);
-    return (int32_t)s->nodes.size() - 1;
+    uint32_t ni = (uint32_t)s->nodes.size() - 1;
+    // CreateNode: one light per MeshPartLight of the mesh (DynamicScene.cpp:340-341)
+    for (const auto& al : s->meshes[mesh].auto_lights)
+        if (!scene_add_light(s, ni, al.mat, al.L)) {
+            s->lights.erase(std::remove_if(s->lights.begin(), s->lights.end(),
+                                           [&](const ctl_host_scene::Light& l) { return l.node == ni; }),
+                            s->lights.end());
+            s->nodes.pop_back();
+            return -1;
+        }
+    return (int32_t)ni;
 }
 
 CTL_API int32_t ctl_host_scene_add_area_light(ctl_host_scene* s, uint32_t node, uint32_t local_material,
@@ -212,13 +237,10 @@ CTL_API int32_t ctl_host_scene_add_area_light(ctl_host_scene* s, uint32_t node, 
     if (!s || node >= s->nodes.size()) { set_host_error("add_area_light: bad node"); return -1; }
     const auto& mesh = s->meshes[s->nodes[node].mesh];
     if (local_material >= mesh.materials.size()) { set_host_error("add_area_light: bad material"); return -1; }
-    uint32_t perNode = 0;
-    for (auto& l : s->lights) perNode += l.node == node;
-    if (perNode >= 2) { set_host_error("add_area_light: MAX_AREALIGHT_NUM (2) lights per node"); return -1; }
-    if (s->lights.size() >= CTL_MAX_NUM_LIGHTS) { set_host_error("add_area_light: MAX_NUM_LIGHTS (16)"); return -1; }
-    ctl_host_scene::Light l{node, local_material, {radiance[0], radiance[1], radiance[2]}};
-    s->lights.push_back(l);
-    return (int32_t)s->lights.size() - 1;
+    if (!scene_add_light(s, node, local_material, radiance)) return -1;
+    for (size_t i = 0; i < s->lights.size(); i++)
+        if (s->lights[i].node == node && s->lights[i].local_mat == local_material) return (int32_t)i;
+    return -1;
 }
 
 CTL_API ctl_status ctl_host_scene_set_camera(ctl_host_scene* s, const float pos[3], const float target[3],
@@ -313,12 +335,34 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
     s->kmeshes.clear(); s->knodes.clear(); s->scene_bvh.clear(); s->xf.clear(); s->inv_xf.clear();
     s->klights.clear(); s->light_tris.clear(); s->light_tri_cdf.clear();
     s->max_mesh_depth = 0;
+    s->compiled = false;
 
     std::vector<Box> meshBox(s->meshes.size());
     // --- per mesh: BVH, Woop entries, TriangleData, materials
     for (size_t mi = 0; mi < s->meshes.size(); mi++) {
         const auto& M = s->meshes[mi];
-        uint32_t ntri = (uint32_t)(M.idx.size() / 3);
+        uint32_t ntri = M.n_triangles();
+        if (M.precompiled) {   // .xmsh mesh: arrays relocated as they are (Mesh::getKernelData)
+            ctl_kernel_mesh km;
+            km.triangle_offset = (uint32_t)s->tri_data.size();
+            km.bvh_node_offset = (uint32_t)(s->bvh_nodes.size() * 4);
+            km.bvh_triangle_offset = (uint32_t)(s->woop.size() * 3);
+            km.bvh_indices_offset = (uint32_t)s->woop.size();
+            km.std_material_offset = (uint32_t)s->materials.size();
+            s->kmeshes.push_back(km);
+            s->tri_data.insert(s->tri_data.end(), M.c_tri.begin(), M.c_tri.end());
+            s->bvh_nodes.insert(s->bvh_nodes.end(), M.c_nodes.begin(), M.c_nodes.end());
+            s->woop.insert(s->woop.end(), M.c_woop.begin(), M.c_woop.end());
+            s->tri_indices.insert(s->tri_indices.end(), M.c_idx.begin(), M.c_idx.end());
+            for (auto m : M.materials) {
+                m.node_light_index = 0xffffffffu;
+                s->materials.push_back(m);
+            }
+            memcpy(meshBox[mi].lo, M.c_box, 12);
+            memcpy(meshBox[mi].hi, M.c_box + 3, 12);
+            s->max_mesh_depth = std::max(s->max_mesh_depth, M.c_depth);
+            continue;
+        }
         auto V = [&](uint32_t vi) { return mk3(M.v[3 * vi], M.v[3 * vi + 1], M.v[3 * vi + 2]); };
         std::vector<Box> boxes(ntri);
         parallel_for(ntri, threads, [&](uint64_t b, uint64_t e) {
@@ -404,6 +448,11 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
             s->materials.push_back(m);
         }
     }
+    s->kmesh_box.resize(6 * s->meshes.size());
+    for (size_t mi = 0; mi < s->meshes.size(); mi++) {
+        memcpy(&s->kmesh_box[6 * mi], meshBox[mi].lo, 12);
+        memcpy(&s->kmesh_box[6 * mi + 3], meshBox[mi].hi, 12);
+    }
 
     // --- nodes (instances), transforms, top-level BVH
     Box sceneBox;
@@ -470,7 +519,7 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         kl.cdf_first = (uint32_t)s->light_tri_cdf.size();
         kl.node_idx = L.node;
         const auto& M = s->meshes[kn.mesh_index];
-        uint32_t ntri = (uint32_t)(M.idx.size() / 3);
+        uint32_t ntri = M.n_triangles();
         // entries of this mesh: [bvh_indices_offset, next mesh)
         uint64_t e0 = km.bvh_indices_offset;
         uint64_t e1 = (kn.mesh_index + 1 < s->kmeshes.size()) ? s->kmeshes[kn.mesh_index + 1].bvh_indices_offset
@@ -551,6 +600,7 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
     camera_setup(s->cam_pos, s->cam_tar, s->cam_up, s->cam_fov, s->cam_near, s->cam_far, s->cam_w, s->cam_h, d.camera);
     d.flags = s->flags;
     *out = d;
+    s->compiled = true;
     return CTL_OK;
 }
 

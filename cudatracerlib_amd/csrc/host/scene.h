@@ -17,6 +17,20 @@ struct ctl_host_scene {
         std::vector<float> uv;        // per-vertex uv (may be empty)
         std::vector<uint8_t> mat;     // per triangle (may be empty)
         std::vector<ctl_material> materials;
+        // compiled mesh loaded from an .xmsh file (xmsh.cpp): the arrays are
+        // taken as they are, compile() only relocates them
+        bool precompiled = false;
+        std::vector<ctl_triangle_data> c_tri;
+        std::vector<ctl_bvh_node> c_nodes;
+        std::vector<ctl_woop_tri> c_woop;
+        std::vector<ctl_tri_index> c_idx;
+        float c_box[6] = {0, 0, 0, 0, 0, 0};   // m_sLocalBox minV, maxV
+        uint32_t c_depth = 0;
+        // MeshPartLight entries resolved to material indices: every node
+        // created on the mesh gets these lights (DynamicScene.cpp:340-341)
+        struct AutoLight { uint32_t mat; float L[3]; };
+        std::vector<AutoLight> auto_lights;
+        uint32_t n_triangles() const { return precompiled ? (uint32_t)c_tri.size() : (uint32_t)(idx.size() / 3); }
     };
     struct Node { uint32_t mesh; bool has_xf; ctl::m44 xf; };
     struct Light { uint32_t node; uint32_t local_mat; float L[3]; };
@@ -48,8 +62,10 @@ struct ctl_host_scene {
     std::vector<float> light_tri_cdf;
     std::vector<ctl_texture> textures;   // added by ctl_host_scene_add_texture (kept across compiles)
     std::vector<uint32_t> tex_data;
+    std::vector<float> kmesh_box;        // 6 floats per mesh: local box of the last compile
     ctl_scene_desc desc{};
     uint32_t max_mesh_depth = 0;
+    bool compiled = false;
 };
 
 namespace ctl {
@@ -61,4 +77,9 @@ void woop_get(const ctl_woop_tri& in, f3& v0, f3& v1, f3& v2);
 void camera_setup(const float pos[3], const float tar[3], const float up[3], float fov_deg, float nearc, float farc,
                   uint32_t w, uint32_t h, ctl_camera& out);
 void set_host_error(const std::string& s);
+// adds lights to node `node` (area light of material `local_mat`); replaces
+// the radiance when the node already has a light on that material
+// (DynamicScene::CreateLight, DynamicScene.cpp:689-711); false + error set
+// when a per-node / per-scene limit is hit
+bool scene_add_light(ctl_host_scene* s, uint32_t node, uint32_t local_mat, const float L[3]);
 }  // namespace ctl

@@ -450,6 +450,33 @@ CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags);
 CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth,
                                                  uint32_t bins, uint32_t max_leaf);
 CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, ctl_scene_desc* out);
+
+/* Compiled meshes (.xmsh).  Replaces Mesh::Mesh(path, IInStream&, ...)
+ * (Engine/Mesh.cpp:46-98) as called by DynamicScene::CreateNode(path)
+ * (DynamicScene.cpp:270-345) on a static mesh file (leading u32
+ * MeshCompileType 0; Animated files are refused): loads the box, MeshPartLights, TriangleData,
+ * BVHNodeData, TriIntersectorData and TriIntersectorData2 arrays of the file
+ * as they are (no rebuild).  Every node later created on the mesh gets one
+ * area light per MeshPartLight, matched to a material by name
+ * (DynamicScene.cpp:340-341, 689-734).  A reference Material record is a
+ * build-specific variant blob: pass its size (sizeof(Material) of the writing
+ * build) and the flattened kernel materials in file order; only each record's
+ * leading FixedString<64> Name is read.  With materials == NULL the records
+ * must be the CTL_XMSH_MATERIAL_RECORD_SIZE-byte records written by
+ * ctl_host_scene_write_xmsh (Name + ctl_material).  The arrays are checked to
+ * form one tree (children and entries in range, depth <= 64) before they are
+ * accepted.  Returns the mesh index, or -1 (ctl_host_last_error). */
+#define CTL_XMSH_MATERIAL_RECORD_SIZE 148u
+CTL_API int32_t ctl_host_scene_add_xmsh(ctl_host_scene* s, const void* data, uint64_t size,
+                                        uint32_t material_record_size, const ctl_material* materials,
+                                        uint32_t n_materials);
+/* Writes mesh `mesh` of the last compile as an .xmsh stream: the byte layout
+ * of Mesh::CompileMesh + ConstructBVH (Mesh.cpp:279-288,
+ * MeshLoader/BVHBuilderHelper.cpp:129-147), materials as
+ * CTL_XMSH_MATERIAL_RECORD_SIZE-byte records named "material<i>", one
+ * MeshPartLight per lit material.  out == NULL: only *size is set. */
+CTL_API ctl_status ctl_host_scene_write_xmsh(ctl_host_scene* s, uint32_t mesh, void* out, uint64_t capacity,
+                                             uint64_t* size);
 CTL_API const char* ctl_host_last_error(void);
 
 /* Synthetic workloads of BASELINE.json (seed 0x5EED): 1 = C1 Cornell box
