@@ -25,10 +25,10 @@ import os
 import numpy as np
 
 from . import _abi
-from ._abi import (PTParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK, CTL_SCENE_BINARY_BVH,
+from ._abi import (PTParams, WptParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK, CTL_SCENE_BINARY_BVH,
                    CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT)
 
-__all__ = ["HostScene", "Tracer", "PathTracer", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
+__all__ = ["HostScene", "Tracer", "PathTracer", "WavefrontPathTracer", "WptParams", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
            "roughdielectric_material", "set_alpha_map",
            "CTL_SCENE_HALF_HOST_QUIRK", "CTL_SCENE_BINARY_BVH", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "lib", "diffuse_material"]
 
@@ -318,3 +318,30 @@ class PathTracer(Tracer):
         _check(self._L.ctl_render_pass_stats(self._ctx, C.byref(self.params), fb_ptr, out, stream), self._ctx,
                "ctl_render_pass_stats")
         return list(out)
+
+
+class WavefrontPathTracer(Tracer):
+    """WavefrontPathTracer (Integrators/PseudoRealtime/WavefrontPathTracer.h:24-67): path
+    tracing over a DoubleRayBuffer, the batch traversal's second caller.  Defaults
+    Direct=1, MaxPathLength=50, RRStartDepth=5 (WavefrontPathTracer.h:32-37)."""
+
+    def __init__(self, device=0, direct=True, max_path_length=50, rr_start_depth=5):
+        super().__init__(device)
+        self.params = WptParams(1 if direct else 0, max_path_length, rr_start_depth, 0, 0)
+        self.passes_done = 0
+
+    def do_pass(self, fb_ptr, pass_index, new_trace=False, stream=0):
+        """Tracer::DoPass (Kernel/Tracer.h:209-248): UpdateKernel's sampler tables of
+        `pass_index`, m_uPassesDone++ (reset by new_trace), then DoRender into fb."""
+        if new_trace:
+            self.passes_done = 0
+        self.generate_samples(pass_index, stream)
+        self.passes_done += 1
+        self.params.passes_done = self.passes_done
+        _check(self._L.ctl_wpt_render_pass(self._ctx, C.byref(self.params), fb_ptr, stream), self._ctx,
+               "ctl_wpt_render_pass")
+
+    def last_pass_ms(self):
+        ms = C.c_float()
+        _check(self._L.ctl_last_pass_ms(self._ctx, C.byref(ms)), self._ctx, "ctl_last_pass_ms")
+        return ms.value

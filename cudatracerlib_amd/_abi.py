@@ -136,6 +136,11 @@ class PTParams(C.Structure):
                 ("rank", C.c_uint32), ("flags", C.c_uint32)]
 
 
+class WptParams(C.Structure):
+    _fields_ = [("direct", C.c_int32), ("max_path_length", C.c_int32), ("rr_start_depth", C.c_int32),
+                ("passes_done", C.c_uint32), ("flags", C.c_uint32)]
+
+
 # Every symbol include/ctl_trace.h declares: (name, restype, argtypes)
 _vp = C.c_void_p
 SYMBOLS = [
@@ -148,6 +153,7 @@ SYMBOLS = [
     ("ctl_sampler_upload", C.c_int32, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
     ("ctl_intersect", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, _vp]),
     ("ctl_render_pass", C.c_int32, [_vp, C.POINTER(PTParams), _vp, _vp]),
+    ("ctl_wpt_render_pass", C.c_int32, [_vp, C.POINTER(WptParams), _vp, _vp]),
     ("ctl_rays_traced", C.c_uint64, [_vp]),
     ("ctl_reset_rays", C.c_int32, [_vp, _vp]),
     ("ctl_sync", C.c_int32, [_vp, _vp]),

@@ -177,6 +177,29 @@ CTL_HD float half_to_float(uint32_t h16, bool host_quirk) {
     return bits_f((int32_t)b);
 }
 
+// float -> unsigned short of a value in [0, 65536); NaN -> 0 (the conversion
+// both targets' cvt instructions give, made explicit).
+CTL_HD uint16_t u16_trunc(float f) { return (f != f) ? (uint16_t)0 : (uint16_t)(int32_t)f; }
+
+// NormalizedFloat3ToUchar2_Spherical (Compression.h:12-18)
+CTL_HD uint16_t normal_encode16(f3 v) {
+    float theta = (cr_acos(v.z) * (255.0f / CTL_PI));
+    float phi = (cr_atan2(v.y, v.x) * (255.0f / (2.0f * CTL_PI)));
+    phi = phi < 0 ? (phi + 255) : phi;
+    return (uint16_t)(((uint32_t)u16_trunc(theta) << 8) | (uint32_t)u16_trunc(phi));
+}
+
+// half((float)x).ToFloat() for a pixel coordinate x <= 65504: __float2half_rn
+// (Math/half.h:21-24, device branch) keeps 11 significant bits, ties to even.
+CTL_HD float half_round_int(uint32_t x) {
+    if (x < 2048u) return (float)x;
+    uint32_t sh = 0;
+    while ((x >> sh) >= 2048u) sh++;
+    uint32_t q = x >> sh, r = x & ((1u << sh) - 1u), h = 1u << (sh - 1u);
+    if (r > h || (r == h && (q & 1u))) q++;
+    return (float)(q << sh);
+}
+
 // Uchar2ToNormalizedFloat3_Spherical (Compression.h:20-31)
 CTL_HD f3 normal_decode16(uint32_t v16) {
     const float PI_4 = CTL_PI / 4.0f, PI_2 = CTL_PI / 2.0f;

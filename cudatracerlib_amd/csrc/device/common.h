@@ -308,6 +308,8 @@ struct WfState {
     size_t capacity;
 };
 
+struct WptBuffers;
+
 }  // namespace ctl
 
 struct ctl_ctx {
@@ -334,6 +336,7 @@ struct ctl_ctx {
     uint32_t* d_powers = nullptr;               // XORWOW step powers for sampler_kernel
     ctl::WfState wf{};
     std::vector<void*> wf_allocs;
+    ctl::WptBuffers* wpt = nullptr;             // WavefrontPathTracer queues (wpt.hip)
     int cu_count = 256;
 };
 
@@ -352,4 +355,10 @@ int resident_blocks(ctl_ctx* c, K kernel, size_t lds) {
 // wavefront.hip
 int wavefront_pass(ctl_ctx* c, const PathParams& P, ctl_pixel* fb, bool stats, hipStream_t s);
 void wavefront_free(ctl_ctx* c);
+// wpt.hip
+int wpt_pass(ctl_ctx* c, const ctl_wpt_params* p, ctl_pixel* fb, hipStream_t s);
+void wpt_free(ctl_ctx* c);
+// ctl_trace.hip: the batch traversal launch and the ray counter, for wpt.hip
+int intersect_launch(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit, hipStream_t s);
+int count_rays(ctl_ctx* c, uint64_t n, hipStream_t s);
 }

@@ -477,6 +477,7 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
     (void)hipDeviceSynchronize();
     free_scene(c);
     ctl::wavefront_free(c);
+    ctl::wpt_free(c);
     for (int i = 0; i < 2; i++) {
         if (c->d_s1[i]) (void)hipFree(c->d_s1[i]);
         if (c->d_s2[i]) (void)hipFree(c->d_s2[i]);
@@ -846,6 +847,17 @@ static ctl_status add_rays(ctl_ctx* c, uint64_t n, hipStream_t s) {
     CTL_HIP(c, hipGetLastError());
     return CTL_OK;
 }
+
+}  // extern "C"
+
+namespace ctl {
+int intersect_launch(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit, hipStream_t s) {
+    return launch_intersect(c, n, rays, hits, any_hit, false, s);
+}
+int count_rays(ctl_ctx* c, uint64_t n, hipStream_t s) { return add_rays(c, n, s); }
+}  // namespace ctl
+
+extern "C" {
 
 CTL_API uint64_t ctl_rays_traced(ctl_ctx* c) {
     if (!c) return 0;

@@ -1,0 +1,432 @@
+// wpt.hip — WavefrontPathTracer (Integrators/PseudoRealtime/WavefrontPathTracer.cu:17-189)
+// over a DoubleRayBuffer (Kernel/DoubleRayBuffer.h:13-231): the second caller of
+// the batch traversal (ctl_intersect's kernel).
+//
+// Per bounce:
+//   traverse   payload rays, closest hit; last bounce's shadow rays, closest hit
+//              (DoubleRayBuffer::FinishIteration, DoubleRayBuffer.h:84-112)
+//   iterate    one thread per payload element: pathIterateKernel's body
+//              (WavefrontPathTracer.cu:51-150) -> continuation ray, shadow ray,
+//              flags; AddSample of finished paths
+//   scan       block totals -> exclusive offsets (one block)
+//   scatter    stable compaction of continuations and shadow rays
+//
+// The reference assigns queue slots with atomicInc (insertPayloadElement /
+// insertSecondaryRay) and a path's random numbers come from its slot
+// (g_SamplerData(rayIdx), WavefrontPathTracer.cu:58), so its image depends on
+// the order the atomics resolve.  The stable compaction here reproduces the
+// sequential order of those atomics — element j's shadow ray and continuation
+// get the slots a one-thread run would give them — which makes the pass
+// deterministic and lets the CPU oracle follow it bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+
+#include "common.h"
+
+namespace ctl {
+
+// WavefrontPTRayData (WavefrontPathTracer.h:11-22), 64 B
+struct WptPay {
+    float4 a;   // throughput xyz | bsdf_pdf
+    float4 b;   // L xyz | dDist
+    float4 c;   // directF xyz | bits: half x (pixel) | half y << 16, stored as the rounded floats' integers
+    uint4 d;    // dIdx | specular_bounce | prev_normal (16-bit spherical code) | unused
+};
+static_assert(sizeof(WptPay) == 64, "payload is 64 B");
+
+struct WptBuffers {
+    size_t capacity = 0;
+    WptPay* pay[2] = {nullptr, nullptr};
+    ctl_ray* rays[2] = {nullptr, nullptr};
+    ctl_hit* hits = nullptr;
+    ctl_ray* sec_tmp = nullptr;    // shadow ray of element j (uncompacted)
+    ctl_ray* sec = nullptr;        // compacted shadow rays of the last bounce
+    ctl_hit* sec_hits = nullptr;
+    uint8_t* flags = nullptr;      // bit 0: continues, bit 1: shadow ray
+    uint2* blocks = nullptr;       // per-block counts -> exclusive offsets
+    uint32_t* totals = nullptr;    // device: {continuations, shadow rays}
+    uint32_t* h_totals = nullptr;  // pinned host copy
+    std::vector<void*> allocs;
+};
+
+namespace {
+
+struct WptArgs {
+    uint32_t width, height, nseq, len;
+    int32_t depth, max_path_length, rr_start_depth;
+    uint32_t skip;       // rng.skip(iterationIdx + 2), iterationIdx = m_uPassesDone
+    bool half_quirk;
+};
+
+__device__ __forceinline__ SamplerDev wpt_rng(const float* s1, const float2* s2, const WptArgs& A, uint32_t idx,
+                                              uint32_t skip) {
+    SamplerDev r;
+    r.s1 = s1; r.s2 = s2; r.nseq = A.nseq; r.len = A.len;
+    r.a = idx % A.nseq; r.b = (idx / A.nseq) % A.nseq;
+    r.d1 = skip; r.d2 = skip;
+    return r;
+}
+
+// pathCreateKernelWPT (WavefrontPathTracer.cu:17-49) with one sample per pixel:
+// the payload slot of pixel i is i (rayidx order).
+__global__ __launch_bounds__(kBlock) void wpt_create_kernel(DevScene S, WptArgs A, const float* s1, const float2* s2,
+                                                            uint32_t n, ctl_ray* rays, WptPay* pay) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t x = i % A.width, y = i / A.width;
+    SamplerDev rng = wpt_rng(s1, s2, A, i, 0);
+    // sampleSensorRay(r, Vec2f(x, y) + rng.randomFloat2(), rng.randomFloat2()): arguments left to right
+    const f2 pX = mk2((float)x, (float)y) + rng.next2();
+    (void)rng.next2();
+    f3 o, d;
+    sensor_ray(S, pX, o, d);
+    ctl_ray r;
+    r.o[0] = o.x; r.o[1] = o.y; r.o[2] = o.z; r.tmin = S.ray_eps;
+    r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z; r.tmax = FLT_MAX;
+    rays[i] = r;
+    WptPay p;
+    p.a = make_float4(1.0f, 1.0f, 1.0f, 0.0f);   // throughput = W = Spectrum(1) (Sensor.cu:117)
+    p.b = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    p.c = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((uint32_t)half_round_int(x) | ((uint32_t)half_round_int(y) << 16)));
+    p.d = make_uint4(0xffffffffu, 1u, 0u, 0u);
+    pay[i] = p;
+}
+
+// KernelDynamicScene::sampleEmitter (KernelDynamicScene.cu:25-39)
+__device__ __forceinline__ uint32_t sample_emitter(const DevScene& S, f2& sample, float& emPdf) {
+    const uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
+    uint32_t first = 0, cnt = nl;   // STL_upper_bound
+    while (cnt > 0) {
+        uint32_t c2 = cnt / 2, mid = first + c2;
+        if (!(sample.x < S.light_cdf[mid])) { first = mid + 1; cnt -= c2 + 1; }
+        else cnt = c2;
+    }
+    const uint32_t idx = first < nl ? first : nl - 1;
+    const float fU = S.light_cdf[idx], fL = idx > 0 ? S.light_cdf[idx - 1] : 0.0f;
+    sample.x = (sample.x - fL) / (fU - fL);
+    emPdf = fU - fL;
+    return idx;
+}
+
+// pathIterateKernel<NEXT_EVENT_EST> body for payload element j (WavefrontPathTracer.cu:56-148).
+template <bool NEE, bool FULL>
+__global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs A, const float* s1, const float2* s2,
+                                                             uint32_t n, WptPay* pay, ctl_ray* rays,
+                                                             const ctl_hit* __restrict__ hits,
+                                                             const ctl_hit* __restrict__ sec_hits, ctl_ray* sec_tmp,
+                                                             uint8_t* flags, uint2* blocks, ctl_pixel* fb) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    bool cont = false, shadow = false;
+    if (j < n) {
+        WptPay p = pay[j];
+        const ctl_ray ray = rays[j];
+        const ctl_hit h = hits[j];
+        SamplerDev rng = wpt_rng(s1, s2, A, j, A.skip);   // rng.skip(iterationIdx + 2): plus the camera sample
+        spec tp = mk3(p.a.x, p.a.y, p.a.z), L = mk3(p.b.x, p.b.y, p.b.z);
+        float bpdf = p.a.w;
+        bool specular = p.d.y != 0;
+        if (NEE && A.depth > 0 && p.d.x != 0xffffffffu) {
+            // accessSecondaryRay: closest hit of the shadow ray against the light distance
+            if (sec_hits[p.d.x].dist >= p.b.w * (1 - S.ray_eps)) L = L + mk3(p.c.x, p.c.y, p.c.z);
+            p.d.x = 0xffffffffu;
+            p.c.x = p.c.y = p.c.z = 0.0f;
+        }
+        bool terminated = A.depth + 1 == A.max_path_length;
+        const f3 ro = mk3(ray.o[0], ray.o[1], ray.o[2]), rd = mk3(ray.d[0], ray.d[1], ray.d[2]);
+        ctl_ray next;
+        if ((uint32_t)h.tri_idx != 0xffffffffu) {
+            // traversalResult::toResult (TraceHelper.cu:44-51): 16-bit barycentrics
+            const uint32_t bc = (uint32_t)h.bary;
+            const f2 bary = mk2((float)(bc & 0xffffu) / 65535.0f, (float)(bc >> 16) / 65535.0f);
+            // TraceResult::getBsdfSample (TraceResult.cu:16-45); wo has no value yet -> (0,0,1)
+            bsdf_rec b;
+            b.wo = mk3(0.0f, 0.0f, 1.0f);
+            b.sampled_type = 0;
+            b.type_mask = kEAll;
+            dgeom dg;
+            dg.P = ro + h.dist * rd;
+            const uint32_t tri = (uint32_t)h.tri_idx, node = (uint32_t)h.node_idx;
+            const ctl_triangle_data td = S.tri_data[tri];
+            const ctl_node* N = S.nodes + node;
+            fill_dg(td, load_m44(S.xf + 4 * node), bary, A.half_quirk, LutDecode{S.normal_lut}, dg);
+            dg.dudx = dg.dudy = dg.dvdx = dg.dvdy = 0.0f;
+            dg.has_partials = false;   // no ray differentials in the wavefront tracer
+            b.wi = to_local(dg.sys, -rd);
+            const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N->material_offset];
+            if (mat.two_sided && b.wi.z < 0) {
+                dg.n = -dg.n;
+                dg.sys.n = -dg.sys.n;
+                b.wi.z *= -1.0f;
+            }
+            const TexView tex{S.textures, S.tex_data};
+            if (mat.node_light_index != 0xffffffffu) {
+                const uint32_t li = N->lights[mat.node_light_index];
+                const ctl_light Lt = S.lights[li];
+                float misWeight = 1.0f;
+                if (NEE && !(A.depth == 0 || specular)) {
+                    direct_rec dRec;   // DirectSamplingRecFromRay with the stored previous normal
+                    dRec.ref = ro; dRec.refN = LutDecode{S.normal_lut}(p.d.z); dRec.p = dg.P; dRec.n = dg.n;
+                    dRec.d = rd; dRec.dist = h.dist; dRec.measure = kESolidAngle;
+                    float direct_pdf = light_pdf_direct(Lt, dRec) * (S.light_cdf[li] - (li == 0 ? 0.0f : S.light_cdf[li - 1]));
+                    misWeight = power_heuristic(bpdf, direct_pdf);
+                }
+                f3 w = -rd;
+                spec Le = (dot(dg.sys.n, w) <= 0) ? mk3s(0.0f) : mk3(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
+                L = L + (misWeight * Le) * tp;
+            }
+            bool surviveRR = true;
+            if (A.depth >= A.rr_start_depth) {
+                if (rng.next1() < spec_max(tp)) tp = spec_div(tp, spec_max(tp));
+                else surviveRR = false;
+            }
+            if (A.depth + 1 != A.max_path_length && surviveRR) {
+                spec f = FULL ? bsdf_sample(mat, b, bpdf, rng.next2(), dg, &tex)
+                              : diffuse_sample(mat, b, bpdf, rng.next2());
+                specular = (b.sampled_type & kEDelta) != 0;
+                const f3 out = to_world(dg.sys, b.wo);
+                p.d.x = 0xffffffffu;
+                if (NEE && (mat.combined_type & kESmooth) != 0) {
+                    direct_rec dRec;   // DirectSamplingRecord(P, sys.n)
+                    dRec.ref = dg.P; dRec.refN = dg.sys.n; dRec.p = dg.P; dRec.n = dg.sys.n; dRec.measure = kEArea;
+                    // sampleEmitterDirect (KernelDynamicScene.cu:98-117): one 2D sample picks the
+                    // light and, rescaled, the point on it; no lights -> no emitter, value 0
+                    f2 sample = rng.next2();
+                    float emPdf = 0.0f;
+                    if (S.n_lights) {
+                    const uint32_t lidx = sample_emitter(S, sample, emPdf);
+                    spec value = light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, sample);
+                    if (dRec.pdf != 0) {
+                        dRec.pdf *= emPdf;
+                        value = spec_div(value, emPdf);
+                    } else {
+                        value = mk3s(0.0f);
+                    }
+                    if (!spec_zero(value)) {
+                        b.type_mask = kEAll & ~kEDelta;
+                        b.wo = to_local(dg.sys, dRec.d);
+                        spec bsdfVal = FULL ? bsdf_f(mat, b, dg, &tex) : diffuse_f(mat, b);
+                        const float bsdfPdf = FULL ? bsdf_pdf(mat, b) : diffuse_pdf(mat, b);
+                        const float directPdf = dRec.pdf;   // measure is ESolidAngle after sampleDirect
+                        const float weight = power_heuristic(directPdf, bsdfPdf);
+                        const spec dF = tp * value * bsdfVal * weight;
+                        p.c.x = dF.x; p.c.y = dF.y; p.c.z = dF.z;
+                        p.b.w = dRec.dist;
+                        ctl_ray sr;
+                        sr.o[0] = dg.P.x; sr.o[1] = dg.P.y; sr.o[2] = dg.P.z; sr.tmin = S.ray_eps;
+                        sr.d[0] = dRec.d.x; sr.d[1] = dRec.d.y; sr.d[2] = dRec.d.z; sr.tmax = FLT_MAX;
+                        sec_tmp[j] = sr;
+                        shadow = true;   // dIdx = its slot, set by the scatter
+                    }
+                    }
+                }
+                p.d.z = normal_encode16(dg.sys.n);
+                tp = tp * f;
+                next.o[0] = dg.P.x; next.o[1] = dg.P.y; next.o[2] = dg.P.z; next.tmin = S.ray_eps;
+                next.d[0] = out.x; next.d[1] = out.y; next.d[2] = out.z; next.tmax = FLT_MAX;
+                cont = true;
+            } else {
+                terminated = true;
+            }
+        } else {
+            terminated = true;
+            L = L + (1.0f * tp) * mk3s(0.0f);   // misWeight * throughput * EvalEnvironment (no env map)
+        }
+        if (terminated) {
+            const uint32_t hx = __float_as_uint(p.c.w) & 0xffffu, hy = __float_as_uint(p.c.w) >> 16;
+            PathParams P{};
+            P.width = A.width; P.height = A.height;
+            add_sample(fb, P, mk2((float)hx, (float)hy), L);
+        }
+        if (cont) {
+            p.a = make_float4(tp.x, tp.y, tp.z, bpdf);
+            p.b.x = L.x; p.b.y = L.y; p.b.z = L.z;
+            p.d.y = specular ? 1u : 0u;
+            pay[j] = p;
+            rays[j] = next;
+        }
+        flags[j] = (uint8_t)((cont ? 1u : 0u) | (shadow ? 2u : 0u));
+    }
+    const int nc = __syncthreads_count(cont), ns = __syncthreads_count(shadow);
+    if (threadIdx.x == 0) blocks[blockIdx.x] = make_uint2((uint32_t)nc, (uint32_t)ns);
+}
+
+// Exclusive scan of the per-block counts in one 1024-thread block.
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void wpt_scan_kernel(uint2* blocks, uint32_t nb, uint32_t* totals) {
+    __shared__ uint32_t sc[kScanThreads], ss[kScanThreads];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nb + kScanThreads - 1) / kScanThreads;
+    const uint32_t b0 = std::min(nb, t * per), b1 = std::min(nb, b0 + per);
+    uint32_t c = 0, s = 0;
+    for (uint32_t i = b0; i < b1; i++) { uint2 v = blocks[i]; c += v.x; s += v.y; }
+    sc[t] = c; ss[t] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < kScanThreads; off <<= 1) {   // Hillis-Steele inclusive scan
+        uint32_t ac = t >= off ? sc[t - off] : 0u, as = t >= off ? ss[t - off] : 0u;
+        __syncthreads();
+        sc[t] += ac; ss[t] += as;
+        __syncthreads();
+    }
+    uint32_t oc = sc[t] - c, os = ss[t] - s;
+    for (uint32_t i = b0; i < b1; i++) {
+        uint2 v = blocks[i];
+        blocks[i] = make_uint2(oc, os);
+        oc += v.x; os += v.y;
+    }
+    if (t == kScanThreads - 1) { totals[0] = sc[t]; totals[1] = ss[t]; }
+}
+
+// Stable compaction: slot = block offset + preceding waves + preceding lanes.
+__global__ __launch_bounds__(kBlock) void wpt_scatter_kernel(uint32_t n, const uint8_t* __restrict__ flags,
+                                                             const uint2* __restrict__ blocks,
+                                                             const WptPay* __restrict__ pay_in,
+                                                             const ctl_ray* __restrict__ rays_in,
+                                                             const ctl_ray* __restrict__ sec_tmp, WptPay* pay_out,
+                                                             ctl_ray* rays_out, ctl_ray* sec_out) {
+    __shared__ uint32_t wc[kBlock / 64], ws[kBlock / 64];
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t f = j < n ? flags[j] : 0u;
+    const bool cont = f & 1u, sh = f & 2u;
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint64_t mc = __ballot(cont), ms = __ballot(sh);
+    if (lane == 0) { wc[wave] = (uint32_t)__popcll(mc); ws[wave] = (uint32_t)__popcll(ms); }
+    __syncthreads();
+    uint32_t pc = blocks[blockIdx.x].x + (uint32_t)__popcll(mc & lt), ps = blocks[blockIdx.x].y + (uint32_t)__popcll(ms & lt);
+    for (uint32_t w = 0; w < wave; w++) { pc += wc[w]; ps += ws[w]; }
+    if (cont) {
+        WptPay p = pay_in[j];
+        p.d.x = sh ? ps : 0xffffffffu;   // insertSecondaryRay's index
+        pay_out[pc] = p;
+        rays_out[pc] = rays_in[j];
+    }
+    if (sh) sec_out[ps] = sec_tmp[j];
+}
+
+template <class T>
+bool wpt_alloc(WptBuffers* B, T** p, size_t n) {
+    if (hipMalloc((void**)p, n * sizeof(T) + 64) != hipSuccess) return false;
+    B->allocs.push_back((void*)*p);
+    return true;
+}
+
+#define WPT_HIP(call)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) {                                                \
+            c->err = std::string("wpt: ") + #call + ": " + hipGetErrorString(e_); \
+            return CTL_ERR_HIP;                                                \
+        }                                                                      \
+    } while (0)
+
+}  // namespace
+
+void wpt_free(ctl_ctx* c) {
+    WptBuffers* B = c->wpt;
+    if (!B) return;
+    for (void* p : B->allocs) (void)hipFree(p);
+    if (B->h_totals) (void)hipHostFree(B->h_totals);
+    delete B;
+    c->wpt = nullptr;
+}
+
+int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s) {
+    const ctl_camera& cam = c->scene.camera;
+    const uint64_t items = (uint64_t)cam.width * cam.height;
+    if (items == 0) return CTL_OK;
+    if (cam.width > 65504u || cam.height > 65504u) {   // pixel coordinates travel as half
+        c->err = "wpt: image larger than the half-precision pixel coordinates allow";
+        return CTL_ERR_INVALID;
+    }
+    if (items > 0x7fffffffull) { c->err = "wpt: too many pixels"; return CTL_ERR_INVALID; }
+    if (!c->wpt) c->wpt = new WptBuffers();
+    WptBuffers* B = c->wpt;
+    const uint32_t nb_max = (uint32_t)((items + kBlock - 1) / kBlock);
+    if (B->capacity < items) {
+        WPT_HIP(hipStreamSynchronize(s));
+        wpt_free(c);
+        c->wpt = B = new WptBuffers();
+        const size_t n = items;
+        bool ok = wpt_alloc(B, &B->pay[0], n) && wpt_alloc(B, &B->pay[1], n) && wpt_alloc(B, &B->rays[0], n) &&
+                  wpt_alloc(B, &B->rays[1], n) && wpt_alloc(B, &B->hits, n) && wpt_alloc(B, &B->sec_tmp, n) &&
+                  wpt_alloc(B, &B->sec, n) && wpt_alloc(B, &B->sec_hits, n) && wpt_alloc(B, &B->flags, n) &&
+                  wpt_alloc(B, &B->blocks, nb_max) && wpt_alloc(B, &B->totals, 4) &&
+                  hipHostMalloc((void**)&B->h_totals, 4 * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
+        if (!ok) { wpt_free(c); c->err = "wpt: buffer allocation failed"; return CTL_ERR_NOMEM; }
+        B->capacity = items;
+    }
+    WptArgs A;
+    A.width = cam.width; A.height = cam.height;
+    A.nseq = c->nseq; A.len = c->len;
+    A.max_path_length = prm->max_path_length;
+    A.rr_start_depth = prm->rr_start_depth;
+    A.skip = prm->passes_done + 2u;
+    A.half_quirk = c->half_quirk;
+    A.depth = 0;
+    const float* s1 = c->d_s1[c->active];
+    const float2* s2 = c->d_s2[c->active];
+    const bool nee = prm->direct != 0, full = c->scene.full_shading != 0;
+
+    uint32_t n = (uint32_t)items, n_sec = 0;
+    int cur = 0;
+    uint64_t traced = 0;
+    hipLaunchKernelGGL(wpt_create_kernel, dim3(nb_max), dim3(kBlock), 0, s, c->scene, A, s1, s2, n, B->rays[0],
+                       B->pay[0]);
+    WPT_HIP(hipGetLastError());
+    for (int depth = 0;; depth++) {
+        // FinishIteration: payload rays, then the secondary buffer (closest hit)
+        int r = intersect_launch(c, n, B->rays[cur], B->hits, 0, s);
+        if (r != CTL_OK) return r;
+        if (n_sec) {
+            r = intersect_launch(c, n_sec, B->sec, B->sec_hits, 0, s);
+            if (r != CTL_OK) return r;
+        }
+        traced += (uint64_t)n + n_sec;
+        A.depth = depth;
+        const uint32_t nb = (n + kBlock - 1) / kBlock;
+#define WPT_IT(NE, FU)                                                                                             \
+    hipLaunchKernelGGL((wpt_iterate_kernel<NE, FU>), dim3(nb), dim3(kBlock), 0, s, c->scene, A, s1, s2, n,        \
+                       B->pay[cur], B->rays[cur], B->hits, B->sec_hits, B->sec_tmp, B->flags, B->blocks, fb)
+        if (nee) { if (full) WPT_IT(true, true); else WPT_IT(true, false); }
+        else { if (full) WPT_IT(false, true); else WPT_IT(false, false); }
+#undef WPT_IT
+        hipLaunchKernelGGL(wpt_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, B->blocks, nb, B->totals);
+        hipLaunchKernelGGL(wpt_scatter_kernel, dim3(nb), dim3(kBlock), 0, s, n, B->flags, B->blocks, B->pay[cur],
+                           B->rays[cur], B->sec_tmp, B->pay[1 - cur], B->rays[1 - cur], B->sec);
+        WPT_HIP(hipGetLastError());
+        WPT_HIP(hipMemcpyAsync(B->h_totals, B->totals, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        WPT_HIP(hipStreamSynchronize(s));
+        n = B->h_totals[0];
+        n_sec = B->h_totals[1];
+        cur = 1 - cur;
+        // while (!m_ray_buf->isEmpty() && ++pass < maxPathLength)
+        if (n == 0 || depth + 1 >= prm->max_path_length) break;
+    }
+    return count_rays(c, traced, s);
+}
+
+}  // namespace ctl
+
+using namespace ctl;
+
+extern "C" {
+
+CTL_API ctl_status ctl_wpt_render_pass(ctl_ctx* c, const ctl_wpt_params* p, ctl_pixel* d_fb, void* stream) {
+    if (!c || !p || !d_fb) return CTL_ERR_INVALID;
+    if (!c->has_scene) { c->err = "wpt_render_pass: no scene uploaded"; return CTL_ERR_STATE; }
+    if (c->active < 0) { c->err = "wpt_render_pass: no sampler tables (call ctl_sampler_generate)"; return CTL_ERR_STATE; }
+    if (p->max_path_length < 1) { c->err = "wpt_render_pass: MaxPathLength must be >= 1"; return CTL_ERR_INVALID; }
+    if (p->rr_start_depth < 1) { c->err = "wpt_render_pass: RRStartDepth must be >= 1"; return CTL_ERR_INVALID; }
+    if (hipSetDevice(c->device) != hipSuccess) { c->err = "wpt_render_pass: hipSetDevice failed"; return CTL_ERR_HIP; }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (hipEventRecord(c->pass_ev[0], s) != hipSuccess) { c->err = "wpt_render_pass: event record failed"; return CTL_ERR_HIP; }
+    int r = wpt_pass(c, p, d_fb, s);
+    if (r != CTL_OK) return (ctl_status)r;
+    if (hipEventRecord(c->pass_ev[1], s) != hipSuccess) { c->err = "wpt_render_pass: event record failed"; return CTL_ERR_HIP; }
+    c->pass_timed = true;
+    return CTL_OK;
+}
+
+}  // extern "C"

@@ -102,13 +102,6 @@ uint16_t float_to_half(float f) {   // Math/half.h:21-60, host branch
     return ir;
 }
 
-uint16_t normal_encode16(f3 v) {   // NormalizedFloat3ToUchar2_Spherical (Math/Compression.h:12-18)
-    float theta = (cr_acos(v.z) * (255.0f / CTL_PI));
-    float phi = (cr_atan2(v.y, v.x) * (255.0f / (2.0f * CTL_PI)));
-    phi = phi < 0 ? (phi + 255) : phi;
-    return (uint16_t)(((uint16_t)theta << 8) | (uint16_t)phi);
-}
-
 // TriangleData(P, matIndex, T, N) (TriangleData.cu:10-68); UVs decoded with the
 // host half decode, as the reference's compile step always runs on the host.
 void triangle_data(const f3 P[3], uint8_t mat, const f2 T[3], const f3 N[3], ctl_triangle_data& out) {

@@ -339,6 +339,33 @@ CTL_API ctl_status ctl_last_pass_ms(ctl_ctx* ctx, float* ms);
 CTL_API ctl_status ctl_camera_rays(ctl_ctx* ctx, const ctl_pt_params* params, ctl_ray* d_rays, int64_t capacity,
                                    int64_t* n_out, void* stream);
 
+/* ---- WavefrontPathTracer over a DoubleRayBuffer -------- */
+
+/* WavefrontPathTracer parameters (Integrators/PseudoRealtime/WavefrontPathTracer.h:27-38). */
+typedef struct {
+    int32_t direct;            /* KEY_Direct, default 1                          */
+    int32_t max_path_length;   /* KEY_MaxPathLength, default 50                  */
+    int32_t rr_start_depth;    /* KEY_RRStartDepth, default 5                    */
+    uint32_t passes_done;      /* Tracer::m_uPassesDone inside this DoRender: 1  */
+                               /* for the first pass of a trace (Tracer.h:231)   */
+    uint32_t flags;            /* reserved, 0                                    */
+} ctl_wpt_params;
+
+/* One WavefrontPathTracer::DoRender (WavefrontPathTracer.cu:152-189) into
+ * d_fb[width*height]: pathCreateKernelWPT (one camera ray per pixel, the
+ * uniform block sampler's single sample), then per bounce the
+ * DoubleRayBuffer::FinishIteration batch traversals (payload rays closest-hit,
+ * the previous bounce's shadow rays closest-hit, DoubleRayBuffer.h:84-112) and
+ * pathIterateKernel<Direct> (WavefrontPathTracer.cu:51-150), until the buffer
+ * is empty or MaxPathLength bounces.  Payload and shadow-ray slots are assigned
+ * in fetch order (a stable compaction), so the image is the reference's under
+ * the sequential schedule of its insertion atomics, and deterministic.  Uses
+ * the sampler tables of the last ctl_sampler_generate.  Synchronises `stream`
+ * once per bounce (the host reads the queue lengths, as the reference's
+ * CopyFromSymbol does).  Rays counted by ctl_rays_traced: every traversal of
+ * the batch (the reference's counter only counts traceRay, so it reports 0). */
+CTL_API ctl_status ctl_wpt_render_pass(ctl_ctx* ctx, const ctl_wpt_params* params, ctl_pixel* d_fb, void* stream);
+
 /* ---- final-image stage -------------------------------------- */
 
 /* PixelVarianceInfo (Kernel/PixelVarianceBuffer.h:10-63), 44 B. */

@@ -775,6 +775,226 @@ void add_sample(ctl_pixel* fb, uint32_t w, uint32_t h, float sx, float sy, Spec 
     p.weight_sum += 1.0f;
 }
 
+// ---------------------------------------------------------------------------
+// WavefrontPathTracer::DoRender over DoubleRayBuffer
+// (Integrators/PseudoRealtime/WavefrontPathTracer.cu:17-189, Kernel/DoubleRayBuffer.h:13-231),
+// run with the queue atomics resolved in fetch order: element j of a bounce
+// inserts its shadow ray and then its continuation before element j+1 does.
+// ---------------------------------------------------------------------------
+struct WptPayload {   // WavefrontPTRayData (WavefrontPathTracer.h:11-22)
+    Spec throughput, L, directF;
+    float hx = 0, hy = 0;   // half((float)x).ToFloat()
+    float dDist = 0;
+    uint32_t dIdx = UINT_MAX;
+    bool specular_bounce = true;
+    float bsdf_pdf = 0;
+    uint32_t prev_normal = 0;
+};
+
+float half_round_int(uint32_t x) {   // __float2half_rn of a pixel coordinate (half.h:21-24)
+    if (x < 2048u) return (float)x;
+    uint32_t sh = 0;
+    while ((x >> sh) >= 2048u) sh++;
+    uint32_t q = x >> sh, r = x & ((1u << sh) - 1u), h = 1u << (sh - 1u);
+    if (r > h || (r == h && (q & 1u))) q++;
+    return (float)(q << sh);
+}
+
+// One DoubleRayBuffer::FinishIteration traversal: closest hit with the ray's
+// tmin for spans and triangles (intersectKernel), as traversalResult.
+void wpt_batch(const SceneView& S, const std::vector<ctl_ray>& rays, std::vector<ctl_hit>& hits, int tie, int threads) {
+    hits.assign(rays.size(), ctl_hit{});
+    std::atomic<size_t> next{0};
+    auto worker = [&]() {
+        for (;;) {
+            size_t base = next.fetch_add(256);
+            if (base >= rays.size()) break;
+            size_t end = std::min(rays.size(), base + 256);
+            for (size_t i = base; i < end; i++) {
+                const ctl_ray& r = rays[i];
+                Hit h;
+                h.t = r.tmax; h.tri = UINT_MAX; h.node = UINT_MAX; h.u = h.v = 0;
+                trace_two_level(S, v3(r.o[0], r.o[1], r.o[2]), v3(r.d[0], r.d[1], r.d[2]), r.tmin, r.tmin, h, false,
+                                tie, nullptr);
+                ctl_hit& o = hits[i];
+                o.dist = h.t;
+                if (h.tri == UINT_MAX) { o.node_idx = -1; o.tri_idx = -1; o.bary = 0; }
+                else {
+                    o.node_idx = (int32_t)h.node; o.tri_idx = (int32_t)h.tri;
+                    uint16_t xd = (uint16_t)(h.u * 65535), yd = (uint16_t)(h.v * 65535);   // fromResult
+                    o.bary = (int32_t)(((uint32_t)yd << 16) | (uint32_t)xd);
+                }
+            }
+        }
+    };
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; i++) ts.emplace_back(worker);
+    for (auto& t : ts) t.join();
+}
+
+ctl_ray wpt_ray(V3 o, V3 d, float eps) {   // DoubleRayBuffer::convert (DoubleRayBuffer.h:224-230)
+    ctl_ray r;
+    r.o[0] = o.x; r.o[1] = o.y; r.o[2] = o.z; r.tmin = eps;
+    r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z; r.tmax = FLT_MAX;
+    return r;
+}
+
+uint64_t wpt_render(const ctl_scene_desc* d, bool nee, int maxPathLength, int rrStartDepth, uint32_t passesDone,
+                    uint64_t pass_index, ctl_pixel* fb, int tie, int threads) {
+    const uint32_t nseq = 4096, len = 30;
+    std::vector<float> s1((size_t)nseq * len), s2((size_t)nseq * len * 2);
+    sampler_tables(pass_index, nseq, len, s1.data(), s2.data());
+    const ctl_camera& cam = d->camera;
+    const uint32_t W = cam.width, H = cam.height;
+    const bool quirk = (d->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
+    const float eps = d->ray_eps;
+    SceneView S{d};
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+    // pathCreateKernelWPT (WavefrontPathTracer.cu:17-49): one sample per pixel
+    std::vector<WptPayload> pay(W * (size_t)H);
+    std::vector<ctl_ray> rays(pay.size());
+    for (uint32_t i = 0; i < W * H; i++) {
+        uint32_t x = i % W, y = i / W;
+        Sampler rng{s1.data(), s2.data(), nseq, len, i};
+        V2 pX = v2((float)x, (float)y) + rng.randomFloat2();   // arguments of sampleSensorRay, left to right
+        (void)rng.randomFloat2();
+        V3 o, dd;
+        sensor_ray(cam, pX, o, dd);
+        WptPayload& p = pay[i];
+        p.hx = half_round_int(x); p.hy = half_round_int(y);
+        p.throughput = v3s(1.0f);
+        p.L = v3s(0.0f);
+        p.directF = v3s(0.0f);
+        rays[i] = wpt_ray(o, dd, eps);
+    }
+    std::vector<ctl_ray> sec;            // secondary buffer 2 (inserted this bounce)
+    std::vector<ctl_hit> hits, secHits;  // secHits: buffer 1 after the swap
+    uint64_t traced = 0;
+    for (int pass = 0;; pass++) {
+        // FinishIteration
+        wpt_batch(S, rays, hits, tie, threads);
+        wpt_batch(S, sec, secHits, tie, threads);
+        traced += rays.size() + sec.size();
+        std::vector<WptPayload> npay;
+        std::vector<ctl_ray> nrays, nsec;
+        // pathIterateKernel<NEXT_EVENT_EST> (WavefrontPathTracer.cu:51-150)
+        for (size_t j = 0; j < pay.size(); j++) {
+            WptPayload p = pay[j];
+            const ctl_ray& r = rays[j];
+            const ctl_hit& h = hits[j];
+            V3 rori = v3(r.o[0], r.o[1], r.o[2]), rdir = v3(r.d[0], r.d[1], r.d[2]);
+            Sampler rng{s1.data(), s2.data(), nseq, len, (uint32_t)j};
+            rng.d1 += passesDone + 2; rng.d2 += passesDone + 2;   // rng.skip(iterationIdx + 2)
+            if (nee && pass > 0 && p.dIdx != UINT_MAX) {
+                if (secHits[p.dIdx].dist >= p.dDist * (1 - eps)) p.L = p.L + p.directF;
+                p.dIdx = UINT_MAX;
+                p.directF = v3s(0.0f);
+            }
+            bool terminated = pass + 1 == maxPathLength;
+            if ((uint32_t)h.tri_idx != UINT_MAX) {
+                uint32_t bc = (uint32_t)h.bary;
+                V2 bary = v2((float)(bc & 0xffffu) / 65535.0f, (float)(bc >> 16) / 65535.0f);   // toResult
+                BRec bRec;   // a fresh record each element; wo given (0,0,1) before the first sample
+                bRec.wo = v3(0, 0, 1);
+                bRec.sampledType = 0;
+                bRec.typeMask = EAll;
+                bRec.dg.P = rori + h.dist * rdir;
+                uint32_t tri = (uint32_t)h.tri_idx, node = (uint32_t)h.node_idx;
+                fill_dg(S, bary, tri, node, bRec.dg, quirk);
+                bRec.wi = toLocal(bRec.dg.sys, -rdir);
+                const ctl_material& mat = d->materials[mat_index(S, tri, node)];
+                if (mat.two_sided && bRec.wi.z < 0) {
+                    bRec.dg.n = -bRec.dg.n;
+                    bRec.dg.sys.n = -bRec.dg.sys.n;
+                    bRec.wi.z *= -1.0f;
+                }
+                uint32_t li = light_index(S, tri, node);
+                if (li != UINT_MAX) {
+                    float misWeight = 1.0f;
+                    const ctl_light& L = d->lights[li];
+                    if (nee && !(pass == 0 || p.specular_bounce)) {
+                        DRec dRec;   // DirectSamplingRecFromRay with Uchar2ToNormalizedFloat3(prev_normal)
+                        dRec.ref = rori; dRec.refN = normal_decode((uint16_t)p.prev_normal); dRec.p = bRec.dg.P;
+                        dRec.n = bRec.dg.n; dRec.d = rdir; dRec.dist = h.dist; dRec.measure = ESolidAngle;
+                        float direct_pdf = light_pdf_direct(L, dRec) * pdf_emitter(S, li);
+                        misWeight = power_heuristic(p.bsdf_pdf, direct_pdf);
+                    }
+                    V3 w = -rdir;
+                    Spec Le = (dot(bRec.dg.sys.n, w) <= 0) ? v3s(0.0f) : v3(L.radiance[0], L.radiance[1], L.radiance[2]);
+                    p.L = p.L + (misWeight * Le) * p.throughput;
+                }
+                bool surviveRR = true;
+                if (pass >= rrStartDepth) {
+                    if (rng.randomFloat() < spec_max(p.throughput)) p.throughput = spec_div(p.throughput, spec_max(p.throughput));
+                    else surviveRR = false;
+                }
+                if (pass + 1 != maxPathLength && surviveRR) {
+                    Spec f = bsdf_sample(d, mat, bRec, p.bsdf_pdf, rng.randomFloat2());
+                    p.specular_bounce = (bRec.sampledType & EDelta) != 0;
+                    V3 outDir = toWorld(bRec.dg.sys, bRec.wo);
+                    p.dIdx = UINT_MAX;
+                    if (nee && (mat.combined_type & ESmooth) != 0) {
+                        DRec dRec;   // DirectSamplingRecord(P, sys.n)
+                        dRec.p = bRec.dg.P; dRec.n = bRec.dg.sys.n; dRec.measure = EArea;
+                        dRec.ref = bRec.dg.P; dRec.refN = bRec.dg.sys.n;
+                        // sampleEmitterDirect (KernelDynamicScene.cu:98-117) + sampleEmitter (:25-39)
+                        V2 sample = rng.randomFloat2();
+                        Spec value = v3s(0.0f);
+                        if (d->n_lights) {
+                            uint32_t n = omin(d->n_lights, (uint32_t)CTL_MAX_NUM_LIGHTS);
+                            const float* cdf = d->light_cdf;
+                            const float* first = cdf; uint32_t count = n;   // STL_upper_bound
+                            while (count > 0) {
+                                uint32_t c2 = count / 2; const float* mid = first + c2;
+                                if (!(sample.x < *mid)) { first = ++mid; count -= c2 + 1; } else count = c2;
+                            }
+                            uint32_t idx = (uint32_t)(first - cdf);
+                            if (idx >= n) idx = n - 1;
+                            float fU = cdf[idx], fL = idx > 0 ? cdf[idx - 1] : 0.0f;
+                            sample.x = (sample.x - fL) / (fU - fL);
+                            float emPdf = fU - fL;
+                            value = light_sample_direct(S, d->lights[idx], dRec, sample);
+                            if (dRec.pdf != 0) {
+                                dRec.pdf *= emPdf;
+                                value = spec_div(value, emPdf);
+                            } else {
+                                value = v3s(0.0f);
+                            }
+                        }
+                        if (!spec_zero(value)) {
+                            bRec.typeMask = EAll & ~EDelta;
+                            bRec.wo = toLocal(bRec.dg.sys, dRec.d);
+                            Spec bsdfVal = bsdf_f(d, mat, bRec);
+                            const float bsdfPdf = bsdf_pdf(d, mat, bRec);
+                            const float directPdf = dRec.pdf;   // ESolidAngle after sampleDirect
+                            const float weight = power_heuristic(directPdf, bsdfPdf);
+                            p.directF = p.throughput * value * bsdfVal * weight;
+                            p.dDist = dRec.dist;
+                            p.dIdx = (uint32_t)nsec.size();   // insertSecondaryRay
+                            nsec.push_back(wpt_ray(bRec.dg.P, dRec.d, eps));
+                        }
+                    }
+                    p.prev_normal = normal_encode(bRec.dg.sys.n);
+                    p.throughput = p.throughput * f;
+                    npay.push_back(p);   // insertPayloadElement
+                    nrays.push_back(wpt_ray(bRec.dg.P, outDir, eps));
+                } else {
+                    terminated = true;
+                }
+            } else {
+                terminated = true;
+                p.L = p.L + (1.0f * p.throughput) * v3s(0.0f);   // misWeight * throughput * EvalEnvironment
+            }
+            if (terminated) add_sample(fb, W, H, p.hx, p.hy, p.L);
+        }
+        pay.swap(npay);
+        rays.swap(nrays);
+        sec.swap(nsec);
+        if (pay.empty() || pass + 1 >= maxPathLength) break;
+    }
+    return traced;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -1018,6 +1238,13 @@ void oracle_camera_rays(const ctl_scene_desc* desc, uint64_t pass_index, ctl_ray
             r.o[0] = o.x; r.o[1] = o.y; r.o[2] = o.z; r.tmin = desc->ray_eps;
             r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z; r.tmax = FLT_MAX;
         }
+}
+
+// WavefrontPathTracer pass (ctl_wpt_render_pass); returns the rays traversed.
+uint64_t oracle_wpt_render_pass(const ctl_scene_desc* desc, int32_t direct, int32_t max_path_length,
+                                int32_t rr_start_depth, uint32_t passes_done, uint64_t pass_index, ctl_pixel* fb,
+                                int32_t tie, int32_t threads) {
+    return wpt_render(desc, direct != 0, max_path_length, rr_start_depth, passes_done, pass_index, fb, tie, threads);
 }
 
 // Host-side compile pieces, for checking the product's scene compiler.

@@ -237,7 +237,8 @@ static inline uint16_t normal_encode(V3 v) {
     float theta = (cr_acos(v.z) * (255.0f / O_PI));
     float phi = (cr_atan2(v.y, v.x) * (255.0f / (2.0f * O_PI)));
     phi = phi < 0 ? (phi + 255) : phi;
-    return (uint16_t)(((uint16_t)theta << 8) | (uint16_t)phi);
+    auto u16 = [](float f) { return (f != f) ? (uint16_t)0 : (uint16_t)(int32_t)f; };   // NaN -> 0
+    return (uint16_t)(((uint32_t)u16(theta) << 8) | (uint32_t)u16(phi));
 }
 static inline V3 normal_decode(uint16_t v) {
     const float PI_4 = O_PI / 4.0f, PI_2 = O_PI / 2.0f;

@@ -398,3 +398,67 @@ def test_render_alpha_tested_traversal(ctl, orc, tracer, dev, mode, bvh):
     d2.materials = plain
     no_alpha, _ = oracle_render(orc, d2, p, 3, 96, 64)
     assert not np.array_equal(no_alpha.view(np.uint32), want.view(np.uint32))
+
+
+# ---- WavefrontPathTracer over the batch traversal ----------
+
+def wpt_gpu(ctl, desc, direct, passes, w, h, dev, max_path_length=50, rr=5, first_pass=1):
+    wt = ctl.WavefrontPathTracer(0, direct=direct, max_path_length=max_path_length, rr_start_depth=rr)
+    wt.upload_scene(desc)
+    fb = torch.zeros((w * h, 7), dtype=torch.float32, device=dev)
+    wt.reset_rays()
+    for k in range(passes):
+        wt.do_pass(fb.data_ptr(), first_pass + k, new_trace=(k == 0))
+    torch.cuda.synchronize()
+    out = fb.cpu().numpy(), wt.rays_traced()
+    wt.close()
+    return out
+
+
+def wpt_oracle(orc, desc, direct, passes, w, h, max_path_length=50, rr=5, first_pass=1):
+    fb = np.zeros((w * h, 7), np.float32)
+    rays = 0
+    for k in range(passes):
+        rays += orc.oracle_wpt_render_pass(C.byref(desc), int(direct), max_path_length, rr, k + 1, first_pass + k,
+                                           oracle.ptr(fb), tie_rule(desc), 0)
+    return fb, rays
+
+
+@pytest.mark.parametrize("config,scale,w,h", [(1, 1.0, 64, 64), (2, 0.25, 96, 64), (3, 0.003, 64, 48),
+                                              (5, 0.003, 64, 48)])
+@pytest.mark.parametrize("direct", [1, 0])
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_wpt_pass_bit_exact(ctl, orc, dev, config, scale, w, h, direct, bvh):
+    """WavefrontPathTracer::DoRender with DoubleRayBuffer queues in fetch order:
+    bit-exact framebuffer and the same number of traversed rays as the oracle."""
+    d = scene(ctl, config, scale, w, h)
+    if bvh == "binary":
+        d = binary_bvh(d)
+    want, wrays = wpt_oracle(orc, d, direct, 2, w, h)
+    got, grays = wpt_gpu(ctl, d, direct, 2, w, h, dev)
+    assert grays == wrays
+    assert want[:, 6].min() == 2 and np.isfinite(got).all()
+    bad = np.nonzero((want.view(np.uint32) != got.view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
+
+
+@pytest.mark.parametrize("mpl,rr", [(1, 5), (2, 1), (7, 2)])
+def test_wpt_short_paths(ctl, orc, dev, mpl, rr):
+    d = scene(ctl, 2, 0.25, 96, 64)
+    want, wrays = wpt_oracle(orc, d, 1, 2, 96, 64, mpl, rr, first_pass=3)
+    got, grays = wpt_gpu(ctl, d, 1, 2, 96, 64, dev, mpl, rr, first_pass=3)
+    assert grays == wrays
+    assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
+
+
+def test_wpt_converges_to_path_tracer(ctl, orc, tracer, dev):
+    """Different sample streams, same integral: the wavefront tracer's image mean
+    matches the PathTracer's within Monte-Carlo noise (C1, 48 passes)."""
+    w = h = 48
+    d = scene(ctl, 1, 1.0, w, h)
+    a, _ = wpt_gpu(ctl, d, 1, 48, w, h, dev)
+    p = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
+    b, _ = render_gpu(ctl, tracer, d, p, 48, w, h, dev, first_pass=1)
+    ma = (a[:, :3] / a[:, 6:7]).mean(0)
+    mb = (b[:, :3] / b[:, 6:7]).mean(0)
+    assert np.all(np.abs(ma - mb) <= 0.03 * mb + 1e-4), (ma, mb)
