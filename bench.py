@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--rr-start", type=int, default=5)
     ap.add_argument("--shadow-any-hit", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--wpt-passes", type=int, default=3, help="WavefrontPathTracer leg passes (0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--schedule", default="persistent", choices=["persistent", "megakernel", "wavefront"])
@@ -122,6 +123,8 @@ def primary_ray_leg(pt, dev, stream, sptr, torch, pass_index, launches=10):
     achieved = alg / (ms * 1e-3) / 1e9
     return {
         "kernel": "intersect_kernel<closest,single> (ctl_intersect over ctl_camera_rays)",
+        "note": "coherent camera rays reuse the top BVH levels from L2/MALL, so the algorithmic-byte "
+                "model exceeds the HBM traffic here and frac > 1; the path kernel's roofline is the bound",
         "rays_per_launch": int(n),
         "ms_per_launch": round(ms, 4),
         "mrays_s": round(n / ms / 1e3, 2),
@@ -129,6 +132,30 @@ def primary_ray_leg(pt, dev, stream, sptr, torch, pass_index, launches=10):
                      "frac": round(achieved / 8000.0, 4), "alg_bytes_per_launch": int(alg),
                      "inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3])},
     }
+
+
+def wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_index, passes):
+    """WavefrontPathTracer::DoRender (ctl_wpt_render_pass) on the same context and
+    scene: the batch traversal's second caller.  The first
+    pass allocates the queues and is not counted."""
+    import ctypes as C
+    fb = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
+    prm = ctl.WptParams(1, 50, 5, 0, 0)
+    L = ctl.lib()
+    ms, rays = [], []
+    for k in range(passes + 1):
+        pt.generate_samples(pass_index + k, sptr)
+        prm.passes_done = k + 1
+        pt.reset_rays(sptr)
+        if L.ctl_wpt_render_pass(pt._ctx, C.byref(prm), C.c_void_p(fb.data_ptr()), C.c_void_p(sptr)) != 0:
+            raise RuntimeError("ctl_wpt_render_pass: " + L.ctl_last_error(pt._ctx).decode())
+        if k:
+            ms.append(pt.last_pass_ms())
+            rays.append(pt.rays_traced())
+    per = sum(ms) / len(ms)
+    return {"integrator": "WavefrontPathTracer (DoubleRayBuffer queues + batch traversal)",
+            "passes": passes, "ms_per_pass": round(per, 3), "rays_per_pass": int(sum(rays) / len(rays)),
+            "mrays_s": round(sum(rays) / (sum(ms) * 1e-3) / 1e6, 2)}
 
 
 def main():
@@ -229,6 +256,8 @@ def main():
 
     rays = pt.rays_traced()
     prim = primary_ray_leg(pt, dev, stream, sptr, torch, pass_base + a.steps * world) if rank == 0 else None
+    wpt = (wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_base + a.steps * world + 1, a.wpt_passes)
+           if rank == 0 and a.wpt_passes > 0 else None)
     tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     rr = torch.tensor([rays], dtype=torch.int64, device=dev)
     if world > 1:
@@ -297,6 +326,7 @@ def main():
                                       "rays": int(st[0])},
             },
             "primary_rays": prim,
+            "wavefront_tracer": wpt,
             "image_weight_sum": wsum,
             "scene_build_s": round(t_build, 2),
         }
