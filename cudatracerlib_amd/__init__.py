@@ -146,6 +146,32 @@ class HostScene:
             _check(1, None, "add_texture")
         return r
 
+    def add_animated_mesh(self, vertices, normals, bone_indices, bone_weights, indices, materials, mat_index=None,
+                          uvs=None):
+        """Skinned mesh (AnimatedMesh): rest pose `vertices`/`normals` (n, 3), 8 bone
+        indices and 8 weights (n, 8) uint8 per vertex (weight w means w/255)."""
+        v = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+        nrm = np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 3)
+        bi = np.ascontiguousarray(bone_indices, dtype=np.uint8).reshape(-1, 8)
+        bw = np.ascontiguousarray(bone_weights, dtype=np.uint8).reshape(-1, 8)
+        av = (_abi.AnimVertex * v.shape[0])()
+        for k in range(v.shape[0]):
+            av[k].pos[:] = v[k].tolist()
+            av[k].normal[:] = nrm[k].tolist()
+            av[k].bone_indices = int(bi[k].view(np.uint64)[0])
+            av[k].bone_weights = int(bw[k].view(np.uint64)[0])
+        i = np.ascontiguousarray(indices, dtype=np.uint32).reshape(-1, 3)
+        mats = (Material * len(materials))(*materials)
+        mi = None if mat_index is None else np.ascontiguousarray(mat_index, dtype=np.uint8)
+        uv = None if uvs is None else np.ascontiguousarray(uvs, dtype=np.float32)
+        self._keep = getattr(self, "_keep", []) + [av, i, mi, uv, mats]
+        r = self._L.ctl_host_scene_add_animated_mesh(
+            self._h, av, v.shape[0], i.ctypes.data, i.shape[0], None if uv is None else uv.ctypes.data,
+            None if mi is None else mi.ctypes.data, mats, len(materials))
+        if r < 0:
+            _check(1, None, "add_animated_mesh")
+        return r
+
     def add_xmsh(self, data, materials=None, material_record_size=_abi.CTL_XMSH_MATERIAL_RECORD_SIZE):
         """Compiled mesh from an .xmsh stream (bytes or a path) — Mesh::Mesh(path, IInStream&)
         (Engine/Mesh.cpp:46-98).  Reference files: pass sizeof(Material) of the writing build as
@@ -247,6 +273,22 @@ class Tracer:
         _check(self._L.ctl_intersect_stats(self._ctx, int(n), rays_ptr, hits_ptr, 1 if any_hit else 0, out, stream),
                self._ctx, "ctl_intersect_stats")
         return list(out)
+
+    def animate(self, anim, frame0, frame1, lerp, stream=0):
+        """AnimatedMesh::k_ComputeState on the device: frame0/frame1 = (n_bones, 4, 4) bone matrices."""
+        f0 = np.ascontiguousarray(frame0, dtype=np.float32).reshape(-1, 16)
+        f1 = np.ascontiguousarray(frame1, dtype=np.float32).reshape(-1, 16)
+        if f0.shape != f1.shape:
+            raise ValueError("frames differ in bone count")
+        _check(self._L.ctl_scene_animate(self._ctx, int(anim), f0.ctypes.data, f1.ctypes.data, f0.shape[0],
+                                         float(lerp), stream), self._ctx, "ctl_scene_animate")
+
+    def read_array(self, which, first, count, dtype, width):
+        """Device scene array slice (ctl_scene_read) as a (count, width) numpy array."""
+        out = np.zeros((count, width), dtype)
+        _check(self._L.ctl_scene_read(self._ctx, int(which), int(first), int(count), out.ctypes.data), self._ctx,
+               "ctl_scene_read")
+        return out
 
     def rays_traced(self):
         return int(self._L.ctl_rays_traced(self._ctx))

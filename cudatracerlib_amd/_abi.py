@@ -14,6 +14,7 @@ CTL_OK = 0
 CTL_SCENE_HALF_HOST_QUIRK = 1
 CTL_SCENE_BINARY_BVH = 2
 CTL_XMSH_MATERIAL_RECORD_SIZE = 148
+CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS = range(6)
 CTL_BSDF_DIFFUSE = 1
 CTL_EDIFFUSE_REFLECTION = 0x2
 CTL_EGLOSSY_REFLECTION = 0x8
@@ -99,6 +100,16 @@ class Camera(C.Structure):
                 ("height", C.c_uint32)]
 
 
+class AnimVertex(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("normal", C.c_float * 3), ("bone_indices", C.c_uint64),
+                ("bone_weights", C.c_uint64)]
+
+
+class AnimMesh(C.Structure):
+    _fields_ = [("mesh", C.c_uint32), ("vertex_first", C.c_uint32), ("vertex_count", C.c_uint32),
+                ("tri_first", C.c_uint32), ("tri_count", C.c_uint32), ("max_bone", C.c_uint32)]
+
+
 class SceneDesc(C.Structure):
     _fields_ = [
         ("tri_data", C.POINTER(TriangleData)), ("n_tri_data", C.c_uint64),
@@ -122,6 +133,10 @@ class SceneDesc(C.Structure):
         ("ray_eps", C.c_float),
         ("camera", Camera),
         ("flags", C.c_uint32),
+        ("mesh_boxes", C.POINTER(C.c_float)),
+        ("anim_vertices", C.POINTER(AnimVertex)), ("n_anim_vertices", C.c_uint32),
+        ("anim_triangles", C.POINTER(C.c_uint32)), ("n_anim_triangles", C.c_uint32),
+        ("anim_meshes", C.POINTER(AnimMesh)), ("n_anim_meshes", C.c_uint32),
     ]
 
 
@@ -178,6 +193,10 @@ SYMBOLS = [
     ("ctl_host_scene_set_flags", C.c_int32, [_vp, C.c_uint32]),
     ("ctl_host_scene_set_bvh_params", C.c_int32, [_vp, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("ctl_host_scene_compile", C.c_int32, [_vp, C.c_uint32, C.POINTER(SceneDesc)]),
+    ("ctl_host_scene_add_animated_mesh", C.c_int32, [_vp, C.POINTER(AnimVertex), C.c_uint32, _vp, C.c_uint32, _vp,
+                                                     _vp, C.POINTER(Material), C.c_uint32]),
+    ("ctl_scene_animate", C.c_int32, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_float, _vp]),
+    ("ctl_scene_read", C.c_int32, [_vp, C.c_uint32, C.c_uint64, C.c_uint64, _vp]),
     ("ctl_host_scene_add_xmsh", C.c_int32, [_vp, _vp, C.c_uint64, C.c_uint32, _vp, C.c_uint32]),
     ("ctl_host_scene_write_xmsh", C.c_int32, [_vp, C.c_uint32, _vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("ctl_host_last_error", C.c_char_p, []),

@@ -1,0 +1,487 @@
+// anim.hip — animated (skinned) meshes on the device: AnimatedMesh::k_ComputeState
+// (Engine/AnimatedMesh.cpp:163-184) as a chain of data-parallel kernels.
+//
+//   skin     g_ComputeVertices (AnimatedMesh.cu:29-43): per vertex, two 8-bone
+//            matrix blends, TransformPoint / TransformDirection, lerp
+//   tris     g_ComputeTriangles -> TriangleData::setData (TriangleData.cu:35-63)
+//   woop     AnimProvider::setObject (AnimatedMesh.cpp:113-117): every BVH entry
+//   refit    bottom-up box refit of the mesh's binary tree and of its 4-wide
+//            copy, one launch per tree level (deepest first)
+//   scene    instance boxes (mesh box x node transform), refit of the scene's
+//            binary and 4-wide trees, scene box -> m_rayTraceEps
+//
+// The reference re-derives the mesh tree on the host with BVHRebuilder (refit
+// plus subtree rotations, BVHRebuilder.cpp:281-340); the tree shape is not
+// observable through traversal, so the compiled topology is kept and only the
+// boxes move.  A box is a min/max over the same vertices whatever the order,
+// so the refit boxes are exact and the CPU oracle reproduces them bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cstring>
+
+#include "common.h"
+#include "../ctl_anim.h"
+#include "../host/bvh_wide.h"
+
+namespace ctl {
+
+struct AnimTree {
+    uint32_t base = 0;                  // binary: float4 offset of node 0; wide: wide-node index of node 0
+    std::vector<uint32_t> level_off;    // [levels + 1] offsets into order, deepest level first
+    uint32_t* d_order = nullptr;        // node indices relative to base
+    bool valid = false;
+};
+
+struct AnimMeshPlan {
+    ctl_anim_mesh am;
+    ctl_kernel_mesh km;
+    uint32_t n_entries = 0;
+    AnimTree bin, wide;
+};
+
+struct AnimState {
+    std::vector<AnimMeshPlan> meshes;
+    AnimTree scene_bin, scene_wide;
+    const ctl_anim_vertex* d_verts = nullptr;
+    const uint32_t* d_tris = nullptr;
+    float* d_mesh_boxes = nullptr;      // 6 per mesh
+    float* d_inst_boxes = nullptr;      // 6 per node
+    float* d_eps = nullptr;             // scene box (6) + eps
+    float* h_eps = nullptr;             // pinned
+    float4* d_P = nullptr;
+    float4* d_N = nullptr;
+    size_t tmp_cap = 0;
+    float* d_bones[2] = {nullptr, nullptr};
+    size_t bones_cap = 0;
+    uint32_t n_meshes = 0, n_nodes = 0;
+    std::vector<void*> allocs;
+};
+
+namespace {
+
+constexpr int32_t kSent = 0x76543210;
+constexpr int kAB = 256;
+
+__device__ __forceinline__ void box_empty(float lo[3], float hi[3]) {
+    lo[0] = lo[1] = lo[2] = FLT_MAX;
+    hi[0] = hi[1] = hi[2] = -FLT_MAX;
+}
+__device__ __forceinline__ void box_extend(float lo[3], float hi[3], const float* plo, const float* phi) {
+    for (int k = 0; k < 3; k++) { lo[k] = tmin(lo[k], plo[k]); hi[k] = tmax(hi[k], phi[k]); }
+}
+
+__global__ __launch_bounds__(kAB) void anim_skin_kernel(const ctl_anim_vertex* __restrict__ V, uint32_t n,
+                                                       const float* __restrict__ b0, const float* __restrict__ b1,
+                                                       float t, float4* P, float4* N) {
+    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
+    if (i >= n) return;
+    f3 p, nn;
+    skin_vertex(V[i], b0, b1, t, p, nn);
+    P[i] = make_float4(p.x, p.y, p.z, 0.0f);
+    N[i] = make_float4(nn.x, nn.y, nn.z, 0.0f);
+}
+
+__device__ __forceinline__ f3 ld3(const float4* a, uint32_t i) { float4 q = a[i]; return mk3(q.x, q.y, q.z); }
+
+__global__ __launch_bounds__(kAB) void anim_tri_kernel(const uint32_t* __restrict__ tris, uint32_t n,
+                                                      const float4* __restrict__ P, const float4* __restrict__ N,
+                                                      ctl_triangle_data* td) {
+    const uint32_t t = blockIdx.x * kAB + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t a = tris[3 * t], b = tris[3 * t + 1], c = tris[3 * t + 2];
+    ctl_triangle_data r = td[t];
+    // g_ComputeTriangles runs setData on the device: UVs read back with __half2float
+    triangle_set_data(r.w, ld3(P, a), ld3(P, b), ld3(P, c), ld3(N, a), ld3(N, b), ld3(N, c), false);
+    td[t] = r;
+}
+
+__global__ __launch_bounds__(kAB) void anim_woop_kernel(const uint32_t* __restrict__ idx, uint32_t n,
+                                                       const uint32_t* __restrict__ tris,
+                                                       const float4* __restrict__ P, float4* woop) {
+    const uint32_t e = blockIdx.x * kAB + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t t = idx[e] >> 1;
+    float v[12];
+    woop_set_hd(ld3(P, tris[3 * t]), ld3(P, tris[3 * t + 1]), ld3(P, tris[3 * t + 2]), v);
+    woop[3 * e] = make_float4(v[0], v[1], v[2], v[3]);
+    woop[3 * e + 1] = make_float4(v[4], v[5], v[6], v[7]);
+    woop[3 * e + 2] = make_float4(v[8], v[9], v[10], v[11]);
+}
+
+// Box of a leaf value: mesh trees (SCENE = false) read the triangles of the
+// leaf's entry run; the scene tree's leaves are instances (~node).
+struct LeafCtx {
+    const uint32_t* idx;     // mesh entries (TriIntersectorData2), relative to the mesh
+    const uint32_t* tris;    // mesh triangle vertex indices
+    const float4* P;         // skinned positions
+    const float* inst;       // instance boxes (scene)
+};
+
+template <bool SCENE>
+__device__ __forceinline__ void leaf_box(const LeafCtx& L, int32_t v, float lo[3], float hi[3]) {
+    if (SCENE) {
+        const float* b = L.inst + 6 * (uint32_t)~v;
+        for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
+        return;
+    }
+    box_empty(lo, hi);
+    uint32_t e = (uint32_t)~v;
+    for (;;) {
+        const uint32_t code = L.idx[e++];
+        const uint32_t t = code >> 1;
+        for (int k = 0; k < 3; k++) {
+            const float4 p = L.P[L.tris[3 * t + k]];
+            const float q[3] = {p.x, p.y, p.z};
+            box_extend(lo, hi, q, q);
+        }
+        if (code & 1) break;
+    }
+}
+
+// BVHNodeData child boxes (the reference layout, TriIntersectorData.h:44-50)
+__device__ __forceinline__ void bin_child_box(const float* nd, int c, float lo[3], float hi[3]) {
+    const int o = c ? 4 : 0, z = c ? 10 : 8;
+    lo[0] = nd[o]; hi[0] = nd[o + 1]; lo[1] = nd[o + 2]; hi[1] = nd[o + 3]; lo[2] = nd[z]; hi[2] = nd[z + 1];
+}
+__device__ __forceinline__ void bin_set_child_box(float* nd, int c, const float lo[3], const float hi[3]) {
+    const int o = c ? 4 : 0, z = c ? 10 : 8;
+    nd[o] = lo[0]; nd[o + 1] = hi[0]; nd[o + 2] = lo[1]; nd[o + 3] = hi[1]; nd[z] = lo[2]; nd[z + 1] = hi[2];
+}
+__device__ __forceinline__ void bin_node_box(const float* nd, float lo[3], float hi[3]) {
+    box_empty(lo, hi);
+    for (int c = 0; c < 2; c++) {
+        if (__float_as_int(nd[12 + c]) == kSent) continue;
+        float a[3], b[3];
+        bin_child_box(nd, c, a, b);
+        box_extend(lo, hi, a, b);
+    }
+}
+
+template <bool SCENE>
+__global__ __launch_bounds__(kAB) void refit_bin_kernel(float* nodes, const uint32_t* __restrict__ order, uint32_t n,
+                                                       LeafCtx L) {
+    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
+    if (i >= n) return;
+    float* nd = nodes + 16 * (size_t)order[i];
+    for (int c = 0; c < 2; c++) {
+        const int32_t v = __float_as_int(nd[12 + c]);
+        if (v == kSent) continue;
+        float lo[3], hi[3];
+        if (v < 0) leaf_box<SCENE>(L, v, lo, hi);
+        else bin_node_box(nodes + 16 * (size_t)(v >> 2), lo, hi);
+        bin_set_child_box(nd, c, lo, hi);
+    }
+}
+
+__device__ __forceinline__ void wide_node_box(const WideNode& w, float lo[3], float hi[3]) {
+    box_empty(lo, hi);
+    for (int s = 0; s < 4; s++) {
+        if (w.child[s] == kSent) continue;
+        const float a[3] = {w.lo_x[s], w.lo_y[s], w.lo_z[s]}, b[3] = {w.hi_x[s], w.hi_y[s], w.hi_z[s]};
+        box_extend(lo, hi, a, b);
+    }
+}
+
+template <bool SCENE>
+__global__ __launch_bounds__(kAB) void refit_wide_kernel(WideNode* nodes, const uint32_t* __restrict__ order, uint32_t n,
+                                                        LeafCtx L) {
+    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
+    if (i >= n) return;
+    WideNode& w = nodes[order[i]];
+    for (int s = 0; s < 4; s++) {
+        const int32_t v = w.child[s];
+        if (v == kSent) continue;
+        float lo[3], hi[3];
+        if (v < 0) leaf_box<SCENE>(L, v, lo, hi);
+        else wide_node_box(nodes[v], lo, hi);
+        w.lo_x[s] = lo[0]; w.lo_y[s] = lo[1]; w.lo_z[s] = lo[2];
+        w.hi_x[s] = hi[0]; w.hi_y[s] = hi[1]; w.hi_z[s] = hi[2];
+    }
+}
+
+// m_sLocalBox of the refit mesh: the union of its root's children.
+__global__ void mesh_box_kernel(const float* root, float* out) {
+    float lo[3], hi[3];
+    bin_node_box(root, lo, hi);
+    for (int k = 0; k < 3; k++) { out[k] = lo[k]; out[3 + k] = hi[k]; }
+}
+
+__global__ __launch_bounds__(kAB) void inst_box_kernel(const ctl_node* __restrict__ nodes, const float4* __restrict__ xf,
+                                                      uint32_t n, const float* __restrict__ mesh_boxes, float* out) {
+    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
+    if (i >= n) return;
+    const float* mb = mesh_boxes + 6 * nodes[i].mesh_index;
+    const float4* r = xf + 4 * i;
+    m44 m;
+    for (int k = 0; k < 4; k++) { m.d[4 * k] = r[k].x; m.d[4 * k + 1] = r[k].y; m.d[4 * k + 2] = r[k].z; m.d[4 * k + 3] = r[k].w; }
+    instance_box(m, mb, mb + 3, out + 6 * i, out + 6 * i + 3);
+}
+
+// scene box = union of the instance boxes; eps = 1e-4 * |size| (DynamicScene.cpp:587)
+__global__ void scene_eps_kernel(const float* inst, uint32_t n, float* out) {
+    float lo[3], hi[3];
+    box_empty(lo, hi);
+    for (uint32_t i = 0; i < n; i++) box_extend(lo, hi, inst + 6 * i, inst + 6 * i + 3);
+    for (int k = 0; k < 3; k++) { out[k] = lo[k]; out[3 + k] = hi[k]; }
+    const f3 size = mk3(hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]);
+    out[6] = 1e-4f * length(size);
+}
+
+template <class T>
+bool anim_alloc(AnimState* A, T** p, size_t n) {
+    if (hipMalloc((void**)p, n * sizeof(T) + 64) != hipSuccess) return false;
+    A->allocs.push_back((void*)*p);
+    return true;
+}
+
+template <class T>
+bool anim_upload(AnimState* A, T** dst, const T* src, size_t n) {
+    if (!anim_alloc(A, dst, n)) return false;
+    return n == 0 || hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
+}
+
+// Level plan of a tree: depth of every inner node by DFS from its root,
+// grouped deepest first.  `kids(k, out)` lists the inner children of node k.
+template <class KIDS>
+bool plan_tree(AnimState* A, AnimTree& T, uint32_t base, uint32_t n_nodes, uint32_t root, KIDS kids, std::string& err) {
+    T.base = base;
+    if (n_nodes == 0 || root >= n_nodes) { err = "refit plan: empty tree"; return false; }
+    std::vector<int> depth(n_nodes, -1);
+    std::vector<uint32_t> st{root};
+    depth[root] = 0;
+    int maxd = 0;
+    while (!st.empty()) {
+        const uint32_t k = st.back();
+        st.pop_back();
+        uint32_t ch[4];
+        const int nc = kids(k, ch);
+        for (int i = 0; i < nc; i++) {
+            if (ch[i] >= n_nodes || depth[ch[i]] >= 0) { err = "refit plan: malformed tree"; return false; }
+            depth[ch[i]] = depth[k] + 1;
+            maxd = std::max(maxd, depth[ch[i]]);
+            st.push_back(ch[i]);
+        }
+    }
+    std::vector<uint32_t> order;
+    T.level_off.clear();
+    for (int d = maxd; d >= 0; d--) {
+        T.level_off.push_back((uint32_t)order.size());
+        for (uint32_t k = 0; k < n_nodes; k++)
+            if (depth[k] == d) order.push_back(k);
+    }
+    T.level_off.push_back((uint32_t)order.size());
+    if (!anim_upload(A, &T.d_order, order.data(), order.size())) { err = "refit plan: upload failed"; return false; }
+    T.valid = true;
+    return true;
+}
+
+bool plan_binary(AnimState* A, AnimTree& T, const ctl_bvh_node* nodes, uint32_t n_nodes, uint32_t base_f4,
+                 uint32_t root, std::string& err) {
+    return plan_tree(A, T, base_f4, n_nodes, root, [&](uint32_t k, uint32_t* out) {
+        int n = 0;
+        for (int c = 0; c < 2; c++) {
+            int32_t v;
+            memcpy(&v, &nodes[k].v[12 + c], 4);
+            if (v >= 0 && v != kSent) out[n++] = (uint32_t)v >> 2;
+        }
+        return n;
+    }, err);
+}
+
+bool plan_wide(AnimState* A, AnimTree& T, const WideNode* nodes, uint32_t n_nodes, uint32_t base, std::string& err) {
+    return plan_tree(A, T, base, n_nodes, 0, [&](uint32_t k, uint32_t* out) {
+        int n = 0;
+        for (int s = 0; s < 4; s++) {
+            const int32_t v = nodes[k].child[s];
+            if (v >= 0 && v != kSent) out[n++] = (uint32_t)v;
+        }
+        return n;
+    }, err);
+}
+
+template <bool SCENE>
+void launch_refit(hipStream_t s, const AnimTree& T, float* bin_base, WideNode* wide_base, const LeafCtx& L) {
+    for (size_t l = 0; l + 1 < T.level_off.size(); l++) {
+        const uint32_t first = T.level_off[l], cnt = T.level_off[l + 1] - first;
+        if (!cnt) continue;
+        const dim3 g((cnt + kAB - 1) / kAB);
+        if (bin_base) hipLaunchKernelGGL(refit_bin_kernel<SCENE>, g, dim3(kAB), 0, s, bin_base, T.d_order + first, cnt, L);
+        else hipLaunchKernelGGL(refit_wide_kernel<SCENE>, g, dim3(kAB), 0, s, wide_base, T.d_order + first, cnt, L);
+    }
+}
+
+}  // namespace
+
+void anim_free(ctl_ctx* c) {
+    AnimState* A = c->anim;
+    if (!A) return;
+    for (void* p : A->allocs) (void)hipFree(p);
+    if (A->h_eps) (void)hipHostFree(A->h_eps);
+    delete A;
+    c->anim = nullptr;
+}
+
+// Called by ctl_scene_upload once the scene arrays are on the device.
+// wn / wbase / sw: the 4-wide trees built on upload (empty for binary scenes).
+int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>& wn,
+               const std::vector<uint32_t>& wbase, const std::vector<WideNode>& sw) {
+    anim_free(c);
+    if (!d->mesh_boxes) return CTL_OK;
+    c->anim = new AnimState();
+    AnimState* A = c->anim;
+    std::string err;
+    auto fail = [&](const std::string& m) { c->err = "scene_upload: " + m; anim_free(c); return (int)CTL_ERR_INVALID; };
+    A->n_meshes = d->n_meshes;
+    A->n_nodes = d->n_nodes;
+    if (!anim_upload(A, &A->d_mesh_boxes, d->mesh_boxes, 6ull * d->n_meshes) ||
+        !anim_alloc(A, &A->d_inst_boxes, 6ull * std::max(1u, d->n_nodes)) || !anim_alloc(A, &A->d_eps, 8) ||
+        hipHostMalloc((void**)&A->h_eps, 8 * sizeof(float), hipHostMallocDefault) != hipSuccess)
+        return fail("animation state allocation failed");
+    if (d->n_anim_meshes == 0) return CTL_OK;
+    if (!anim_upload(A, (ctl_anim_vertex**)&A->d_verts, d->anim_vertices, d->n_anim_vertices) ||
+        !anim_upload(A, (uint32_t**)&A->d_tris, d->anim_triangles, 3ull * d->n_anim_triangles))
+        return fail("animation upload failed");
+    const bool wide = !wn.empty();
+    size_t tmp = 0;
+    for (uint32_t a = 0; a < d->n_anim_meshes; a++) {
+        AnimMeshPlan P;
+        P.am = d->anim_meshes[a];
+        if (P.am.mesh >= d->n_meshes) return fail("animated mesh index out of range");
+        if ((uint64_t)P.am.vertex_first + P.am.vertex_count > d->n_anim_vertices ||
+            (uint64_t)P.am.tri_first + P.am.tri_count > d->n_anim_triangles)
+            return fail("animated mesh ranges out of range");
+        P.km = d->meshes[P.am.mesh];
+        const bool last = P.am.mesh + 1 == d->n_meshes;
+        const uint64_t n0 = P.km.bvh_node_offset / 4;
+        const uint64_t n1 = last ? d->n_bvh_nodes : d->meshes[P.am.mesh + 1].bvh_node_offset / 4;
+        const uint64_t e0 = P.km.bvh_indices_offset;
+        const uint64_t e1 = last ? d->n_tri_indices : d->meshes[P.am.mesh + 1].bvh_indices_offset;
+        const uint64_t t1 = last ? d->n_tri_data : d->meshes[P.am.mesh + 1].triangle_offset;
+        if (n1 <= n0 || e1 < e0 || t1 - P.km.triangle_offset != P.am.tri_count || P.km.bvh_triangle_offset != 3 * e0)
+            return fail("animated mesh does not match its compiled arrays");
+        for (uint64_t i = 0; i < 3ull * P.am.tri_count; i++)
+            if (d->anim_triangles[3ull * P.am.tri_first + i] >= P.am.vertex_count) return fail("animated vertex index out of range");
+        for (uint64_t e = e0; e < e1; e++)
+            if ((d->tri_indices[e] >> 1) >= P.am.tri_count) return fail("animated mesh entry out of range");
+        P.n_entries = (uint32_t)(e1 - e0);
+        if (!plan_binary(A, P.bin, d->bvh_nodes + n0, (uint32_t)(n1 - n0), P.km.bvh_node_offset, 0, err)) return fail(err);
+        if (wide) {
+            const uint32_t wb = wbase[P.am.mesh];
+            const uint32_t we = P.am.mesh + 1 < wbase.size() ? wbase[P.am.mesh + 1] : (uint32_t)wn.size();
+            if (!plan_wide(A, P.wide, wn.data() + wb, we - wb, wb, err)) return fail(err);
+        }
+        tmp = std::max<size_t>(tmp, P.am.vertex_count);
+        A->meshes.push_back(std::move(P));
+    }
+    if (d->n_nodes > 0 && d->scene_start_node >= 0 && d->n_scene_bvh_nodes > 0) {
+        if (!plan_binary(A, A->scene_bin, d->scene_bvh_nodes, d->n_scene_bvh_nodes, 0,
+                         (uint32_t)d->scene_start_node >> 2, err))
+            return fail(err);
+        if (wide && !sw.empty() && !plan_wide(A, A->scene_wide, sw.data(), (uint32_t)sw.size(), 0, err)) return fail(err);
+    }
+    if (!anim_alloc(A, &A->d_P, tmp) || !anim_alloc(A, &A->d_N, tmp)) return fail("animation buffers allocation failed");
+    A->tmp_cap = tmp;
+    return CTL_OK;
+}
+
+}  // namespace ctl
+
+using namespace ctl;
+
+extern "C" {
+
+CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4x4* frame0, const ctl_float4x4* frame1,
+                                     uint32_t n_bones, float lerp, void* stream) {
+    if (!c || !frame0 || !frame1 || n_bones == 0) return CTL_ERR_INVALID;
+    if (!c->has_scene || !c->anim) { c->err = "scene_animate: no scene uploaded"; return CTL_ERR_STATE; }
+    AnimState* A = c->anim;
+    if (anim >= A->meshes.size()) { c->err = "scene_animate: animated mesh index out of range"; return CTL_ERR_INVALID; }
+    const AnimMeshPlan& P = A->meshes[anim];
+    if (P.am.max_bone >= n_bones) { c->err = "scene_animate: a vertex uses a bone index >= n_bones"; return CTL_ERR_INVALID; }
+    if (hipSetDevice(c->device) != hipSuccess) { c->err = "scene_animate: hipSetDevice failed"; return CTL_ERR_HIP; }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const size_t nb = 16ull * n_bones;
+    if (A->bones_cap < nb) {
+        if (hipStreamSynchronize(s) != hipSuccess) { c->err = "scene_animate: sync failed"; return CTL_ERR_HIP; }
+        if (!anim_alloc(A, &A->d_bones[0], nb) || !anim_alloc(A, &A->d_bones[1], nb)) {
+            c->err = "scene_animate: bone buffer allocation failed";
+            return CTL_ERR_NOMEM;
+        }
+        A->bones_cap = nb;
+    }
+    if (hipMemcpyAsync(A->d_bones[0], frame0, nb * sizeof(float), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(A->d_bones[1], frame1, nb * sizeof(float), hipMemcpyHostToDevice, s) != hipSuccess) {
+        c->err = "scene_animate: bone upload failed";
+        return CTL_ERR_HIP;
+    }
+    DevScene& S = c->scene;
+    const uint32_t nv = P.am.vertex_count, nt = P.am.tri_count, ne = P.n_entries;
+    const uint32_t* tris = A->d_tris + 3ull * P.am.tri_first;
+    if (nv) hipLaunchKernelGGL(anim_skin_kernel, dim3((nv + kAB - 1) / kAB), dim3(kAB), 0, s, A->d_verts + P.am.vertex_first,
+                               nv, A->d_bones[0], A->d_bones[1], lerp, A->d_P, A->d_N);
+    if (nt) hipLaunchKernelGGL(anim_tri_kernel, dim3((nt + kAB - 1) / kAB), dim3(kAB), 0, s, tris, nt, A->d_P, A->d_N,
+                               const_cast<ctl_triangle_data*>(S.tri_data) + P.km.triangle_offset);
+    const uint32_t* idx = S.tri_idx + P.km.bvh_indices_offset;
+    if (ne) hipLaunchKernelGGL(anim_woop_kernel, dim3((ne + kAB - 1) / kAB), dim3(kAB), 0, s, idx, ne, tris, A->d_P,
+                               const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset);
+    LeafCtx L{idx, tris, A->d_P, nullptr};
+    float* bin = reinterpret_cast<float*>(const_cast<float4*>(S.bvh) + P.bin.base);
+    launch_refit<false>(s, P.bin, bin, nullptr, L);
+    if (P.wide.valid)
+        launch_refit<false>(s, P.wide, nullptr, reinterpret_cast<WideNode*>(const_cast<float4*>(S.wbvh)) + P.wide.base, L);
+    hipLaunchKernelGGL(mesh_box_kernel, dim3(1), dim3(1), 0, s, bin, A->d_mesh_boxes + 6 * P.am.mesh);
+    // instances, scene trees, epsilon
+    if (A->n_nodes) {
+        hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf,
+                           A->n_nodes, A->d_mesh_boxes, A->d_inst_boxes);
+        LeafCtx LS{nullptr, nullptr, nullptr, A->d_inst_boxes};
+        if (A->scene_bin.valid)
+            launch_refit<true>(s, A->scene_bin, reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh)), nullptr, LS);
+        if (A->scene_wide.valid)
+            launch_refit<true>(s, A->scene_wide, nullptr, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), LS);
+        hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps);
+        if (hipMemcpyAsync(A->h_eps, A->d_eps, 7 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            c->err = "scene_animate: epsilon readback failed";
+            return CTL_ERR_HIP;
+        }
+        S.ray_eps = A->h_eps[6];
+    }
+    if (hipGetLastError() != hipSuccess) { c->err = "scene_animate: launch failed"; return CTL_ERR_HIP; }
+    return CTL_OK;
+}
+
+CTL_API ctl_status ctl_scene_read(ctl_ctx* c, uint32_t array, uint64_t first, uint64_t count, void* dst) {
+    if (!c || (!dst && count)) return CTL_ERR_INVALID;
+    if (!c->has_scene) { c->err = "scene_read: no scene uploaded"; return CTL_ERR_STATE; }
+    const DevScene& S = c->scene;
+    const void* src = nullptr;
+    size_t elem = 0;
+    uint64_t n = 0;
+    switch (array) {
+        case CTL_ARRAY_TRI_DATA: src = S.tri_data; elem = sizeof(ctl_triangle_data); n = c->n_tri_data; break;
+        case CTL_ARRAY_WOOP: src = S.woop; elem = sizeof(ctl_woop_tri); n = c->n_woop; break;
+        case CTL_ARRAY_BVH_NODES: src = S.bvh; elem = sizeof(ctl_bvh_node); n = c->n_bvh_nodes; break;
+        case CTL_ARRAY_SCENE_BVH: src = S.scene_bvh; elem = sizeof(ctl_bvh_node); n = c->n_scene_bvh; break;
+        case CTL_ARRAY_MESH_BOXES:
+            if (!c->anim) { c->err = "scene_read: the scene had no mesh boxes"; return CTL_ERR_STATE; }
+            src = c->anim->d_mesh_boxes; elem = 6 * sizeof(float); n = c->anim->n_meshes; break;
+        case CTL_ARRAY_RAY_EPS:
+            if (first != 0 || count > 1) { c->err = "scene_read: ray eps is one value"; return CTL_ERR_INVALID; }
+            if (count) memcpy(dst, &S.ray_eps, sizeof(float));
+            return CTL_OK;
+        default: c->err = "scene_read: unknown array"; return CTL_ERR_INVALID;
+    }
+    if (first > n || count > n - first) { c->err = "scene_read: range out of bounds"; return CTL_ERR_INVALID; }
+    if (!count) return CTL_OK;
+    if (hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(dst, (const char*)src + first * elem, count * elem, hipMemcpyDeviceToHost) != hipSuccess) {
+        c->err = "scene_read: copy failed";
+        return CTL_ERR_HIP;
+    }
+    return CTL_OK;
+}
+
+}  // extern "C"

@@ -309,6 +309,7 @@ struct WfState {
 };
 
 struct WptBuffers;
+struct AnimState;
 
 }  // namespace ctl
 
@@ -337,6 +338,8 @@ struct ctl_ctx {
     ctl::WfState wf{};
     std::vector<void*> wf_allocs;
     ctl::WptBuffers* wpt = nullptr;             // WavefrontPathTracer queues (wpt.hip)
+    ctl::AnimState* anim = nullptr;             // animated meshes, refit plans (anim.hip)
+    uint64_t n_tri_data = 0, n_woop = 0, n_bvh_nodes = 0, n_scene_bvh = 0;   // uploaded array lengths
     int cu_count = 256;
 };
 
@@ -355,6 +358,11 @@ int resident_blocks(ctl_ctx* c, K kernel, size_t lds) {
 // wavefront.hip
 int wavefront_pass(ctl_ctx* c, const PathParams& P, ctl_pixel* fb, bool stats, hipStream_t s);
 void wavefront_free(ctl_ctx* c);
+// anim.hip
+struct WideNode;
+int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>& wn, const std::vector<uint32_t>& wbase,
+               const std::vector<WideNode>& sw);
+void anim_free(ctl_ctx* c);
 // wpt.hip
 int wpt_pass(ctl_ctx* c, const ctl_wpt_params* p, ctl_pixel* fb, hipStream_t s);
 void wpt_free(ctl_ctx* c);

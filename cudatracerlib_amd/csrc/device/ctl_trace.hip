@@ -392,6 +392,7 @@ static std::string g_create_err;
 static void free_scene(ctl_ctx* c) {
     for (void* p : c->scene_allocs) (void)hipFree(p);
     c->scene_allocs.clear();
+    ctl::anim_free(c);
     c->has_scene = false;
 }
 
@@ -478,6 +479,7 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
     free_scene(c);
     ctl::wavefront_free(c);
     ctl::wpt_free(c);
+    ctl::anim_free(c);
     for (int i = 0; i < 2; i++) {
         if (c->d_s1[i]) (void)hipFree(c->d_s1[i]);
         if (c->d_s2[i]) (void)hipFree(c->d_s2[i]);
@@ -570,9 +572,10 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     // 4-wide trees for the device traversal (host/bvh_wide.h), unless the
     // caller asks for the reference's binary visit order
     const bool wide = (d->flags & CTL_SCENE_BINARY_BVH) == 0 && d->n_bvh_nodes > 0;
+    std::vector<WideNode> wn, sw;
+    std::vector<uint32_t> wbase;
     if (wide) {
-        std::vector<WideNode> wn, sw;
-        std::vector<uint32_t> wbase(d->n_meshes, 0);
+        wbase.assign(d->n_meshes, 0);
         try {
             for (uint32_t m = 0; m < d->n_meshes; m++) {
                 const size_t first = d->meshes[m].bvh_node_offset / 4;
@@ -635,6 +638,12 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     }
     c->scene = S;
     c->half_quirk = (d->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
+    c->n_tri_data = d->n_tri_data;
+    c->n_woop = d->n_woop_tris;
+    c->n_bvh_nodes = d->n_bvh_nodes;
+    c->n_scene_bvh = d->n_scene_bvh_nodes;
+    int ar = ctl::anim_setup(c, d, wn, wbase, sw);
+    if (ar != CTL_OK) { free_scene(c); return (ctl_status)ar; }
     c->has_scene = true;
     return CTL_OK;
 }

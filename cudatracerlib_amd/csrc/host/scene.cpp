@@ -10,6 +10,7 @@
 #include "bvh_build.h"
 #include "ref_split.h"
 #include "../ctl_shade.h"
+#include "../ctl_anim.h"
 
 #include <algorithm>
 #include <atomic>
@@ -22,18 +23,7 @@ namespace ctl {
 static thread_local std::string g_host_error;
 void set_host_error(const std::string& s) { g_host_error = s; }
 
-void woop_set(f3 a, f3 b, f3 c, ctl_woop_tri& out) {
-    m44 m;
-    m.set_col(0, mk4(a - c, 0));
-    m.set_col(1, mk4(b - c, 0));
-    m.set_col(2, mk4(cross(a - c, b - c), 0));
-    m.set_col(3, mk4(c, 1));
-    m = inverse(m);
-    f4 A = mk4(m.at(2, 0), m.at(2, 1), m.at(2, 2), -m.at(2, 3));
-    f4 B = m.row(0), C = m.row(1);
-    float v[12] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, C.x, C.y, C.z, C.w};
-    memcpy(out.v, v, sizeof(v));
-}
+void woop_set(f3 a, f3 b, f3 c, ctl_woop_tri& out) { woop_set_hd(a, b, c, out.v); }
 
 void woop_get(const ctl_woop_tri& in, f3& v0, f3& v1, f3& v2) {
     m44 m = m44_identity();
@@ -83,25 +73,6 @@ void camera_setup(const float pos[3], const float tar[3], const float up[3], flo
 
 namespace {
 
-uint16_t float_to_half(float f) {   // Math/half.h:21-60, host branch
-    uint32_t ia; memcpy(&ia, &f, 4);
-    uint16_t ir = (ia >> 16) & 0x8000;
-    if ((ia & 0x7f800000) == 0x7f800000) {
-        if ((ia & 0x7fffffff) == 0x7f800000) ir |= 0x7c00;
-        else ir = 0x7fff;
-    } else if ((ia & 0x7f800000) >= 0x33000000) {
-        int shift = (int)((ia >> 23) & 0xff) - 127;
-        if (shift > 15) ir |= 0x7c00;
-        else {
-            ia = (ia & 0x007fffff) | 0x00800000;
-            if (shift < -14) { ir |= ia >> (-1 - shift); ia = ia << (32 - (-1 - shift)); }
-            else { ir |= ia >> (24 - 11); ia = ia << (32 - (24 - 11)); ir = ir + ((14 + shift) << 10); }
-            if ((ia > 0x80000000u) || ((ia == 0x80000000u) && (ir & 1))) ir++;
-        }
-    }
-    return ir;
-}
-
 // TriangleData(P, matIndex, T, N) (TriangleData.cu:10-68); UVs decoded with the
 // host half decode, as the reference's compile step always runs on the host.
 void triangle_data(const f3 P[3], uint8_t mat, const f2 T[3], const f3 N[3], ctl_triangle_data& out) {
@@ -109,27 +80,7 @@ void triangle_data(const f3 P[3], uint8_t mat, const f2 T[3], const f3 N[3], ctl
     w[1] = (uint32_t)mat << 16;
     for (int i = 0; i < 3; i++)
         w[5 + i] = (uint32_t)float_to_half(T[i].x) | ((uint32_t)float_to_half(T[i].y) << 16);
-    f2 t0 = mk2(half_to_float(w[5] & 0xffff, true), half_to_float(w[5] >> 16, true));
-    f2 t1 = mk2(half_to_float(w[6] & 0xffff, true), half_to_float(w[6] >> 16, true));
-    f2 t2 = mk2(half_to_float(w[7] & 0xffff, true), half_to_float(w[7] >> 16, true));
-    f3 dP1 = P[1] - P[0], dP2 = P[2] - P[0];
-    f2 dUV1 = t1 - t0, dUV2 = t2 - t0;
-    float determinant = dUV1.x * dUV2.y - dUV1.y * dUV2.x;
-    f3 dpdu, dpdv;
-    if (determinant == 0) {
-        f3 a, b, n = normalize(cross(dP1, dP2));
-        coordinate_system(n, a, b);
-        dpdu = a; dpdv = b;
-    } else {
-        float invDet = 1.0f / determinant;
-        dpdu = ((dUV2.y * dP1 - dUV1.y * dP2) * invDet);
-        dpdv = ((-dUV2.x * dP1 + dUV1.x * dP2) * invDet);
-    }
-    w[0] = (uint32_t)normal_encode16(N[0]) | ((uint32_t)normal_encode16(N[1]) << 16);
-    w[1] = (uint32_t)normal_encode16(N[2]) | (w[1] & 0xffff0000u);
-    w[2] = float_to_half(dpdu.x) | ((uint32_t)float_to_half(dpdu.y) << 16);
-    w[3] = float_to_half(dpdu.z) | ((uint32_t)float_to_half(dpdv.x) << 16);
-    w[4] = float_to_half(dpdv.y) | ((uint32_t)float_to_half(dpdv.z) << 16);
+    triangle_set_data(w, P[0], P[1], P[2], N[0], N[1], N[2], true);
     memcpy(out.w, w, 32);
 }
 
@@ -202,6 +153,28 @@ CTL_API int32_t ctl_host_scene_add_mesh(ctl_host_scene* s, const float* vertices
     m.materials.assign(materials, materials + n_materials);
     s->meshes.push_back(std::move(m));
     return (int32_t)s->meshes.size() - 1;
+}
+
+CTL_API int32_t ctl_host_scene_add_animated_mesh(ctl_host_scene* s, const ctl_anim_vertex* vertices,
+                                                 uint32_t n_vertices, const uint32_t* indices, uint32_t n_triangles,
+                                                 const float* uvs, const uint8_t* mat_index,
+                                                 const ctl_material* materials, uint32_t n_materials) {
+    if (!s || !vertices || n_vertices == 0) { set_host_error("add_animated_mesh: no vertices"); return -1; }
+    std::vector<float> pos(3ull * n_vertices), nrm(3ull * n_vertices);
+    uint32_t max_bone = 0;
+    for (uint32_t i = 0; i < n_vertices; i++) {
+        for (int k = 0; k < 3; k++) { pos[3ull * i + k] = vertices[i].pos[k]; nrm[3ull * i + k] = vertices[i].normal[k]; }
+        uint64_t b = vertices[i].bone_indices;
+        for (int k = 0; k < 8; k++, b >>= 8) max_bone = std::max(max_bone, (uint32_t)(b & 0xff));
+    }
+    int32_t r = ctl_host_scene_add_mesh(s, pos.data(), n_vertices, indices, n_triangles, nrm.data(), uvs, mat_index,
+                                        materials, n_materials);
+    if (r < 0) return r;
+    auto& M = s->meshes[r];
+    M.animated = true;
+    M.anim_v.assign(vertices, vertices + n_vertices);
+    M.max_bone = max_bone;
+    return r;
 }
 
 CTL_API int32_t ctl_host_scene_add_node(ctl_host_scene* s, uint32_t mesh, const float* xf16) {
@@ -374,7 +347,7 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         bp.bins = s->sah_bins;
         bp.max_leaf = s->max_leaf;
         BvhOutput bo;
-        if (s->split_alpha > 0.0f && s->split_depth > 0) {
+        if (s->split_alpha > 0.0f && s->split_depth > 0 && !M.animated) {
             // references of large triangles split in space (ref_split.h)
             std::vector<float> tv((size_t)ntri * 9);
             parallel_for(ntri, threads, [&](uint64_t b, uint64_t e) {
@@ -446,6 +419,21 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         memcpy(&s->kmesh_box[6 * mi], meshBox[mi].lo, 12);
         memcpy(&s->kmesh_box[6 * mi + 3], meshBox[mi].hi, 12);
     }
+    s->k_anim_vertices.clear(); s->k_anim_tris.clear(); s->k_anim_meshes.clear();
+    for (size_t mi = 0; mi < s->meshes.size(); mi++) {
+        const auto& M = s->meshes[mi];
+        if (!M.animated) continue;
+        ctl_anim_mesh am;
+        am.mesh = (uint32_t)mi;
+        am.vertex_first = (uint32_t)s->k_anim_vertices.size();
+        am.vertex_count = (uint32_t)M.anim_v.size();
+        am.tri_first = (uint32_t)(s->k_anim_tris.size() / 3);
+        am.tri_count = M.n_triangles();
+        am.max_bone = M.max_bone;
+        s->k_anim_vertices.insert(s->k_anim_vertices.end(), M.anim_v.begin(), M.anim_v.end());
+        s->k_anim_tris.insert(s->k_anim_tris.end(), M.idx.begin(), M.idx.end());
+        s->k_anim_meshes.push_back(am);
+    }
 
     // --- nodes (instances), transforms, top-level BVH
     Box sceneBox;
@@ -468,18 +456,7 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         s->inv_xf.push_back(b);
         const Box& mb = meshBox[N.mesh];
         Box wb;
-        for (int k = 0; k < 3; k++) { wb.lo[k] = FLT_MAX; wb.hi[k] = -FLT_MAX; }
-        for (int c = 0; c < 8; c++) {
-            f3 p = mk3((c & 1) ? mb.hi[0] : mb.lo[0], (c & 2) ? mb.hi[1] : mb.lo[1], (c & 4) ? mb.hi[2] : mb.lo[2]);
-            f3 q = xform_point(N.xf, p);
-            float qq[3] = {q.x, q.y, q.z};
-            for (int k = 0; k < 3; k++) { wb.lo[k] = tmin(wb.lo[k], qq[k]); wb.hi[k] = tmax(wb.hi[k], qq[k]); }
-        }
-        // conservative slack against rounding of the corner transform
-        for (int k = 0; k < 3; k++) {
-            float ext = tmax(fabsf(wb.lo[k]), fabsf(wb.hi[k])) * 1e-6f + 1e-30f;
-            wb.lo[k] -= ext; wb.hi[k] += ext;
-        }
+        instance_box(N.xf, mb.lo, mb.hi, wb.lo, wb.hi);
         nodeBox[ni] = wb;
         for (int k = 0; k < 3; k++) { sceneBox.lo[k] = tmin(sceneBox.lo[k], wb.lo[k]); sceneBox.hi[k] = tmax(sceneBox.hi[k], wb.hi[k]); }
     }
@@ -498,6 +475,10 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
     NormalDecodeHost ndec;
     for (size_t li = 0; li < s->lights.size(); li++) {
         const auto& L = s->lights[li];
+        if (s->meshes[s->nodes[L.node].mesh].animated) {
+            set_host_error("compile: area lights on animated meshes are not supported");
+            return CTL_ERR_INVALID;
+        }
         ctl_node& kn = s->knodes[L.node];
         const ctl_kernel_mesh& km = s->kmeshes[kn.mesh_index];
         ctl_material& mat = s->materials[kn.material_offset + L.local_mat];
@@ -564,6 +545,10 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
     d.nodes = s->knodes.data(); d.n_nodes = (uint32_t)s->knodes.size();
     d.scene_bvh_nodes = s->scene_bvh.data(); d.n_scene_bvh_nodes = (uint32_t)s->scene_bvh.size();
     d.scene_start_node = startNode;
+    d.mesh_boxes = s->kmesh_box.data();
+    d.anim_vertices = s->k_anim_vertices.data(); d.n_anim_vertices = (uint32_t)s->k_anim_vertices.size();
+    d.anim_triangles = s->k_anim_tris.data(); d.n_anim_triangles = (uint32_t)(s->k_anim_tris.size() / 3);
+    d.anim_meshes = s->k_anim_meshes.data(); d.n_anim_meshes = (uint32_t)s->k_anim_meshes.size();
     d.node_xf = s->xf.data(); d.node_inv_xf = s->inv_xf.data();
     d.lights = s->klights.data(); d.n_lights = (uint32_t)s->klights.size();
     d.light_tris = s->light_tris.data(); d.n_light_tris = (uint32_t)s->light_tris.size();

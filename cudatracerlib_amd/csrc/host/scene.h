@@ -30,6 +30,10 @@ struct ctl_host_scene {
         // created on the mesh gets these lights (DynamicScene.cpp:340-341)
         struct AutoLight { uint32_t mat; float L[3]; };
         std::vector<AutoLight> auto_lights;
+        // skinned mesh (ctl_host_scene_add_animated_mesh): v/n hold the rest pose
+        bool animated = false;
+        std::vector<ctl_anim_vertex> anim_v;
+        uint32_t max_bone = 0;
         uint32_t n_triangles() const { return precompiled ? (uint32_t)c_tri.size() : (uint32_t)(idx.size() / 3); }
     };
     struct Node { uint32_t mesh; bool has_xf; ctl::m44 xf; };
@@ -63,6 +67,9 @@ struct ctl_host_scene {
     std::vector<ctl_texture> textures;   // added by ctl_host_scene_add_texture (kept across compiles)
     std::vector<uint32_t> tex_data;
     std::vector<float> kmesh_box;        // 6 floats per mesh: local box of the last compile
+    std::vector<ctl_anim_vertex> k_anim_vertices;
+    std::vector<uint32_t> k_anim_tris;
+    std::vector<ctl_anim_mesh> k_anim_meshes;
     ctl_scene_desc desc{};
     uint32_t max_mesh_depth = 0;
     bool compiled = false;

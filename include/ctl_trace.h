@@ -230,6 +230,26 @@ enum {
     CTL_SCENE_BINARY_BVH = 1u << 1
 };
 
+/* AnimatedVertex (Engine/AnimatedMesh.h:10-22), 40 B: rest position and
+ * normal, 8 bone indices (u8 each, low byte first) and 8 weights (u8, w/255). */
+typedef struct {
+    float pos[3];
+    float normal[3];
+    uint64_t bone_indices;
+    uint64_t bone_weights;
+} ctl_anim_vertex;
+
+/* One animated (skinned) mesh of a compiled scene (e_KernelAnimatedMesh,
+ * AnimatedMesh.h:57-67): its vertices are anim_vertices[vertex_first ..
+ * +vertex_count), its triangles' vertex indices (local to the mesh)
+ * anim_triangles[3*tri_first .. 3*(tri_first+tri_count)). */
+typedef struct {
+    uint32_t mesh;           /* index into meshes[]                  */
+    uint32_t vertex_first, vertex_count;
+    uint32_t tri_first, tri_count;
+    uint32_t max_bone;       /* largest bone index any vertex uses   */
+} ctl_anim_mesh;
+
 /* Everything KernelDynamicScene (Engine/KernelDynamicScene.h:28-57) holds that
  * the traversal + PathTracer path reads. */
 typedef struct {
@@ -258,6 +278,13 @@ typedef struct {
     float ray_eps;                      /* m_rayTraceEps, DynamicScene.cpp:587  */
     ctl_camera camera;                  /* m_Camera                             */
     uint32_t flags;                     /* CTL_SCENE_*                          */
+    /* Mesh::m_sLocalBox per mesh (6 floats: min xyz, max xyz): the instance
+     * boxes of the scene BVH are these boxes transformed (SceneBVH.cpp:77-100) */
+    const float* mesh_boxes;
+    /* animated meshes (AnimatedMesh::k_ComputeState input, AnimatedMesh.cpp:163-184) */
+    const ctl_anim_vertex* anim_vertices; uint32_t n_anim_vertices;
+    const uint32_t* anim_triangles;     uint32_t n_anim_triangles;   /* 3 indices each */
+    const ctl_anim_mesh* anim_meshes;   uint32_t n_anim_meshes;
 } ctl_scene_desc;
 
 /* PathTracer parameters (Integrators/PathTracer.h:10-19) + multi-GPU tiling. */
@@ -338,6 +365,36 @@ CTL_API ctl_status ctl_last_pass_ms(ctl_ctx* ctx, float* ms);
  * tile_size^2); d_rays must hold that many (query with capacity 0). */
 CTL_API ctl_status ctl_camera_rays(ctl_ctx* ctx, const ctl_pt_params* params, ctl_ray* d_rays, int64_t capacity,
                                    int64_t* n_out, void* stream);
+
+/* ---- animated meshes: skinning + BVH refit ------------ */
+
+/* AnimatedMesh::k_ComputeState (Engine/AnimatedMesh.cpp:163-184) for animated
+ * mesh `anim` (index into desc->anim_meshes) of the uploaded scene, on the
+ * device: skins every vertex between bone matrices frame0 and frame1
+ * (g_ComputeVertices, AnimatedMesh.cu:29-43; n_bones row-major float4x4 each,
+ * host memory), rewrites its TriangleData (g_ComputeTriangles ->
+ * TriangleData::setData) and TriIntersectorData (AnimProvider::setObject,
+ * AnimatedMesh.cpp:113-117), refits its BVH boxes bottom-up, then the
+ * instance boxes and the scene BVH, and recomputes the ray epsilon from the
+ * new scene box (DynamicScene.cpp:587).  The refit keeps the compiled tree
+ * (the reference's BVHRebuilder also rotates subtrees, BVHRebuilder.cpp:281-340;
+ * traversal results do not depend on the tree).  Synchronises `stream` once
+ * (the epsilon is a host-side kernel argument). */
+CTL_API ctl_status ctl_scene_animate(ctl_ctx* ctx, uint32_t anim, const ctl_float4x4* frame0,
+                                     const ctl_float4x4* frame1, uint32_t n_bones, float lerp, void* stream);
+
+/* Copies `count` elements from element `first` of a device scene array to
+ * host memory (Stream<T>::CopyFromDevice, e.g. AnimatedMesh.cpp:178), for
+ * inspecting what ctl_scene_animate wrote.  Synchronous. */
+enum {
+    CTL_ARRAY_TRI_DATA = 0,    /* ctl_triangle_data   */
+    CTL_ARRAY_WOOP = 1,        /* ctl_woop_tri        */
+    CTL_ARRAY_BVH_NODES = 2,   /* ctl_bvh_node        */
+    CTL_ARRAY_SCENE_BVH = 3,   /* ctl_bvh_node        */
+    CTL_ARRAY_MESH_BOXES = 4,  /* 6 floats per mesh   */
+    CTL_ARRAY_RAY_EPS = 5      /* 1 float             */
+};
+CTL_API ctl_status ctl_scene_read(ctl_ctx* ctx, uint32_t array, uint64_t first, uint64_t count, void* host_dst);
 
 /* ---- WavefrontPathTracer over a DoubleRayBuffer -------- */
 
@@ -477,6 +534,17 @@ CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags);
 CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth,
                                                  uint32_t bins, uint32_t max_leaf);
 CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, ctl_scene_desc* out);
+
+/* Skinned mesh (AnimatedMesh, Engine/AnimatedMesh.h:71-110): compiled in its
+ * rest pose (vertex positions as given; no reference splitting, so every
+ * triangle has one BVH reference) and re-posed on the device by
+ * ctl_scene_animate.  uvs: 2 floats per vertex or NULL; mat_index as
+ * ctl_host_scene_add_mesh.  Area lights on animated meshes are refused at
+ * compile (their ShapeSet would go stale).  Returns the mesh index or -1. */
+CTL_API int32_t ctl_host_scene_add_animated_mesh(ctl_host_scene* s, const ctl_anim_vertex* vertices,
+                                                 uint32_t n_vertices, const uint32_t* indices, uint32_t n_triangles,
+                                                 const float* uvs, const uint8_t* mat_index,
+                                                 const ctl_material* materials, uint32_t n_materials);
 
 /* Compiled meshes (.xmsh).  Replaces Mesh::Mesh(path, IInStream&, ...)
  * (Engine/Mesh.cpp:46-98) as called by DynamicScene::CreateNode(path)

@@ -995,6 +995,153 @@ uint64_t wpt_render(const ctl_scene_desc* d, bool nee, int maxPathLength, int rr
     return traced;
 }
 
+// ---------------------------------------------------------------------------
+// AnimatedMesh::k_ComputeState (Engine/AnimatedMesh.cpp:163-184) on copies of
+// the compiled arrays, with the compiled tree refit (boxes only).
+// ---------------------------------------------------------------------------
+M44 skin_matrix(const float* bones, uint64_t idx, uint64_t wgt) {   // d_Compute (AnimatedMesh.cu:13-27)
+    M44 mat;
+    for (int k = 0; k < 16; k++) mat.d[k] = 0.0f;
+    for (int i = 0; i < 8; i++) {
+        uint32_t j = (uint32_t)(idx & 0xff);
+        float w = (float)(uint32_t)(wgt & 0xff) / 255.0f;
+        idx >>= 8; wgt >>= 8;
+        for (int k = 0; k < 16; k++) mat.d[k] = mat.d[k] + bones[16 * j + k] * w;   // mat + m * w
+    }
+    return mat;
+}
+
+// TriangleData::setData (TriangleData.cu:35-63) as run on the device by
+// g_ComputeTriangles: the UV halves are read back with the IEEE decode.
+void tri_set_data_device(uint32_t w[8], V3 v0, V3 v1, V3 vv2, V3 n0, V3 n1, V3 n2) {
+    V2 t0 = v2(half_to_float_ieee(w[5] & 0xffff), half_to_float_ieee(w[5] >> 16));
+    V2 t1 = v2(half_to_float_ieee(w[6] & 0xffff), half_to_float_ieee(w[6] >> 16));
+    V2 t2 = v2(half_to_float_ieee(w[7] & 0xffff), half_to_float_ieee(w[7] >> 16));
+    V3 dP1 = v1 - v0, dP2 = vv2 - v0;
+    V2 dUV1 = t1 - t0, dUV2 = t2 - t0;
+    float determinant = dUV1.x * dUV2.y - dUV1.y * dUV2.x;
+    V3 dpdu, dpdv;
+    if (determinant == 0) {
+        V3 a, b, n = normalize(cross(dP1, dP2));
+        coordinateSystem(n, a, b);
+        dpdu = a; dpdv = b;
+    } else {
+        float invDet = 1.0f / determinant;
+        dpdu = ((dUV2.y * dP1 - dUV1.y * dP2) * invDet);
+        dpdv = ((-dUV2.x * dP1 + dUV1.x * dP2) * invDet);
+    }
+    w[0] = (uint32_t)normal_encode(n0) | ((uint32_t)normal_encode(n1) << 16);
+    w[1] = (uint32_t)normal_encode(n2) | (w[1] & 0xffff0000u);
+    w[2] = float_to_half(dpdu.x) | ((uint32_t)float_to_half(dpdu.y) << 16);
+    w[3] = float_to_half(dpdu.z) | ((uint32_t)float_to_half(dpdv.x) << 16);
+    w[4] = float_to_half(dpdv.y) | ((uint32_t)float_to_half(dpdv.z) << 16);
+}
+
+struct Box6 { float lo[3], hi[3]; };
+Box6 box_empty() { Box6 b; for (int k = 0; k < 3; k++) { b.lo[k] = FLT_MAX; b.hi[k] = -FLT_MAX; } return b; }
+void box_add(Box6& b, const Box6& o) {
+    for (int k = 0; k < 3; k++) { b.lo[k] = omin(b.lo[k], o.lo[k]); b.hi[k] = omax(b.hi[k], o.hi[k]); }
+}
+void box_add(Box6& b, V3 p) {
+    Box6 q; q.lo[0] = q.hi[0] = p.x; q.lo[1] = q.hi[1] = p.y; q.lo[2] = q.hi[2] = p.z;
+    box_add(b, q);
+}
+// BVHNodeData child boxes (TriIntersectorData.h:44-50)
+Box6 node_child(const ctl_bvh_node& n, int c) {
+    const int o = c ? 4 : 0, z = c ? 10 : 8;
+    Box6 b;
+    b.lo[0] = n.v[o]; b.hi[0] = n.v[o + 1]; b.lo[1] = n.v[o + 2]; b.hi[1] = n.v[o + 3]; b.lo[2] = n.v[z]; b.hi[2] = n.v[z + 1];
+    return b;
+}
+void node_set_child(ctl_bvh_node& n, int c, const Box6& b) {
+    const int o = c ? 4 : 0, z = c ? 10 : 8;
+    n.v[o] = b.lo[0]; n.v[o + 1] = b.hi[0]; n.v[o + 2] = b.lo[1]; n.v[o + 3] = b.hi[1]; n.v[z] = b.lo[2]; n.v[z + 1] = b.hi[2];
+}
+int32_t node_kid(const ctl_bvh_node& n, int c) { int32_t v; std::memcpy(&v, &n.v[12 + c], 4); return v; }
+
+// refits node k's child boxes from its subtree; returns the union of its children
+template <class LEAF>
+Box6 refit(ctl_bvh_node* nodes, uint32_t k, const LEAF& leaf) {
+    Box6 all = box_empty();
+    for (int c = 0; c < 2; c++) {
+        int32_t v = node_kid(nodes[k], c);
+        if (v == 0x76543210) continue;
+        Box6 b = v < 0 ? leaf(v) : refit(nodes, (uint32_t)v >> 2, leaf);
+        node_set_child(nodes[k], c, b);
+        box_add(all, b);
+    }
+    return all;
+}
+
+void instance_box(const M44& xf, const float lo[3], const float hi[3], Box6& o) {   // scene compile's node box
+    o = box_empty();
+    for (int c = 0; c < 8; c++) {
+        V3 p = v3((c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]);
+        V3 q = transformPoint(xf, p);
+        box_add(o, q);
+    }
+    for (int k = 0; k < 3; k++) {
+        float ext = omax(std::fabs(o.lo[k]), std::fabs(o.hi[k])) * 1e-6f + 1e-30f;
+        o.lo[k] -= ext; o.hi[k] += ext;
+    }
+}
+
+void animate(const ctl_scene_desc* d, uint32_t anim, const float* b0, const float* b1, float t, ctl_triangle_data* tri,
+             float* woop, ctl_bvh_node* nodes, ctl_bvh_node* scene, float* mesh_boxes, float* eps) {
+    const ctl_anim_mesh& am = d->anim_meshes[anim];
+    const ctl_kernel_mesh& km = d->meshes[am.mesh];
+    const bool last = am.mesh + 1 == d->n_meshes;
+    const uint64_t e1 = last ? d->n_tri_indices : d->meshes[am.mesh + 1].bvh_indices_offset;
+    // g_ComputeVertices (AnimatedMesh.cu:29-43)
+    std::vector<V3> P(am.vertex_count), N(am.vertex_count);
+    for (uint32_t i = 0; i < am.vertex_count; i++) {
+        const ctl_anim_vertex& v = d->anim_vertices[am.vertex_first + i];
+        M44 m0 = skin_matrix(b0, v.bone_indices, v.bone_weights), m1 = skin_matrix(b1, v.bone_indices, v.bone_weights);
+        V3 p = v3(v.pos[0], v.pos[1], v.pos[2]), n = v3(v.normal[0], v.normal[1], v.normal[2]);
+        V3 p0 = transformPoint(m0, p), p1 = transformPoint(m1, p);
+        P[i] = p0 * (1.0f - t) + p1 * t;   // math::lerp (MathFunc.h:161)
+        V3 n0 = transformDirection(m0, n), n1 = transformDirection(m1, n);
+        N[i] = normalize(n0 * (1.0f - t) + n1 * t);
+    }
+    const uint32_t* T = d->anim_triangles + 3ull * am.tri_first;
+    // g_ComputeTriangles
+    for (uint32_t i = 0; i < am.tri_count; i++) {
+        uint32_t* w = tri[km.triangle_offset + i].w;
+        tri_set_data_device(w, P[T[3 * i]], P[T[3 * i + 1]], P[T[3 * i + 2]], N[T[3 * i]], N[T[3 * i + 1]], N[T[3 * i + 2]]);
+    }
+    // AnimProvider::setObject for every entry
+    for (uint64_t e = km.bvh_indices_offset; e < e1; e++) {
+        uint32_t i = d->tri_indices[e] >> 1;
+        woop_set(P[T[3 * i]], P[T[3 * i + 1]], P[T[3 * i + 2]], woop + 12 * e);
+    }
+    // refit of the mesh tree; leaves = the triangles of their entry run
+    const uint32_t* idx = d->tri_indices + km.bvh_indices_offset;
+    auto leaf = [&](int32_t v) {
+        Box6 b = box_empty();
+        for (uint32_t e = (uint32_t)~v;; e++) {
+            uint32_t i = idx[e] >> 1;
+            for (int k = 0; k < 3; k++) box_add(b, P[T[3 * i + k]]);
+            if (idx[e] & 1) break;
+        }
+        return b;
+    };
+    Box6 mb = refit(nodes + km.bvh_node_offset / 4, 0, leaf);
+    for (int k = 0; k < 3; k++) { mesh_boxes[6 * am.mesh + k] = mb.lo[k]; mesh_boxes[6 * am.mesh + 3 + k] = mb.hi[k]; }
+    // instances, scene tree, epsilon (DynamicScene.cpp:587)
+    std::vector<Box6> inst(d->n_nodes);
+    Box6 sb = box_empty();
+    for (uint32_t i = 0; i < d->n_nodes; i++) {
+        M44 xf; std::memcpy(xf.d, d->node_xf[i].m, 64);
+        const float* m = mesh_boxes + 6 * d->nodes[i].mesh_index;
+        instance_box(xf, m, m + 3, inst[i]);
+        box_add(sb, inst[i]);
+    }
+    if (d->n_nodes && d->scene_start_node >= 0 && d->n_scene_bvh_nodes)
+        refit(scene, (uint32_t)d->scene_start_node >> 2, [&](int32_t v) { return inst[(uint32_t)~v]; });
+    V3 size = v3(sb.hi[0] - sb.lo[0], sb.hi[1] - sb.lo[1], sb.hi[2] - sb.lo[2]);
+    *eps = 1e-4f * length(size);
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -1245,6 +1392,13 @@ uint64_t oracle_wpt_render_pass(const ctl_scene_desc* desc, int32_t direct, int3
                                 int32_t rr_start_depth, uint32_t passes_done, uint64_t pass_index, ctl_pixel* fb,
                                 int32_t tie, int32_t threads) {
     return wpt_render(desc, direct != 0, max_path_length, rr_start_depth, passes_done, pass_index, fb, tie, threads);
+}
+
+// AnimatedMesh::k_ComputeState on caller-owned copies of the compiled arrays.
+void oracle_animate(const ctl_scene_desc* desc, uint32_t anim, const float* bones0, const float* bones1, float lerp,
+                    ctl_triangle_data* tri, float* woop, ctl_bvh_node* nodes, ctl_bvh_node* scene, float* mesh_boxes,
+                    float* eps) {
+    animate(desc, anim, bones0, bones1, lerp, tri, woop, nodes, scene, mesh_boxes, eps);
 }
 
 // Host-side compile pieces, for checking the product's scene compiler.

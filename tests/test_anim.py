@@ -1,0 +1,259 @@
+"""Animated (skinned) meshes: AnimatedMesh::k_ComputeState (Engine/AnimatedMesh.cpp:163-184,
+AnimatedMesh.cu:13-70) on the device through ctl_scene_animate, against the
+oracle's restatement (skinning, TriangleData::setData on the device, Woop
+data, box refit of the compiled trees, instance boxes, ray epsilon).  The
+reference ships no animation fixture: the skinned tube below is synthetic
+(parity pinned by the reference source, checked bit for bit against the
+oracle, and BVH-independently against brute-force traversal)."""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import binary_bvh, oracle_intersect, oracle_render, random_rays, tie_rule
+
+
+def skinned_tube(nseg=24, nring=16, radius=0.5, length=4.0):
+    """Cylinder along +y, two bones blended linearly along its length."""
+    V, Nrm, BI, BW, UV = [], [], [], [], []
+    for i in range(nseg + 1):
+        y = length * i / nseg
+        f = i / nseg
+        w0 = int(round(255 * (1 - f)))
+        for j in range(nring):
+            a = 2 * math.pi * j / nring
+            V.append([radius * math.cos(a), y, radius * math.sin(a)])
+            Nrm.append([math.cos(a), 0.0, math.sin(a)])
+            BI.append([0, 1, 0, 0, 0, 0, 0, 0])
+            BW.append([w0, 255 - w0, 0, 0, 0, 0, 0, 0])
+            UV.append([j / nring, f])
+    T = []
+    for i in range(nseg):
+        for j in range(nring):
+            a, b = i * nring + j, i * nring + (j + 1) % nring
+            c, d = a + nring, b + nring
+            T += [[a, c, b], [b, c, d]]
+    return (np.array(V, np.float32), np.array(Nrm, np.float32), np.array(BI, np.uint8), np.array(BW, np.uint8),
+            np.array(T, np.uint32), np.array(UV, np.float32))
+
+
+def rot_z(deg, pivot):
+    c, s = math.cos(math.radians(deg)), math.sin(math.radians(deg))
+    R = np.eye(4, dtype=np.float32)
+    R[0, 0], R[0, 1], R[1, 0], R[1, 1] = c, -s, s, c
+    P = np.eye(4, dtype=np.float32); P[:3, 3] = pivot
+    Pi = np.eye(4, dtype=np.float32); Pi[:3, 3] = [-p for p in pivot]
+    return (P @ R @ Pi).astype(np.float32)
+
+
+def frames():
+    f0 = np.stack([np.eye(4, dtype=np.float32), rot_z(20, [0, 2, 0])])
+    t = np.eye(4, dtype=np.float32); t[:3, 3] = [0.1, 0.0, -0.05]
+    f1 = np.stack([t, rot_z(55, [0, 2, 0])])
+    return f0, f1
+
+
+def build_scene(ctl, w=64, h=48, light_on_tube=False):
+    v, n, bi, bw, tris, uv = skinned_tube()
+    s = ctl.HostScene()
+    m_tube = s.add_animated_mesh(v, n, bi, bw, tris, [ctl.diffuse_material(0.7, 0.5, 0.3)], uvs=uv)
+    ground = np.array([[-6, -0.5, -6], [6, -0.5, -6], [6, -0.5, 6], [-6, -0.5, 6]], np.float32)
+    m_g = s.add_mesh(ground, [[0, 2, 1], [0, 3, 2]], [ctl.diffuse_material(0.5, 0.5, 0.5)])
+    lq = np.array([[-1, 6, -1], [1, 6, -1], [1, 6, 1], [-1, 6, 1]], np.float32)
+    m_l = s.add_mesh(lq, [[0, 1, 2], [0, 2, 3]], [ctl.diffuse_material(0.0, 0.0, 0.0)])
+    n_tube = s.add_node(m_tube)
+    s.add_node(m_tube, [1, 0, 0, 2.5, 0, 1, 0, 0, 0, 0, 1, 0.5, 0, 0, 0, 1])   # second instance
+    s.add_node(m_g)
+    nl = s.add_node(m_l)
+    s.add_area_light(n_tube if light_on_tube else nl, 0, [20.0, 18.0, 15.0])
+    s.set_camera([1.2, 2.5, -9], [1.2, 1.8, 0], [0, 1, 0], 50, w, h)
+    return s
+
+
+def _arr(ptr, ctype, n):
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=(n,)).copy()
+
+
+def oracle_animated(ctl, orc, d, f0, f1, lerp):
+    """Arrays after k_ComputeState, and a desc pointing at them."""
+    A = ctl._abi
+    tri = _arr(d.tri_data, C.c_uint32, d.n_tri_data * 8)
+    woop = _arr(d.woop_tris, C.c_float, d.n_woop_tris * 12)
+    nodes = _arr(d.bvh_nodes, C.c_float, d.n_bvh_nodes * 16)
+    scene = _arr(d.scene_bvh_nodes, C.c_float, max(1, d.n_scene_bvh_nodes) * 16)
+    boxes = _arr(d.mesh_boxes, C.c_float, d.n_meshes * 6)
+    eps = np.zeros(1, np.float32)
+    b0 = np.ascontiguousarray(f0, np.float32)
+    b1 = np.ascontiguousarray(f1, np.float32)
+    orc.oracle_animate(C.byref(d), 0, oracle.ptr(b0), oracle.ptr(b1), lerp, oracle.ptr(tri), oracle.ptr(woop),
+                       oracle.ptr(nodes), oracle.ptr(scene), oracle.ptr(boxes), oracle.ptr(eps))
+    d2 = type(d).from_buffer_copy(d)
+    d2.tri_data = C.cast(tri.ctypes.data, C.POINTER(A.TriangleData))
+    d2.woop_tris = C.cast(woop.ctypes.data, C.POINTER(A.WoopTri))
+    d2.bvh_nodes = C.cast(nodes.ctypes.data, C.POINTER(A.BVHNode))
+    d2.scene_bvh_nodes = C.cast(scene.ctypes.data, C.POINTER(A.BVHNode))
+    d2.mesh_boxes = C.cast(boxes.ctypes.data, C.POINTER(C.c_float))
+    d2.ray_eps = float(eps[0])
+    keep = (tri, woop, nodes, scene, boxes)
+    return d2, keep, eps[0]
+
+
+# ---------------------------------------------------------------------------- CPU
+
+def test_animated_mesh_compiles_like_a_static_mesh(ctl):
+    """Rest pose: the same arrays as add_mesh without reference splitting, plus
+    the AnimatedVertex / triangle / mesh records of the desc."""
+    v, n, bi, bw, tris, uv = skinned_tube()
+    mats = [ctl.diffuse_material(0.7, 0.5, 0.3)]
+    a = ctl.HostScene()
+    a.add_animated_mesh(v, n, bi, bw, tris, mats, uvs=uv)
+    a.add_node(0)
+    a.set_camera([0, 2, -9], [0, 2, 0], [0, 1, 0], 50, 16, 16)
+    da = a.compile()
+    b = ctl.HostScene()
+    b.set_bvh_params(0.0, 0)
+    b.add_mesh(v, tris, mats, normals=n, uvs=uv)
+    b.add_node(0)
+    b.set_camera([0, 2, -9], [0, 2, 0], [0, 1, 0], 50, 16, 16)
+    db = b.compile()
+    for f, ct, w in [("tri_data", C.c_uint32, 8), ("woop_tris", C.c_uint32, 12), ("bvh_nodes", C.c_uint32, 16)]:
+        cnt = {"tri_data": da.n_tri_data, "woop_tris": da.n_woop_tris, "bvh_nodes": da.n_bvh_nodes}[f]
+        assert np.array_equal(_arr(getattr(da, f), ct, cnt * w), _arr(getattr(db, f), ct, cnt * w)), f
+    assert da.n_anim_meshes == 1 and da.n_anim_vertices == len(v) and da.n_anim_triangles == len(tris)
+    am = da.anim_meshes[0]
+    assert (am.mesh, am.vertex_first, am.vertex_count, am.tri_first, am.tri_count, am.max_bone) == \
+        (0, 0, len(v), 0, len(tris), 1)
+    av = da.anim_vertices[5]
+    assert list(av.pos) == v[5].tolist() and av.bone_weights == int(bw[5].view(np.uint64)[0])
+    assert db.n_anim_meshes == 0
+
+
+def test_area_light_on_animated_mesh_refused(ctl):
+    s = build_scene(ctl, light_on_tube=True)
+    with pytest.raises(ctl.CTLError, match="animated"):
+        s.compile()
+
+
+def test_oracle_refit_at_rest_reproduces_the_build(ctl, orc):
+    """Identity bones, lerp 0: the refit boxes equal the builder's child boxes and
+    the Woop data the compile's (both are exact functions of the vertices)."""
+    eye = np.stack([np.eye(4, dtype=np.float32)] * 2)
+    v, n, bi, bw, tris, uv = skinned_tube()
+    # weights (w0, 255 - w0) blend the identity to a matrix that is not exactly
+    # the identity: one bone at weight 255 keeps the rest pose exact
+    s = ctl.HostScene()
+    s.add_animated_mesh(v, n, np.zeros_like(bi), np.array([[255, 0, 0, 0, 0, 0, 0, 0]] * len(v), np.uint8), tris,
+                        [ctl.diffuse_material(0.5, 0.5, 0.5)], uvs=uv)
+    s.add_node(0)
+    s.add_node(0, [1, 0, 0, 3, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1])
+    s.set_camera([0, 2, -9], [0, 2, 0], [0, 1, 0], 50, 16, 16)
+    d = s.compile()
+    d3, keep3, eps3 = oracle_animated(ctl, orc, d, eye[:1], eye[:1], 0.0)
+    assert np.array_equal(keep3[1].view(np.uint32), _arr(d.woop_tris, C.c_uint32, d.n_woop_tris * 12))
+    assert np.array_equal(keep3[2].view(np.uint32), _arr(d.bvh_nodes, C.c_uint32, d.n_bvh_nodes * 16))
+    assert np.array_equal(keep3[3][:d.n_scene_bvh_nodes * 16].view(np.uint32),
+                          _arr(d.scene_bvh_nodes, C.c_uint32, d.n_scene_bvh_nodes * 16))
+    assert np.float32(eps3) == np.float32(d.ray_eps)
+
+
+# ---------------------------------------------------------------------------- GPU
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_animate_arrays_bit_exact(ctl, orc, dev, bvh):
+    A = ctl._abi
+    s = build_scene(ctl)
+    d = s.compile()
+    if bvh == "binary":
+        d = binary_bvh(d)
+    f0, f1 = frames()
+    pt = ctl.PathTracer(0)
+    pt.upload_scene(d)
+    pt.animate(0, f0, f1, 0.25)      # a first pose, then the one compared: each call starts from the rest pose
+    pt.animate(0, f0, f1, 0.4)
+    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.4)
+    tri, woop, nodes, scene, boxes = keep
+    got = pt.read_array(A.CTL_ARRAY_TRI_DATA, 0, d.n_tri_data, np.uint32, 8)
+    assert np.array_equal(got.ravel(), tri)
+    assert not np.array_equal(tri, _arr(d.tri_data, C.c_uint32, d.n_tri_data * 8))   # it moved
+    got = pt.read_array(A.CTL_ARRAY_WOOP, 0, d.n_woop_tris, np.uint32, 12)
+    assert np.array_equal(got.ravel(), woop.view(np.uint32))
+    got = pt.read_array(A.CTL_ARRAY_BVH_NODES, 0, d.n_bvh_nodes, np.uint32, 16)
+    assert np.array_equal(got.ravel(), nodes.view(np.uint32))
+    got = pt.read_array(A.CTL_ARRAY_SCENE_BVH, 0, d.n_scene_bvh_nodes, np.uint32, 16)
+    assert np.array_equal(got.ravel(), scene[:d.n_scene_bvh_nodes * 16].view(np.uint32))
+    got = pt.read_array(A.CTL_ARRAY_MESH_BOXES, 0, d.n_meshes, np.float32, 6)
+    assert np.array_equal(got.ravel().view(np.uint32), boxes.view(np.uint32))
+    got = pt.read_array(A.CTL_ARRAY_RAY_EPS, 0, 1, np.float32, 1)
+    assert got[0, 0] == eps
+    pt.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_animated_traversal_and_render_bit_exact(ctl, orc, dev, bvh):
+    """Refit trees (binary and the 4-wide copy) traverse to the oracle's hits on
+    the oracle's animated arrays; hits agree with brute force; a 2-pass render
+    is bit-exact."""
+    w, h = 64, 48
+    s = build_scene(ctl, w, h)
+    d = s.compile()
+    if bvh == "binary":
+        d = binary_bvh(d)
+    f0, f1 = frames()
+    pt = ctl.PathTracer(0)
+    pt.upload_scene(d)
+    pt.animate(0, f0, f1, 0.6)
+    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.6)
+    rays = random_rays(d2, 20000, seed=3)
+    want = oracle_intersect(orc, d2, rays, tie=tie_rule(d2))
+    r = torch.from_numpy(rays).to(dev)
+    hits = torch.zeros((rays.shape[0], 4), dtype=torch.int32, device=dev)
+    pt.intersect_buffers(rays.shape[0], r.data_ptr(), hits.data_ptr(), False)
+    torch.cuda.synchronize()
+    got = hits.cpu().numpy()
+    assert np.array_equal(got, want)
+    hit = want[:, 2] != -1
+    assert hit.sum() > 1000
+    bt = np.zeros(rays.shape[0], np.float32)
+    btri = np.zeros(rays.shape[0], np.uint32)
+    orc.oracle_brute_force(C.byref(d2), rays.shape[0], oracle.ptr(rays), oracle.ptr(bt), oracle.ptr(btri), 0)
+    assert np.array_equal(got[:, 0].view(np.float32)[hit], bt[hit])
+    p = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
+    want_fb, wrays = oracle_render(orc, d2, p, 2, w, h)
+    fb = torch.zeros((w * h, 7), dtype=torch.float32, device=dev)
+    pt.params = p
+    pt.reset_rays()
+    for k in range(2):
+        pt.do_pass(fb.data_ptr(), k)
+    torch.cuda.synchronize()
+    got_fb = fb.cpu().numpy()
+    assert pt.rays_traced() == wrays
+    assert np.array_equal(got_fb.view(np.uint32), want_fb.view(np.uint32))
+    pt.close()
+
+
+@pytest.mark.gpu
+def test_animate_rejects_bad_bones(ctl, dev):
+    s = build_scene(ctl)
+    d = s.compile()
+    pt = ctl.PathTracer(0)
+    pt.upload_scene(d)
+    eye = np.stack([np.eye(4, dtype=np.float32)])
+    with pytest.raises(ctl.CTLError, match="bone"):
+        pt.animate(0, eye, eye, 0.5)         # the tube uses bone 1
+    with pytest.raises(ctl.CTLError):
+        pt.animate(1, eye, eye, 0.5)         # one animated mesh only
+    pt.close()
