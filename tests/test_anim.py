@@ -158,6 +158,23 @@ def test_oracle_refit_at_rest_reproduces_the_build(ctl, orc):
     assert np.float32(eps3) == np.float32(d.ray_eps)
 
 
+def test_oracle_refit_traversal_matches_brute_force(ctl, orc):
+    """The refit tree bounds the moved triangles: traceRay over it finds what a
+    scan over every triangle finds (BVH-independent truth)."""
+    from helpers import oracle_trace
+    s = build_scene(ctl)
+    d = s.compile()
+    f0, f1 = frames()
+    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.8)
+    rays = random_rays(d2, 20000, seed=5)
+    t, u, v, tri, node, st = oracle_trace(orc, d2, rays, mode=0)
+    bt = np.zeros(rays.shape[0], np.float32)
+    btri = np.zeros(rays.shape[0], np.uint32)
+    orc.oracle_brute_force(C.byref(d2), rays.shape[0], oracle.ptr(rays), oracle.ptr(bt), oracle.ptr(btri), 0)
+    assert (tri != 0xFFFFFFFF).sum() > 2000
+    assert np.array_equal(t, bt) and np.array_equal(tri, btri)
+
+
 # ---------------------------------------------------------------------------- GPU
 
 torch = pytest.importorskip("torch")
@@ -217,7 +234,7 @@ def test_animated_traversal_and_render_bit_exact(ctl, orc, dev, bvh):
     pt.upload_scene(d)
     pt.animate(0, f0, f1, 0.6)
     d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.6)
-    rays = random_rays(d2, 20000, seed=3)
+    rays = random_rays(d2, 20000, seed=3, tmin=d2.ray_eps)   # batch tmin = traceRay's eps (brute force below)
     want = oracle_intersect(orc, d2, rays, tie=tie_rule(d2))
     r = torch.from_numpy(rays).to(dev)
     hits = torch.zeros((rays.shape[0], 4), dtype=torch.int32, device=dev)
