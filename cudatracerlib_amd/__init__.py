@@ -154,17 +154,16 @@ class HostScene:
         nrm = np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 3)
         bi = np.ascontiguousarray(bone_indices, dtype=np.uint8).reshape(-1, 8)
         bw = np.ascontiguousarray(bone_weights, dtype=np.uint8).reshape(-1, 8)
-        av = (_abi.AnimVertex * v.shape[0])()
-        for k in range(v.shape[0]):
-            av[k].pos[:] = v[k].tolist()
-            av[k].normal[:] = nrm[k].tolist()
-            av[k].bone_indices = int(bi[k].view(np.uint64)[0])
-            av[k].bone_weights = int(bw[k].view(np.uint64)[0])
+        dt = np.dtype([("pos", np.float32, 3), ("normal", np.float32, 3), ("bi", np.uint8, 8), ("bw", np.uint8, 8)])
+        assert dt.itemsize == C.sizeof(_abi.AnimVertex)
+        rec = np.zeros(v.shape[0], dt)
+        rec["pos"], rec["normal"], rec["bi"], rec["bw"] = v, nrm, bi, bw
+        av = C.cast(rec.ctypes.data, C.POINTER(_abi.AnimVertex))
         i = np.ascontiguousarray(indices, dtype=np.uint32).reshape(-1, 3)
         mats = (Material * len(materials))(*materials)
         mi = None if mat_index is None else np.ascontiguousarray(mat_index, dtype=np.uint8)
         uv = None if uvs is None else np.ascontiguousarray(uvs, dtype=np.float32)
-        self._keep = getattr(self, "_keep", []) + [av, i, mi, uv, mats]
+        self._keep = getattr(self, "_keep", []) + [rec, i, mi, uv, mats]
         r = self._L.ctl_host_scene_add_animated_mesh(
             self._h, av, v.shape[0], i.ctypes.data, i.shape[0], None if uv is None else uv.ctypes.data,
             None if mi is None else mi.ctypes.data, mats, len(materials))

@@ -4,11 +4,13 @@
 //   skin     g_ComputeVertices (AnimatedMesh.cu:29-43): per vertex, two 8-bone
 //            matrix blends, TransformPoint / TransformDirection, lerp
 //   tris     g_ComputeTriangles -> TriangleData::setData (TriangleData.cu:35-63)
-//   woop     AnimProvider::setObject (AnimatedMesh.cpp:113-117): every BVH entry
-//   refit    bottom-up box refit of the mesh's binary tree and of its 4-wide
-//            copy, one launch per tree level (deepest first)
+//   refit    bottom-up box refit of the mesh's binary tree, one launch per wide
+//            level (deepest first) and one single-block launch for the narrow
+//            top levels; the leaf boxes rewrite every entry's Woop data on the
+//            way (AnimProvider::setObject, AnimatedMesh.cpp:113-117); the 4-wide
+//            copy then gathers its boxes from the binary children they came from
 //   scene    instance boxes (mesh box x node transform), refit of the scene's
-//            binary and 4-wide trees, scene box -> m_rayTraceEps
+//            binary tree + gather into its 4-wide copy, scene box -> m_rayTraceEps
 //
 // The reference re-derives the mesh tree on the host with BVHRebuilder (refit
 // plus subtree rotations, BVHRebuilder.cpp:281-340); the tree shape is not
@@ -28,9 +30,20 @@
 namespace ctl {
 
 struct AnimTree {
-    uint32_t base = 0;                  // binary: float4 offset of node 0; wide: wide-node index of node 0
+    uint32_t base = 0;                  // float4 offset of the tree's node 0
     std::vector<uint32_t> level_off;    // [levels + 1] offsets into order, deepest level first
     uint32_t* d_order = nullptr;        // node indices relative to base
+    uint32_t* d_level_off = nullptr;
+    uint32_t top_first = 0;             // levels from here on are small: one single-block launch
+    bool valid = false;
+};
+
+// A 4-wide copy's boxes after the binary refit: slot q of the wide tree takes
+// the box of binary (node, child) src[q] (recorded by collapse_wide).
+struct WideGather {
+    uint32_t base = 0;                  // wide-node index of the tree's node 0
+    uint32_t n_slots = 0;               // 4 x nodes
+    uint32_t* d_src = nullptr;
     bool valid = false;
 };
 
@@ -38,12 +51,14 @@ struct AnimMeshPlan {
     ctl_anim_mesh am;
     ctl_kernel_mesh km;
     uint32_t n_entries = 0;
-    AnimTree bin, wide;
+    AnimTree bin;
+    WideGather wide;
 };
 
 struct AnimState {
     std::vector<AnimMeshPlan> meshes;
-    AnimTree scene_bin, scene_wide;
+    AnimTree scene_bin;
+    WideGather scene_wide;
     const ctl_anim_vertex* d_verts = nullptr;
     const uint32_t* d_tris = nullptr;
     float* d_mesh_boxes = nullptr;      // 6 per mesh
@@ -63,6 +78,7 @@ namespace {
 
 constexpr int32_t kSent = 0x76543210;
 constexpr int kAB = 256;
+constexpr uint32_t kTopMax = 4096;   // levels at most this wide go to the single-block refit
 
 __device__ __forceinline__ void box_empty(float lo[3], float hi[3]) {
     lo[0] = lo[1] = lo[2] = FLT_MAX;
@@ -72,13 +88,19 @@ __device__ __forceinline__ void box_extend(float lo[3], float hi[3], const float
     for (int k = 0; k < 3; k++) { lo[k] = tmin(lo[k], plo[k]); hi[k] = tmax(hi[k], phi[k]); }
 }
 
+// Bone matrices of both frames staged in LDS (<= 256 bones x 2 x 64 B = 32 KB):
+// each vertex reads 8 matrices per frame.
 __global__ __launch_bounds__(kAB) void anim_skin_kernel(const ctl_anim_vertex* __restrict__ V, uint32_t n,
                                                        const float* __restrict__ b0, const float* __restrict__ b1,
-                                                       float t, float4* P, float4* N) {
+                                                       uint32_t n_bones, float t, float4* P, float4* N) {
+    extern __shared__ float bones[];
+    const uint32_t nf = 16 * n_bones;
+    for (uint32_t k = threadIdx.x; k < 2 * nf; k += kAB) bones[k] = k < nf ? b0[k] : b1[k - nf];
+    __syncthreads();
     const uint32_t i = blockIdx.x * kAB + threadIdx.x;
     if (i >= n) return;
     f3 p, nn;
-    skin_vertex(V[i], b0, b1, t, p, nn);
+    skin_vertex(V[i], bones, bones + nf, t, p, nn);
     P[i] = make_float4(p.x, p.y, p.z, 0.0f);
     N[i] = make_float4(nn.x, nn.y, nn.z, 0.0f);
 }
@@ -97,25 +119,13 @@ __global__ __launch_bounds__(kAB) void anim_tri_kernel(const uint32_t* __restric
     td[t] = r;
 }
 
-__global__ __launch_bounds__(kAB) void anim_woop_kernel(const uint32_t* __restrict__ idx, uint32_t n,
-                                                       const uint32_t* __restrict__ tris,
-                                                       const float4* __restrict__ P, float4* woop) {
-    const uint32_t e = blockIdx.x * kAB + threadIdx.x;
-    if (e >= n) return;
-    const uint32_t t = idx[e] >> 1;
-    float v[12];
-    woop_set_hd(ld3(P, tris[3 * t]), ld3(P, tris[3 * t + 1]), ld3(P, tris[3 * t + 2]), v);
-    woop[3 * e] = make_float4(v[0], v[1], v[2], v[3]);
-    woop[3 * e + 1] = make_float4(v[4], v[5], v[6], v[7]);
-    woop[3 * e + 2] = make_float4(v[8], v[9], v[10], v[11]);
-}
-
 // Box of a leaf value: mesh trees (SCENE = false) read the triangles of the
 // leaf's entry run; the scene tree's leaves are instances (~node).
 struct LeafCtx {
     const uint32_t* idx;     // mesh entries (TriIntersectorData2), relative to the mesh
     const uint32_t* tris;    // mesh triangle vertex indices
     const float4* P;         // skinned positions
+    float4* woop;            // mesh TriIntersectorData (3 float4 per entry), rewritten on the way
     const float* inst;       // instance boxes (scene)
 };
 
@@ -126,16 +136,25 @@ __device__ __forceinline__ void leaf_box(const LeafCtx& L, int32_t v, float lo[3
         for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
         return;
     }
+    // every entry belongs to exactly one leaf: its Woop data (AnimProvider::setObject,
+    // AnimatedMesh.cpp:113-117) is rewritten here, from the vertices the box reads
     box_empty(lo, hi);
     uint32_t e = (uint32_t)~v;
-    for (;;) {
-        const uint32_t code = L.idx[e++];
+    for (;; e++) {
+        const uint32_t code = L.idx[e];
         const uint32_t t = code >> 1;
+        f3 p[3];
         for (int k = 0; k < 3; k++) {
-            const float4 p = L.P[L.tris[3 * t + k]];
-            const float q[3] = {p.x, p.y, p.z};
+            const float4 q4 = L.P[L.tris[3 * t + k]];
+            const float q[3] = {q4.x, q4.y, q4.z};
+            p[k] = mk3(q4.x, q4.y, q4.z);
             box_extend(lo, hi, q, q);
         }
+        float w[12];
+        woop_set_hd(p[0], p[1], p[2], w);
+        L.woop[3 * e] = make_float4(w[0], w[1], w[2], w[3]);
+        L.woop[3 * e + 1] = make_float4(w[4], w[5], w[6], w[7]);
+        L.woop[3 * e + 2] = make_float4(w[8], w[9], w[10], w[11]);
         if (code & 1) break;
     }
 }
@@ -175,30 +194,40 @@ __global__ __launch_bounds__(kAB) void refit_bin_kernel(float* nodes, const uint
     }
 }
 
-__device__ __forceinline__ void wide_node_box(const WideNode& w, float lo[3], float hi[3]) {
-    box_empty(lo, hi);
-    for (int s = 0; s < 4; s++) {
-        if (w.child[s] == kSent) continue;
-        const float a[3] = {w.lo_x[s], w.lo_y[s], w.lo_z[s]}, b[3] = {w.hi_x[s], w.hi_y[s], w.hi_z[s]};
-        box_extend(lo, hi, a, b);
+// The levels that hold few nodes (the top of the tree) in one block, level by
+// level with a barrier in between, instead of one launch each.
+template <bool SCENE>
+__global__ __launch_bounds__(1024) void refit_bin_top_kernel(float* nodes, const uint32_t* __restrict__ order,
+                                                            const uint32_t* __restrict__ level_off, uint32_t n_levels,
+                                                            LeafCtx L) {
+    for (uint32_t l = 0; l < n_levels; l++) {
+        for (uint32_t i = level_off[l] + threadIdx.x; i < level_off[l + 1]; i += 1024) {
+            float* nd = nodes + 16 * (size_t)order[i];
+            for (int c = 0; c < 2; c++) {
+                const int32_t v = __float_as_int(nd[12 + c]);
+                if (v == kSent) continue;
+                float lo[3], hi[3];
+                if (v < 0) leaf_box<SCENE>(L, v, lo, hi);
+                else bin_node_box(nodes + 16 * (size_t)(v >> 2), lo, hi);
+                bin_set_child_box(nd, c, lo, hi);
+            }
+        }
+        __syncthreads();
     }
 }
 
-template <bool SCENE>
-__global__ __launch_bounds__(kAB) void refit_wide_kernel(WideNode* nodes, const uint32_t* __restrict__ order, uint32_t n,
-                                                        LeafCtx L) {
-    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
-    if (i >= n) return;
-    WideNode& w = nodes[order[i]];
-    for (int s = 0; s < 4; s++) {
-        const int32_t v = w.child[s];
-        if (v == kSent) continue;
-        float lo[3], hi[3];
-        if (v < 0) leaf_box<SCENE>(L, v, lo, hi);
-        else wide_node_box(nodes[v], lo, hi);
-        w.lo_x[s] = lo[0]; w.lo_y[s] = lo[1]; w.lo_z[s] = lo[2];
-        w.hi_x[s] = hi[0]; w.hi_y[s] = hi[1]; w.hi_z[s] = hi[2];
-    }
+__global__ __launch_bounds__(kAB) void wide_gather_kernel(WideNode* wide, const uint32_t* __restrict__ src,
+                                                         uint32_t n_slots, const float* __restrict__ bin) {
+    const uint32_t q = blockIdx.x * kAB + threadIdx.x;
+    if (q >= n_slots) return;
+    const uint32_t sidx = src[q];
+    if (sidx == 0xffffffffu) return;
+    float lo[3], hi[3];
+    bin_child_box(bin + 16 * (size_t)(sidx >> 1), (int)(sidx & 1u), lo, hi);
+    WideNode& w = wide[q >> 2];
+    const uint32_t sl = q & 3u;
+    w.lo_x[sl] = lo[0]; w.lo_y[sl] = lo[1]; w.lo_z[sl] = lo[2];
+    w.hi_x[sl] = hi[0]; w.hi_y[sl] = hi[1]; w.hi_z[sl] = hi[2];
 }
 
 // m_sLocalBox of the refit mesh: the union of its root's children.
@@ -272,7 +301,14 @@ bool plan_tree(AnimState* A, AnimTree& T, uint32_t base, uint32_t n_nodes, uint3
             if (depth[k] == d) order.push_back(k);
     }
     T.level_off.push_back((uint32_t)order.size());
-    if (!anim_upload(A, &T.d_order, order.data(), order.size())) { err = "refit plan: upload failed"; return false; }
+    const uint32_t nl = (uint32_t)T.level_off.size() - 1;
+    T.top_first = nl;
+    while (T.top_first > 0 && T.level_off[T.top_first] - T.level_off[T.top_first - 1] <= kTopMax) T.top_first--;
+    if (!anim_upload(A, &T.d_order, order.data(), order.size()) ||
+        !anim_upload(A, &T.d_level_off, T.level_off.data(), T.level_off.size())) {
+        err = "refit plan: upload failed";
+        return false;
+    }
     T.valid = true;
     return true;
 }
@@ -290,26 +326,32 @@ bool plan_binary(AnimState* A, AnimTree& T, const ctl_bvh_node* nodes, uint32_t 
     }, err);
 }
 
-bool plan_wide(AnimState* A, AnimTree& T, const WideNode* nodes, uint32_t n_nodes, uint32_t base, std::string& err) {
-    return plan_tree(A, T, base, n_nodes, 0, [&](uint32_t k, uint32_t* out) {
-        int n = 0;
-        for (int s = 0; s < 4; s++) {
-            const int32_t v = nodes[k].child[s];
-            if (v >= 0 && v != kSent) out[n++] = (uint32_t)v;
-        }
-        return n;
-    }, err);
+bool plan_gather(AnimState* A, WideGather& G, const uint32_t* src, uint32_t n_nodes, uint32_t base, std::string& err) {
+    G.base = base;
+    G.n_slots = 4 * n_nodes;
+    if (!anim_upload(A, &G.d_src, src, G.n_slots)) { err = "refit plan: upload failed"; return false; }
+    G.valid = true;
+    return true;
 }
 
 template <bool SCENE>
-void launch_refit(hipStream_t s, const AnimTree& T, float* bin_base, WideNode* wide_base, const LeafCtx& L) {
-    for (size_t l = 0; l + 1 < T.level_off.size(); l++) {
+void launch_refit(hipStream_t s, const AnimTree& T, float* bin_base, const LeafCtx& L) {
+    for (uint32_t l = 0; l < T.top_first; l++) {
         const uint32_t first = T.level_off[l], cnt = T.level_off[l + 1] - first;
         if (!cnt) continue;
-        const dim3 g((cnt + kAB - 1) / kAB);
-        if (bin_base) hipLaunchKernelGGL(refit_bin_kernel<SCENE>, g, dim3(kAB), 0, s, bin_base, T.d_order + first, cnt, L);
-        else hipLaunchKernelGGL(refit_wide_kernel<SCENE>, g, dim3(kAB), 0, s, wide_base, T.d_order + first, cnt, L);
+        hipLaunchKernelGGL(refit_bin_kernel<SCENE>, dim3((cnt + kAB - 1) / kAB), dim3(kAB), 0, s, bin_base,
+                           T.d_order + first, cnt, L);
     }
+    const uint32_t nl = (uint32_t)T.level_off.size() - 1;
+    if (T.top_first < nl)
+        hipLaunchKernelGGL(refit_bin_top_kernel<SCENE>, dim3(1), dim3(1024), 0, s, bin_base, T.d_order,
+                           T.d_level_off + T.top_first, nl - T.top_first, L);
+}
+
+void launch_gather(hipStream_t s, const WideGather& G, WideNode* wide_base, const float* bin_base) {
+    if (!G.valid || !G.n_slots) return;
+    hipLaunchKernelGGL(wide_gather_kernel, dim3((G.n_slots + kAB - 1) / kAB), dim3(kAB), 0, s, wide_base + G.base,
+                       G.d_src, G.n_slots, bin_base);
 }
 
 }  // namespace
@@ -326,7 +368,8 @@ void anim_free(ctl_ctx* c) {
 // Called by ctl_scene_upload once the scene arrays are on the device.
 // wn / wbase / sw: the 4-wide trees built on upload (empty for binary scenes).
 int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>& wn,
-               const std::vector<uint32_t>& wbase, const std::vector<WideNode>& sw) {
+               const std::vector<uint32_t>& wbase, const std::vector<WideNode>& sw,
+               const std::vector<uint32_t>& wsrc, const std::vector<uint32_t>& ssrc) {
     anim_free(c);
     if (!d->mesh_boxes) return CTL_OK;
     c->anim = new AnimState();
@@ -370,7 +413,8 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
         if (wide) {
             const uint32_t wb = wbase[P.am.mesh];
             const uint32_t we = P.am.mesh + 1 < wbase.size() ? wbase[P.am.mesh + 1] : (uint32_t)wn.size();
-            if (!plan_wide(A, P.wide, wn.data() + wb, we - wb, wb, err)) return fail(err);
+            if (wsrc.size() != 4 * wn.size()) return fail("wide source map missing");
+            if (!plan_gather(A, P.wide, wsrc.data() + 4ull * wb, we - wb, wb, err)) return fail(err);
         }
         tmp = std::max<size_t>(tmp, P.am.vertex_count);
         A->meshes.push_back(std::move(P));
@@ -379,7 +423,10 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
         if (!plan_binary(A, A->scene_bin, d->scene_bvh_nodes, d->n_scene_bvh_nodes, 0,
                          (uint32_t)d->scene_start_node >> 2, err))
             return fail(err);
-        if (wide && !sw.empty() && !plan_wide(A, A->scene_wide, sw.data(), (uint32_t)sw.size(), 0, err)) return fail(err);
+        if (wide && !sw.empty()) {
+            if (ssrc.size() != 4 * sw.size()) return fail("wide source map missing");
+            if (!plan_gather(A, A->scene_wide, ssrc.data(), (uint32_t)sw.size(), 0, err)) return fail(err);
+        }
     }
     if (!anim_alloc(A, &A->d_P, tmp) || !anim_alloc(A, &A->d_N, tmp)) return fail("animation buffers allocation failed");
     A->tmp_cap = tmp;
@@ -400,6 +447,7 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
     if (anim >= A->meshes.size()) { c->err = "scene_animate: animated mesh index out of range"; return CTL_ERR_INVALID; }
     const AnimMeshPlan& P = A->meshes[anim];
     if (P.am.max_bone >= n_bones) { c->err = "scene_animate: a vertex uses a bone index >= n_bones"; return CTL_ERR_INVALID; }
+    if (n_bones > 256) { c->err = "scene_animate: more than 256 bones (bone indices are 8-bit)"; return CTL_ERR_INVALID; }
     if (hipSetDevice(c->device) != hipSuccess) { c->err = "scene_animate: hipSetDevice failed"; return CTL_ERR_HIP; }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const size_t nb = 16ull * n_bones;
@@ -419,28 +467,26 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
     DevScene& S = c->scene;
     const uint32_t nv = P.am.vertex_count, nt = P.am.tri_count, ne = P.n_entries;
     const uint32_t* tris = A->d_tris + 3ull * P.am.tri_first;
-    if (nv) hipLaunchKernelGGL(anim_skin_kernel, dim3((nv + kAB - 1) / kAB), dim3(kAB), 0, s, A->d_verts + P.am.vertex_first,
-                               nv, A->d_bones[0], A->d_bones[1], lerp, A->d_P, A->d_N);
+    if (nv) hipLaunchKernelGGL(anim_skin_kernel, dim3((nv + kAB - 1) / kAB), dim3(kAB), 2 * nb * sizeof(float), s,
+                               A->d_verts + P.am.vertex_first, nv, A->d_bones[0], A->d_bones[1], n_bones, lerp, A->d_P,
+                               A->d_N);
     if (nt) hipLaunchKernelGGL(anim_tri_kernel, dim3((nt + kAB - 1) / kAB), dim3(kAB), 0, s, tris, nt, A->d_P, A->d_N,
                                const_cast<ctl_triangle_data*>(S.tri_data) + P.km.triangle_offset);
     const uint32_t* idx = S.tri_idx + P.km.bvh_indices_offset;
-    if (ne) hipLaunchKernelGGL(anim_woop_kernel, dim3((ne + kAB - 1) / kAB), dim3(kAB), 0, s, idx, ne, tris, A->d_P,
-                               const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset);
-    LeafCtx L{idx, tris, A->d_P, nullptr};
+    (void)ne;   // the Woop data is rewritten by the leaf boxes of the refit
+    LeafCtx L{idx, tris, A->d_P, const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset, nullptr};
     float* bin = reinterpret_cast<float*>(const_cast<float4*>(S.bvh) + P.bin.base);
-    launch_refit<false>(s, P.bin, bin, nullptr, L);
-    if (P.wide.valid)
-        launch_refit<false>(s, P.wide, nullptr, reinterpret_cast<WideNode*>(const_cast<float4*>(S.wbvh)) + P.wide.base, L);
+    launch_refit<false>(s, P.bin, bin, L);
+    launch_gather(s, P.wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.wbvh)), bin);
     hipLaunchKernelGGL(mesh_box_kernel, dim3(1), dim3(1), 0, s, bin, A->d_mesh_boxes + 6 * P.am.mesh);
     // instances, scene trees, epsilon
     if (A->n_nodes) {
         hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf,
                            A->n_nodes, A->d_mesh_boxes, A->d_inst_boxes);
-        LeafCtx LS{nullptr, nullptr, nullptr, A->d_inst_boxes};
-        if (A->scene_bin.valid)
-            launch_refit<true>(s, A->scene_bin, reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh)), nullptr, LS);
-        if (A->scene_wide.valid)
-            launch_refit<true>(s, A->scene_wide, nullptr, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), LS);
+        LeafCtx LS{nullptr, nullptr, nullptr, nullptr, A->d_inst_boxes};
+        float* sbin = reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh));
+        if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
+        launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);
         hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps);
         if (hipMemcpyAsync(A->h_eps, A->d_eps, 7 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {

@@ -361,7 +361,7 @@ void wavefront_free(ctl_ctx* c);
 // anim.hip
 struct WideNode;
 int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>& wn, const std::vector<uint32_t>& wbase,
-               const std::vector<WideNode>& sw);
+               const std::vector<WideNode>& sw, const std::vector<uint32_t>& wsrc, const std::vector<uint32_t>& ssrc);
 void anim_free(ctl_ctx* c);
 // wpt.hip
 int wpt_pass(ctl_ctx* c, const ctl_wpt_params* p, ctl_pixel* fb, hipStream_t s);

@@ -573,18 +573,22 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     // caller asks for the reference's binary visit order
     const bool wide = (d->flags & CTL_SCENE_BINARY_BVH) == 0 && d->n_bvh_nodes > 0;
     std::vector<WideNode> wn, sw;
-    std::vector<uint32_t> wbase;
+    std::vector<uint32_t> wbase, wsrc, ssrc;   // src maps: only for the refit of animated scenes
+    const bool want_src = d->n_anim_meshes > 0;
     if (wide) {
         wbase.assign(d->n_meshes, 0);
         try {
+            std::vector<uint32_t> ms;
             for (uint32_t m = 0; m < d->n_meshes; m++) {
                 const size_t first = d->meshes[m].bvh_node_offset / 4;
                 if (first >= d->n_bvh_nodes) throw std::runtime_error("mesh BVH offset out of range");
                 wbase[m] = (uint32_t)wn.size();
-                collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn);
+                collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn, want_src ? &ms : nullptr);
+                if (want_src) wsrc.insert(wsrc.end(), ms.begin(), ms.end());
             }
             if (d->n_nodes > 0 && d->scene_start_node >= 0)
-                collapse_wide(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, sw);
+                collapse_wide(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, sw,
+                              want_src ? &ssrc : nullptr);
         } catch (const std::exception& e) {
             free_scene(c);
             c->err = std::string("scene_upload: ") + e.what();
@@ -642,7 +646,7 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     c->n_woop = d->n_woop_tris;
     c->n_bvh_nodes = d->n_bvh_nodes;
     c->n_scene_bvh = d->n_scene_bvh_nodes;
-    int ar = ctl::anim_setup(c, d, wn, wbase, sw);
+    int ar = ctl::anim_setup(c, d, wn, wbase, sw, wsrc, ssrc);
     if (ar != CTL_OK) { free_scene(c); return (ctl_status)ar; }
     c->has_scene = true;
     return CTL_OK;

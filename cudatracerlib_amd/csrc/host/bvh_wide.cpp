@@ -12,6 +12,7 @@ const int32_t kSentinel = 0x76543210;
 struct Kid {
     float lo[3], hi[3];
     int32_t v;
+    uint32_t src;   // binary node index << 1 | child slot holding this box
 };
 
 inline bool is_inner(int32_t v) { return v >= 0 && v != kSentinel; }
@@ -22,7 +23,9 @@ inline float kid_area(const Kid& k) {
 }
 
 // Children of binary node `idx` with the boxes stored in it (BVHNodeData::getLeft/getRight).
-void binary_kids(const ctl_bvh_node& n, Kid& a, Kid& b) {
+void binary_kids(const ctl_bvh_node& n, uint32_t idx, Kid& a, Kid& b) {
+    a.src = idx << 1;
+    b.src = (idx << 1) | 1u;
     a.lo[0] = n.v[0]; a.hi[0] = n.v[1]; a.lo[1] = n.v[2]; a.hi[1] = n.v[3]; a.lo[2] = n.v[8]; a.hi[2] = n.v[9];
     b.lo[0] = n.v[4]; b.hi[0] = n.v[5]; b.lo[1] = n.v[6]; b.hi[1] = n.v[7]; b.lo[2] = n.v[10]; b.hi[2] = n.v[11];
     std::memcpy(&a.v, &n.v[12], 4);
@@ -34,6 +37,7 @@ struct Collapser {
     size_t n_nodes;
     std::vector<WideNode>& out;
     size_t base;
+    std::vector<uint32_t>* src;
 
     const ctl_bvh_node& node_of(int32_t v) const {
         size_t i = (size_t)v / 4;
@@ -45,7 +49,7 @@ struct Collapser {
         if (depth > 256) throw std::runtime_error("wide BVH: tree too deep");
         Kid k[4];
         int nk = 2;
-        binary_kids(node_of(v), k[0], k[1]);
+        binary_kids(node_of(v), (uint32_t)v >> 2, k[0], k[1]);
         while (nk < 4) {
             int best = -1;
             float bestArea = -1.0f;
@@ -53,12 +57,16 @@ struct Collapser {
                 if (is_inner(k[i].v) && kid_area(k[i]) > bestArea) { bestArea = kid_area(k[i]); best = i; }
             if (best < 0) break;
             Kid a, b;
-            binary_kids(node_of(k[best].v), a, b);
+            binary_kids(node_of(k[best].v), (uint32_t)k[best].v >> 2, a, b);
             k[best] = a;
             k[nk++] = b;
         }
         const size_t me = out.size();
         out.push_back(WideNode{});
+        if (src) {
+            src->resize(out.size() * 4 - 4 * base, 0xffffffffu);
+            for (int i = 0; i < nk; i++) (*src)[4 * (me - base) + i] = k[i].src;
+        }
         int32_t child[4];
         for (int i = 0; i < 4; i++) {
             if (i >= nk) { child[i] = kSentinel; continue; }
@@ -79,9 +87,11 @@ struct Collapser {
 
 }  // namespace
 
-int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out) {
+int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out,
+                      std::vector<uint32_t>* src) {
     if (!is_inner(root_value) || n_nodes == 0) throw std::runtime_error("wide BVH: root is not an inner node");
-    Collapser c{nodes, n_nodes, out, out.size()};
+    if (src) src->clear();
+    Collapser c{nodes, n_nodes, out, out.size(), src};
     return c.emit(root_value, 0);
 }
 

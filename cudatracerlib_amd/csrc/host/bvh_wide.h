@@ -32,6 +32,11 @@ static_assert(sizeof(WideNode) == 128, "wide node is 128 B");
 // >= 0 inner node float4 offset, i.e. 4 x node index) of `nodes` and appends
 // the wide nodes to `out`.  Returns the root's index relative to the first
 // node appended; child indices are relative to that first node as well.
-int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out);
+// src (optional): for every emitted node's 4 slots, the binary node index << 1 |
+// child slot the slot's box was taken from (0xFFFFFFFF for unused slots),
+// indexed like the appended nodes — what a refit of the binary tree needs to
+// refresh the wide boxes with one gather.
+int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out,
+                      std::vector<uint32_t>* src = nullptr);
 
 }  // namespace ctl
