@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--split-depth", type=int, default=8)
     ap.add_argument("--bins", type=int, default=0, help="SAH bins (0: library default)")
     ap.add_argument("--max-leaf", type=int, default=0, help="max leaf size (0: library default)")
-    ap.add_argument("--bvh", default="wide", choices=["wide", "binary"],
+    ap.add_argument("--bvh", default="wide", choices=["wide", "wideq", "binary"],
                     help="device traversal: 4-wide collapsed BVH, or the reference's binary order")
     return ap.parse_args()
 
@@ -186,6 +186,8 @@ def main():
     desc = hs.compile(threads=threads)
     if a.bvh == "binary":
         desc.flags |= ctl.CTL_SCENE_BINARY_BVH
+    elif a.bvh == "wideq":
+        desc.flags |= ctl._abi.CTL_SCENE_WIDE_QUANT
     t_build = time.perf_counter() - t0
     log(f"[rank {rank}] scene config {a.config}: {desc.n_tri_data} tris, {desc.n_bvh_nodes} BVH nodes, "
         f"built in {t_build:.1f}s with {threads} threads")

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("CTL_LIB") or os.path.join(_HERE, "_lib", "libctl_trac
 CTL_OK = 0
 CTL_SCENE_HALF_HOST_QUIRK = 1
 CTL_SCENE_BINARY_BVH = 2
+CTL_SCENE_WIDE_QUANT = 4
 CTL_XMSH_MATERIAL_RECORD_SIZE = 148
 CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS = range(6)
 CTL_BSDF_DIFFUSE = 1

@@ -23,6 +23,7 @@
 
 #include "../../../include/ctl_trace.h"
 #include "../host/bvh_wide.h"
+#include "../ctl_qnode.h"
 #include "common.h"
 
 namespace ctl {
@@ -594,11 +595,37 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
             c->err = std::string("scene_upload: ") + e.what();
             return CTL_ERR_INVALID;
         }
-        const WideNode* wd; UP(wn.data(), wn.size(), &wd);
-        const WideNode* swd; UP(sw.data(), sw.size(), &swd);
+        // 64-B quantized nodes on request (not when the refit will rewrite float nodes)
+        bool quant = (d->flags & CTL_SCENE_WIDE_QUANT) != 0 && !want_src;
+        std::vector<QWideNode> qn, qs;
+        auto encode = [](const std::vector<WideNode>& in, std::vector<QWideNode>& out) {
+            out.resize(in.size());
+            for (size_t i = 0; i < in.size(); i++) {
+                const WideNode& w = in[i];
+                const float lo[3][4] = {{w.lo_x[0], w.lo_x[1], w.lo_x[2], w.lo_x[3]},
+                                        {w.lo_y[0], w.lo_y[1], w.lo_y[2], w.lo_y[3]},
+                                        {w.lo_z[0], w.lo_z[1], w.lo_z[2], w.lo_z[3]}};
+                const float hi[3][4] = {{w.hi_x[0], w.hi_x[1], w.hi_x[2], w.hi_x[3]},
+                                        {w.hi_y[0], w.hi_y[1], w.hi_y[2], w.hi_y[3]},
+                                        {w.hi_z[0], w.hi_z[1], w.hi_z[2], w.hi_z[3]}};
+                if (!quantize_wide(lo, hi, w.child, out[i])) return false;
+            }
+            return true;
+        };
+        if (quant) quant = encode(wn, qn) && encode(sw, qs);
+        if (quant) {
+            const QWideNode* qd; UP(qn.data(), qn.size(), &qd);
+            const QWideNode* sqd; UP(qs.data(), qs.size(), &sqd);
+            S.wbvh = reinterpret_cast<const float4*>(qd);
+            S.scene_wbvh = reinterpret_cast<const float4*>(sqd);
+        } else {
+            const WideNode* wd; UP(wn.data(), wn.size(), &wd);
+            const WideNode* swd; UP(sw.data(), sw.size(), &swd);
+            S.wbvh = reinterpret_cast<const float4*>(wd);
+            S.scene_wbvh = reinterpret_cast<const float4*>(swd);
+        }
+        S.quant = quant ? 1 : 0;
         UP(wbase.data(), wbase.size(), &S.mesh_wbase);
-        S.wbvh = reinterpret_cast<const float4*>(wd);
-        S.scene_wbvh = reinterpret_cast<const float4*>(swd);
         S.wide = 1;
         S.tie_min = 1;
         c->wide_nodes = wn.size();

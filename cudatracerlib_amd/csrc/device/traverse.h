@@ -75,6 +75,7 @@ struct DevScene {
     uint32_t alpha;              // KernelDynamicScene::doAlphaMapping (some material has an alpha map)
     uint32_t tie_min;            // exact-t ties -> lowest (triangle, node) instead of first found
     uint32_t s_wnode_base;
+    uint32_t quant;              // wide trees in the 64-B quantized format (ctl_qnode.h)
 };
 
 struct TraceStats { uint32_t nodes, tris, inst; };
@@ -269,11 +270,32 @@ struct Traverser {
     // the others pushed far-to-near.  Same postponed-leaf / wave-exit rule.
     __device__ __forceinline__ void inner_wide(const DevScene& S, LaneStack& st, TraceStats* stats) {
         const float4* nodes = (SINGLE || level) ? S.wbvh : S.scene_wbvh;
+        const bool quant = S.quant != 0;
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
-            const float4* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 8u;
-            const float4 lox = n[0], hix = n[1], loy = n[2], hiy = n[3], loz = n[4], hiz = n[5];
-            int4 ch = reinterpret_cast<const int4*>(n)[6];
-            asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
+            float4 lox, hix, loy, hiy, loz, hiz;
+            int4 ch;
+            if (quant) {
+                // 64-B node: decode p + q * s per bound (ctl_qnode.h), then the float slab test
+                const float4* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 4u;
+                const float4 a = n[0], b = n[1], c = n[2];
+                ch = reinterpret_cast<const int4*>(n)[3];
+                asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
+                const uint32_t wlx = __float_as_uint(b.z), whx = __float_as_uint(b.w);
+                const uint32_t wly = __float_as_uint(c.x), why = __float_as_uint(c.y);
+                const uint32_t wlz = __float_as_uint(c.z), whz = __float_as_uint(c.w);
+#define CTL_QDEC(W, P, SC, K) ((P) + (float)(((W) >> (8 * K)) & 0xffu) * (SC))
+#define CTL_QDEC4(W, P, SC) make_float4(CTL_QDEC(W, P, SC, 0), CTL_QDEC(W, P, SC, 1), CTL_QDEC(W, P, SC, 2), CTL_QDEC(W, P, SC, 3))
+                lox = CTL_QDEC4(wlx, a.x, a.w); hix = CTL_QDEC4(whx, a.x, a.w);
+                loy = CTL_QDEC4(wly, a.y, b.x); hiy = CTL_QDEC4(why, a.y, b.x);
+                loz = CTL_QDEC4(wlz, a.z, b.y); hiz = CTL_QDEC4(whz, a.z, b.y);
+#undef CTL_QDEC4
+#undef CTL_QDEC
+            } else {
+                const float4* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 8u;
+                lox = n[0]; hix = n[1]; loy = n[2]; hiy = n[3]; loz = n[4]; hiz = n[5];
+                ch = reinterpret_cast<const int4*>(n)[6];
+                asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
+            }
             if (STATS) stats->nodes++;
             int k0, k1, k2, k3, c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
 #define CTL_WIDE_CHILD(K, C, comp)                                                                   \

@@ -77,6 +77,18 @@ def binary_bvh(desc):
     return d
 
 
+def wide_quant(desc):
+    """Copy of a compiled scene desc that selects the 64-B quantized 4-wide nodes."""
+    d = type(desc).from_buffer_copy(desc)
+    d.flags |= 4
+    return d
+
+
+def select_bvh(desc, bvh):
+    return {"wide": desc, "wideq": wide_quant(desc) if bvh == "wideq" else desc,
+            "binary": binary_bvh(desc) if bvh == "binary" else desc}[bvh]
+
+
 def oracle_render(orc, desc, params, passes, w, h, threads=0, fb=None, first_pass=0):
     if fb is None:
         fb = np.zeros((w * h, 7), np.float32)

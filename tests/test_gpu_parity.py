@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle
-from helpers import binary_bvh, camera_rays, oracle_intersect, oracle_render, random_rays, tie_rule
+from helpers import binary_bvh, camera_rays, oracle_intersect, oracle_render, random_rays, select_bvh, tie_rule
 
 pytestmark = pytest.mark.gpu
 
@@ -49,11 +49,9 @@ def gpu_intersect(tracer, desc, rays, any_hit, dev):
 
 @pytest.mark.parametrize("config,scale", [(1, 1.0), (2, 0.25), (3, 0.004)])
 @pytest.mark.parametrize("kind", ["random", "camera"])
-@pytest.mark.parametrize("bvh", ["wide", "binary"])
+@pytest.mark.parametrize("bvh", ["wide", "wideq", "binary"])
 def test_intersect_closest_bit_exact(ctl, orc, tracer, dev, config, scale, kind, bvh):
-    d = scene(ctl, config, scale, 96, 64)
-    if bvh == "binary":
-        d = binary_bvh(d)
+    d = select_bvh(scene(ctl, config, scale, 96, 64), bvh)
     rays = random_rays(d, 50000, seed=config) if kind == "random" else camera_rays(d, 96, 64, seed=config)
     if kind == "random":
         rays[::3, 3] = np.float32(d.ray_eps)      # some rays with tmin > 0
@@ -100,11 +98,9 @@ def render_gpu(ctl, tracer, desc, params, passes, w, h, dev, first_pass=0):
 @pytest.mark.parametrize("config,scale,w,h,passes", [(1, 1.0, 64, 64, 4), (2, 0.25, 96, 64, 2), (3, 0.003, 64, 48, 2)])
 @pytest.mark.parametrize("any_hit", [1, 0])
 @pytest.mark.parametrize("mode", ["persistent", "wavefront", "megakernel"])
-@pytest.mark.parametrize("bvh", ["wide", "binary"])
+@pytest.mark.parametrize("bvh", ["wide", "wideq", "binary"])
 def test_render_pass_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, passes, any_hit, mode, bvh):
-    d = scene(ctl, config, scale, w, h)
-    if bvh == "binary":
-        d = binary_bvh(d)
+    d = select_bvh(scene(ctl, config, scale, w, h), bvh)
     p = ctl.PTParams(1, 50, 5, any_hit, 64, 1, 0, {"persistent": 0, "megakernel": ctl.CTL_PT_MEGAKERNEL,
                                                  "wavefront": ctl.CTL_PT_WAVEFRONT}[mode])
     want, wrays = oracle_render(orc, d, p, passes, w, h)

@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B of bench variants (short runs, no CPU baseline): tools_ab.sh "<args A>" "<args B>" ...
+set -o pipefail
+mkdir -p gpurun_out/ab
+export TMPDIR=/tmp
+i=0
+for v in "$@"; do
+  timeout -k 10 300 python bench.py --steps 16 --warmup 2 --no-cpu-baseline --wpt-passes 0 $v > gpurun_out/ab/$i.json 2> gpurun_out/ab/$i.err || { echo "FAILED: $v"; tail -5 gpurun_out/ab/$i.err; exit 1; }
+  python -c "import json,sys; j=json.load(open('gpurun_out/ab/$i.json')); print('$v', '->', j['value'], 'Mrays/s', j['roofline']['per_launch_ms'], 'ms', 'frac', j['roofline']['frac'])"
+  i=$((i+1))
+done
