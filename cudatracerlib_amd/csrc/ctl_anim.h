@@ -74,24 +74,30 @@ CTL_HD void triangle_set_data(uint32_t w[8], f3 v0, f3 v1, f3 v2, f3 n0, f3 n1, 
     w[4] = float_to_half(dpdv.y) | ((uint32_t)float_to_half(dpdv.z) << 16);
 }
 
-// d_Compute (AnimatedMesh.cu:13-27): sum over the 8 (bone, weight/255) slots.
-CTL_HD m44 skin_matrix(const float* bones, uint64_t idx, uint64_t wgt) {
+// d_Compute (AnimatedMesh.cu:13-27): sum over the 8 (bone, weight/255) slots;
+// w[i] = (weight byte i) / 255.0f, the same for both frames.  Bone j's matrix
+// starts at bones + stride * j (the device pads the stride against LDS bank
+// conflicts).
+CTL_HD m44 skin_matrix(const float* bones, uint32_t stride, uint64_t idx, const float w[8]) {
     m44 mat;
     for (int k = 0; k < 16; k++) mat.d[k] = 0.0f;
     for (int i = 0; i < 8; i++) {
         const uint32_t j = (uint32_t)(idx & 0xff);
-        const float w = (float)(uint32_t)(wgt & 0xff) / 255.0f;
-        idx >>= 8; wgt >>= 8;
-        const float* m = bones + 16 * j;
-        for (int k = 0; k < 16; k++) mat.d[k] = mat.d[k] + m[k] * w;
+        idx >>= 8;
+        const float* m = bones + stride * j;
+        for (int k = 0; k < 16; k++) mat.d[k] = mat.d[k] + m[k] * w[i];
     }
     return mat;
 }
 
 // g_ComputeVertices (AnimatedMesh.cu:29-43): position and normal between two frames.
-CTL_HD void skin_vertex(const ctl_anim_vertex& v, const float* bones0, const float* bones1, float t, f3& P, f3& N) {
-    const m44 m0 = skin_matrix(bones0, v.bone_indices, v.bone_weights);
-    const m44 m1 = skin_matrix(bones1, v.bone_indices, v.bone_weights);
+CTL_HD void skin_vertex(const ctl_anim_vertex& v, const float* bones0, const float* bones1, uint32_t stride, float t,
+                        f3& P, f3& N) {
+    float w[8];
+    uint64_t wgt = v.bone_weights;
+    for (int i = 0; i < 8; i++, wgt >>= 8) w[i] = (float)(uint32_t)(wgt & 0xff) / 255.0f;
+    const m44 m0 = skin_matrix(bones0, stride, v.bone_indices, w);
+    const m44 m1 = skin_matrix(bones1, stride, v.bone_indices, w);
     const f3 p = mk3(v.pos[0], v.pos[1], v.pos[2]), n = mk3(v.normal[0], v.normal[1], v.normal[2]);
     const f3 p0 = xform_point(m0, p), p1 = xform_point(m1, p);
     P = p0 * (1.0f - t) + p1 * t;   // math::lerp (MathFunc.h:161)

@@ -4,11 +4,12 @@
 //   skin     g_ComputeVertices (AnimatedMesh.cu:29-43): per vertex, two 8-bone
 //            matrix blends, TransformPoint / TransformDirection, lerp
 //   tris     g_ComputeTriangles -> TriangleData::setData (TriangleData.cu:35-63)
+//   entries  per BVH entry: Woop data (AnimProvider::setObject, AnimatedMesh.cpp:
+//            113-117) and the triangle's box
 //   refit    bottom-up box refit of the mesh's binary tree, one launch per wide
 //            level (deepest first) and one single-block launch for the narrow
-//            top levels; the leaf boxes rewrite every entry's Woop data on the
-//            way (AnimProvider::setObject, AnimatedMesh.cpp:113-117); the 4-wide
-//            copy then gathers its boxes from the binary children they came from
+//            top levels; the 4-wide copy then gathers its boxes from the binary
+//            children they came from
 //   scene    instance boxes (mesh box x node transform), refit of the scene's
 //            binary tree + gather into its 4-wide copy, scene box -> m_rayTraceEps
 //
@@ -67,6 +68,7 @@ struct AnimState {
     float* h_eps = nullptr;             // pinned
     float4* d_P = nullptr;
     float4* d_N = nullptr;
+    float4* d_ebox = nullptr;           // 2 per BVH entry
     size_t tmp_cap = 0;
     float* d_bones[2] = {nullptr, nullptr};
     size_t bones_cap = 0;
@@ -78,7 +80,7 @@ namespace {
 
 constexpr int32_t kSent = 0x76543210;
 constexpr int kAB = 256;
-constexpr uint32_t kTopMax = 4096;   // levels at most this wide go to the single-block refit
+constexpr uint32_t kTopMax = 512;    // levels at most this wide go to the single-block refit
 
 __device__ __forceinline__ void box_empty(float lo[3], float hi[3]) {
     lo[0] = lo[1] = lo[2] = FLT_MAX;
@@ -93,14 +95,18 @@ __device__ __forceinline__ void box_extend(float lo[3], float hi[3], const float
 __global__ __launch_bounds__(kAB) void anim_skin_kernel(const ctl_anim_vertex* __restrict__ V, uint32_t n,
                                                        const float* __restrict__ b0, const float* __restrict__ b1,
                                                        uint32_t n_bones, float t, float4* P, float4* N) {
+    // stride 17 floats: lanes reading the same element of different bones hit different banks
     extern __shared__ float bones[];
-    const uint32_t nf = 16 * n_bones;
-    for (uint32_t k = threadIdx.x; k < 2 * nf; k += kAB) bones[k] = k < nf ? b0[k] : b1[k - nf];
+    const uint32_t nf = 17 * n_bones;
+    for (uint32_t k = threadIdx.x; k < 32 * n_bones; k += kAB) {
+        const uint32_t f = k >> 4, j = (f < n_bones ? f : f - n_bones), e = k & 15u;
+        bones[(f < n_bones ? 0 : nf) + 17 * j + e] = f < n_bones ? b0[16 * j + e] : b1[16 * j + e];
+    }
     __syncthreads();
     const uint32_t i = blockIdx.x * kAB + threadIdx.x;
     if (i >= n) return;
     f3 p, nn;
-    skin_vertex(V[i], bones, bones + nf, t, p, nn);
+    skin_vertex(V[i], bones, bones + nf, 17, t, p, nn);
     P[i] = make_float4(p.x, p.y, p.z, 0.0f);
     N[i] = make_float4(nn.x, nn.y, nn.z, 0.0f);
 }
@@ -119,13 +125,29 @@ __global__ __launch_bounds__(kAB) void anim_tri_kernel(const uint32_t* __restric
     td[t] = r;
 }
 
-// Box of a leaf value: mesh trees (SCENE = false) read the triangles of the
-// leaf's entry run; the scene tree's leaves are instances (~node).
+// Per BVH entry: its Woop data (AnimProvider::setObject, AnimatedMesh.cpp:113-117)
+// and its triangle's box, one thread per entry.
+__global__ __launch_bounds__(kAB) void anim_entry_kernel(const uint32_t* __restrict__ idx, uint32_t n,
+                                                        const uint32_t* __restrict__ tris,
+                                                        const float4* __restrict__ P, float4* woop, float4* ebox) {
+    const uint32_t e = blockIdx.x * kAB + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t t = idx[e] >> 1;
+    const f3 a = ld3(P, tris[3 * t]), b = ld3(P, tris[3 * t + 1]), c = ld3(P, tris[3 * t + 2]);
+    float w[12];
+    woop_set_hd(a, b, c, w);
+    woop[3 * e] = make_float4(w[0], w[1], w[2], w[3]);
+    woop[3 * e + 1] = make_float4(w[4], w[5], w[6], w[7]);
+    woop[3 * e + 2] = make_float4(w[8], w[9], w[10], w[11]);
+    ebox[2 * e] = make_float4(tmin(tmin(a.x, b.x), c.x), tmin(tmin(a.y, b.y), c.y), tmin(tmin(a.z, b.z), c.z), 0.0f);
+    ebox[2 * e + 1] = make_float4(tmax(tmax(a.x, b.x), c.x), tmax(tmax(a.y, b.y), c.y), tmax(tmax(a.z, b.z), c.z), 0.0f);
+}
+
+// Box of a leaf value: mesh trees (SCENE = false) take the union of their entry
+// run's triangle boxes; the scene tree's leaves are instances (~node).
 struct LeafCtx {
     const uint32_t* idx;     // mesh entries (TriIntersectorData2), relative to the mesh
-    const uint32_t* tris;    // mesh triangle vertex indices
-    const float4* P;         // skinned positions
-    float4* woop;            // mesh TriIntersectorData (3 float4 per entry), rewritten on the way
+    const float4* ebox;      // entry triangle boxes (lo, hi)
     const float* inst;       // instance boxes (scene)
 };
 
@@ -136,26 +158,12 @@ __device__ __forceinline__ void leaf_box(const LeafCtx& L, int32_t v, float lo[3
         for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
         return;
     }
-    // every entry belongs to exactly one leaf: its Woop data (AnimProvider::setObject,
-    // AnimatedMesh.cpp:113-117) is rewritten here, from the vertices the box reads
     box_empty(lo, hi);
-    uint32_t e = (uint32_t)~v;
-    for (;; e++) {
-        const uint32_t code = L.idx[e];
-        const uint32_t t = code >> 1;
-        f3 p[3];
-        for (int k = 0; k < 3; k++) {
-            const float4 q4 = L.P[L.tris[3 * t + k]];
-            const float q[3] = {q4.x, q4.y, q4.z};
-            p[k] = mk3(q4.x, q4.y, q4.z);
-            box_extend(lo, hi, q, q);
-        }
-        float w[12];
-        woop_set_hd(p[0], p[1], p[2], w);
-        L.woop[3 * e] = make_float4(w[0], w[1], w[2], w[3]);
-        L.woop[3 * e + 1] = make_float4(w[4], w[5], w[6], w[7]);
-        L.woop[3 * e + 2] = make_float4(w[8], w[9], w[10], w[11]);
-        if (code & 1) break;
+    for (uint32_t e = (uint32_t)~v;; e++) {
+        const float4 a = L.ebox[2 * e], b = L.ebox[2 * e + 1];
+        const float q0[3] = {a.x, a.y, a.z}, q1[3] = {b.x, b.y, b.z};
+        box_extend(lo, hi, q0, q1);
+        if (L.idx[e] & 1) break;
     }
 }
 
@@ -387,7 +395,7 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
         !anim_upload(A, (uint32_t**)&A->d_tris, d->anim_triangles, 3ull * d->n_anim_triangles))
         return fail("animation upload failed");
     const bool wide = !wn.empty();
-    size_t tmp = 0;
+    size_t tmp = 0, etmp = 0;
     for (uint32_t a = 0; a < d->n_anim_meshes; a++) {
         AnimMeshPlan P;
         P.am = d->anim_meshes[a];
@@ -417,6 +425,7 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
             if (!plan_gather(A, P.wide, wsrc.data() + 4ull * wb, we - wb, wb, err)) return fail(err);
         }
         tmp = std::max<size_t>(tmp, P.am.vertex_count);
+        etmp = std::max<size_t>(etmp, P.n_entries);
         A->meshes.push_back(std::move(P));
     }
     if (d->n_nodes > 0 && d->scene_start_node >= 0 && d->n_scene_bvh_nodes > 0) {
@@ -428,7 +437,8 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
             if (!plan_gather(A, A->scene_wide, ssrc.data(), (uint32_t)sw.size(), 0, err)) return fail(err);
         }
     }
-    if (!anim_alloc(A, &A->d_P, tmp) || !anim_alloc(A, &A->d_N, tmp)) return fail("animation buffers allocation failed");
+    if (!anim_alloc(A, &A->d_P, tmp) || !anim_alloc(A, &A->d_N, tmp) || !anim_alloc(A, &A->d_ebox, 2 * etmp))
+        return fail("animation buffers allocation failed");
     A->tmp_cap = tmp;
     return CTL_OK;
 }
@@ -467,14 +477,15 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
     DevScene& S = c->scene;
     const uint32_t nv = P.am.vertex_count, nt = P.am.tri_count, ne = P.n_entries;
     const uint32_t* tris = A->d_tris + 3ull * P.am.tri_first;
-    if (nv) hipLaunchKernelGGL(anim_skin_kernel, dim3((nv + kAB - 1) / kAB), dim3(kAB), 2 * nb * sizeof(float), s,
+    if (nv) hipLaunchKernelGGL(anim_skin_kernel, dim3((nv + kAB - 1) / kAB), dim3(kAB), 34 * n_bones * sizeof(float), s,
                                A->d_verts + P.am.vertex_first, nv, A->d_bones[0], A->d_bones[1], n_bones, lerp, A->d_P,
                                A->d_N);
     if (nt) hipLaunchKernelGGL(anim_tri_kernel, dim3((nt + kAB - 1) / kAB), dim3(kAB), 0, s, tris, nt, A->d_P, A->d_N,
                                const_cast<ctl_triangle_data*>(S.tri_data) + P.km.triangle_offset);
     const uint32_t* idx = S.tri_idx + P.km.bvh_indices_offset;
-    (void)ne;   // the Woop data is rewritten by the leaf boxes of the refit
-    LeafCtx L{idx, tris, A->d_P, const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset, nullptr};
+    if (ne) hipLaunchKernelGGL(anim_entry_kernel, dim3((ne + kAB - 1) / kAB), dim3(kAB), 0, s, idx, ne, tris, A->d_P,
+                               const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset, A->d_ebox);
+    LeafCtx L{idx, A->d_ebox, nullptr};
     float* bin = reinterpret_cast<float*>(const_cast<float4*>(S.bvh) + P.bin.base);
     launch_refit<false>(s, P.bin, bin, L);
     launch_gather(s, P.wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.wbvh)), bin);
@@ -483,7 +494,7 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
     if (A->n_nodes) {
         hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf,
                            A->n_nodes, A->d_mesh_boxes, A->d_inst_boxes);
-        LeafCtx LS{nullptr, nullptr, nullptr, nullptr, A->d_inst_boxes};
+        LeafCtx LS{nullptr, nullptr, A->d_inst_boxes};
         float* sbin = reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh));
         if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
         launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);
