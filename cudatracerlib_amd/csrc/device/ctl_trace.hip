@@ -51,7 +51,7 @@ static_assert(sizeof(ctl_pixel_variance) == 44, "PixelVarianceInfo is 44 B");
 #define CTL_PERSIST_WAVES_FULL 3   // ... with the C5 shading (out-of-line texture / microfacet calls)
 #endif
 #ifndef CTL_PERSIST_WAVES
-#define CTL_PERSIST_WAVES 6   // waves/SIMD for the persistent path kernel: measured best on C3
+#define CTL_PERSIST_WAVES 5   // waves/SIMD for the persistent path kernel: measured best on C3 (5: 1550, 6: 1522, 4: 1540 Mrays/s)
                               // (4: 732, 5: 758, 6: 789, 7: 781, 8: 768 Mrays/s); its spills
                               // save path state around the traversal, outside the traversal loops
 #endif
