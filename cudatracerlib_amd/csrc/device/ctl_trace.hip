@@ -51,9 +51,8 @@ static_assert(sizeof(ctl_pixel_variance) == 44, "PixelVarianceInfo is 44 B");
 #define CTL_PERSIST_WAVES_FULL 3   // ... with the C5 shading (out-of-line texture / microfacet calls)
 #endif
 #ifndef CTL_PERSIST_WAVES
-#define CTL_PERSIST_WAVES 5   // waves/SIMD for the persistent path kernel: measured best on C3 (5: 1550, 6: 1522, 4: 1540 Mrays/s)
-                              // (4: 732, 5: 758, 6: 789, 7: 781, 8: 768 Mrays/s); its spills
-                              // save path state around the traversal, outside the traversal loops
+#define CTL_PERSIST_WAVES 4   // waves/SIMD for the persistent path kernel, measured on C3 with the packed
+                              // wide-node step: 2: 1576, 3: 1590, 4: 1666, 5: 1601, 6: 1505 Mrays/s
 #endif
 
 namespace {
@@ -398,12 +397,16 @@ static void free_scene(ctl_ctx* c) {
 }
 
 template <class T>
-static ctl_status upload(ctl_ctx* c, const T* src, size_t count, const T** dst) {
+static ctl_status upload(ctl_ctx* c, const T* src, size_t count, const T** dst, size_t pad = 0) {
     size_t bytes = count * sizeof(T);
     void* p = nullptr;
-    hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+    hipError_t e = hipMalloc(&p, bytes + pad * sizeof(T) ? bytes + pad * sizeof(T) : 16);
     if (e != hipSuccess) { c->err = std::string("hipMalloc: ") + hipGetErrorString(e); return CTL_ERR_NOMEM; }
     c->scene_allocs.push_back(p);
+    if (pad) {
+        e = hipMemset(static_cast<char*>(p) + bytes, 0, pad * sizeof(T));
+        if (e != hipSuccess) { c->err = std::string("hipMemset: ") + hipGetErrorString(e); return CTL_ERR_HIP; }
+    }
     if (bytes) {
         e = hipMemcpy(p, src, bytes, hipMemcpyHostToDevice);
         if (e != hipSuccess) { c->err = std::string("hipMemcpy: ") + hipGetErrorString(e); return CTL_ERR_HIP; }
@@ -546,11 +549,12 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     free_scene(c);
     DevScene S{};
     ctl_status r;
-#define UP(src, cnt, dst)                                         \
-    if ((r = upload(c, src, cnt, dst)) != CTL_OK) { free_scene(c); return r; }
+#define UP(src, cnt, dst, ...)                                    \
+    if ((r = upload(c, src, cnt, dst, ##__VA_ARGS__)) != CTL_OK) { free_scene(c); return r; }
     const ctl_bvh_node* bvh; UP(d->bvh_nodes, d->n_bvh_nodes, &bvh);
-    const ctl_woop_tri* woop; UP(d->woop_tris, d->n_woop_tris, &woop);
-    UP(d->tri_indices, d->n_tri_indices, &S.tri_idx);
+    // one zeroed entry past the end: the leaf loop loads entry i+1 while it tests entry i
+    const ctl_woop_tri* woop; UP(d->woop_tris, d->n_woop_tris, &woop, 1);
+    UP(d->tri_indices, d->n_tri_indices, &S.tri_idx, 1);
     UP(d->tri_data, d->n_tri_data, &S.tri_data);
     UP(d->materials, d->n_materials, &S.mats);
     UP(d->meshes, d->n_meshes, &S.meshes);

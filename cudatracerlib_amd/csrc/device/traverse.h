@@ -226,13 +226,20 @@ struct Traverser {
         return material_alpha_test(m, TexView{S.textures, S.tex_data}, uv);
     }
 
+    // Leaf entries from ~leafAddr until the last-in-leaf flag.  Entry i+1 is
+    // loaded while entry i is tested (the uploads carry one zeroed entry past
+    // the end), so a leaf costs one dependent load latency, not one per entry.
     __device__ __forceinline__ void leaf_tris(const DevScene& S, TraceStats* stats) {
-        for (int triAddr = ~leafAddr;; triAddr++) {
-            const float4* tv = S.woop + triBase + (uint32_t)triAddr * 3u;
-            const float4 v00 = tv[0];
-            const float4 v11 = tv[1];
-            const float4 v22 = tv[2];
-            const uint32_t index = S.tri_idx[idxBase + (uint32_t)triAddr];
+        uint32_t triAddr = (uint32_t)(~leafAddr);
+        const float4* tv = S.woop + triBase + triAddr * 3u;
+        const uint32_t* ti = S.tri_idx + idxBase + triAddr;
+        float4 v00 = tv[0], v11 = tv[1], v22 = tv[2];
+        uint32_t index = ti[0];
+        for (;;) {
+            tv += 3;
+            ti += 1;
+            const float4 n00 = tv[0], n11 = tv[1], n22 = tv[2];
+            const uint32_t nindex = ti[0];
             if (STATS) stats->tris++;
             float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
             float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
@@ -261,20 +268,119 @@ struct Traverser {
                 }
             }
             if (index & 1) break;
+            v00 = n00; v11 = n11; v22 = n22; index = nindex;
         }
     }
 
-    // 4-wide inner-node loop: the four child slabs of a 128-B node, hit
-    // children ordered near-first by a 5-comparator sorting network on their
-    // entry distance (non-negative floats compare as ints), the nearest taken,
-    // the others pushed far-to-near.  Same postponed-leaf / wave-exit rule.
-    __device__ __forceinline__ void inner_wide(const DevScene& S, LaneStack& st, TraceStats* stats) {
+    // 4-wide inner-node loop over 128-B float nodes (host/bvh_wide.h).
+    //  * slabs in packed fp32 (v_pk_mul_f32 / v_pk_add_f32 on child pairs, the
+    //    same mul-then-sub rounding as the reference's scalar code);
+    //  * per-axis min/max as v_min/v_max_f32.  These differ from the
+    //    reference's `a < b ? a : b` only on a {-0, +0} pair (and NaN); under
+    //    the int-ordered span that can only add visits to boxes that end behind
+    //    the ray origin, which hold no hit with t > eps, so hits are unchanged;
+    //  * empty child slots carry NaN boxes: their span compare is false, so no
+    //    sentinel test per child;
+    //  * hit children sorted near-first by a 5-comparator network on the entry
+    //    distances (non-negative floats compare as ints), the nearest taken,
+    //    the others pushed far-to-near;
+    //  * stack: with room for three pushes in LDS, the two top entries are read
+    //    before the node arrives and the pushes are three unconditional
+    //    ds_writes (slots above the new top hold garbage), so a step carries no
+    //    stack branches and no dependent LDS read; deep stacks take the
+    //    generic push/pop.
+    // Same postponed-leaf / wave-exit rule as the binary loop.
+    __device__ __forceinline__ void inner_wide_float(const DevScene& S, LaneStack& st, TraceStats* stats) {
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f* nodes = reinterpret_cast<const v4f*>((SINGLE || level) ? S.wbvh : S.scene_wbvh);
+        const v2f ix = {cur.idx, cur.idx}, iy = {cur.idy, cur.idy}, iz = {cur.idz, cur.idz};
+        const v2f ox = {cur.oodx, cur.oodx}, oy = {cur.oody, cur.oody}, oz = {cur.oodz, cur.oodz};
+        const int tminBits = __float_as_int(span_tmin);
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
+            const int sp = st.sp;
+            const bool fast = sp + 3 <= kLdsStack;
+            const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
+            const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
+            const v4f* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 8u;
+            const v4f lox = n[0], hix = n[1], loy = n[2], hiy = n[3], loz = n[4], hiz = n[5];
+            int4 ch = reinterpret_cast<const int4*>(n)[6];
+            asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
+            if (STATS) stats->nodes++;
+            const v2f ax01 = lox.xy * ix - ox, ax23 = lox.zw * ix - ox;
+            const v2f bx01 = hix.xy * ix - ox, bx23 = hix.zw * ix - ox;
+            const v2f ay01 = loy.xy * iy - oy, ay23 = loy.zw * iy - oy;
+            const v2f by01 = hiy.xy * iy - oy, by23 = hiy.zw * iy - oy;
+            const v2f az01 = loz.xy * iz - oz, az23 = loz.zw * iz - oz;
+            const v2f bz01 = hiz.xy * iz - oz, bz23 = hiz.zw * iz - oz;
+            const int tBits = __float_as_int(h.t);
+            int k0, k1, k2, k3, c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+#define CTL_WIDE_CHILD(K, AX, BX, AY, BY, AZ, BZ)                                                        \
+            {                                                                                            \
+                const int zlo = min(__float_as_int(AZ), __float_as_int(BZ));                             \
+                const int zhi = max(__float_as_int(AZ), __float_as_int(BZ));                             \
+                const float cmin = __int_as_float(imax3(__float_as_int(fminf(AX, BX)),                    \
+                                                        __float_as_int(fminf(AY, BY)), max(zlo, tminBits))); \
+                const float cmax = __int_as_float(imin3(__float_as_int(fmaxf(AX, BX)),                    \
+                                                        __float_as_int(fmaxf(AY, BY)), min(zhi, tBits)));  \
+                K = (cmax >= cmin) ? __float_as_int(cmin) : 0x7fffffff;                                  \
+            }
+            CTL_WIDE_CHILD(k0, ax01.x, bx01.x, ay01.x, by01.x, az01.x, bz01.x)
+            CTL_WIDE_CHILD(k1, ax01.y, bx01.y, ay01.y, by01.y, az01.y, bz01.y)
+            CTL_WIDE_CHILD(k2, ax23.x, bx23.x, ay23.x, by23.x, az23.x, bz23.x)
+            CTL_WIDE_CHILD(k3, ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y)
+#undef CTL_WIDE_CHILD
+#define CTL_CX(KA, CA, KB, CB)                      \
+            {                                       \
+                const bool sw = KB < KA;            \
+                const int tk = sw ? KB : KA, tc = sw ? CB : CA; \
+                KB = sw ? KA : KB; CB = sw ? CA : CB; \
+                KA = tk; CA = tc;                   \
+            }
+            CTL_CX(k0, c0, k1, c1)
+            CTL_CX(k2, c2, k3, c3)
+            CTL_CX(k0, c0, k2, c2)
+            CTL_CX(k1, c1, k3, c3)
+            CTL_CX(k1, c1, k2, c2)
+#undef CTL_CX
+            if (fast) {
+                const int m = (k0 != 0x7fffffff) + (k1 != 0x7fffffff) + (k2 != 0x7fffffff) + (k3 != 0x7fffffff);
+                // far-to-near pushes c[m-1] .. c[1] land in slots sp .. sp+m-2
+                int* slot = &ctl_lds_stack[sp * kStackBlock + st.tid];
+                slot[0] = m == 4 ? c3 : (m == 3 ? c2 : c1);
+                slot[kStackBlock] = m == 4 ? c2 : c1;
+                slot[2 * kStackBlock] = c1;
+                int next, below, nsp;
+                if (m == 0) { next = top1; below = top2; nsp = sp - 1; }
+                else { next = c0; below = m == 1 ? top1 : c1; nsp = sp + m - 1; }
+                if (next < 0 && leafAddr >= 0) {
+                    leafAddr = next;
+                    next = below;
+                    nsp--;
+                }
+                nodeAddr = next;
+                st.sp = nsp;
+            } else {
+                if (k3 != 0x7fffffff) st.push(c3);
+                if (k2 != 0x7fffffff) st.push(c2);
+                if (k1 != 0x7fffffff) st.push(c1);
+                nodeAddr = (k0 != 0x7fffffff) ? c0 : st.pop();
+                if (nodeAddr < 0 && leafAddr >= 0) {
+                    leafAddr = nodeAddr;
+                    nodeAddr = st.pop();
+                }
+            }
+            if (!__any(leafAddr >= 0)) break;
+        }
+    }
+
+    // 4-wide loop over 64-B quantized nodes (ctl_qnode.h, CTL_SCENE_WIDE_QUANT).
+    __device__ __forceinline__ void inner_wide_quant(const DevScene& S, LaneStack& st, TraceStats* stats) {
         const float4* nodes = (SINGLE || level) ? S.wbvh : S.scene_wbvh;
-        const bool quant = S.quant != 0;
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
             float4 lox, hix, loy, hiy, loz, hiz;
             int4 ch;
-            if (quant) {
+            {
                 // 64-B node: decode p + q * s per bound (ctl_qnode.h), then the float slab test
                 const float4* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 4u;
                 const float4 a = n[0], b = n[1], c = n[2];
@@ -290,11 +396,6 @@ struct Traverser {
                 loz = CTL_QDEC4(wlz, a.z, b.y); hiz = CTL_QDEC4(whz, a.z, b.y);
 #undef CTL_QDEC4
 #undef CTL_QDEC
-            } else {
-                const float4* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 8u;
-                lox = n[0]; hix = n[1]; loy = n[2]; hiy = n[3]; loz = n[4]; hiz = n[5];
-                ch = reinterpret_cast<const int4*>(n)[6];
-                asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
             }
             if (STATS) stats->nodes++;
             int k0, k1, k2, k3, c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
@@ -389,7 +490,10 @@ struct Traverser {
     // One round: inner nodes until every active lane holds a postponed leaf,
     // then the postponed leaves (and the level transitions).
     __device__ __forceinline__ void round(const DevScene& S, LaneStack& st, TraceStats* stats) {
-        if (WIDE) inner_wide(S, st, stats);
+        if (WIDE) {
+            if (S.quant) inner_wide_quant(S, st, stats);
+            else inner_wide_float(S, st, stats);
+        }
         else inner_binary(S, st, stats);
         resumeLeaves = false;
         while (leafAddr < 0) {

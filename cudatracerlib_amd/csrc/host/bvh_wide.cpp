@@ -2,6 +2,7 @@
 #include "bvh_wide.h"
 
 #include <cstring>
+#include <limits>
 #include <stdexcept>
 
 namespace ctl {
@@ -65,7 +66,8 @@ struct Collapser {
         out.push_back(WideNode{});
         if (src) {
             src->resize(out.size() * 4 - 4 * base, 0xffffffffu);
-            for (int i = 0; i < nk; i++) (*src)[4 * (me - base) + i] = k[i].src;
+            for (int i = 0; i < nk; i++)
+                if (k[i].v != kSentinel) (*src)[4 * (me - base) + i] = k[i].src;
         }
         int32_t child[4];
         for (int i = 0; i < 4; i++) {
@@ -73,11 +75,14 @@ struct Collapser {
             child[i] = is_inner(k[i].v) ? emit(k[i].v, depth + 1) : k[i].v;
         }
         WideNode& w = out[me];
+        // empty slots and sentinel children (the right child of a single-leaf
+        // root): quiet-NaN boxes, which fail every slab test (traverse.h)
+        const float e = std::numeric_limits<float>::quiet_NaN();
         for (int i = 0; i < 4; i++) {
-            const bool used = i < nk;
-            w.lo_x[i] = used ? k[i].lo[0] : 0.0f; w.hi_x[i] = used ? k[i].hi[0] : 0.0f;
-            w.lo_y[i] = used ? k[i].lo[1] : 0.0f; w.hi_y[i] = used ? k[i].hi[1] : 0.0f;
-            w.lo_z[i] = used ? k[i].lo[2] : 0.0f; w.hi_z[i] = used ? k[i].hi[2] : 0.0f;
+            const bool used = i < nk && k[i].v != kSentinel;
+            w.lo_x[i] = used ? k[i].lo[0] : e; w.hi_x[i] = used ? k[i].hi[0] : e;
+            w.lo_y[i] = used ? k[i].lo[1] : e; w.hi_y[i] = used ? k[i].hi[1] : e;
+            w.lo_z[i] = used ? k[i].lo[2] : e; w.hi_z[i] = used ? k[i].hi[2] : e;
             w.child[i] = child[i];
             w.pad[i] = 0;
         }

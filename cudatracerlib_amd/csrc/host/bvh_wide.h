@@ -11,6 +11,8 @@
 //                                               0x76543210: empty slot / reference sentinel
 //   int4   pad
 //
+// Empty slots and sentinel children have quiet-NaN boxes (no ray enters them).
+//
 // A binary node becomes a wide node by repeatedly opening the inner child of
 // largest surface area until four children are reached (or only leaves are
 // left).  Leaves, leaf entries and Woop data are shared with the binary tree.
@@ -33,7 +35,7 @@ static_assert(sizeof(WideNode) == 128, "wide node is 128 B");
 // the wide nodes to `out`.  Returns the root's index relative to the first
 // node appended; child indices are relative to that first node as well.
 // src (optional): for every emitted node's 4 slots, the binary node index << 1 |
-// child slot the slot's box was taken from (0xFFFFFFFF for unused slots),
+// child slot the slot's box was taken from (0xFFFFFFFF for empty / sentinel slots),
 // indexed like the appended nodes — what a refit of the binary tree needs to
 // refresh the wide boxes with one gather.
 int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out,
