@@ -182,7 +182,7 @@ def main():
     t0 = time.perf_counter()
     hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
     if a.split_alpha is not None or a.bins or a.max_leaf:
-        hs.set_bvh_params(0.5 if a.split_alpha is None else a.split_alpha, a.split_depth, a.bins, a.max_leaf)
+        hs.set_bvh_params(a.split_alpha, a.split_depth, a.bins, a.max_leaf)
     desc = hs.compile(threads=threads)
     if a.bvh == "binary":
         desc.flags |= ctl.CTL_SCENE_BINARY_BVH

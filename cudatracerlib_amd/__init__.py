@@ -222,9 +222,12 @@ class HostScene:
     def set_flags(self, flags):
         _check(self._L.ctl_host_scene_set_flags(self._h, flags), None, "set_flags")
 
-    def set_bvh_params(self, split_alpha=0.5, split_depth=8, bins=0, max_leaf=0):
+    def set_bvh_params(self, split_alpha=None, split_depth=8, bins=0, max_leaf=0):
         """BVH build knobs: reference splitting of large triangles (split_alpha = 0
-        disables), SAH bins per axis and max leaf size (0 = library default)."""
+        disables, None = library default), SAH bins per axis and max leaf size
+        (0 = library default)."""
+        if split_alpha is None:
+            split_alpha = _abi.CTL_DEFAULT_SPLIT_ALPHA
         _check(self._L.ctl_host_scene_set_bvh_params(self._h, float(split_alpha), int(split_depth), int(bins),
                                                       int(max_leaf)), None, "set_bvh_params")
         return self

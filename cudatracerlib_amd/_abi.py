@@ -14,6 +14,7 @@ CTL_OK = 0
 CTL_SCENE_HALF_HOST_QUIRK = 1
 CTL_SCENE_BINARY_BVH = 2
 CTL_SCENE_WIDE_QUANT = 4
+CTL_DEFAULT_SPLIT_ALPHA = 0.1875   # include/ctl_trace.h
 CTL_XMSH_MATERIAL_RECORD_SIZE = 148
 CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS = range(6)
 CTL_BSDF_DIFFUSE = 1
