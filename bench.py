@@ -171,10 +171,14 @@ def main():
     import cudatracerlib_amd as ctl
     from cudatracerlib_amd import shard
 
-    if world > 1:
-        dist.init_process_group(a.backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        # bind the process group to this rank's GPU so RCCL never guesses the device
+        if a.backend == "nccl":
+            dist.init_process_group(a.backend, device_id=dev)
+        else:
+            dist.init_process_group(a.backend)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
     threads = max(1, int(os.environ.get("OMP_NUM_THREADS", "8")))

@@ -275,10 +275,13 @@ struct Traverser {
     // 4-wide inner-node loop over 128-B float nodes (host/bvh_wide.h).
     //  * slabs in packed fp32 (v_pk_mul_f32 / v_pk_add_f32 on child pairs, the
     //    same mul-then-sub rounding as the reference's scalar code);
-    //  * per-axis min/max as v_min/v_max_f32.  These differ from the
-    //    reference's `a < b ? a : b` only on a {-0, +0} pair (and NaN); under
-    //    the int-ordered span that can only add visits to boxes that end behind
-    //    the ray origin, which hold no hit with t > eps, so hits are unchanged;
+    //  * near/far planes picked per ray in the load address (sign of idir),
+    //    which replaces the reference's per-axis min/max of the slab pair
+    //    (C3: 1977 -> 2105 Mrays/s).  The pick equals `a < b ? a : b` except
+    //    on a {-0, +0} pair (and NaN); under the int-ordered span, clamped
+    //    below by tmin >= +0, that can only add visits to boxes that end behind
+    //    the ray origin, which hold no hit with t > eps, so hits are unchanged.
+    //    CTL_WIDE_MINMAX builds the previous min/max form for A/B runs;
     //  * empty child slots carry NaN boxes: their span compare is false, so no
     //    sentinel test per child;
     //  * hit children sorted near-first by a 5-comparator network on the entry
@@ -297,24 +300,70 @@ struct Traverser {
         const v2f ix = {cur.idx, cur.idx}, iy = {cur.idy, cur.idy}, iz = {cur.idz, cur.idz};
         const v2f ox = {cur.oodx, cur.oodx}, oy = {cur.oody, cur.oody}, oz = {cur.oodz, cur.oodz};
         const int tminBits = __float_as_int(span_tmin);
+#ifndef CTL_WIDE_MINMAX
+        // Near/far planes chosen per ray by the sign of its inverse direction:
+        // for idir >= 0, lo*idir - ood <= hi*idir - ood (rounding is monotone),
+        // so the near plane IS the reference's min of the pair and the far
+        // plane its max; the selection moves into the load address (byte
+        // offsets 0/16 inside each axis' 32-B lo/hi pair) and the per-child
+        // min/max disappear.  NaN (empty) slots still fail the span compare.
+        const char* nbytes = reinterpret_cast<const char*>(nodes);
+        const uint32_t sx = (uint32_t)(__float_as_int(cur.idx) >> 31) & 16u;
+        const uint32_t sy = (uint32_t)(__float_as_int(cur.idy) >> 31) & 16u;
+        const uint32_t sz = (uint32_t)(__float_as_int(cur.idz) >> 31) & 16u;
+        uint32_t onx = sx, ofx = 16u - sx, ony = 32u + sy, ofy = 48u - sy, onz = 64u + sz, ofz = 80u - sz;
+        // opaque to the optimiser: otherwise it splits off + (16 - s) into two ops per load
+        asm volatile("" : "+v"(onx), "+v"(ofx), "+v"(ony), "+v"(ofy), "+v"(onz), "+v"(ofz));
+#endif
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
             const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
+            if (STATS) stats->nodes++;
+            const int tBits = __float_as_int(h.t);
+            int k0, k1, k2, k3;
+#ifndef CTL_WIDE_MINMAX
+            const uint32_t off = (nodeBase + (uint32_t)nodeAddr) << 7;
+            const v4f nx = *reinterpret_cast<const v4f*>(nbytes + (off + onx));
+            const v4f fx = *reinterpret_cast<const v4f*>(nbytes + (off + ofx));
+            const v4f ny = *reinterpret_cast<const v4f*>(nbytes + (off + ony));
+            const v4f fy = *reinterpret_cast<const v4f*>(nbytes + (off + ofy));
+            const v4f nz = *reinterpret_cast<const v4f*>(nbytes + (off + onz));
+            const v4f fz = *reinterpret_cast<const v4f*>(nbytes + (off + ofz));
+            int4 ch = *reinterpret_cast<const int4*>(nbytes + (off + 96u));
+            asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
+            const v2f nx01 = nx.xy * ix - ox, nx23 = nx.zw * ix - ox;
+            const v2f fx01 = fx.xy * ix - ox, fx23 = fx.zw * ix - ox;
+            const v2f ny01 = ny.xy * iy - oy, ny23 = ny.zw * iy - oy;
+            const v2f fy01 = fy.xy * iy - oy, fy23 = fy.zw * iy - oy;
+            const v2f nz01 = nz.xy * iz - oz, nz23 = nz.zw * iz - oz;
+            const v2f fz01 = fz.xy * iz - oz, fz23 = fz.zw * iz - oz;
+            int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+#define CTL_WIDE_CHILD(K, NX, FX, NY, FY, NZ, FZ)                                                       \
+            {                                                                                           \
+                const float cmin = __int_as_float(imax3(__float_as_int(NX), __float_as_int(NY),          \
+                                                        max(__float_as_int(NZ), tminBits)));             \
+                const float cmax = __int_as_float(imin3(__float_as_int(FX), __float_as_int(FY),          \
+                                                        min(__float_as_int(FZ), tBits)));                \
+                K = (cmax >= cmin) ? __float_as_int(cmin) : 0x7fffffff;                                 \
+            }
+            CTL_WIDE_CHILD(k0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x)
+            CTL_WIDE_CHILD(k1, nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y)
+            CTL_WIDE_CHILD(k2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x)
+            CTL_WIDE_CHILD(k3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y)
+#else
             const v4f* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 8u;
             const v4f lox = n[0], hix = n[1], loy = n[2], hiy = n[3], loz = n[4], hiz = n[5];
             int4 ch = reinterpret_cast<const int4*>(n)[6];
             asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
-            if (STATS) stats->nodes++;
             const v2f ax01 = lox.xy * ix - ox, ax23 = lox.zw * ix - ox;
             const v2f bx01 = hix.xy * ix - ox, bx23 = hix.zw * ix - ox;
             const v2f ay01 = loy.xy * iy - oy, ay23 = loy.zw * iy - oy;
             const v2f by01 = hiy.xy * iy - oy, by23 = hiy.zw * iy - oy;
             const v2f az01 = loz.xy * iz - oz, az23 = loz.zw * iz - oz;
             const v2f bz01 = hiz.xy * iz - oz, bz23 = hiz.zw * iz - oz;
-            const int tBits = __float_as_int(h.t);
-            int k0, k1, k2, k3, c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+            int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
 #define CTL_WIDE_CHILD(K, AX, BX, AY, BY, AZ, BZ)                                                        \
             {                                                                                            \
                 const int zlo = min(__float_as_int(AZ), __float_as_int(BZ));                             \
@@ -329,6 +378,7 @@ struct Traverser {
             CTL_WIDE_CHILD(k1, ax01.y, bx01.y, ay01.y, by01.y, az01.y, bz01.y)
             CTL_WIDE_CHILD(k2, ax23.x, bx23.x, ay23.x, by23.x, az23.x, bz23.x)
             CTL_WIDE_CHILD(k3, ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y)
+#endif
 #undef CTL_WIDE_CHILD
 #define CTL_CX(KA, CA, KB, CB)                      \
             {                                       \
