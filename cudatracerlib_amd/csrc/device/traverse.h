@@ -39,6 +39,13 @@ namespace ctl {
 constexpr int kLdsStack = CTL_LDS_STACK;   // stack entries per lane held in LDS
 constexpr int kStackMax = 128;
 
+// The wide inner-node loop hands over to the leaves once fewer than this many
+// lanes of the wave still look for a leaf (1 = the reference's rule: none;
+// C3 sweep: 1 -> 2098, 2 -> 2164, 4 -> 2225, 6 -> 2237, 8 -> 2216, 16 -> 2146 Mrays/s).
+#ifndef CTL_LEAF_BREAK
+#define CTL_LEAF_BREAK 6
+#endif
+
 struct DevScene {
     const float4* bvh;          // mesh BVHNodeData, float4 units
     const float4* woop;         // TriIntersectorData, float4 units
@@ -420,7 +427,7 @@ struct Traverser {
                     nodeAddr = st.pop();
                 }
             }
-            if (!__any(leafAddr >= 0)) break;
+            if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
