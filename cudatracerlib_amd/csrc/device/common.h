@@ -178,9 +178,13 @@ __device__ __forceinline__ f2 primary_ray(const DevScene& S, SamplerDev& rng, ui
 // differentials, partials and the BSDF type switch.  Scenes with constant
 // diffuse materials only take the lean instantiation — the partials are only
 // observable through textures, so both give identical results there.
-template <bool FULL>
+// SINGLE: one-instance scene, so the hit's node is ~start_node for every
+// lane; indexing with that kernel-uniform value turns the node record and its
+// transform into scalar loads.
+template <bool FULL, bool SINGLE = false>
 __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P, SamplerDev& rng, PathVars& v,
                                           const HitRec& r, ShadowReq& sh) {
+    const uint32_t node = SINGLE ? ~(uint32_t)S.start_node : r.node;
     sh.valid = false;
     bsdf_rec b;
     b.wo = v.wo;
@@ -191,8 +195,8 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
     const ctl_triangle_data td = S.tri_data[r.tri];
     // Node fields read in place: a local copy of the struct would be indexed
     // dynamically (lights[]) and so live in scratch.
-    const ctl_node* N = S.nodes + r.node;
-    fill_dg(td, load_m44(S.xf + 4 * r.node), mk2(r.u, r.v), P.half_quirk, LutDecode{S.normal_lut}, dg);
+    const ctl_node* N = S.nodes + node;
+    fill_dg(td, load_m44(S.xf + 4 * node), mk2(r.u, r.v), P.half_quirk, LutDecode{S.normal_lut}, dg);
     b.wi = to_local(dg.sys, -v.rdir);
     const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N->material_offset];
     if (mat.two_sided && b.wi.z < 0) {

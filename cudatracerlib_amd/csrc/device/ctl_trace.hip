@@ -55,7 +55,20 @@ static_assert(sizeof(ctl_pixel_variance) == 44, "PixelVarianceInfo is 44 B");
                               // wide-node step: 2: 1576, 3: 1590, 4: 1666, 5: 1601, 6: 1505 Mrays/s
 #endif
 
+#ifndef CTL_TAIL
+#define CTL_TAIL 1   // persistent path kernel: suspend the trace once fewer lanes than this still traverse
+#endif
+
 namespace {
+
+constexpr int kTail = CTL_TAIL;
+
+// dynamic LDS of path_kernel_persistent: lane stacks + parked traversal state
+template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
+constexpr size_t persistent_lds_bytes() {
+    return kStackLdsBytes +
+           (kTail > 1 ? sizeof(int) * kStackBlock * Traverser<2, STATS, SINGLE, WIDE, FULL>::kSaveFields : 0);
+}
 
 // Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
 // traversals inline in the bounce, as the reference's pathKernel2 runs it.
@@ -82,7 +95,7 @@ struct PathCtx {
             return false;
         }
         ShadowReq sh;
-        const bool cont = shade_hit<FULL>(S, P, rng, v, r2, sh);
+        const bool cont = shade_hit<FULL, SINGLE>(S, P, rng, v, r2, sh);
         if (sh.valid) {
             const bool any = P.shadow_any_hit != 0;
             HitRec h;
@@ -214,7 +227,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
     sh.dist = 0.0f;
     TraceStats ts{0, 0, 0};
     uint32_t rays = 0;
-    bool active = false, exhausted = false, shadowPhase = false, ending = false, ok = true;
+    bool active = false, exhausted = false, shadowPhase = false, ending = false, ok = true, resumed = false;
+#ifdef CTL_PROFILE_TRACE
+    long long prof_trace = 0;
+    const long long prof_start = wall_clock64();
+#endif
     const bool shadowAny = P.shadow_any_hit != 0;
     const int lane = threadIdx.x & 63;
     while (true) {
@@ -252,16 +269,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             HitRec h;
             h.t = (shadowPhase && shadowAny) ? sh.dist - S.ray_eps : FLT_MAX;
             h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
-            const f3 d = shadowPhase ? sh.d : v.rdir;
-            rays++;
+            if (!resumed) rays++;
+#ifdef CTL_PROFILE_TRACE
+            const long long pc0 = wall_clock64();
+#endif
             if (S.n_nodes != 0) {
-                Traverser<2, STATS, SINGLE, WIDE, FULL> T;
-                T.anyhit = shadowPhase && shadowAny;
-                T.init(S, v.rori, d, 0.0f, S.ray_eps, h.t, st, &ts);
-                while (!T.done) T.round(S, st, &ts);
+                typedef Traverser<2, STATS, SINGLE, WIDE, FULL> Tr;
+                Tr T;
+                int* park = ctl_lds_stack + kLdsStack * kStackBlock;
+                if (kTail > 1 && resumed) {
+                    T.restore(S, park, st.tid, 0.0f, S.ray_eps);
+                } else {
+                    T.anyhit = shadowPhase && shadowAny;
+                    T.init(S, v.rori, shadowPhase ? sh.d : v.rdir, 0.0f, S.ray_eps, h.t, st, &ts);
+                }
+                if (kTail > 1) {
+                    // trace until fewer than kTail lanes of the wave are still
+                    // traversing; those park their state and resume next
+                    // iteration while the others shade and take new rays
+                    do {
+                        if (!T.done) T.round(S, st, &ts);
+                    } while (__popcll(__ballot(!T.done)) >= kTail);
+                    resumed = !T.done;
+                    if (resumed) T.save(park, st.tid);
+                } else {
+                    while (!T.done) T.round(S, st, &ts);
+                }
                 h = T.h;
                 ok &= !st.overflow;
             }
+#ifdef CTL_PROFILE_TRACE
+            prof_trace += wall_clock64() - pc0;
+#endif
+            if (resumed) continue;
             bool cont;
             if (shadowPhase) {
                 if (!shadow_occluded(S, shadowAny, h, sh.dist)) v.cl = v.cl + sh.add;
@@ -271,7 +311,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                 v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);   // no environment map
                 cont = false;
             } else {
-                ending = !shade_hit<FULL>(S, P, rng, v, h, sh);
+                ending = !shade_hit<FULL, SINGLE>(S, P, rng, v, h, sh);
                 shadowPhase = sh.valid;
                 cont = sh.valid || (!ending && v.depth++ < P.max_path_length);
             }
@@ -288,6 +328,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
         wave_add_u64(&counters[3], ts.tris);
         wave_add_u64(&counters[4], ts.inst);
     }
+#ifdef CTL_PROFILE_TRACE
+    // wall-clock ticks (100 MHz) per wave: in the trace call site / in the kernel
+    if (lane == 0) {
+        atomicAdd(&counters[5], (unsigned long long)prof_trace);
+        atomicAdd(&counters[6], (unsigned long long)(wall_clock64() - prof_start));
+    }
+#endif
 }
 
 // Batch closest/any hit (intersectKernel<ANY_HIT>, TraceHelper.cu:326-734):
@@ -826,9 +873,10 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
 #define PK(ST, SG, WD, FU)                                                                                       \
         do {                                                                                                     \
             static int nb = 0;                                                                                   \
-            if (!nb) nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD, FU>, kStackLdsBytes);            \
+            constexpr size_t lds = persistent_lds_bytes<ST, SG, WD, FU>();                                      \
+            if (!nb) nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD, FU>, lds);                        \
             hipLaunchKernelGGL((path_kernel_persistent<ST, SG, WD, FU>), dim3((unsigned)std::min<uint64_t>(nb, want)), \
-                               dim3(kBlock), kStackLdsBytes, s, c->scene, P, s1, s2, fb, threads, cursor,        \
+                               dim3(kBlock), lds, s, c->scene, P, s1, s2, fb, threads, cursor,                   \
                                c->d_counters);                                                                   \
         } while (0)
 #define PK2(ST, SG, WD) do { if (full) PK(ST, SG, WD, true); else PK(ST, SG, WD, false); } while (0)
@@ -852,7 +900,18 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
 }
 
 CTL_API ctl_status ctl_render_pass(ctl_ctx* c, const ctl_pt_params* params, ctl_pixel* d_fb, void* stream) {
+#ifdef CTL_PROFILE_TRACE
+    ctl_status r = launch_pass(c, params, d_fb, false, stream);
+    unsigned long long v[2];
+    if (hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)) == hipSuccess &&
+        hipMemcpy(v, c->d_counters + 5, sizeof(v), hipMemcpyDeviceToHost) == hipSuccess) {
+        fprintf(stderr, "[profile] trace/total wave time %.4f (%llu / %llu)\n", (double)v[0] / (double)v[1], v[0], v[1]);
+        (void)hipMemset(c->d_counters + 5, 0, sizeof(v));
+    }
+    return r;
+#else
     return launch_pass(c, params, d_fb, false, stream);
+#endif
 }
 
 CTL_API ctl_status ctl_last_pass_ms(ctl_ctx* c, float* ms) {

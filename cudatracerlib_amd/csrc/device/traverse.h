@@ -220,6 +220,54 @@ struct Traverser {
         }
     }
 
+    // Suspended traversal state, parked in LDS ([field][thread] after the
+    // lane stacks, see path_kernel_persistent) while the rest of the wave
+    // shades; the lane's stack entries stay where they are.  Bit-exact resume:
+    // every field that round() reads is stored as is.
+    static constexpr int kSaveFields = SINGLE ? 20 : 39;
+    __device__ __forceinline__ void save(int* area, int tid) const {
+        int f = 0;
+        auto put = [&](int v) { area[(f++) * kStackBlock + tid] = v; };
+        auto putf = [&](float v) { put(__float_as_int(v)); };
+        putf(cur.ox); putf(cur.oy); putf(cur.oz); putf(cur.dx); putf(cur.dy); putf(cur.dz);
+        putf(cur.idx); putf(cur.idy); putf(cur.idz); putf(cur.oodx); putf(cur.oody); putf(cur.oodz);
+        putf(h.t); putf(h.u); putf(h.v); put((int)h.tri); put((int)h.node);
+        put(nodeAddr); put(leafAddr);
+        put((resumeLeaves ? 1 : 0) | (anyhit ? 2 : 0));
+        if (!SINGLE) {
+            putf(world.ox); putf(world.oy); putf(world.oz); putf(world.dx); putf(world.dy); putf(world.dz);
+            putf(world.idx); putf(world.idy); putf(world.idz); putf(world.oodx); putf(world.oody); putf(world.oodz);
+            put(level); put(meshSent); put((int)nodeBase); put((int)triBase); put((int)idxBase);
+            put((int)triOffset); put((int)instIdx);
+        }
+    }
+    // span_tmin / tri_tmin are the caller's (they do not change during a trace)
+    __device__ __forceinline__ void restore(const DevScene& S, const int* area, int tid, float smin, float tmn) {
+        int f = 0;
+        auto get = [&]() { return area[(f++) * kStackBlock + tid]; };
+        auto getf = [&]() { return __int_as_float(get()); };
+        cur.ox = getf(); cur.oy = getf(); cur.oz = getf(); cur.dx = getf(); cur.dy = getf(); cur.dz = getf();
+        cur.idx = getf(); cur.idy = getf(); cur.idz = getf(); cur.oodx = getf(); cur.oody = getf(); cur.oodz = getf();
+        h.t = getf(); h.u = getf(); h.v = getf(); h.tri = (uint32_t)get(); h.node = (uint32_t)get();
+        nodeAddr = get(); leafAddr = get();
+        const int fl = get();
+        resumeLeaves = (fl & 1) != 0;
+        anyhit = (fl & 2) != 0;
+        done = false;
+        span_tmin = smin; tri_tmin = tmn;
+        if (SINGLE) {
+            level = 1; meshSent = 0;
+            nodeBase = WIDE ? S.s_wnode_base : S.s_node_base;
+            triBase = S.s_tri_base; idxBase = S.s_idx_base; triOffset = S.s_tri_offset;
+            instIdx = ~(uint32_t)S.start_node;
+        } else {
+            world.ox = getf(); world.oy = getf(); world.oz = getf(); world.dx = getf(); world.dy = getf(); world.dz = getf();
+            world.idx = getf(); world.idy = getf(); world.idz = getf(); world.oodx = getf(); world.oody = getf(); world.oodz = getf();
+            level = get(); meshSent = get(); nodeBase = (uint32_t)get(); triBase = (uint32_t)get();
+            idxBase = (uint32_t)get(); triOffset = (uint32_t)get(); instIdx = (uint32_t)get();
+        }
+    }
+
     // TriangleData UV set 0 at (u, v) -> Material::AlphaTest (TraceHelper.cu:140-152)
     __device__ __forceinline__ bool alpha_survives(const DevScene& S, uint32_t gtri, float u, float v) const {
         const ctl_triangle_data td = S.tri_data[gtri];
