@@ -25,6 +25,7 @@
 #include "../host/bvh_wide.h"
 #include "../ctl_qnode.h"
 #include "common.h"
+#include "balance.h"
 
 namespace ctl {
 void sampler_tables(uint64_t pass, uint32_t nseq, uint32_t len, float* seq1d, float* seq2d);
@@ -62,12 +63,16 @@ static_assert(sizeof(ctl_pixel_variance) == 44, "PixelVarianceInfo is 44 B");
 namespace {
 
 constexpr int kTail = CTL_TAIL;
+#ifndef CTL_BALANCE
+#define CTL_BALANCE 0   // persistent path kernel: idle lanes take subtrees of busy lanes' rays (balance.h; measured slower, see DESIGN)
+#endif
 
 // dynamic LDS of path_kernel_persistent: lane stacks + parked traversal state
 template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
 constexpr size_t persistent_lds_bytes() {
     return kStackLdsBytes +
-           (kTail > 1 ? sizeof(int) * kStackBlock * Traverser<2, STATS, SINGLE, WIDE, FULL>::kSaveFields : 0);
+           (kTail > 1 ? sizeof(int) * kStackBlock * Traverser<2, STATS, SINGLE, WIDE, FULL>::kSaveFields
+                      : (SINGLE && WIDE && !STATS && CTL_BALANCE ? kBalLdsBytes : 0));
 }
 
 // Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
@@ -265,42 +270,63 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             if (__all(exhausted)) break;
             continue;
         }
+        // one-instance scenes with the 4-wide tree: the wave balances its
+        // traversals (balance.h); every lane takes part, with or without a ray
+        constexpr bool kBalance = SINGLE && WIDE && !STATS && CTL_BALANCE && kTail <= 1;
+        HitRec h;
         if (active) {
-            HitRec h;
             h.t = (shadowPhase && shadowAny) ? sh.dist - S.ray_eps : FLT_MAX;
             h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
             if (!resumed) rays++;
-#ifdef CTL_PROFILE_TRACE
-            const long long pc0 = wall_clock64();
-#endif
+        }
+        if (kBalance) {
             if (S.n_nodes != 0) {
-                typedef Traverser<2, STATS, SINGLE, WIDE, FULL> Tr;
-                Tr T;
-                int* park = ctl_lds_stack + kLdsStack * kStackBlock;
-                if (kTail > 1 && resumed) {
-                    T.restore(S, park, st.tid, 0.0f, S.ray_eps);
-                } else {
-                    T.anyhit = shadowPhase && shadowAny;
-                    T.init(S, v.rori, shadowPhase ? sh.d : v.rdir, 0.0f, S.ray_eps, h.t, st, &ts);
-                }
-                if (kTail > 1) {
-                    // trace until fewer than kTail lanes of the wave are still
-                    // traversing; those park their state and resume next
-                    // iteration while the others shade and take new rays
-                    do {
-                        if (!T.done) T.round(S, st, &ts);
-                    } while (__popcll(__ballot(!T.done)) >= kTail);
-                    resumed = !T.done;
-                    if (resumed) T.save(park, st.tid);
-                } else {
-                    while (!T.done) T.round(S, st, &ts);
-                }
-                h = T.h;
-                ok &= !st.overflow;
-            }
 #ifdef CTL_PROFILE_TRACE
-            prof_trace += wall_clock64() - pc0;
+                const long long pc0 = wall_clock64();
 #endif
+                const HitRec hb = trace_balanced<STATS, FULL>(S, st, &ts, active, v.rori, shadowPhase ? sh.d : v.rdir,
+                                                              h.t, shadowPhase && shadowAny);
+                if (active) h = hb;
+                ok &= !st.overflow;
+#ifdef CTL_PROFILE_TRACE
+                prof_trace += wall_clock64() - pc0;
+#endif
+            }
+        }
+        if (active) {
+            if (!kBalance) {
+#ifdef CTL_PROFILE_TRACE
+                const long long pc0 = wall_clock64();
+#endif
+                if (S.n_nodes != 0) {
+                    typedef Traverser<2, STATS, SINGLE, WIDE, FULL> Tr;
+                    Tr T;
+                    int* park = ctl_lds_stack + kLdsStack * kStackBlock;
+                    if (kTail > 1 && resumed) {
+                        T.restore(S, park, st.tid, 0.0f, S.ray_eps);
+                    } else {
+                        T.anyhit = shadowPhase && shadowAny;
+                        T.init(S, v.rori, shadowPhase ? sh.d : v.rdir, 0.0f, S.ray_eps, h.t, st, &ts);
+                    }
+                    if (kTail > 1) {
+                        // trace until fewer than kTail lanes of the wave are still
+                        // traversing; those park their state and resume next
+                        // iteration while the others shade and take new rays
+                        do {
+                            if (!T.done) T.round(S, st, &ts);
+                        } while (__popcll(__ballot(!T.done)) >= kTail);
+                        resumed = !T.done;
+                        if (resumed) T.save(park, st.tid);
+                    } else {
+                        while (!T.done) T.round(S, st, &ts);
+                    }
+                    h = T.h;
+                    ok &= !st.overflow;
+                }
+#ifdef CTL_PROFILE_TRACE
+                prof_trace += wall_clock64() - pc0;
+#endif
+            }
             if (resumed) continue;
             bool cont;
             if (shadowPhase) {
@@ -334,6 +360,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
         atomicAdd(&counters[5], (unsigned long long)prof_trace);
         atomicAdd(&counters[6], (unsigned long long)(wall_clock64() - prof_start));
     }
+    wave_add_u64(&counters[8], ts.inner_lanes);
+    wave_add_u64(&counters[9], ts.inner_waves);
+    wave_add_u64(&counters[10], ts.leaf_lanes);
+    wave_add_u64(&counters[11], ts.leaf_waves);
+    wave_add_u64(&counters[12], ts.inner_r);
+    wave_add_u64(&counters[13], ts.rounds);
+    wave_add_u64(&counters[14], ts.leafphase_in);
 #endif
 }
 
@@ -489,8 +522,8 @@ CTL_API ctl_ctx* ctl_create(int32_t device) {
     ctl_ctx* c = new ctl_ctx();
     c->device = device;
     c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    if (hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->d_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc(&c->d_counters, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_counters, 0, 16 * sizeof(unsigned long long)) != hipSuccess) {
         delete c;
         return fail("ctl_create: counter allocation failed");
     }
@@ -902,10 +935,15 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
 CTL_API ctl_status ctl_render_pass(ctl_ctx* c, const ctl_pt_params* params, ctl_pixel* d_fb, void* stream) {
 #ifdef CTL_PROFILE_TRACE
     ctl_status r = launch_pass(c, params, d_fb, false, stream);
-    unsigned long long v[2];
+    unsigned long long v[10];
     if (hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)) == hipSuccess &&
         hipMemcpy(v, c->d_counters + 5, sizeof(v), hipMemcpyDeviceToHost) == hipSuccess) {
-        fprintf(stderr, "[profile] trace/total wave time %.4f (%llu / %llu)\n", (double)v[0] / (double)v[1], v[0], v[1]);
+        fprintf(stderr, "[profile] trace/total wave time %.4f (%llu / %llu); inner loop: %llu wave iterations, "
+                        "%.1f lanes each; leaf entries: %llu wave iterations, %.1f lanes each\n",
+                (double)v[0] / (double)v[1], v[0], v[1], v[4], (double)v[3] / (double)v[4], v[6],
+                (double)v[5] / (double)v[6]);
+        fprintf(stderr, "[profile] lanes in the round per inner iteration %.1f; rounds %llu, lanes holding a leaf at the "
+                        "leaf phase %.1f\n", (double)v[7] / (double)v[4], v[8], (double)v[9] / (double)v[8]);
         (void)hipMemset(c->d_counters + 5, 0, sizeof(v));
     }
     return r;

@@ -85,7 +85,27 @@ struct DevScene {
     uint32_t quant;              // wide trees in the 64-B quantized format (ctl_qnode.h)
 };
 
-struct TraceStats { uint32_t nodes, tris, inst; };
+struct TraceStats {
+    uint32_t nodes, tris, inst;
+#ifdef CTL_PROFILE_TRACE
+    // SIMD occupancy of the traversal loops: per lane, iterations it was active
+    // in; per wave (counted on the first active lane), iterations executed
+    uint32_t inner_lanes = 0, inner_waves = 0, leaf_lanes = 0, leaf_waves = 0;
+    uint32_t round_r = 0, inner_r = 0, rounds = 0, leafphase_in = 0;
+#endif
+};
+#ifdef CTL_PROFILE_TRACE
+#define CTL_PROF_COUNT(stats, L, W)                                                    \
+    do {                                                                              \
+        (stats)->L++;                                                                 \
+        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) {          \
+            (stats)->W++;                                                             \
+            if (&(stats)->W == &(stats)->inner_waves) (stats)->inner_r += (stats)->round_r; \
+        }                                                                             \
+    } while (0)
+#else
+#define CTL_PROF_COUNT(stats, L, W) do {} while (0)
+#endif
 
 struct HitRec {
     float t, u, v;
@@ -295,6 +315,7 @@ struct Traverser {
             ti += 1;
             const float4 n00 = tv[0], n11 = tv[1], n22 = tv[2];
             const uint32_t nindex = ti[0];
+            CTL_PROF_COUNT(stats, leaf_lanes, leaf_waves);
             if (STATS) stats->tris++;
             float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
             float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
@@ -375,6 +396,7 @@ struct Traverser {
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
             const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
+            CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
             if (STATS) stats->nodes++;
             const int tBits = __float_as_int(h.t);
             int k0, k1, k2, k3;
@@ -595,12 +617,22 @@ struct Traverser {
     // One round: inner nodes until every active lane holds a postponed leaf,
     // then the postponed leaves (and the level transitions).
     __device__ __forceinline__ void round(const DevScene& S, LaneStack& st, TraceStats* stats) {
+#ifdef CTL_PROFILE_TRACE
+        stats->round_r = (uint32_t)__popcll(__ballot(1));
+        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) stats->rounds++;
+#endif
         if (WIDE) {
             if (S.quant) inner_wide_quant(S, st, stats);
             else inner_wide_float(S, st, stats);
         }
         else inner_binary(S, st, stats);
         resumeLeaves = false;
+#ifdef CTL_PROFILE_TRACE
+        {
+            const uint32_t nl = (uint32_t)__popcll(__ballot(leafAddr < 0));
+            if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) stats->leafphase_in += nl;
+        }
+#endif
         while (leafAddr < 0) {
             if (SINGLE || level == 1) {
                 if (leafAddr != -214783648) {
