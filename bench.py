@@ -171,6 +171,10 @@ def main():
     import cudatracerlib_amd as ctl
     from cudatracerlib_amd import shard
 
+    # one GPU per rank; ranks beyond the visible GPUs wrap around (a gloo
+    # rehearsal of the N-rank path on a one-GPU box)
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

@@ -161,6 +161,7 @@ __device__ __forceinline__ HitRec trace_balanced(const DevScene& S, LaneStack& s
                     T.nodeBase = S.s_wnode_base; T.triBase = S.s_tri_base; T.idxBase = S.s_idx_base;
                     T.triOffset = S.s_tri_offset; T.instIdx = inst;
                     T.resumeLeaves = false;
+                    T.leaf2 = 0;
                     T.done = false;
                     st.sp = 0;
                     st.push(CTL_SENTINEL);

@@ -42,8 +42,17 @@ constexpr int kStackMax = 128;
 // The wide inner-node loop hands over to the leaves once fewer than this many
 // lanes of the wave still look for a leaf (1 = the reference's rule: none;
 // C3 sweep: 1 -> 2098, 2 -> 2164, 4 -> 2225, 6 -> 2237, 8 -> 2216, 16 -> 2146 Mrays/s).
+// One-instance wide traversal: a lane that already postpones a leaf may park
+// a second one and keep visiting inner nodes (1), instead of leaving the
+// inner-node loop at its second leaf (0).  C3: 1 -> 2184, 0 -> 2202 Mrays/s.
+#ifndef CTL_LEAF2
+#define CTL_LEAF2 0
+#endif
 #ifndef CTL_LEAF_BREAK
 #define CTL_LEAF_BREAK 6
+#endif
+#ifndef CTL_LEAF_BREAK_ON_SECOND
+#define CTL_LEAF_BREAK_ON_SECOND 0   // count lanes with a free second leaf slot instead
 #endif
 
 struct DevScene {
@@ -195,11 +204,13 @@ __device__ __forceinline__ void xform_rows(const float4* M, f3 p, f3 d, f3& po, 
 // has alpha maps; the batch intersectKernel never alpha-tests.
 template <int ANY, bool STATS, bool SINGLE, bool WIDE = false, bool ALPHA = false>
 struct Traverser {
+    static constexpr bool kLeaf2 = CTL_LEAF2 && SINGLE && WIDE;
     RayLocal cur;
     RayLocal world;   // unused when SINGLE
     HitRec h;
     float span_tmin, tri_tmin;
     int nodeAddr, leafAddr, level, meshSent;
+    int leaf2;   // second postponed leaf (CTL_LEAF2, one-instance wide traversal), 0 = none
     uint32_t nodeBase, triBase, idxBase, triOffset, instIdx;
     bool done, resumeLeaves;
     bool anyhit;   // ANY == 2 only
@@ -221,6 +232,7 @@ struct Traverser {
         done = (S.n_nodes == 0);
         resumeLeaves = false;
         meshSent = 0;
+        leaf2 = 0;
         if (SINGLE) {
             // start_node < 0: TracerayTemplate calls the instance callback directly (BVHTraversal.h:130-131)
             if (STATS) stats->inst++;
@@ -244,7 +256,7 @@ struct Traverser {
     // lane stacks, see path_kernel_persistent) while the rest of the wave
     // shades; the lane's stack entries stay where they are.  Bit-exact resume:
     // every field that round() reads is stored as is.
-    static constexpr int kSaveFields = SINGLE ? 20 : 39;
+    static constexpr int kSaveFields = SINGLE ? 21 : 40;
     __device__ __forceinline__ void save(int* area, int tid) const {
         int f = 0;
         auto put = [&](int v) { area[(f++) * kStackBlock + tid] = v; };
@@ -252,7 +264,7 @@ struct Traverser {
         putf(cur.ox); putf(cur.oy); putf(cur.oz); putf(cur.dx); putf(cur.dy); putf(cur.dz);
         putf(cur.idx); putf(cur.idy); putf(cur.idz); putf(cur.oodx); putf(cur.oody); putf(cur.oodz);
         putf(h.t); putf(h.u); putf(h.v); put((int)h.tri); put((int)h.node);
-        put(nodeAddr); put(leafAddr);
+        put(nodeAddr); put(leafAddr); put(leaf2);
         put((resumeLeaves ? 1 : 0) | (anyhit ? 2 : 0));
         if (!SINGLE) {
             putf(world.ox); putf(world.oy); putf(world.oz); putf(world.dx); putf(world.dy); putf(world.dz);
@@ -269,7 +281,7 @@ struct Traverser {
         cur.ox = getf(); cur.oy = getf(); cur.oz = getf(); cur.dx = getf(); cur.dy = getf(); cur.dz = getf();
         cur.idx = getf(); cur.idy = getf(); cur.idz = getf(); cur.oodx = getf(); cur.oody = getf(); cur.oodz = getf();
         h.t = getf(); h.u = getf(); h.v = getf(); h.tri = (uint32_t)get(); h.node = (uint32_t)get();
-        nodeAddr = get(); leafAddr = get();
+        nodeAddr = get(); leafAddr = get(); leaf2 = get();
         const int fl = get();
         resumeLeaves = (fl & 1) != 0;
         anyhit = (fl & 2) != 0;
@@ -484,6 +496,10 @@ struct Traverser {
                     leafAddr = next;
                     next = below;
                     nsp--;
+                } else if (kLeaf2 && next < 0 && leaf2 >= 0) {
+                    leaf2 = next;
+                    next = below;
+                    nsp--;
                 }
                 nodeAddr = next;
                 st.sp = nsp;
@@ -495,9 +511,12 @@ struct Traverser {
                 if (nodeAddr < 0 && leafAddr >= 0) {
                     leafAddr = nodeAddr;
                     nodeAddr = st.pop();
+                } else if (kLeaf2 && nodeAddr < 0 && leaf2 >= 0) {
+                    leaf2 = nodeAddr;
+                    nodeAddr = st.pop();
                 }
             }
-            if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
+            if (__popcll(__ballot(CTL_LEAF_BREAK_ON_SECOND && kLeaf2 ? leaf2 >= 0 : leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
@@ -638,6 +657,11 @@ struct Traverser {
                 if (leafAddr != -214783648) {
                     leaf_tris(S, stats);
                     if (done) return;
+                }
+                if (kLeaf2 && leaf2 < 0) {
+                    leafAddr = leaf2;
+                    leaf2 = 0;
+                    continue;
                 }
                 leafAddr = nodeAddr;
                 if (nodeAddr < 0) nodeAddr = st.pop();
