@@ -268,8 +268,9 @@ def main():
     prim = primary_ray_leg(pt, dev, stream, sptr, torch, pass_base + a.steps * world) if rank == 0 else None
     wpt = (wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_base + a.steps * world + 1, a.wpt_passes)
            if rank == 0 and a.wpt_passes > 0 else None)
-    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    rr = torch.tensor([rays], dtype=torch.int64, device=dev)
+    red = dev if a.backend == "nccl" else torch.device("cpu")
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=red)
+    rr = torch.tensor([rays], dtype=torch.int64, device=red)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dist.all_reduce(rr, op=dist.ReduceOp.SUM)
@@ -317,7 +318,8 @@ def main():
                 "resolution": [W, H],
                 "spp": passes,
                 "tile": 64,
-                "parallelism": f"image-tile shard x{world} + RCCL reduce" if world > 1 else "single GPU",
+                "parallelism": (f"image-tile shard x{world} + {'RCCL' if a.backend == 'nccl' else a.backend} reduce"
+                                if world > 1 else "single GPU"),
                 "total_rays": total_rays,
             },
             "roofline": {

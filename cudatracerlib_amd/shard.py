@@ -29,5 +29,12 @@ def owned_tiles(width, height, tile, world, rank):
 def reduce_framebuffer(fb, dist, dst=0):
     """Sum the per-rank PixelData framebuffers to `dst` (RCCL over xGMI on GPUs,
     gloo on CPU).  Ownership is disjoint, so the fp32 sum is exact."""
+    if fb.is_cuda and dist.get_backend() == "gloo":
+        # gloo reduces host tensors only (CPU rehearsals of the N-rank path)
+        host = fb.cpu()
+        dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM)
+        if dist.get_rank() == dst:
+            fb.copy_(host)
+        return fb
     dist.reduce(fb, dst=dst, op=dist.ReduceOp.SUM)
     return fb
