@@ -371,6 +371,8 @@ void anim_free(ctl_ctx* c);
 int wpt_pass(ctl_ctx* c, const ctl_wpt_params* p, ctl_pixel* fb, hipStream_t s);
 void wpt_free(ctl_ctx* c);
 // ctl_trace.hip: the batch traversal launch and the ray counter, for wpt.hip
-int intersect_launch(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit, hipStream_t s);
+// (rays, hits)[0, n) and, in the same launch, (rays2, hits2)[0, n2)
+int intersect_launch(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit, hipStream_t s,
+                     int64_t n2 = 0, const ctl_ray* rays2 = nullptr, ctl_hit* hits2 = nullptr);
 int count_rays(ctl_ctx* c, uint64_t n, hipStream_t s);
 }

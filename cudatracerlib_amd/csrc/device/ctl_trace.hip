@@ -376,8 +376,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
 // atomic cursor between traversal rounds (the reference fetches per warp per
 // batch of 32 rays, :379-399), so waves stay full on incoherent rays.
 template <bool ANY, bool STATS, bool SINGLE, bool WIDE>
+// Two segments (rays, hits)[0, n) then (rays2, hits2)[0, n2) in one launch: the
+// wavefront tracer's payload and secondary batches share one resident grid and
+// one tail.
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
+                                                           int64_t n2, const ctl_ray* rays2, ctl_hit* hits2,
                                                            uint32_t* cursor, unsigned long long* counters) {
+    const int64_t total = n + n2;
     CTL_LANE_STACK(st);
     TraceStats ts{0, 0, 0};
     Traverser<ANY ? 1 : 0, STATS, SINGLE, WIDE> T;
@@ -394,7 +399,7 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, int64_t n
                 uint16_t xd = (uint16_t)(T.h.u * 65535), yd = (uint16_t)(T.h.v * 65535);
                 res.w = ((uint32_t)yd << 16) | (uint32_t)xd;
             }
-            reinterpret_cast<uint4*>(hits)[ray] = res;
+            reinterpret_cast<uint4*>(ray < n ? hits + ray : hits2 + (ray - n))[0] = res;
             ovf |= st.overflow;
             haveRay = false;
         }
@@ -407,10 +412,10 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, int64_t n
             base = __shfl(base, leader);
             if (need) {
                 const int64_t k = (int64_t)base + __popcll(mask & ((1ull << lane) - 1ull));
-                if (k < n) {
+                if (k < total) {
                     ray = k;
                     haveRay = true;
-                    const float4* r4 = reinterpret_cast<const float4*>(rays + k);
+                    const float4* r4 = reinterpret_cast<const float4*>(k < n ? rays + k : rays2 + (k - n));
                     const float4 o = r4[0], d = r4[1];
                     T.init(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), o.w, o.w, d.w, st, &ts);
                 } else {
@@ -800,23 +805,25 @@ CTL_API ctl_status ctl_sampler_generate(ctl_ctx* c, uint64_t pass_index, void* s
 }
 
 static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit,
-                                   bool stats, void* stream) {
-    if (!c || n < 0 || (n > 0 && (!rays || !hits))) return CTL_ERR_INVALID;
+                                   bool stats, void* stream, int64_t n2 = 0, const ctl_ray* rays2 = nullptr,
+                                   ctl_hit* hits2 = nullptr) {
+    if (!c || n < 0 || (n > 0 && (!rays || !hits)) || n2 < 0 || (n2 > 0 && (!rays2 || !hits2))) return CTL_ERR_INVALID;
     if (!c->has_scene) { c->err = "intersect: no scene uploaded"; return CTL_ERR_STATE; }
-    if (n > 0xffffffffll) { c->err = "intersect: more than 2^32-1 rays per call"; return CTL_ERR_INVALID; }
+    if (n + n2 > 0xffffffffll) { c->err = "intersect: more than 2^32-1 rays per call"; return CTL_ERR_INVALID; }
     CTL_HIP(c, hipSetDevice(c->device));
-    if (n == 0) return CTL_OK;
+    if (n + n2 == 0) return CTL_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     uint32_t* cursor = c->d_cursors;
     CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(uint32_t), s));
     const bool single = c->scene.single != 0;
-    const uint64_t want = ((uint64_t)n + kBlock - 1) / kBlock;
+    const uint64_t want = ((uint64_t)(n + n2) + kBlock - 1) / kBlock;
 #define IK(AN, ST, SG, WD)                                                                                       \
     do {                                                                                                         \
         static int nb = 0;                                                                                       \
         if (!nb) nb = resident_blocks(c, intersect_kernel<AN, ST, SG, WD>, kStackLdsBytes);                      \
         hipLaunchKernelGGL((intersect_kernel<AN, ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)),     \
-                           dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, cursor, c->d_counters);     \
+                           dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, n2, rays2, hits2, cursor,  \
+                           c->d_counters);                                                                       \
     } while (0)
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;
@@ -992,8 +999,9 @@ static ctl_status add_rays(ctl_ctx* c, uint64_t n, hipStream_t s) {
 }  // extern "C"
 
 namespace ctl {
-int intersect_launch(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit, hipStream_t s) {
-    return launch_intersect(c, n, rays, hits, any_hit, false, s);
+int intersect_launch(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit, hipStream_t s,
+                     int64_t n2, const ctl_ray* rays2, ctl_hit* hits2) {
+    return launch_intersect(c, n, rays, hits, any_hit, false, s, n2, rays2, hits2);
 }
 int count_rays(ctl_ctx* c, uint64_t n, hipStream_t s) { return add_rays(c, n, s); }
 }  // namespace ctl

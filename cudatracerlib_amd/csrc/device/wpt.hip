@@ -376,13 +376,10 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
                        B->pay[0]);
     WPT_HIP(hipGetLastError());
     for (int depth = 0;; depth++) {
-        // FinishIteration: payload rays, then the secondary buffer (closest hit)
-        int r = intersect_launch(c, n, B->rays[cur], B->hits, 0, s);
+        // FinishIteration: payload rays, then the secondary buffer (closest
+        // hit), as one launch over both batches (one resident grid, one tail)
+        int r = intersect_launch(c, n, B->rays[cur], B->hits, 0, s, n_sec, B->sec, B->sec_hits);
         if (r != CTL_OK) return r;
-        if (n_sec) {
-            r = intersect_launch(c, n_sec, B->sec, B->sec_hits, 0, s);
-            if (r != CTL_OK) return r;
-        }
         traced += (uint64_t)n + n_sec;
         A.depth = depth;
         const uint32_t nb = (n + kBlock - 1) / kBlock;
