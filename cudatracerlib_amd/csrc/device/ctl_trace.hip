@@ -379,7 +379,18 @@ template <bool ANY, bool STATS, bool SINGLE, bool WIDE>
 // Two segments (rays, hits)[0, n) then (rays2, hits2)[0, n2) in one launch: the
 // wavefront tracer's payload and secondary batches share one resident grid and
 // one tail.
-__global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
+#ifndef CTL_REFILL_MIN
+#define CTL_REFILL_MIN 40   // batch traversal: refill once at least this many lanes of the wave wait for a ray
+                           // (C3 WPT sweep 1/8/24/32/40/48/56: 1093/1222/1505/1563/1564/1569/1545 Mrays/s)
+#endif
+#ifndef CTL_INTERSECT_WAVES
+#define CTL_INTERSECT_WAVES 0   // waves/SIMD hint for the batch traversal (0: compiler's choice)
+#endif
+__global__ __launch_bounds__(kBlock)
+#if CTL_INTERSECT_WAVES
+__attribute__((amdgpu_waves_per_eu(CTL_INTERSECT_WAVES)))
+#endif
+void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            int64_t n2, const ctl_ray* rays2, ctl_hit* hits2,
                                                            uint32_t* cursor, unsigned long long* counters) {
     const int64_t total = n + n2;
@@ -405,7 +416,7 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S, int64_t n
         }
         const bool need = !haveRay && !exhausted;
         const uint64_t mask = __ballot(need);
-        if (mask) {
+        if (mask && (__popcll(mask) >= CTL_REFILL_MIN || !__any(haveRay))) {
             const int leader = __ffsll((unsigned long long)mask) - 1;
             uint32_t base = 0;
             if (lane == leader) base = atomicAdd(cursor, (uint32_t)__popcll(mask));
