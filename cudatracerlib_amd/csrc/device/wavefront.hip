@@ -82,6 +82,10 @@ __global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S, PathParams P
 // queue entry between traversal rounds (one atomic per wave), so waves stay
 // full while long rays finish (dynamic fetch, cf. intersectKernel's warp
 // fetch at TraceHelper.cu:379-399, here per round instead of per batch).
+#ifndef CTL_WF_REFILL_MIN
+#define CTL_WF_REFILL_MIN 40   // refill once this many lanes of the wave wait (as the batch traversal)
+#endif
+constexpr int kWfRefillMin = CTL_WF_REFILL_MIN;
 template <int MODE, bool STATS, bool SINGLE, bool WIDE, bool ALPHA>
 __global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S, WfState W, const uint32_t* queue,
                                                           const uint32_t* countp, uint32_t* cursor,
@@ -113,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S, WfState W,
         }
         const bool need = !haveRay && !exhausted;
         const uint64_t mask = __ballot(need);
-        if (mask) {
+        if (mask && (__popcll(mask) >= kWfRefillMin || !__any(haveRay))) {
             const int leader = __ffsll((unsigned long long)mask) - 1;
             uint32_t base = 0;
             if (lane == leader) base = atomicAdd(cursor, (uint32_t)__popcll(mask));
