@@ -16,7 +16,8 @@ CTL_SCENE_BINARY_BVH = 2
 CTL_SCENE_WIDE_QUANT = 4
 CTL_DEFAULT_SPLIT_ALPHA = 0.1875   # include/ctl_trace.h
 CTL_XMSH_MATERIAL_RECORD_SIZE = 148
-CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS = range(6)
+(CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS,
+ CTL_ARRAY_SAMPLES_1D, CTL_ARRAY_SAMPLES_2D) = range(8)
 CTL_BSDF_DIFFUSE = 1
 CTL_EDIFFUSE_REFLECTION = 0x2
 CTL_EGLOSSY_REFLECTION = 0x8

@@ -512,7 +512,10 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
 
 CTL_API ctl_status ctl_scene_read(ctl_ctx* c, uint32_t array, uint64_t first, uint64_t count, void* dst) {
     if (!c || (!dst && count)) return CTL_ERR_INVALID;
-    if (!c->has_scene) { c->err = "scene_read: no scene uploaded"; return CTL_ERR_STATE; }
+    if (!c->has_scene && array != CTL_ARRAY_SAMPLES_1D && array != CTL_ARRAY_SAMPLES_2D) {
+        c->err = "scene_read: no scene uploaded";
+        return CTL_ERR_STATE;
+    }
     const DevScene& S = c->scene;
     const void* src = nullptr;
     size_t elem = 0;
@@ -529,6 +532,13 @@ CTL_API ctl_status ctl_scene_read(ctl_ctx* c, uint32_t array, uint64_t first, ui
             if (first != 0 || count > 1) { c->err = "scene_read: ray eps is one value"; return CTL_ERR_INVALID; }
             if (count) memcpy(dst, &S.ray_eps, sizeof(float));
             return CTL_OK;
+        case CTL_ARRAY_SAMPLES_1D:
+        case CTL_ARRAY_SAMPLES_2D:
+            if (c->active < 0) { c->err = "scene_read: no sampler tables (call ctl_sampler_generate)"; return CTL_ERR_STATE; }
+            if (array == CTL_ARRAY_SAMPLES_1D) { src = c->d_s1[c->active]; elem = sizeof(float); }
+            else { src = c->d_s2[c->active]; elem = sizeof(float2); }
+            n = (uint64_t)c->nseq * c->len;
+            break;
         default: c->err = "scene_read: unknown array"; return CTL_ERR_INVALID;
     }
     if (first > n || count > n - first) { c->err = "scene_read: range out of bounds"; return CTL_ERR_INVALID; }

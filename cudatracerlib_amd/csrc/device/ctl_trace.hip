@@ -121,27 +121,42 @@ struct PathCtx {
 constexpr int kJumpBits = 24;
 struct XorwowDev { uint32_t v[5]; uint32_t d; };
 
+// One wave per sequence: the GF(2) matrix-vector product of each jump is
+// split over the lanes by input bit (lane j holds state bits j, j+64, j+128)
+// and XOR-reduced across the wave, so a jump costs one round of column loads
+// and a 6-step butterfly instead of ~80 dependent column loads on one lane.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x ^= (uint32_t)__shfl_xor((int)x, m);
+    return x;
+}
+
 __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict__ powers, XorwowDev base,
                                                       uint32_t nseq, uint32_t len, float* s1, float2* s2) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= nseq) return;
+    const uint32_t q = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (q >= nseq) return;   // whole wave
     const uint32_t off = q * len * 3;
     uint32_t v[5] = {base.v[0], base.v[1], base.v[2], base.v[3], base.v[4]};
     for (int k = 0; k < kJumpBits; k++) {
-        if (!((off >> k) & 1u)) continue;
+        if (!((off >> k) & 1u)) continue;   // uniform over the wave
         const uint32_t* M = powers + k * 800;
+        const bool lo = lane < 32;
+        const uint32_t sh = (uint32_t)(lane & 31);
+        const uint32_t w0 = lo ? v[0] : v[1], w1 = lo ? v[2] : v[3];
         uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
-        for (int w = 0; w < 5; w++) {
-            uint32_t bits = v[w];
-            while (bits) {
-                int b = __builtin_ctz(bits);
-                bits &= bits - 1;
-                const uint32_t* c = M + (w * 32 + b) * 5;
+        auto col = [&](uint32_t word, int b) {
+            if ((word >> sh) & 1u) {
+                const uint32_t* c = M + b * 5;
                 r0 ^= c[0]; r1 ^= c[1]; r2 ^= c[2]; r3 ^= c[3]; r4 ^= c[4];
             }
-        }
-        v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
+        };
+        col(w0, lane);
+        col(w1, lane + 64);
+        if (lo) col(v[4], lane + 128);
+        v[0] = wave_xor(r0); v[1] = wave_xor(r1); v[2] = wave_xor(r2); v[3] = wave_xor(r3); v[4] = wave_xor(r4);
     }
+    if (lane != 0) return;
     uint32_t d = base.d + 362437u * off;
     auto next = [&]() -> float {
         uint32_t t = v[0] ^ (v[0] >> 2);
@@ -807,7 +822,7 @@ CTL_API ctl_status ctl_sampler_generate(ctl_ctx* c, uint64_t pass_index, void* s
     int b = c->next_buf;
     XorwowDev base;
     ctl::sampler_pass_state(pass_index, c->nseq, c->len, base.v, &base.d);
-    hipLaunchKernelGGL(sampler_kernel, dim3((c->nseq + 255) / 256), dim3(256), 0, s, c->d_powers, base, c->nseq,
+    hipLaunchKernelGGL(sampler_kernel, dim3((c->nseq + 3) / 4), dim3(256), 0, s, c->d_powers, base, c->nseq,
                        c->len, c->d_s1[b], c->d_s2[b]);
     CTL_HIP(c, hipGetLastError());
     c->active = b;

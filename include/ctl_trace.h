@@ -398,7 +398,10 @@ enum {
     CTL_ARRAY_BVH_NODES = 2,   /* ctl_bvh_node        */
     CTL_ARRAY_SCENE_BVH = 3,   /* ctl_bvh_node        */
     CTL_ARRAY_MESH_BOXES = 4,  /* 6 floats per mesh   */
-    CTL_ARRAY_RAY_EPS = 5      /* 1 float             */
+    CTL_ARRAY_RAY_EPS = 5,     /* 1 float             */
+    CTL_ARRAY_SAMPLES_1D = 6,  /* float, element-major [len][num_sequences]: the tables of the last
+                                  ctl_sampler_generate / ctl_sampler_upload */
+    CTL_ARRAY_SAMPLES_2D = 7   /* float2, same layout */
 };
 CTL_API ctl_status ctl_scene_read(ctl_ctx* ctx, uint32_t array, uint64_t first, uint64_t count, void* host_dst);
 

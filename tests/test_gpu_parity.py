@@ -458,3 +458,25 @@ def test_wpt_converges_to_path_tracer(ctl, orc, tracer, dev):
     ma = (a[:, :3] / a[:, 6:7]).mean(0)
     mb = (b[:, :3] / b[:, 6:7]).mean(0)
     assert np.all(np.abs(ma - mb) <= 0.03 * mb + 1e-4), (ma, mb)
+
+
+@pytest.mark.parametrize("pass_index", [0, 1, 7, 1000, 123456])
+def test_device_sampler_tables_bit_exact(ctl, orc, dev, pass_index):
+    """sampler_kernel (wave-parallel XORWOW jumps) == the oracle's SequenceSampler
+    tables of the same pass (CudaRNG(7539414) stream, Kernel/Sampler.h:36-55)."""
+    pt = ctl.PathTracer(0)
+    try:
+        nseq, ln = 4096, 30
+        pt.generate_samples(pass_index)
+        got1 = np.zeros(nseq * ln, np.float32)
+        got2 = np.zeros(nseq * ln * 2, np.float32)
+        L = ctl.lib()
+        assert L.ctl_scene_read(pt._ctx, ctl._abi.CTL_ARRAY_SAMPLES_1D, 0, nseq * ln, got1.ctypes.data) == 0
+        assert L.ctl_scene_read(pt._ctx, ctl._abi.CTL_ARRAY_SAMPLES_2D, 0, nseq * ln, got2.ctypes.data) == 0
+        want1 = np.zeros_like(got1)
+        want2 = np.zeros_like(got2)
+        orc.oracle_sampler_tables(pass_index, nseq, ln, oracle.ptr(want1), oracle.ptr(want2))
+        assert np.array_equal(got1.view(np.uint32), want1.view(np.uint32))
+        assert np.array_equal(got2.view(np.uint32), want2.view(np.uint32))
+    finally:
+        pt.close()
