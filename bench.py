@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--split-depth", type=int, default=8)
     ap.add_argument("--bins", type=int, default=0, help="SAH bins (0: library default)")
     ap.add_argument("--max-leaf", type=int, default=0, help="max leaf size (0: library default)")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="diagnostic: one process renders rank 0's share of an N-rank job "
+                         "(N passes per step over the tiles with tile %% N == 0), no collective")
     ap.add_argument("--bvh", default="wide", choices=["wide", "wideq", "binary"],
                     help="device traversal: 4-wide collapsed BVH, or the reference's binary order")
     return ap.parse_args()
@@ -165,6 +168,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         log(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # image-tile shards: one per rank, or N emulated ranks in this one process
+    shards = a.emulate_ranks if (world == 1 and a.emulate_ranks > 1) else world
     import torch
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -201,7 +206,7 @@ def main():
         f"built in {t_build:.1f}s with {threads} threads")
 
     pt = ctl.PathTracer(local, max_path_length=a.max_path_length, rr_start_depth=a.rr_start,
-                        shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, num_ranks=world, rank=rank,
+                        shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, num_ranks=shards, rank=rank,
                         schedule=a.schedule)
     pt.upload_scene(desc)
     W, H = a.width, a.height
@@ -224,24 +229,33 @@ def main():
     # kernel of each pass stays outside the brackets but inside the step time.
     kev = []
 
+    # One shard's N passes of a step go through one ctl_render_passes launch
+    # (same framebuffer as N sequential passes), so a rank owning 1/N of the
+    # tiles keeps the resident grid as busy as a full-image pass does.
     def step(s, timed=False):
-        for pidx in shard.step_pass_indices(s, world, pass_base):
-            pt.generate_samples(pidx, sptr)
+        pidx = shard.step_pass_indices(s, shards, pass_base)
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+        if len(pidx) == 1:
+            pt.generate_samples(pidx[0], sptr)
             if timed:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
             pt.render_pass(fb.data_ptr(), sptr)
+        else:
             if timed:
-                e1.record(stream)
-                kev.append((e0, e1))
+                e0.record(stream)
+            pt.render_passes(fb.data_ptr(), pidx[0], len(pidx), sptr)
+        if timed:
+            e1.record(stream)
+            kev.append((e0, e1))
 
     for s in range(a.warmup):
         step(s)
     steps_done = a.warmup
     torch.cuda.synchronize(dev)
     fb.zero_()
-    pass_base = steps_done * world   # fresh passes for the timed image
+    pass_base = steps_done * shards   # fresh passes for the timed image
     pt.reset_rays(sptr)
     if world > 1:
         dist.barrier()
@@ -265,8 +279,8 @@ def main():
     kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in kev)
 
     rays = pt.rays_traced()
-    prim = primary_ray_leg(pt, dev, stream, sptr, torch, pass_base + a.steps * world) if rank == 0 else None
-    wpt = (wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_base + a.steps * world + 1, a.wpt_passes)
+    prim = primary_ray_leg(pt, dev, stream, sptr, torch, pass_base + a.steps * shards) if rank == 0 else None
+    wpt = (wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_base + a.steps * shards + 1, a.wpt_passes)
            if rank == 0 and a.wpt_passes > 0 else None)
     red = dev if a.backend == "nccl" else torch.device("cpu")
     tt = torch.tensor([elapsed], dtype=torch.float64, device=red)
@@ -278,12 +292,13 @@ def main():
     total_rays = int(rr.item())
 
     if rank == 0:
-        passes = a.steps * world
+        passes = a.steps * shards
         img = fb.view(H, W, 7)
         wsum = float(img[..., 6].sum().item())
         launches = len(kev)   # path-kernel launches on this rank in the timed region
         per_launch_ms = kernel_ms / launches
-        achieved = alg_bytes_per_pass / (per_launch_ms * 1e-3) / 1e9
+        passes_per_launch = shards   # one ctl_render_passes launch per step when sharded
+        achieved = alg_bytes_per_pass * passes_per_launch / (per_launch_ms * 1e-3) / 1e9
         traffic = None
         tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
         if os.path.exists(tf):
@@ -321,6 +336,7 @@ def main():
                 "parallelism": (f"image-tile shard x{world} + {'RCCL' if a.backend == 'nccl' else a.backend} reduce"
                                 if world > 1 else "single GPU"),
                 "total_rays": total_rays,
+                **({"emulated_ranks": shards} if shards != world else {}),
             },
             "roofline": {
                 "bound": "hbm",
@@ -336,7 +352,10 @@ def main():
                         "physical HBM bytes per launch are in `traffic`",
                 "launches_timed": launches,
                 "gpu_step_ms": round(step_ms / a.steps, 3),
-                "alg_bytes_per_launch": int(alg_bytes_per_pass),
+                "alg_bytes_per_launch": int(alg_bytes_per_pass * passes_per_launch),
+                "passes_per_launch": passes_per_launch,
+                **({"launch": "ctl_render_passes: the step's sampler tables, one path-kernel launch over all "
+                              "its passes, slice fold (all inside the bracket)"} if passes_per_launch > 1 else {}),
                 "per_launch_ms": round(per_launch_ms, 3),
                 "visits_per_launch": {"inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3]),
                                       "rays": int(st[0])},

@@ -342,6 +342,12 @@ class PathTracer(Tracer):
         _check(self._L.ctl_render_pass(self._ctx, C.byref(self.params), fb_ptr, stream), self._ctx,
                "ctl_render_pass")
 
+    def render_passes(self, fb_ptr, first_pass, n_passes, stream=0):
+        """Passes first_pass .. first_pass + n_passes - 1 in one launch (ctl_render_passes):
+        the framebuffer of n_passes do_pass calls."""
+        _check(self._L.ctl_render_passes(self._ctx, C.byref(self.params), int(first_pass), int(n_passes), fb_ptr,
+                                         stream), self._ctx, "ctl_render_passes")
+
     def last_pass_ms(self):
         """Device time of the last render pass (Tracer::getLastTimeSpentRenderingSec)."""
         ms = C.c_float()

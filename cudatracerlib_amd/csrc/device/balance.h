@@ -61,7 +61,7 @@ __device__ __forceinline__ HitRec trace_balanced(const DevScene& S, LaneStack& s
     const int lane = tid & 63;
     const int wbase = tid & ~63;
     const uint64_t ltmask = (1ull << lane) - 1ull;
-    int* B = ctl_lds_stack + kLdsStack * kStackBlock;
+    int* B = ctl_lds_stack + kExtraLdsOff;
     unsigned long long* slot = reinterpret_cast<unsigned long long*>(B);
     float2* uv = reinterpret_cast<float2*>(B + 512);
     int* pend = B + 1024;

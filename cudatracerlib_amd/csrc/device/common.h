@@ -110,6 +110,43 @@ __device__ __forceinline__ void add_sample(ctl_pixel* fb, const PathParams& P, f
     }
 }
 
+// Work item k of a pass covers pixel work_pixel(k).  Its finished sample lands
+// on floor(pX) (Image::AddSample, Engine/Image.cu:22-44), which is the pixel
+// itself or, when the jitter rounds up, its right / lower / lower-right
+// neighbour, so two samples of one pass can meet on a pixel.  The path kernels
+// therefore never add into the framebuffer: each work item stores its sample
+// in its own slot (rgb, code), and fold_samples_kernel adds, per target pixel,
+// the samples that landed there in work-item order, pass by pass -- the
+// additions and their order of one sequential AddSample per work item.
+// code: 0 = no sample (dropped as AddSample drops it), 1 + dx + 2 dy = landed
+// on (px + dx, py + dy).
+struct SampleSlots {
+    float4* s;            // [pass slot][work item]
+    uint32_t per_pass;    // work items of one pass
+};
+__device__ __forceinline__ void store_sample(const PathParams& P, const SampleSlots& S, uint32_t ps, uint32_t kk,
+                                             uint32_t px, uint32_t py, f2 pX, spec col) {
+    col.x = tmax(0.0f, col.x); col.y = tmax(0.0f, col.y); col.z = tmax(0.0f, col.z);
+    const int x = (int)floorf(pX.x), y = (int)floorf(pX.y);
+    const bool valid = !(isnan(col.x) || isnan(col.y) || isnan(col.z)) && isfinite(col.x) && isfinite(col.y) &&
+                       isfinite(col.z) && col.x >= 0.0f && col.y >= 0.0f && col.z >= 0.0f;
+    const int dx = x - (int)px, dy = y - (int)py;
+    float code = 0.0f;
+    if (x >= 0 && x < (int)P.width && y >= 0 && y < (int)P.height && valid && (dx | dy) >= 0 && dx <= 1 && dy <= 1)
+        code = (float)(1 + dx + 2 * dy);
+    S.s[(size_t)ps * S.per_pass + kk] = make_float4(col.x, col.y, col.z, code);
+}
+
+// inverse of work_pixel: owned pixel -> work item (false when another rank owns it)
+__device__ __forceinline__ bool pixel_work(const PathParams& P, uint32_t x, uint32_t y, uint32_t& k) {
+    const uint32_t ts = P.tile_size;
+    const uint32_t tile = (y / ts) * P.tiles_x + x / ts;
+    if (tile % P.num_ranks != P.rank) return false;
+    const uint32_t xx = x % ts, yy = y % ts;
+    k = (tile / P.num_ranks) * ts * ts + ((yy / 8) * (ts / 8) + xx / 8) * 64 + (yy % 8) * 8 + xx % 8;
+    return true;
+}
+
 // Loop-carried variables of PathTrace<true> (PathTracer.cu:10-33).  wo and
 // brdf_pdf persist: diffuse_sample leaves them untouched when it rejects a
 // sample, and the reference then continues with the previous values.
@@ -327,6 +364,14 @@ struct ctl_ctx {
     uint32_t nseq = 4096, len = 30;
     float* d_s1[2] = {nullptr, nullptr};
     float2* d_s2[2] = {nullptr, nullptr};
+    // ctl_render_passes: sampler tables of every pass of one launch, and the
+    // per-pass sample slices of the owned tiles (folded into the caller's
+    // framebuffer in pass order)
+    float* d_mt1 = nullptr;
+    float2* d_mt2 = nullptr;
+    uint32_t mt_cap = 0;        // tables allocated
+    float4* d_slices = nullptr; // SampleSlots of the path kernels (common.h)
+    uint64_t slices_cap = 0;    // float4 elements allocated
     float* h_s1[2] = {nullptr, nullptr};
     float* h_s2[2] = {nullptr, nullptr};
     hipEvent_t ev[2] = {nullptr, nullptr};

@@ -70,7 +70,7 @@ constexpr int kTail = CTL_TAIL;
 // dynamic LDS of path_kernel_persistent: lane stacks + parked traversal state
 template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
 constexpr size_t persistent_lds_bytes() {
-    return kStackLdsBytes +
+    return kStackLdsBytes + sizeof(int) * kStackBlock +
            (kTail > 1 ? sizeof(int) * kStackBlock * Traverser<2, STATS, SINGLE, WIDE, FULL>::kSaveFields
                       : (SINGLE && WIDE && !STATS && CTL_BALANCE ? kBalLdsBytes : 0));
 }
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict
 // One path per thread (the reference's pathKernel2 launch shape).
 template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
 __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
-                                                      ctl_pixel* fb, unsigned long long* counters) {
+                                                      ctl_pixel* fb, unsigned long long* counters, SampleSlots PS) {
     CTL_LANE_STACK(st);
     const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     uint32_t rays = 0;
@@ -193,10 +193,12 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
         const f2 pX = primary_ray(S, rng, px, py, o, dw);
         C.v.begin(pX, o, dw);
         while (C.bounce()) {}
-        add_sample(fb, P, pX, mk3s(1.0f) * C.v.cl);
+        store_sample(P, PS, 0, (uint32_t)g, px, py, pX, mk3s(1.0f) * C.v.cl);
         rays = C.rays;
         ts = C.ts;
         ok = C.ok;
+    } else if (g < PS.per_pass) {
+        PS.s[g] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // work item outside the image: no sample
     }
     wave_add_u64(&counters[0], rays);
     if (!ok) atomicAdd(&counters[1], 1ull);
@@ -238,9 +240,21 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
 template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? (FULL ? CTL_PERSIST_WAVES_FULL : CTL_PERSIST_WAVES) : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
                                                                  const float2* s2, ctl_pixel* fb, uint64_t items,
-                                                                 uint32_t* cursor, unsigned long long* counters) {
+                                                                 uint32_t* cursor, unsigned long long* counters,
+                                                                 SampleSlots PS, uint32_t tbl) {
+    // Work item k renders pass slot k / PS.per_pass (sampler tables at
+    // s1/s2 + slot * tbl) of work item k % PS.per_pass; every finished sample
+    // goes to its own slot, folded into fb afterwards (store_sample).
     CTL_LANE_STACK(st);
     SamplerDev rng{s1, s2, P.nseq, P.len, 0, 0, 0, 0};
+    // work item of the lane's path (pass slot * PS.per_pass + item), parked in
+    // LDS for the path's lifetime instead of holding a VGPR through the traces
+    int* pkw = ctl_lds_stack + kPathWordOff + threadIdx.x;
+    // k -> (pass slot, item of the pass): a few subtractions (slots <= passes per launch)
+    auto split = [&](uint32_t k, uint32_t& ps, uint32_t& kk) {
+        ps = 0; kk = k;
+        while (kk >= PS.per_pass) { kk -= PS.per_pass; ps++; }
+    };
     PathVars v;
     ShadowReq sh;
     sh.valid = false;
@@ -264,12 +278,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             base = __shfl(base, leader);
             if (need) {
                 const uint32_t k = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-                uint32_t px, py;
+                uint32_t px, py, ps, kk;
+                split(k, ps, kk);
                 if (k >= items) {
                     exhausted = true;
-                } else if (work_pixel(P, k, px, py)) {
+                } else if (work_pixel(P, kk, px, py)) {
                     const uint32_t idx = py * P.width + px;
-                    rng.a = idx % P.nseq; rng.b = (idx / P.nseq) % P.nseq; rng.d1 = 0; rng.d2 = 0;
+                    // the pass slot's tables start ps * tbl elements in: folded into
+                    // the two sequence offsets so the table bases stay kernel-uniform
+                    rng.a = idx % P.nseq + ps * tbl; rng.b = (idx / P.nseq) % P.nseq + ps * tbl;
+                    rng.d1 = 0; rng.d2 = 0;
+                    *pkw = (int)k;
                     f3 o, dw;
                     const f2 pX = primary_ray(S, rng, px, py, o, dw);
                     v.begin(pX, o, dw);
@@ -277,7 +296,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                     ending = false;
                     // loop head of PathTrace: `while (depth++ < MaxPathLength)`
                     if (v.depth++ < P.max_path_length) active = true;
-                    else add_sample(fb, P, v.pX, mk3s(1.0f) * v.cl);
+                    else store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
+                } else {
+                    PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // work item outside the image: no sample
                 }
             }
         }
@@ -316,7 +337,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                 if (S.n_nodes != 0) {
                     typedef Traverser<2, STATS, SINGLE, WIDE, FULL> Tr;
                     Tr T;
-                    int* park = ctl_lds_stack + kLdsStack * kStackBlock;
+                    int* park = ctl_lds_stack + kExtraLdsOff;
                     if (kTail > 1 && resumed) {
                         T.restore(S, park, st.tid, 0.0f, S.ray_eps);
                     } else {
@@ -357,7 +378,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                 cont = sh.valid || (!ending && v.depth++ < P.max_path_length);
             }
             if (!cont) {
-                add_sample(fb, P, v.pX, mk3s(1.0f) * v.cl);
+                uint32_t px, py, ps, kk;
+                split((uint32_t)*pkw, ps, kk);
+                work_pixel(P, kk, px, py);
+                store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
                 active = false;
             }
         }
@@ -595,6 +619,9 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
     ctl::wavefront_free(c);
     ctl::wpt_free(c);
     ctl::anim_free(c);
+    if (c->d_mt1) (void)hipFree(c->d_mt1);
+    if (c->d_mt2) (void)hipFree(c->d_mt2);
+    if (c->d_slices) (void)hipFree(c->d_slices);
     for (int i = 0; i < 2; i++) {
         if (c->d_s1[i]) (void)hipFree(c->d_s1[i]);
         if (c->d_s2[i]) (void)hipFree(c->d_s2[i]);
@@ -877,10 +904,14 @@ CTL_API ctl_status ctl_intersect(ctl_ctx* c, int64_t n, const ctl_ray* d_rays, c
     return add_rays(c, (uint64_t)n, reinterpret_cast<hipStream_t>(stream));
 }
 
-static ctl_status prepare_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb, PathParams& P) {
+static ctl_status prepare_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb, PathParams& P,
+                               bool need_tables = true) {
     if (!c || !p || !fb) return CTL_ERR_INVALID;
     if (!c->has_scene) { c->err = "render_pass: no scene uploaded"; return CTL_ERR_STATE; }
-    if (c->active < 0) { c->err = "render_pass: no sampler tables (call ctl_sampler_generate)"; return CTL_ERR_STATE; }
+    if (need_tables && c->active < 0) {
+        c->err = "render_pass: no sampler tables (call ctl_sampler_generate)";
+        return CTL_ERR_STATE;
+    }
     if (!p->direct) { c->err = "render_pass: only Direct=1 is supported"; return CTL_ERR_INVALID; }
     uint32_t ts = p->tile_size ? p->tile_size : 64;
     if (ts % 8 != 0) { c->err = "render_pass: tile_size must be a multiple of 8"; return CTL_ERR_INVALID; }
@@ -903,7 +934,11 @@ static ctl_status prepare_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb
 }
 
 static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const PathParams& P, ctl_pixel* fb, bool stats,
-                                  hipStream_t s, uint64_t threads, dim3 grid, const float* s1, const float2* s2);
+                                  hipStream_t s, uint64_t threads, dim3 grid, const float* s1, const float2* s2,
+                                  SampleSlots PS = SampleSlots{nullptr, 0}, uint32_t tbl = 0);
+
+static ctl_status prepare_slots(ctl_ctx* c, uint64_t items, hipStream_t s);
+static void launch_fold(ctl_ctx* c, const PathParams& P, uint32_t per_pass, uint32_t n, ctl_pixel* fb, hipStream_t s);
 
 static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb, bool stats, void* stream) {
     PathParams P;
@@ -918,15 +953,23 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
     const float* s1 = c->d_s1[c->active];
     const float2* s2 = c->d_s2[c->active];
     CTL_HIP(c, hipEventRecord(c->pass_ev[0], s));
-    ctl_status r2 = launch_schedule(c, p, P, fb, stats, s, threads, grid, s1, s2);
+    const bool slots = !(p->flags & CTL_PT_WAVEFRONT);   // the path kernels store samples per work item
+    if (slots) {
+        ctl_status r1 = prepare_slots(c, threads, s);
+        if (r1 != CTL_OK) return r1;
+    }
+    ctl_status r2 = launch_schedule(c, p, P, fb, stats, s, threads, grid, s1, s2,
+                                    SampleSlots{c->d_slices, (uint32_t)threads}, 0);
     if (r2 != CTL_OK) return r2;
+    if (slots) launch_fold(c, P, (uint32_t)threads, 1, fb, s);
     CTL_HIP(c, hipEventRecord(c->pass_ev[1], s));
     c->pass_timed = true;
     return CTL_OK;
 }
 
 static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const PathParams& P, ctl_pixel* fb, bool stats,
-                                  hipStream_t s, uint64_t threads, dim3 grid, const float* s1, const float2* s2) {
+                                  hipStream_t s, uint64_t threads, dim3 grid, const float* s1, const float2* s2,
+                                  SampleSlots PS, uint32_t tbl) {
     if (p->flags & CTL_PT_WAVEFRONT) return (ctl_status)ctl::wavefront_pass(c, P, fb, stats, s);
     const bool single = c->scene.single != 0;
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
@@ -943,7 +986,7 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
             if (!nb) nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD, FU>, lds);                        \
             hipLaunchKernelGGL((path_kernel_persistent<ST, SG, WD, FU>), dim3((unsigned)std::min<uint64_t>(nb, want)), \
                                dim3(kBlock), lds, s, c->scene, P, s1, s2, fb, threads, cursor,                   \
-                               c->d_counters);                                                                   \
+                               c->d_counters, PS, tbl);                                                          \
         } while (0)
 #define PK2(ST, SG, WD) do { if (full) PK(ST, SG, WD, true); else PK(ST, SG, WD, false); } while (0)
         if (stats) { if (single) PK2(true, true, false); else PK2(true, false, false); }
@@ -953,7 +996,7 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
 #undef PK
     } else {
 #define MK(ST, SG, WD, FU) hipLaunchKernelGGL((path_kernel<ST, SG, WD, FU>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, \
-                                              P, s1, s2, fb, c->d_counters)
+                                              P, s1, s2, fb, c->d_counters, PS)
 #define MK2(ST, SG, WD) do { if (full) MK(ST, SG, WD, true); else MK(ST, SG, WD, false); } while (0)
         if (stats) { if (single) MK2(true, true, false); else MK2(true, false, false); }
         else if (wide) { if (single) MK2(false, true, true); else MK2(false, false, true); }
@@ -962,6 +1005,127 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
 #undef MK
     }
     CTL_HIP(c, hipGetLastError());
+    return CTL_OK;
+}
+
+// Sample slots -> framebuffer: per target pixel, the samples that landed on it
+// (its own and the ones that rounded over from the left / upper / upper-left
+// neighbour) in image order of their pixels, pass by pass -- one sequential
+// AddSample per pixel in image order (Image.cu:22-44), as the oracle adds them.
+// Only this rank's pixels are sources (pixel_work).
+__global__ __launch_bounds__(kBlock) void fold_samples_kernel(PathParams P, const float4* __restrict__ slots,
+                                                              uint32_t per_pass, uint32_t n, ctl_pixel* fb) {
+    const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= P.width * P.height) return;
+    const uint32_t x = q % P.width, y = q / P.width;
+    uint32_t ks[4];
+    float codes[4];
+    int nc = 0;
+    // sources in image order: (x-1, y-1), (x, y-1), (x-1, y), (x, y)
+#pragma unroll
+    for (int d = 3; d >= 0; d--) {
+        const uint32_t dx = d & 1, dy = d >> 1;
+        uint32_t k;
+        if (x >= dx && y >= dy && pixel_work(P, x - dx, y - dy, k)) {
+            ks[nc] = k;
+            codes[nc] = (float)(1 + d);
+            nc++;
+        }
+    }
+    if (nc == 0) return;
+    ctl_pixel* pp = fb + q;
+    float r = 0.0f, g = 0.0f, b = 0.0f, w = 0.0f;
+    bool any = false;
+    for (uint32_t k = 0; k < n; k++) {
+        for (int i = 0; i < nc; i++) {
+            const float4 v = slots[(size_t)k * per_pass + ks[i]];
+            if (v.w == codes[i]) {
+                if (!any) { r = pp->rgb[0]; g = pp->rgb[1]; b = pp->rgb[2]; w = pp->weight_sum; any = true; }
+                r += v.x; g += v.y; b += v.z; w += 1.0f;
+            }
+        }
+    }
+    if (any) {
+        pp->rgb[0] = r; pp->rgb[1] = g; pp->rgb[2] = b;
+        pp->weight_sum = w;
+    }
+}
+
+// Sample slots for n passes of per_pass work items, grown on demand.  Every
+// work item writes its slot (code 0 when it has no pixel or AddSample would
+// drop the sample), so no clearing is needed.
+static ctl_status prepare_slots(ctl_ctx* c, uint64_t items, hipStream_t s) {
+    if (c->slices_cap < items) {
+        CTL_HIP(c, hipStreamSynchronize(s));
+        if (c->d_slices) (void)hipFree(c->d_slices);
+        c->d_slices = nullptr; c->slices_cap = 0;
+        if (hipMalloc(&c->d_slices, items * sizeof(float4)) != hipSuccess) {
+            c->err = "render_pass: sample slot allocation failed";
+            return CTL_ERR_NOMEM;
+        }
+        c->slices_cap = items;
+    }
+    return CTL_OK;
+}
+
+static void launch_fold(ctl_ctx* c, const PathParams& P, uint32_t per_pass, uint32_t n, ctl_pixel* fb, hipStream_t s) {
+    const uint64_t px = (uint64_t)P.width * P.height;
+    hipLaunchKernelGGL(fold_samples_kernel, dim3((unsigned)((px + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, P,
+                       c->d_slices, per_pass, n, fb);
+}
+
+CTL_API ctl_status ctl_render_passes(ctl_ctx* c, const ctl_pt_params* params, uint64_t first_pass, uint32_t n_passes,
+                                     ctl_pixel* d_fb, void* stream) {
+    if (!c || !params || !d_fb) return CTL_ERR_INVALID;
+    if (n_passes == 0) return CTL_OK;
+    if (params->flags & (CTL_PT_WAVEFRONT | CTL_PT_MEGAKERNEL)) {
+        // the other schedules: one pass at a time
+        for (uint32_t i = 0; i < n_passes; i++) {
+            ctl_status r = ctl_sampler_generate(c, first_pass + i, stream);
+            if (r == CTL_OK) r = launch_pass(c, params, d_fb, false, stream);
+            if (r != CTL_OK) return r;
+        }
+        return CTL_OK;
+    }
+    PathParams P;
+    ctl_status r = prepare_pass(c, params, d_fb, P, false);
+    if (r != CTL_OK) return r;
+    CTL_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const uint32_t owned = (P.num_tiles > P.rank) ? (P.num_tiles - P.rank + P.num_ranks - 1) / P.num_ranks : 0;
+    const uint64_t per_pass = (uint64_t)owned * P.tile_size * P.tile_size;
+    if (per_pass == 0) return CTL_OK;
+    const uint64_t items = per_pass * n_passes;
+    if (items > 0xffffffffull) { c->err = "render_passes: more than 2^32-1 work items"; return CTL_ERR_INVALID; }
+    const size_t tbl = (size_t)c->nseq * c->len;
+    if (c->mt_cap < n_passes) {
+        CTL_HIP(c, hipStreamSynchronize(s));
+        if (c->d_mt1) (void)hipFree(c->d_mt1);
+        if (c->d_mt2) (void)hipFree(c->d_mt2);
+        c->d_mt1 = nullptr; c->d_mt2 = nullptr; c->mt_cap = 0;
+        if (hipMalloc(&c->d_mt1, tbl * n_passes * sizeof(float)) != hipSuccess ||
+            hipMalloc(&c->d_mt2, tbl * n_passes * sizeof(float2)) != hipSuccess) {
+            c->err = "render_passes: sampler table allocation failed";
+            return CTL_ERR_NOMEM;
+        }
+        c->mt_cap = n_passes;
+    }
+    CTL_HIP(c, hipEventRecord(c->pass_ev[0], s));
+    for (uint32_t i = 0; i < n_passes; i++) {
+        XorwowDev base;
+        ctl::sampler_pass_state(first_pass + i, c->nseq, c->len, base.v, &base.d);
+        hipLaunchKernelGGL(sampler_kernel, dim3((c->nseq + 3) / 4), dim3(256), 0, s, c->d_powers, base, c->nseq, c->len,
+                           c->d_mt1 + i * tbl, c->d_mt2 + i * tbl);
+    }
+    r = prepare_slots(c, items, s);
+    if (r != CTL_OK) return r;
+    r = launch_schedule(c, params, P, d_fb, false, s, items, dim3(1), c->d_mt1, c->d_mt2,
+                        SampleSlots{c->d_slices, (uint32_t)per_pass}, (uint32_t)tbl);
+    if (r != CTL_OK) return r;
+    launch_fold(c, P, (uint32_t)per_pass, n_passes, d_fb, s);
+    CTL_HIP(c, hipGetLastError());
+    CTL_HIP(c, hipEventRecord(c->pass_ev[1], s));
+    c->pass_timed = true;
     return CTL_OK;
 }
 

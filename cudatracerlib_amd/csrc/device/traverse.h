@@ -171,6 +171,10 @@ struct LaneStack {
     name.tid = (int)threadIdx.x;                   \
     name.overflow = false
 constexpr size_t kStackLdsBytes = sizeof(int) * kLdsStack * kStackBlock;
+// path_kernel_persistent keeps one word per thread after the stacks (the work
+// item of the lane's path); the tail/balance experiments' areas follow it
+constexpr int kPathWordOff = kLdsStack * kStackBlock;
+constexpr int kExtraLdsOff = kPathWordOff + kStackBlock;
 
 struct RayLocal {
     float ox, oy, oz, dx, dy, dz;

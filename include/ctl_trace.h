@@ -358,6 +358,16 @@ CTL_API ctl_status ctl_intersect(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays,
 CTL_API ctl_status ctl_render_pass(ctl_ctx* ctx, const ctl_pt_params* params, ctl_pixel* d_fb,
                                    void* stream);
 
+/* n_passes consecutive passes first_pass .. first_pass + n_passes - 1 in one
+ * launch: the same framebuffer as n_passes rounds of ctl_sampler_generate +
+ * ctl_render_pass (Tracer::DoPass called n times, Kernel/Tracer.h:209-248),
+ * with the sampler tables generated inside.  Each pass's samples land in a
+ * per-pass slice of the owned tiles that is folded into d_fb in pass order, so
+ * a rank owning 1/N of the image keeps the resident grid as busy as a
+ * full-image pass.  Asynchronous on `stream`; ctl_last_pass_ms covers the call. */
+CTL_API ctl_status ctl_render_passes(ctl_ctx* ctx, const ctl_pt_params* params, uint64_t first_pass,
+                                     uint32_t n_passes, ctl_pixel* d_fb, void* stream);
+
 /* Device time of the last ctl_render_pass on its stream, in milliseconds
  * (Tracer::getLastTimeSpentRenderingSec, Kernel/Tracer.h:133-140, which times
  * DoPass with cudaEvents, Tracer.h:213,239-244).  Waits for that pass. */

@@ -1318,6 +1318,10 @@ void oracle_brute_force(const ctl_scene_desc* d, int64_t n, const ctl_ray* rays,
 // pixels of the tiles owned by (rank, num_ranks), accumulating into fb.
 // Returns the number of traceRay calls.  pixel_stride > 1 renders only every
 // pixel_stride-th pixel (bounded CPU-baseline samples); stats may be NULL.
+// Paths are traced on worker threads; the samples are then added with
+// AddSample one by one in image order (pixel y*W+x), the order of a
+// single-threaded pass: a jittered sample can land on the neighbouring pixel
+// (floor(x + u) with u close to 1), so adding from the threads would race.
 uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm, uint64_t pass_index,
                             ctl_pixel* fb, int32_t tie, int32_t threads, uint32_t pixel_stride, uint64_t* stats) {
     const uint32_t nseq = 4096, len = 30;
@@ -1332,6 +1336,8 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
     std::atomic<int64_t> nextRow{0};
     std::mutex mtx;
     uint64_t totalRays = 0, acc[3] = {0, 0, 0};
+    struct Smp { float x, y; Spec L; bool set; };
+    std::vector<Smp> smp((size_t)W * H);
     auto worker = [&]() {
         RenderCtx C{SceneView{desc}, nullptr, tie, (desc->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0,
                     prm->shadow_any_hit != 0};
@@ -1352,7 +1358,7 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
                 sensor_ray(cam, pX, o, dd);
                 sensor_ray_diff(cam, pX, xo, dX, dY);
                 Spec col = v3s(1.0f) * path_trace(C, o, dd, xo, dX, xo, dY, prm->max_path_length, prm->rr_start_depth);
-                add_sample(fb, W, H, pX.x, pX.y, col);
+                smp[lin] = Smp{pX.x, pX.y, col, true};
             }
         }
         std::lock_guard<std::mutex> g(mtx);
@@ -1362,6 +1368,8 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
     std::vector<std::thread> tv;
     for (int i = 0; i < threads; i++) tv.emplace_back(worker);
     for (auto& t : tv) t.join();
+    for (size_t i = 0; i < smp.size(); i++)
+        if (smp[i].set) add_sample(fb, W, H, smp[i].x, smp[i].y, smp[i].L);
     if (stats) { stats[0] = totalRays; stats[1] = acc[0]; stats[2] = acc[1]; stats[3] = acc[2]; }
     return totalRays;
 }

@@ -480,3 +480,26 @@ def test_device_sampler_tables_bit_exact(ctl, orc, dev, pass_index):
         assert np.array_equal(got2.view(np.uint32), want2.view(np.uint32))
     finally:
         pt.close()
+
+
+@pytest.mark.parametrize("ranks,rank,n", [(1, 0, 1), (1, 0, 4), (3, 1, 3), (8, 0, 8)])
+@pytest.mark.parametrize("config,scale,w,h", [(2, 0.25, 200, 136), (3, 0.003, 136, 72)])
+def test_render_passes_equals_sequential_passes(ctl, orc, tracer, dev, ranks, rank, n, config, scale, w, h):
+    """ctl_render_passes(first, n) == n rounds of ctl_sampler_generate + ctl_render_pass
+    (and the oracle's passes) bit for bit, on a shard of the tiles."""
+    d = scene(ctl, config, scale, w, h)
+    p = ctl.PTParams(1, 50, 5, 1, 64, ranks, rank, 0)
+    first = 5
+    want, wrays = oracle_render(orc, d, p, n, w, h, first_pass=first)
+    seq, srays = render_gpu(ctl, tracer, d, p, n, w, h, dev, first_pass=first)
+    tracer.params = p
+    fb = torch.zeros((w * h, 7), dtype=torch.float32, device=dev)
+    tracer.reset_rays()
+    tracer.render_passes(fb.data_ptr(), first, n)
+    torch.cuda.synchronize()
+    got = fb.cpu().numpy()
+    assert tracer.rays_traced() == srays == wrays
+    assert want[:, 6].sum() > 0
+    assert np.array_equal(seq.view(np.uint32), want.view(np.uint32))
+    bad = np.nonzero((want.view(np.uint32) != got.view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
