@@ -405,7 +405,7 @@ int resident_blocks(ctl_ctx* c, K kernel, size_t lds) {
 }
 
 // wavefront.hip
-int wavefront_pass(ctl_ctx* c, const PathParams& P, ctl_pixel* fb, bool stats, hipStream_t s);
+int wavefront_pass(ctl_ctx* c, const PathParams& P, const SampleSlots& SS, bool stats, hipStream_t s);
 void wavefront_free(ctl_ctx* c);
 // anim.hip
 struct WideNode;

@@ -953,15 +953,12 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
     const float* s1 = c->d_s1[c->active];
     const float2* s2 = c->d_s2[c->active];
     CTL_HIP(c, hipEventRecord(c->pass_ev[0], s));
-    const bool slots = !(p->flags & CTL_PT_WAVEFRONT);   // the path kernels store samples per work item
-    if (slots) {
-        ctl_status r1 = prepare_slots(c, threads, s);
-        if (r1 != CTL_OK) return r1;
-    }
+    ctl_status r1 = prepare_slots(c, threads, s);   // every schedule stores samples per work item
+    if (r1 != CTL_OK) return r1;
     ctl_status r2 = launch_schedule(c, p, P, fb, stats, s, threads, grid, s1, s2,
                                     SampleSlots{c->d_slices, (uint32_t)threads}, 0);
     if (r2 != CTL_OK) return r2;
-    if (slots) launch_fold(c, P, (uint32_t)threads, 1, fb, s);
+    launch_fold(c, P, (uint32_t)threads, 1, fb, s);
     CTL_HIP(c, hipEventRecord(c->pass_ev[1], s));
     c->pass_timed = true;
     return CTL_OK;
@@ -970,7 +967,7 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
 static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const PathParams& P, ctl_pixel* fb, bool stats,
                                   hipStream_t s, uint64_t threads, dim3 grid, const float* s1, const float2* s2,
                                   SampleSlots PS, uint32_t tbl) {
-    if (p->flags & CTL_PT_WAVEFRONT) return (ctl_status)ctl::wavefront_pass(c, P, fb, stats, s);
+    if (p->flags & CTL_PT_WAVEFRONT) return (ctl_status)ctl::wavefront_pass(c, P, PS, stats, s);
     const bool single = c->scene.single != 0;
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;

@@ -41,8 +41,16 @@ __device__ __forceinline__ uint32_t queue_push(uint32_t* count, bool want) {
     return want ? base + rank : 0xffffffffu;
 }
 
+// Samples go to per-work-item slots (store_sample, common.h), folded into the
+// framebuffer in image order after the pass.
+__device__ __forceinline__ void wf_store(const PathParams& P, const SampleSlots& SS, uint32_t i, f2 pX, spec col) {
+    uint32_t px, py;
+    work_pixel(P, i, px, py);
+    store_sample(P, SS, 0, i, px, py, pX, col);
+}
+
 __global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
-                                                        WfState W, uint64_t n_items, ctl_pixel* fb) {
+                                                        WfState W, uint64_t n_items, SampleSlots SS) {
     for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;; g += (uint64_t)gridDim.x * kBlock) {
         // keep whole waves in the loop so the ballot in queue_push sees every lane
         const bool inRange = g < n_items;
@@ -60,7 +68,7 @@ __global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S, PathParams P
             sensor_ray(S, pX, o, d);
         }
         const bool live = valid && P.max_path_length > 0;
-        if (valid && !live) add_sample(fb, P, pX, mk3s(0.0f) + (mk3s(1.0f) * 1.0f) * mk3s(0.0f));
+        if (valid && !live) wf_store(P, SS, (uint32_t)g, pX, mk3s(0.0f) + (mk3s(1.0f) * 1.0f) * mk3s(0.0f));
         const uint32_t slot = queue_push(&W.counts[0], live);
         if (live) {
             const uint32_t i = (uint32_t)g;
@@ -174,7 +182,7 @@ void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32
 
 template <bool FULL>
 __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
-                                                          WfState W, int bounce, ctl_pixel* fb) {
+                                                          WfState W, int bounce, SampleSlots SS) {
     const uint32_t count = W.counts[2 * bounce];
     const uint32_t* qin = W.q[bounce & 1];
     uint32_t* qout = W.q[(bounce + 1) & 1];
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams
                 W.meta[i] = make_uint4(meta.x, rng.d1 | (rng.d2 << 16), (uint32_t)v.depth | ((v.specular ? 1u : 0u) << 16),
                                        v.has_partials ? 1u : 0u);
                 if (v.has_partials && !meta.w) W.part[i] = make_float4(v.dudx, v.dudy, v.dvdx, v.dvdy);
-                if (terminated && !pushShadow) add_sample(fb, P, v.pX, mk3s(1.0f) * v.cl);
+                if (terminated && !pushShadow) wf_store(P, SS, i, v.pX, mk3s(1.0f) * v.cl);
                 if (pushShadow) {
                     W.sh_o[i] = make_float4(v.rori.x, v.rori.y, v.rori.z, sh.dist - S.ray_eps);
                     W.sh_d[i] = make_float4(sh.d.x, sh.d.y, sh.d.z, sh.dist);
@@ -237,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams
             } else {
                 // miss: loop ends; environment term of PathTracer.cu:98-111 (no env map -> 0)
                 v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);
-                add_sample(fb, P, v.pX, mk3s(1.0f) * v.cl);
+                wf_store(P, SS, i, v.pX, mk3s(1.0f) * v.cl);
             }
             W.cl[i] = make_float4(v.cl.x, v.cl.y, v.cl.z, v.pX.x);
         }
@@ -248,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams
     }
 }
 
-__global__ __launch_bounds__(kBlock) void wf_resolve_kernel(PathParams P, WfState W, int bounce, ctl_pixel* fb) {
+__global__ __launch_bounds__(kBlock) void wf_resolve_kernel(PathParams P, WfState W, int bounce, SampleSlots SS) {
     const uint32_t count = W.counts[2 * bounce + 1];
     for (uint32_t k = blockIdx.x * kBlock + threadIdx.x; k < count; k += gridDim.x * kBlock) {
         const uint32_t i = W.sq[k];
@@ -257,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void wf_resolve_kernel(PathParams P, WfStat
         spec cl = mk3(cl4.x, cl4.y, cl4.z);
         if (!W.sh_occ[i]) cl = cl + mk3(v.x, v.y, v.z);
         W.cl[i] = make_float4(cl.x, cl.y, cl.z, cl4.w);
-        if (v.w != 0.0f) add_sample(fb, P, mk2(cl4.w, W.cf[i].w), mk3s(1.0f) * cl);
+        if (v.w != 0.0f) wf_store(P, SS, i, mk2(cl4.w, W.cf[i].w), mk3s(1.0f) * cl);
     }
 }
 
@@ -276,7 +284,7 @@ void wavefront_free(ctl_ctx* c) {
     c->wf = WfState{};
 }
 
-int wavefront_pass(ctl_ctx* c, const PathParams& P, ctl_pixel* fb, bool stats, hipStream_t s) {
+int wavefront_pass(ctl_ctx* c, const PathParams& P, const SampleSlots& SS, bool stats, hipStream_t s) {
     const uint32_t owned = (P.num_tiles > P.rank) ? (P.num_tiles - P.rank + P.num_ranks - 1) / P.num_ranks : 0;
     const uint64_t items = (uint64_t)owned * P.tile_size * P.tile_size;
     if (items == 0) return 0;
@@ -303,20 +311,25 @@ int wavefront_pass(ctl_ctx* c, const PathParams& P, ctl_pixel* fb, bool stats, h
     const float2* s2 = c->d_s2[c->active];
     const int persist = c->cu_count * 8;
     const unsigned genBlocks = (unsigned)std::min<uint64_t>((items + kBlock - 1) / kBlock, (uint64_t)persist);
-    hipLaunchKernelGGL(wf_gen_kernel, dim3(genBlocks), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, items, fb);
+    // a path cut off by kMaxBounces stores nothing: its slot must read "no sample"
+    if (hipMemsetAsync(SS.s, 0, items * sizeof(float4), s) != hipSuccess) {
+        c->err = "wavefront: memset failed";
+        return CTL_ERR_HIP;
+    }
+    hipLaunchKernelGGL(wf_gen_kernel, dim3(genBlocks), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, items, SS);
     const int maxB = std::min(P.max_path_length, kMaxBounces);
     uint32_t* cursors = W.counts + 2 * (kMaxBounces + 2);
     for (int b = 0; b < maxB; b++) {
         const uint32_t* cnt = &W.counts[2 * b];
         launch_trace<0>(c, s, W.q[b & 1], cnt, &cursors[2 * b], stats);
         if (c->scene.full_shading)
-            hipLaunchKernelGGL((wf_shade_kernel<true>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, fb);
+            hipLaunchKernelGGL((wf_shade_kernel<true>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, SS);
         else
-            hipLaunchKernelGGL((wf_shade_kernel<false>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, fb);
+            hipLaunchKernelGGL((wf_shade_kernel<false>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, SS);
         const uint32_t* scnt = &W.counts[2 * b + 1];
         if (P.shadow_any_hit) launch_trace<1>(c, s, W.sq, scnt, &cursors[2 * b + 1], stats);
         else launch_trace<2>(c, s, W.sq, scnt, &cursors[2 * b + 1], stats);
-        hipLaunchKernelGGL(wf_resolve_kernel, dim3(persist), dim3(kBlock), 0, s, P, W, b, fb);
+        hipLaunchKernelGGL(wf_resolve_kernel, dim3(persist), dim3(kBlock), 0, s, P, W, b, SS);
     }
     if (hipGetLastError() != hipSuccess) { c->err = "wavefront: launch failed"; return CTL_ERR_HIP; }
     return 0;

@@ -503,3 +503,19 @@ def test_render_passes_equals_sequential_passes(ctl, orc, tracer, dev, ranks, ra
     assert np.array_equal(seq.view(np.uint32), want.view(np.uint32))
     bad = np.nonzero((want.view(np.uint32) != got.view(np.uint32)).any(axis=1))[0]
     assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
+
+
+@pytest.mark.parametrize("mode", ["persistent", "wavefront", "megakernel"])
+def test_colliding_samples_all_schedules(ctl, orc, tracer, dev, mode):
+    """Pass 5 at 200x136 has a pixel that receives two samples (a jittered
+    position rounds onto the neighbour, Image.cu:22-44): every schedule adds
+    both, in image order, like the oracle."""
+    w, h = 200, 136
+    d = scene(ctl, 2, 0.25, w, h)
+    p = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, {"persistent": 0, "megakernel": ctl.CTL_PT_MEGAKERNEL,
+                                             "wavefront": ctl.CTL_PT_WAVEFRONT}[mode])
+    want, wrays = oracle_render(orc, d, p, 2, w, h, first_pass=5)
+    got, grays = render_gpu(ctl, tracer, d, p, 2, w, h, dev, first_pass=5)
+    assert grays == wrays
+    assert want[:, 6].max() > 2          # the collision is there
+    assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
