@@ -364,6 +364,61 @@ struct Traverser {
         }
     }
 
+    // Sort the hit children near-first (5-comparator network on the entry
+    // distances; misses carry 0x7fffffff and sort last), take the nearest,
+    // push the others far-to-near, postpone a leaf.  Shared by the float and
+    // quantized 4-wide loops.
+    __device__ __forceinline__ void wide_advance(int k0, int k1, int k2, int k3, int c0, int c1, int c2, int c3,
+                                                 bool fast, int sp, int top1, int top2, LaneStack& st) {
+#define CTL_CX(KA, CA, KB, CB)                      \
+        {                                       \
+            const bool sw = KB < KA;            \
+            const int tk = sw ? KB : KA, tc = sw ? CB : CA; \
+            KB = sw ? KA : KB; CB = sw ? CA : CB; \
+            KA = tk; CA = tc;                   \
+        }
+        CTL_CX(k0, c0, k1, c1)
+        CTL_CX(k2, c2, k3, c3)
+        CTL_CX(k0, c0, k2, c2)
+        CTL_CX(k1, c1, k3, c3)
+        CTL_CX(k1, c1, k2, c2)
+#undef CTL_CX
+        if (fast) {
+            const int m = (k0 != 0x7fffffff) + (k1 != 0x7fffffff) + (k2 != 0x7fffffff) + (k3 != 0x7fffffff);
+            // far-to-near pushes c[m-1] .. c[1] land in slots sp .. sp+m-2
+            int* slot = &ctl_lds_stack[sp * kStackBlock + st.tid];
+            slot[0] = m == 4 ? c3 : (m == 3 ? c2 : c1);
+            slot[kStackBlock] = m == 4 ? c2 : c1;
+            slot[2 * kStackBlock] = c1;
+            int next, below, nsp;
+            if (m == 0) { next = top1; below = top2; nsp = sp - 1; }
+            else { next = c0; below = m == 1 ? top1 : c1; nsp = sp + m - 1; }
+            if (next < 0 && leafAddr >= 0) {
+                leafAddr = next;
+                next = below;
+                nsp--;
+            } else if (kLeaf2 && next < 0 && leaf2 >= 0) {
+                leaf2 = next;
+                next = below;
+                nsp--;
+            }
+            nodeAddr = next;
+            st.sp = nsp;
+        } else {
+            if (k3 != 0x7fffffff) st.push(c3);
+            if (k2 != 0x7fffffff) st.push(c2);
+            if (k1 != 0x7fffffff) st.push(c1);
+            nodeAddr = (k0 != 0x7fffffff) ? c0 : st.pop();
+            if (nodeAddr < 0 && leafAddr >= 0) {
+                leafAddr = nodeAddr;
+                nodeAddr = st.pop();
+            } else if (kLeaf2 && nodeAddr < 0 && leaf2 >= 0) {
+                leaf2 = nodeAddr;
+                nodeAddr = st.pop();
+            }
+        }
+    }
+
     // 4-wide inner-node loop over 128-B float nodes (host/bvh_wide.h).
     //  * slabs in packed fp32 (v_pk_mul_f32 / v_pk_add_f32 on child pairs, the
     //    same mul-then-sub rounding as the reference's scalar code);
@@ -473,118 +528,71 @@ struct Traverser {
             CTL_WIDE_CHILD(k3, ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y)
 #endif
 #undef CTL_WIDE_CHILD
-#define CTL_CX(KA, CA, KB, CB)                      \
-            {                                       \
-                const bool sw = KB < KA;            \
-                const int tk = sw ? KB : KA, tc = sw ? CB : CA; \
-                KB = sw ? KA : KB; CB = sw ? CA : CB; \
-                KA = tk; CA = tc;                   \
-            }
-            CTL_CX(k0, c0, k1, c1)
-            CTL_CX(k2, c2, k3, c3)
-            CTL_CX(k0, c0, k2, c2)
-            CTL_CX(k1, c1, k3, c3)
-            CTL_CX(k1, c1, k2, c2)
-#undef CTL_CX
-            if (fast) {
-                const int m = (k0 != 0x7fffffff) + (k1 != 0x7fffffff) + (k2 != 0x7fffffff) + (k3 != 0x7fffffff);
-                // far-to-near pushes c[m-1] .. c[1] land in slots sp .. sp+m-2
-                int* slot = &ctl_lds_stack[sp * kStackBlock + st.tid];
-                slot[0] = m == 4 ? c3 : (m == 3 ? c2 : c1);
-                slot[kStackBlock] = m == 4 ? c2 : c1;
-                slot[2 * kStackBlock] = c1;
-                int next, below, nsp;
-                if (m == 0) { next = top1; below = top2; nsp = sp - 1; }
-                else { next = c0; below = m == 1 ? top1 : c1; nsp = sp + m - 1; }
-                if (next < 0 && leafAddr >= 0) {
-                    leafAddr = next;
-                    next = below;
-                    nsp--;
-                } else if (kLeaf2 && next < 0 && leaf2 >= 0) {
-                    leaf2 = next;
-                    next = below;
-                    nsp--;
-                }
-                nodeAddr = next;
-                st.sp = nsp;
-            } else {
-                if (k3 != 0x7fffffff) st.push(c3);
-                if (k2 != 0x7fffffff) st.push(c2);
-                if (k1 != 0x7fffffff) st.push(c1);
-                nodeAddr = (k0 != 0x7fffffff) ? c0 : st.pop();
-                if (nodeAddr < 0 && leafAddr >= 0) {
-                    leafAddr = nodeAddr;
-                    nodeAddr = st.pop();
-                } else if (kLeaf2 && nodeAddr < 0 && leaf2 >= 0) {
-                    leaf2 = nodeAddr;
-                    nodeAddr = st.pop();
-                }
-            }
+            wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
             if (__popcll(__ballot(CTL_LEAF_BREAK_ON_SECOND && kLeaf2 ? leaf2 >= 0 : leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
-    // 4-wide loop over 64-B quantized nodes (ctl_qnode.h, CTL_SCENE_WIDE_QUANT).
+    // 4-wide loop over 64-B quantized nodes (ctl_qnode.h, CTL_SCENE_WIDE_QUANT):
+    // four 16-B loads per node instead of seven.  The near/far plane of each
+    // axis is a choice between two packed words (one byte per child), made per
+    // ray; each bound is decoded exactly as the encoder checked it
+    // (p + float(q) * s, mul then add), then the same slab test, sort and
+    // stack update as the float loop.
     __device__ __forceinline__ void inner_wide_quant(const DevScene& S, LaneStack& st, TraceStats* stats) {
-        const float4* nodes = (SINGLE || level) ? S.wbvh : S.scene_wbvh;
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        const char* nbytes = reinterpret_cast<const char*>((SINGLE || level) ? S.wbvh : S.scene_wbvh);
+        const v2f ix = {cur.idx, cur.idx}, iy = {cur.idy, cur.idy}, iz = {cur.idz, cur.idz};
+        const v2f ox = {cur.oodx, cur.oodx}, oy = {cur.oody, cur.oody}, oz = {cur.oodz, cur.oodz};
+        const int tminBits = __float_as_int(span_tmin);
+        const bool negx = __float_as_int(cur.idx) < 0, negy = __float_as_int(cur.idy) < 0;
+        const bool negz = __float_as_int(cur.idz) < 0;
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
-            float4 lox, hix, loy, hiy, loz, hiz;
-            int4 ch;
-            {
-                // 64-B node: decode p + q * s per bound (ctl_qnode.h), then the float slab test
-                const float4* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 4u;
-                const float4 a = n[0], b = n[1], c = n[2];
-                ch = reinterpret_cast<const int4*>(n)[3];
-                asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
-                const uint32_t wlx = __float_as_uint(b.z), whx = __float_as_uint(b.w);
-                const uint32_t wly = __float_as_uint(c.x), why = __float_as_uint(c.y);
-                const uint32_t wlz = __float_as_uint(c.z), whz = __float_as_uint(c.w);
-#define CTL_QDEC(W, P, SC, K) ((P) + (float)(((W) >> (8 * K)) & 0xffu) * (SC))
-#define CTL_QDEC4(W, P, SC) make_float4(CTL_QDEC(W, P, SC, 0), CTL_QDEC(W, P, SC, 1), CTL_QDEC(W, P, SC, 2), CTL_QDEC(W, P, SC, 3))
-                lox = CTL_QDEC4(wlx, a.x, a.w); hix = CTL_QDEC4(whx, a.x, a.w);
-                loy = CTL_QDEC4(wly, a.y, b.x); hiy = CTL_QDEC4(why, a.y, b.x);
-                loz = CTL_QDEC4(wlz, a.z, b.y); hiz = CTL_QDEC4(whz, a.z, b.y);
-#undef CTL_QDEC4
-#undef CTL_QDEC
-            }
+            const int sp = st.sp;
+            const bool fast = sp + 3 <= kLdsStack;
+            const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
+            const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
+            CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
             if (STATS) stats->nodes++;
+            const int tBits = __float_as_int(h.t);
+            const uint32_t off = (nodeBase + (uint32_t)nodeAddr) << 6;
+            const float4 qa = *reinterpret_cast<const float4*>(nbytes + off);
+            const float4 qb = *reinterpret_cast<const float4*>(nbytes + off + 16u);
+            const float4 qc = *reinterpret_cast<const float4*>(nbytes + off + 32u);
+            int4 ch = *reinterpret_cast<const int4*>(nbytes + off + 48u);
+            asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
+            const uint32_t wlx = __float_as_uint(qb.z), whx = __float_as_uint(qb.w);
+            const uint32_t wly = __float_as_uint(qc.x), why = __float_as_uint(qc.y);
+            const uint32_t wlz = __float_as_uint(qc.z), whz = __float_as_uint(qc.w);
+            const uint32_t nxw = negx ? whx : wlx, fxw = negx ? wlx : whx;
+            const uint32_t nyw = negy ? why : wly, fyw = negy ? wly : why;
+            const uint32_t nzw = negz ? whz : wlz, fzw = negz ? wlz : whz;
+#define CTL_QB(W, K) ((float)(((W) >> (8 * (K))) & 0xffu))
+#define CTL_QPAIR(W, P, SC, K0, K1) (v2f{(P), (P)} + v2f{CTL_QB(W, K0), CTL_QB(W, K1)} * v2f{(SC), (SC)})
+            const v2f nx01 = CTL_QPAIR(nxw, qa.x, qa.w, 0, 1) * ix - ox, nx23 = CTL_QPAIR(nxw, qa.x, qa.w, 2, 3) * ix - ox;
+            const v2f fx01 = CTL_QPAIR(fxw, qa.x, qa.w, 0, 1) * ix - ox, fx23 = CTL_QPAIR(fxw, qa.x, qa.w, 2, 3) * ix - ox;
+            const v2f ny01 = CTL_QPAIR(nyw, qa.y, qb.x, 0, 1) * iy - oy, ny23 = CTL_QPAIR(nyw, qa.y, qb.x, 2, 3) * iy - oy;
+            const v2f fy01 = CTL_QPAIR(fyw, qa.y, qb.x, 0, 1) * iy - oy, fy23 = CTL_QPAIR(fyw, qa.y, qb.x, 2, 3) * iy - oy;
+            const v2f nz01 = CTL_QPAIR(nzw, qa.z, qb.y, 0, 1) * iz - oz, nz23 = CTL_QPAIR(nzw, qa.z, qb.y, 2, 3) * iz - oz;
+            const v2f fz01 = CTL_QPAIR(fzw, qa.z, qb.y, 0, 1) * iz - oz, fz23 = CTL_QPAIR(fzw, qa.z, qb.y, 2, 3) * iz - oz;
+#undef CTL_QPAIR
+#undef CTL_QB
             int k0, k1, k2, k3, c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-#define CTL_WIDE_CHILD(K, C, comp)                                                                   \
-            {                                                                                        \
-                const float ax = lox.comp * cur.idx - cur.oodx, bx = hix.comp * cur.idx - cur.oodx;   \
-                const float ay = loy.comp * cur.idy - cur.oody, by = hiy.comp * cur.idy - cur.oody;   \
-                const float az = loz.comp * cur.idz - cur.oodz, bz = hiz.comp * cur.idz - cur.oodz;   \
-                const float cmin = span_begin(ax, bx, ay, by, az, bz, span_tmin);                    \
-                const float cmax = span_end(ax, bx, ay, by, az, bz, h.t);                            \
-                K = (cmax >= cmin && C != CTL_SENTINEL) ? __float_as_int(cmin) : 0x7fffffff;          \
+#define CTL_WIDE_CHILD(K, C, NX, FX, NY, FY, NZ, FZ)                                                    \
+            {                                                                                           \
+                const float cmin = __int_as_float(imax3(__float_as_int(NX), __float_as_int(NY),          \
+                                                        max(__float_as_int(NZ), tminBits)));             \
+                const float cmax = __int_as_float(imin3(__float_as_int(FX), __float_as_int(FY),          \
+                                                        min(__float_as_int(FZ), tBits)));                \
+                K = (cmax >= cmin && C != CTL_SENTINEL) ? __float_as_int(cmin) : 0x7fffffff;            \
             }
-            CTL_WIDE_CHILD(k0, c0, x)
-            CTL_WIDE_CHILD(k1, c1, y)
-            CTL_WIDE_CHILD(k2, c2, z)
-            CTL_WIDE_CHILD(k3, c3, w)
+            CTL_WIDE_CHILD(k0, c0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x)
+            CTL_WIDE_CHILD(k1, c1, nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y)
+            CTL_WIDE_CHILD(k2, c2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x)
+            CTL_WIDE_CHILD(k3, c3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y)
 #undef CTL_WIDE_CHILD
-#define CTL_CX(KA, CA, KB, CB)                      \
-            {                                       \
-                const bool sw = KB < KA;            \
-                const int tk = sw ? KB : KA, tc = sw ? CB : CA; \
-                KB = sw ? KA : KB; CB = sw ? CA : CB; \
-                KA = tk; CA = tc;                   \
-            }
-            CTL_CX(k0, c0, k1, c1)
-            CTL_CX(k2, c2, k3, c3)
-            CTL_CX(k0, c0, k2, c2)
-            CTL_CX(k1, c1, k3, c3)
-            CTL_CX(k1, c1, k2, c2)
-#undef CTL_CX
-            if (k3 != 0x7fffffff) st.push(c3);
-            if (k2 != 0x7fffffff) st.push(c2);
-            if (k1 != 0x7fffffff) st.push(c1);
-            nodeAddr = (k0 != 0x7fffffff) ? c0 : st.pop();
-            if (nodeAddr < 0 && leafAddr >= 0) {
-                leafAddr = nodeAddr;
-                nodeAddr = st.pop();
-            }
-            if (!__any(leafAddr >= 0)) break;
+            wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
+            if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
