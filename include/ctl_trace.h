@@ -354,7 +354,9 @@ CTL_API ctl_status ctl_intersect(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays,
 /* One progressive PathTracer pass (one sample per owned pixel) accumulated
  * into the caller's device framebuffer d_fb[width*height] (PixelData,
  * Engine/Image.cu:22-44).  Uses the tables from the last ctl_sampler_generate /
- * ctl_sampler_upload on the same stream.  Asynchronous on `stream`. */
+ * ctl_sampler_upload on the same stream.  Asynchronous on `stream`.  The
+ * samples go through per-context slots and are added to d_fb in image order
+ * (see DESIGN.md §5), so the passes of one context belong on one stream. */
 CTL_API ctl_status ctl_render_pass(ctl_ctx* ctx, const ctl_pt_params* params, ctl_pixel* d_fb,
                                    void* stream);
 
