@@ -1012,9 +1012,9 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
 // Only this rank's pixels are sources (pixel_work).
 __global__ __launch_bounds__(kBlock) void fold_samples_kernel(PathParams P, const float4* __restrict__ slots,
                                                               uint32_t per_pass, uint32_t n, ctl_pixel* fb) {
-    const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
-    if (q >= P.width * P.height) return;
-    const uint32_t x = q % P.width, y = q / P.width;
+    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= (uint64_t)P.width * P.height) return;
+    const uint32_t x = (uint32_t)(q % P.width), y = (uint32_t)(q / P.width);
     uint32_t ks[4];
     float codes[4];
     int nc = 0;
