@@ -41,7 +41,8 @@ constexpr int kStackMax = 128;
 
 // The wide inner-node loop hands over to the leaves once fewer than this many
 // lanes of the wave still look for a leaf (1 = the reference's rule: none;
-// C3 sweep: 1 -> 2098, 2 -> 2164, 4 -> 2225, 6 -> 2237, 8 -> 2216, 16 -> 2146 Mrays/s).
+// C3 sweep: 1 -> 2098, 2 -> 2164, 4 -> 2225, 6 -> 2237, 8 -> 2216, 16 -> 2146 Mrays/s;
+// later, with the current kernel, 5 / 6 / 7 agree within run-to-run noise, ~2250).
 // One-instance wide traversal: a lane that already postpones a leaf may park
 // a second one and keep visiting inner nodes (1), instead of leaving the
 // inner-node loop at its second leaf (0).  C3: 1 -> 2184, 0 -> 2202 Mrays/s.
@@ -49,7 +50,7 @@ constexpr int kStackMax = 128;
 #define CTL_LEAF2 0
 #endif
 #ifndef CTL_LEAF_BREAK
-#define CTL_LEAF_BREAK 6
+#define CTL_LEAF_BREAK 5
 #endif
 #ifndef CTL_LEAF_BREAK_ON_SECOND
 #define CTL_LEAF_BREAK_ON_SECOND 0   // count lanes with a free second leaf slot instead
