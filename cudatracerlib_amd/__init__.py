@@ -239,6 +239,17 @@ class HostScene:
         return d
 
 
+def bvh_stack_bound(nodes, root_value=0):
+    """(binary, 4-wide) worst-case traversal stack of a reference BVHNodeData
+    tree (ctl_host_bvh_stack_bound); nodes = ctypes array / pointer of BVHNode."""
+    out = (C.c_int32 * 2)()
+    n = len(nodes)
+    st = lib().ctl_host_bvh_stack_bound(C.cast(nodes, C.c_void_p), n, int(root_value), out)
+    if st != 0:
+        raise CTLError("ctl_host_bvh_stack_bound: " + (lib().ctl_host_last_error() or b"").decode())
+    return out[0], out[1]
+
+
 class Tracer:
     """Per-GPU traversal context (InitializeKernel/UpdateKernel/IntersectBuffers)."""
 
@@ -315,7 +326,12 @@ class Tracer:
                self._ctx, "ctl_variance_stats")
 
     def sync(self, stream=0):
+        """Wait for the stream; raises CTLError if a traversal stack overflowed since the last reset_rays."""
         _check(self._L.ctl_sync(self._ctx, stream), self._ctx, "ctl_sync")
+
+    def stack_bound(self):
+        """Worst-case traversal stack (entries per lane) of the uploaded scene."""
+        return int(self._L.ctl_scene_stack_bound(self._ctx))
 
 
 class PathTracer(Tracer):

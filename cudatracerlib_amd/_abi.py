@@ -176,6 +176,8 @@ SYMBOLS = [
     ("ctl_rays_traced", C.c_uint64, [_vp]),
     ("ctl_reset_rays", C.c_int32, [_vp, _vp]),
     ("ctl_sync", C.c_int32, [_vp, _vp]),
+    ("ctl_scene_stack_bound", C.c_int32, [_vp]),
+    ("ctl_host_bvh_stack_bound", C.c_int32, [_vp, C.c_uint64, C.c_int32, _vp]),
     ("ctl_intersect_stats", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, C.POINTER(C.c_uint64), _vp]),
     ("ctl_render_pass_stats", C.c_int32, [_vp, C.POINTER(PTParams), _vp, C.POINTER(C.c_uint64), _vp]),
     ("ctl_last_pass_ms", C.c_int32, [_vp, C.POINTER(C.c_float)]),

@@ -19,6 +19,7 @@ struct PathParams {
     uint32_t tile_size, tiles_x, num_tiles, num_ranks, rank;
     uint32_t nseq, len;
     int32_t shadow_any_hit;
+    int32_t direct;   // KEY_Direct: PathTrace<true> (NEE + MIS) or PathTrace<false>
     bool half_quirk;
 };
 
@@ -205,7 +206,7 @@ __device__ __forceinline__ f2 primary_ray(const DevScene& S, SamplerDev& rng, ui
     return pX;
 }
 
-// One closest hit of PathTrace<true> (PathTracer.cu:35-96): emission with MIS,
+// One closest hit of PathTrace<DIRECT> (PathTracer.cu:35-96; DIRECT = P.direct): emission with MIS,
 // BSDF sample, UniformSampleOneLight up to its occlusion test
 // (TraceAlgorithms.cu:44-73, 92-101; sampleEmitter KernelDynamicScene.cu:25-39),
 // throughput update and Russian roulette.  Returns false when RR ends the path.
@@ -258,7 +259,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
         const uint32_t li = N->lights[mat.node_light_index];
         const ctl_light L = S.lights[li];
         float misWeight = 1.0f;
-        if (!(v.depth == 1 || v.specular)) {
+        if (!(!P.direct || v.depth == 1 || v.specular)) {   // PathTracer.cu:66-67
             direct_rec dRec;
             dRec.ref = v.rori; dRec.refN = v.last_nor; dRec.p = dg.P; dRec.n = dg.n;
             dRec.d = v.rdir; dRec.dist = r.t; dRec.measure = kESolidAngle;
@@ -271,7 +272,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
     }
     spec f = FULL ? bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex) : diffuse_sample(mat, b, v.brdf_pdf, rng.next2());
     v.last_nor = dg.sys.n;
-    if ((mat.combined_type & kESmooth) != 0 && S.n_lights) {
+    if (P.direct && (mat.combined_type & kESmooth) != 0 && S.n_lights) {   // PathTracer.cu:82-83
         f2 sample = rng.next2();
         const uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
         uint32_t first = 0, cnt = nl;   // STL_upper_bound
@@ -377,10 +378,17 @@ struct ctl_ctx {
     hipEvent_t ev[2] = {nullptr, nullptr};
     int next_buf = 0, active = -1;
     unsigned long long* d_counters = nullptr;   // [0] rays [1] overflow [2..4] stats
-    uint32_t* d_cursors = nullptr;              // work cursors: [0] batch intersect [1] path pass
+    unsigned long long* h_overflow = nullptr;   // pinned host copy of d_counters[1], read at ctl_sync
+    bool overflow_seen = false;                 // sticky: a traversal stack overflowed since the last reset
+    // 64-bit work cursors ([0] batch intersect [1] path pass [2] prim pass): resident
+    // lanes fetch once more after the work runs out, which a 32-bit cursor
+    // near 2^32 items would wrap
+    unsigned long long* d_cursors = nullptr;
+    std::vector<std::pair<const void*, std::pair<size_t, int>>> resident;   // resident_blocks cache
     hipEvent_t pass_ev[2] = {nullptr, nullptr}; // bracket the last render pass (ctl_last_pass_ms)
     bool pass_timed = false;
     size_t wide_nodes = 0;
+    int stack_bound = 0;                        // worst-case traversal stack of the uploaded scene
     uint8_t* d_tile_flags = nullptr;            // PixelVarianceBuffer block flags
     size_t tile_flags_cap = 0;
     uint32_t* d_powers = nullptr;               // XORWOW step powers for sampler_kernel
@@ -395,13 +403,18 @@ struct ctl_ctx {
 namespace ctl {
 // Persistent grids = exactly the co-resident blocks (occupancy from the
 // compiled register/LDS footprint x CU count): no block waits for a slot and
-// the atomic work cursor spreads the pass evenly over all CUs.
+// the atomic work cursor spreads the pass evenly over all CUs.  Cached per
+// context (a context is bound to one device and one host thread at a time).
 template <class K>
 int resident_blocks(ctl_ctx* c, K kernel, size_t lds) {
+    const void* key = reinterpret_cast<const void*>(kernel);
+    for (const auto& e : c->resident) if (e.first == key && e.second.first == lds) return e.second.second;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess || per_cu <= 0)
         per_cu = 2;
-    return per_cu * c->cu_count;
+    const int nb = per_cu * c->cu_count;
+    c->resident.push_back({key, {lds, nb}});
+    return nb;
 }
 
 // wavefront.hip

@@ -25,7 +25,6 @@
 #include "../host/bvh_wide.h"
 #include "../ctl_qnode.h"
 #include "common.h"
-#include "balance.h"
 
 namespace ctl {
 void sampler_tables(uint64_t pass, uint32_t nseq, uint32_t len, float* seq1d, float* seq2d);
@@ -56,24 +55,10 @@ static_assert(sizeof(ctl_pixel_variance) == 44, "PixelVarianceInfo is 44 B");
                               // wide-node step: 2: 1576, 3: 1590, 4: 1666, 5: 1601, 6: 1505 Mrays/s
 #endif
 
-#ifndef CTL_TAIL
-#define CTL_TAIL 1   // persistent path kernel: suspend the trace once fewer lanes than this still traverse
-#endif
-
 namespace {
 
-constexpr int kTail = CTL_TAIL;
-#ifndef CTL_BALANCE
-#define CTL_BALANCE 0   // persistent path kernel: idle lanes take subtrees of busy lanes' rays (balance.h; measured slower, see DESIGN)
-#endif
-
-// dynamic LDS of path_kernel_persistent: lane stacks + parked traversal state
-template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
-constexpr size_t persistent_lds_bytes() {
-    return kStackLdsBytes + sizeof(int) * kStackBlock +
-           (kTail > 1 ? sizeof(int) * kStackBlock * Traverser<2, STATS, SINGLE, WIDE, FULL>::kSaveFields
-                      : (SINGLE && WIDE && !STATS && CTL_BALANCE ? kBalLdsBytes : 0));
-}
+// dynamic LDS of path_kernel_persistent: lane stacks + the work item word per lane
+constexpr size_t persistent_lds_bytes() { return kStackLdsBytes + sizeof(int) * kStackBlock; }
 
 // Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
 // traversals inline in the bounce, as the reference's pathKernel2 runs it.
@@ -209,19 +194,6 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
     }
 }
 
-// Persistent path kernel (default schedule).  A resident grid of lanes, each
-// owning one path at a time and one resumable traversal (Traverser::round):
-//  * a lane alternates extension ray -> shade_hit -> shadow ray -> ... ; the
-//    NEE shadow ray is traced right after the bounce that made it, so the
-//    radiance sums happen in the reference's order;
-//  * a lane whose traversal finished shades and starts its next ray before
-//    the next traversal round, and a lane whose path ended does AddSample and
-//    takes the next pixel of the pass from a wave-aggregated atomic cursor;
-//    waves therefore stay full through long rays and the RR tail;
-//  * exactly one traversal and one shading site in the kernel (one I-cache
-//    footprint, lower VGPR peak).
-// Pixels are independent (own sampler index, single owner in the framebuffer)
-// so the framebuffer is bit-identical to path_kernel's.
 // Persistent path kernel with path regeneration (default schedule).  A
 // resident grid of lanes, each owning one path at a time:
 //  * every iteration a lane traces its pending ray to completion (extension
@@ -229,22 +201,22 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
 //    site in the kernel, then shades / resolves it; the shadow ray is traced
 //    right after the bounce that made it, so radiance sums happen in the
 //    reference's order;
-//  * a lane whose path ended does AddSample and takes the next pixel of the
-//    pass from a wave-aggregated atomic cursor, so waves stay full through
+//  * a lane whose path ended stores its sample and takes the next work item
+//    from a wave-aggregated 64-bit atomic cursor, so waves stay full through
 //    the Russian-roulette tail instead of idling until their longest path
 //    ends;
 //  * the traverser is local to an iteration: only the path variables and the
 //    pending ray are loop-carried, keeping the register peak low.
-// Pixels are independent (own sampler index, single owner in the framebuffer)
-// so the framebuffer is bit-identical to path_kernel's.
+// Work items are independent (own sampler index, own sample slot), so the
+// framebuffer is bit-identical to path_kernel's.
 template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? (FULL ? CTL_PERSIST_WAVES_FULL : CTL_PERSIST_WAVES) : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
-                                                                 const float2* s2, ctl_pixel* fb, uint64_t items,
-                                                                 uint32_t* cursor, unsigned long long* counters,
+                                                                 const float2* s2, uint64_t items,
+                                                                 unsigned long long* cursor, unsigned long long* counters,
                                                                  SampleSlots PS, uint32_t tbl) {
     // Work item k renders pass slot k / PS.per_pass (sampler tables at
     // s1/s2 + slot * tbl) of work item k % PS.per_pass; every finished sample
-    // goes to its own slot, folded into fb afterwards (store_sample).
+    // goes to its own slot, folded into the framebuffer afterwards (store_sample).
     CTL_LANE_STACK(st);
     SamplerDev rng{s1, s2, P.nseq, P.len, 0, 0, 0, 0};
     // work item of the lane's path (pass slot * PS.per_pass + item), parked in
@@ -261,7 +233,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
     sh.dist = 0.0f;
     TraceStats ts{0, 0, 0};
     uint32_t rays = 0;
-    bool active = false, exhausted = false, shadowPhase = false, ending = false, ok = true, resumed = false;
+    bool active = false, exhausted = false, shadowPhase = false, ending = false, ok = true;
 #ifdef CTL_PROFILE_TRACE
     long long prof_trace = 0;
     const long long prof_start = wall_clock64();
@@ -273,32 +245,35 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
         const uint64_t mask = __ballot(need);
         if (mask) {
             const int leader = __ffsll((unsigned long long)mask) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(cursor, (uint32_t)__popcll(mask));
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
             base = __shfl(base, leader);
             if (need) {
-                const uint32_t k = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-                uint32_t px, py, ps, kk;
-                split(k, ps, kk);
-                if (k >= items) {
+                const uint64_t k64 = base + (uint64_t)__popcll(mask & ((1ull << lane) - 1ull));
+                if (k64 >= items) {
                     exhausted = true;
-                } else if (work_pixel(P, kk, px, py)) {
-                    const uint32_t idx = py * P.width + px;
-                    // the pass slot's tables start ps * tbl elements in: folded into
-                    // the two sequence offsets so the table bases stay kernel-uniform
-                    rng.a = idx % P.nseq + ps * tbl; rng.b = (idx / P.nseq) % P.nseq + ps * tbl;
-                    rng.d1 = 0; rng.d2 = 0;
-                    *pkw = (int)k;
-                    f3 o, dw;
-                    const f2 pX = primary_ray(S, rng, px, py, o, dw);
-                    v.begin(pX, o, dw);
-                    shadowPhase = false;
-                    ending = false;
-                    // loop head of PathTrace: `while (depth++ < MaxPathLength)`
-                    if (v.depth++ < P.max_path_length) active = true;
-                    else store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
                 } else {
-                    PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // work item outside the image: no sample
+                    const uint32_t k = (uint32_t)k64;   // items < 2^32 (checked on the host)
+                    uint32_t px, py, ps, kk;
+                    split(k, ps, kk);
+                    if (work_pixel(P, kk, px, py)) {
+                        const uint32_t idx = py * P.width + px;
+                        // the pass slot's tables start ps * tbl elements in: folded into
+                        // the two sequence offsets so the table bases stay kernel-uniform
+                        rng.a = idx % P.nseq + ps * tbl; rng.b = (idx / P.nseq) % P.nseq + ps * tbl;
+                        rng.d1 = 0; rng.d2 = 0;
+                        *pkw = (int)k;
+                        f3 o, dw;
+                        const f2 pX = primary_ray(S, rng, px, py, o, dw);
+                        v.begin(pX, o, dw);
+                        shadowPhase = false;
+                        ending = false;
+                        // loop head of PathTrace: `while (depth++ < MaxPathLength)`
+                        if (v.depth++ < P.max_path_length) active = true;
+                        else store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
+                    } else {
+                        PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // work item outside the image: no sample
+                    }
                 }
             }
         }
@@ -306,64 +281,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             if (__all(exhausted)) break;
             continue;
         }
-        // one-instance scenes with the 4-wide tree: the wave balances its
-        // traversals (balance.h); every lane takes part, with or without a ray
-        constexpr bool kBalance = SINGLE && WIDE && !STATS && CTL_BALANCE && kTail <= 1;
-        HitRec h;
         if (active) {
+            HitRec h;
             h.t = (shadowPhase && shadowAny) ? sh.dist - S.ray_eps : FLT_MAX;
             h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
-            if (!resumed) rays++;
-        }
-        if (kBalance) {
+            rays++;
+#ifdef CTL_PROFILE_TRACE
+            const long long pc0 = wall_clock64();
+#endif
             if (S.n_nodes != 0) {
-#ifdef CTL_PROFILE_TRACE
-                const long long pc0 = wall_clock64();
-#endif
-                const HitRec hb = trace_balanced<STATS, FULL>(S, st, &ts, active, v.rori, shadowPhase ? sh.d : v.rdir,
-                                                              h.t, shadowPhase && shadowAny);
-                if (active) h = hb;
+                Traverser<2, STATS, SINGLE, WIDE, FULL> T;
+                T.anyhit = shadowPhase && shadowAny;
+                T.init(S, v.rori, shadowPhase ? sh.d : v.rdir, 0.0f, S.ray_eps, h.t, st, &ts);
+                while (!T.done) T.round(S, st, &ts);
+                h = T.h;
                 ok &= !st.overflow;
-#ifdef CTL_PROFILE_TRACE
-                prof_trace += wall_clock64() - pc0;
-#endif
             }
-        }
-        if (active) {
-            if (!kBalance) {
 #ifdef CTL_PROFILE_TRACE
-                const long long pc0 = wall_clock64();
+            prof_trace += wall_clock64() - pc0;
 #endif
-                if (S.n_nodes != 0) {
-                    typedef Traverser<2, STATS, SINGLE, WIDE, FULL> Tr;
-                    Tr T;
-                    int* park = ctl_lds_stack + kExtraLdsOff;
-                    if (kTail > 1 && resumed) {
-                        T.restore(S, park, st.tid, 0.0f, S.ray_eps);
-                    } else {
-                        T.anyhit = shadowPhase && shadowAny;
-                        T.init(S, v.rori, shadowPhase ? sh.d : v.rdir, 0.0f, S.ray_eps, h.t, st, &ts);
-                    }
-                    if (kTail > 1) {
-                        // trace until fewer than kTail lanes of the wave are still
-                        // traversing; those park their state and resume next
-                        // iteration while the others shade and take new rays
-                        do {
-                            if (!T.done) T.round(S, st, &ts);
-                        } while (__popcll(__ballot(!T.done)) >= kTail);
-                        resumed = !T.done;
-                        if (resumed) T.save(park, st.tid);
-                    } else {
-                        while (!T.done) T.round(S, st, &ts);
-                    }
-                    h = T.h;
-                    ok &= !st.overflow;
-                }
-#ifdef CTL_PROFILE_TRACE
-                prof_trace += wall_clock64() - pc0;
-#endif
-            }
-            if (resumed) continue;
             bool cont;
             if (shadowPhase) {
                 if (!shadow_occluded(S, shadowAny, h, sh.dist)) v.cl = v.cl + sh.add;
@@ -431,7 +367,7 @@ __attribute__((amdgpu_waves_per_eu(CTL_INTERSECT_WAVES)))
 #endif
 void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            int64_t n2, const ctl_ray* rays2, ctl_hit* hits2,
-                                                           uint32_t* cursor, unsigned long long* counters) {
+                                                           unsigned long long* cursor, unsigned long long* counters) {
     const int64_t total = n + n2;
     CTL_LANE_STACK(st);
     TraceStats ts{0, 0, 0};
@@ -457,8 +393,8 @@ void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
         const uint64_t mask = __ballot(need);
         if (mask && (__popcll(mask) >= CTL_REFILL_MIN || !__any(haveRay))) {
             const int leader = __ffsll((unsigned long long)mask) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(cursor, (uint32_t)__popcll(mask));
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
             base = __shfl(base, leader);
             if (need) {
                 const int64_t k = (int64_t)base + __popcll(mask & ((1ull << lane) - 1ull));
@@ -582,8 +518,9 @@ CTL_API ctl_ctx* ctl_create(int32_t device) {
         delete c;
         return fail("ctl_create: counter allocation failed");
     }
-    if (hipMalloc(&c->d_cursors, 16 * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(c->d_cursors, 0, 16 * sizeof(uint32_t)) != hipSuccess ||
+    if (hipMalloc(&c->d_cursors, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_cursors, 0, 16 * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc(&c->h_overflow, sizeof(unsigned long long)) != hipSuccess ||
         hipEventCreate(&c->pass_ev[0]) != hipSuccess || hipEventCreate(&c->pass_ev[1]) != hipSuccess) {
         ctl_destroy(c);
         return fail("ctl_create: cursor/event allocation failed");
@@ -631,6 +568,7 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
     }
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_cursors) (void)hipFree(c->d_cursors);
+    if (c->h_overflow) (void)hipHostFree(c->h_overflow);
     if (c->d_tile_flags) (void)hipFree(c->d_tile_flags);
     for (int i = 0; i < 2; i++)
         if (c->pass_ev[i]) (void)hipEventDestroy(c->pass_ev[i]);
@@ -773,6 +711,36 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
         c->wide_nodes = wn.size();
     }
 #undef UP
+    // Worst-case traversal stack (host/bvh_wide.h), for every traversal the
+    // scene can take (the 4-wide trees, and the binary trees of stats launches
+    // and CTL_SCENE_BINARY_BVH): a scene that could overflow the kStackMax
+    // entries of a lane is refused here, so no ray can end early on a full
+    // stack.  Two levels: top-level stack + the pending top-level entry + the
+    // mesh stack (its sentinel included).
+    try {
+        int mesh_bin = 0, mesh_wide = 0;
+        for (uint32_t m = 0; m < d->n_meshes && d->n_bvh_nodes > 0; m++) {
+            const size_t first = d->meshes[m].bvh_node_offset / 4;
+            mesh_bin = std::max(mesh_bin, binary_stack_bound(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, kStackMax));
+            if (wide) mesh_wide = std::max(mesh_wide, wide_stack_bound(wn.data() + wbase[m], wn.size() - wbase[m], 0, kStackMax));
+        }
+        int bound = std::max(mesh_bin, mesh_wide);
+        if (d->n_nodes > 0 && d->scene_start_node >= 0) {
+            const int top_bin = binary_stack_bound(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, kStackMax);
+            const int top_wide = wide ? wide_stack_bound(sw.data(), sw.size(), 0, kStackMax) : 0;
+            bound = std::max(top_bin + 1 + mesh_bin, wide ? top_wide + 1 + mesh_wide : 0);
+        }
+        if (bound > kStackMax) {
+            free_scene(c);
+            c->err = "scene_upload: the BVH needs a deeper traversal stack than " + std::to_string(kStackMax) + " entries";
+            return CTL_ERR_INVALID;
+        }
+        c->stack_bound = bound;
+    } catch (const std::exception& e) {
+        free_scene(c);
+        c->err = std::string("scene_upload: ") + e.what();
+        return CTL_ERR_INVALID;
+    }
     S.bvh = reinterpret_cast<const float4*>(bvh);
     S.woop = reinterpret_cast<const float4*>(woop);
     S.scene_bvh = reinterpret_cast<const float4*>(sb);
@@ -862,18 +830,18 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
                                    ctl_hit* hits2 = nullptr) {
     if (!c || n < 0 || (n > 0 && (!rays || !hits)) || n2 < 0 || (n2 > 0 && (!rays2 || !hits2))) return CTL_ERR_INVALID;
     if (!c->has_scene) { c->err = "intersect: no scene uploaded"; return CTL_ERR_STATE; }
+    if (c->overflow_seen) return CTL_ERR_STATE;   // c->err names the overflow (ctl_sync)
     if (n + n2 > 0xffffffffll) { c->err = "intersect: more than 2^32-1 rays per call"; return CTL_ERR_INVALID; }
     CTL_HIP(c, hipSetDevice(c->device));
     if (n + n2 == 0) return CTL_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    uint32_t* cursor = c->d_cursors;
-    CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(uint32_t), s));
+    unsigned long long* cursor = c->d_cursors;
+    CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
     const bool single = c->scene.single != 0;
     const uint64_t want = ((uint64_t)(n + n2) + kBlock - 1) / kBlock;
 #define IK(AN, ST, SG, WD)                                                                                       \
     do {                                                                                                         \
-        static int nb = 0;                                                                                       \
-        if (!nb) nb = resident_blocks(c, intersect_kernel<AN, ST, SG, WD>, kStackLdsBytes);                      \
+        const int nb = resident_blocks(c, intersect_kernel<AN, ST, SG, WD>, kStackLdsBytes);                     \
         hipLaunchKernelGGL((intersect_kernel<AN, ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)),     \
                            dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, n2, rays2, hits2, cursor,  \
                            c->d_counters);                                                                       \
@@ -908,11 +876,11 @@ static ctl_status prepare_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb
                                bool need_tables = true) {
     if (!c || !p || !fb) return CTL_ERR_INVALID;
     if (!c->has_scene) { c->err = "render_pass: no scene uploaded"; return CTL_ERR_STATE; }
+    if (c->overflow_seen) return CTL_ERR_STATE;   // c->err names the overflow (ctl_sync)
     if (need_tables && c->active < 0) {
         c->err = "render_pass: no sampler tables (call ctl_sampler_generate)";
         return CTL_ERR_STATE;
     }
-    if (!p->direct) { c->err = "render_pass: only Direct=1 is supported"; return CTL_ERR_INVALID; }
     uint32_t ts = p->tile_size ? p->tile_size : 64;
     if (ts % 8 != 0) { c->err = "render_pass: tile_size must be a multiple of 8"; return CTL_ERR_INVALID; }
     uint32_t nr = p->num_ranks ? p->num_ranks : 1;
@@ -929,6 +897,7 @@ static ctl_status prepare_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb
     P.rank = p->rank;
     P.nseq = c->nseq; P.len = c->len;
     P.shadow_any_hit = p->shadow_any_hit;
+    P.direct = p->direct != 0;
     P.half_quirk = c->half_quirk;
     return CTL_OK;
 }
@@ -973,16 +942,15 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
     const bool wide = c->scene.wide != 0 && !stats;
     const bool full = c->scene.full_shading != 0;
     if (!(p->flags & CTL_PT_MEGAKERNEL)) {
-        uint32_t* cursor = c->d_cursors + 1;
-        CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(uint32_t), s));
+        unsigned long long* cursor = c->d_cursors + 1;
+        CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
         const uint64_t want = (threads + kBlock - 1) / kBlock;
 #define PK(ST, SG, WD, FU)                                                                                       \
         do {                                                                                                     \
-            static int nb = 0;                                                                                   \
-            constexpr size_t lds = persistent_lds_bytes<ST, SG, WD, FU>();                                      \
-            if (!nb) nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD, FU>, lds);                        \
+            constexpr size_t lds = persistent_lds_bytes();                                                      \
+            const int nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD, FU>, lds);                      \
             hipLaunchKernelGGL((path_kernel_persistent<ST, SG, WD, FU>), dim3((unsigned)std::min<uint64_t>(nb, want)), \
-                               dim3(kBlock), lds, s, c->scene, P, s1, s2, fb, threads, cursor,                   \
+                               dim3(kBlock), lds, s, c->scene, P, s1, s2, threads, cursor,                       \
                                c->d_counters, PS, tbl);                                                          \
         } while (0)
 #define PK2(ST, SG, WD) do { if (full) PK(ST, SG, WD, true); else PK(ST, SG, WD, false); } while (0)
@@ -1093,7 +1061,7 @@ CTL_API ctl_status ctl_render_passes(ctl_ctx* c, const ctl_pt_params* params, ui
     const uint64_t per_pass = (uint64_t)owned * P.tile_size * P.tile_size;
     if (per_pass == 0) return CTL_OK;
     const uint64_t items = per_pass * n_passes;
-    if (items > 0xffffffffull) { c->err = "render_passes: more than 2^32-1 work items"; return CTL_ERR_INVALID; }
+    if (items >= 0xffffffffull) { c->err = "render_passes: 2^32-1 or more work items"; return CTL_ERR_INVALID; }
     const size_t tbl = (size_t)c->nseq * c->len;
     if (c->mt_cap < n_passes) {
         CTL_HIP(c, hipStreamSynchronize(s));
@@ -1195,28 +1163,43 @@ int count_rays(ctl_ctx* c, uint64_t n, hipStream_t s) { return add_rays(c, n, s)
 
 extern "C" {
 
+static void note_overflow(ctl_ctx* c, unsigned long long lanes) {
+    if (!lanes) return;
+    c->overflow_seen = true;
+    c->err = "traversal stack overflow on " + std::to_string(lanes) + " lanes (results invalid; ctl_reset_rays clears)";
+}
+
 CTL_API uint64_t ctl_rays_traced(ctl_ctx* c) {
     if (!c) return 0;
     unsigned long long v[2] = {0, 0};
     if (hipSetDevice(c->device) != hipSuccess) return 0;
     if (hipDeviceSynchronize() != hipSuccess) return 0;
     if (hipMemcpy(v, c->d_counters, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return 0;
-    if (v[1]) c->err = "traversal stack overflow on " + std::to_string(v[1]) + " lanes";
+    note_overflow(c, v[1]);
     return v[0];
 }
+
+CTL_API int32_t ctl_scene_stack_bound(const ctl_ctx* c) { return c && c->has_scene ? c->stack_bound : 0; }
 
 CTL_API ctl_status ctl_reset_rays(ctl_ctx* c, void* stream) {
     if (!c) return CTL_ERR_INVALID;
     CTL_HIP(c, hipSetDevice(c->device));
     CTL_HIP(c, hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), reinterpret_cast<hipStream_t>(stream)));
+    c->overflow_seen = false;
     return CTL_OK;
 }
 
+// The sync point of the C ABI: waits for the stream, then reports a traversal
+// stack overflow of any earlier launch as CTL_ERR_STATE (sticky until
+// ctl_reset_rays; every later render / intersect call refuses to run).
 CTL_API ctl_status ctl_sync(ctl_ctx* c, void* stream) {
     if (!c) return CTL_ERR_INVALID;
     CTL_HIP(c, hipSetDevice(c->device));
-    CTL_HIP(c, hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
-    return CTL_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    CTL_HIP(c, hipMemcpyAsync(c->h_overflow, c->d_counters + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    CTL_HIP(c, hipStreamSynchronize(s));
+    note_overflow(c, *c->h_overflow);
+    return c->overflow_seen ? CTL_ERR_STATE : CTL_OK;
 }
 
 static ctl_status read_stats(ctl_ctx* c, uint64_t out[4], uint64_t rays_before, hipStream_t s) {
@@ -1226,7 +1209,8 @@ static ctl_status read_stats(ctl_ctx* c, uint64_t out[4], uint64_t rays_before, 
     out[0] = v[0] - rays_before;
     out[1] = v[2]; out[2] = v[3]; out[3] = v[4];
     CTL_HIP(c, hipMemset(c->d_counters + 2, 0, 3 * sizeof(unsigned long long)));
-    if (v[1]) { c->err = "traversal stack overflow"; return CTL_ERR_STATE; }
+    note_overflow(c, v[1]);
+    if (c->overflow_seen) return CTL_ERR_STATE;
     return CTL_OK;
 }
 

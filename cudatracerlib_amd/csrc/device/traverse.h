@@ -43,17 +43,8 @@ constexpr int kStackMax = 128;
 // lanes of the wave still look for a leaf (1 = the reference's rule: none;
 // C3 sweep: 1 -> 2098, 2 -> 2164, 4 -> 2225, 6 -> 2237, 8 -> 2216, 16 -> 2146 Mrays/s;
 // later, with the current kernel, 5 / 6 / 7 agree within run-to-run noise, ~2250).
-// One-instance wide traversal: a lane that already postpones a leaf may park
-// a second one and keep visiting inner nodes (1), instead of leaving the
-// inner-node loop at its second leaf (0).  C3: 1 -> 2184, 0 -> 2202 Mrays/s.
-#ifndef CTL_LEAF2
-#define CTL_LEAF2 0
-#endif
 #ifndef CTL_LEAF_BREAK
 #define CTL_LEAF_BREAK 5
-#endif
-#ifndef CTL_LEAF_BREAK_ON_SECOND
-#define CTL_LEAF_BREAK_ON_SECOND 0   // count lanes with a free second leaf slot instead
 #endif
 
 struct DevScene {
@@ -209,13 +200,11 @@ __device__ __forceinline__ void xform_rows(const float4* M, f3 p, f3 d, f3& po, 
 // has alpha maps; the batch intersectKernel never alpha-tests.
 template <int ANY, bool STATS, bool SINGLE, bool WIDE = false, bool ALPHA = false>
 struct Traverser {
-    static constexpr bool kLeaf2 = CTL_LEAF2 && SINGLE && WIDE;
     RayLocal cur;
     RayLocal world;   // unused when SINGLE
     HitRec h;
     float span_tmin, tri_tmin;
     int nodeAddr, leafAddr, level, meshSent;
-    int leaf2;   // second postponed leaf (CTL_LEAF2, one-instance wide traversal), 0 = none
     uint32_t nodeBase, triBase, idxBase, triOffset, instIdx;
     bool done, resumeLeaves;
     bool anyhit;   // ANY == 2 only
@@ -237,7 +226,6 @@ struct Traverser {
         done = (S.n_nodes == 0);
         resumeLeaves = false;
         meshSent = 0;
-        leaf2 = 0;
         if (SINGLE) {
             // start_node < 0: TracerayTemplate calls the instance callback directly (BVHTraversal.h:130-131)
             if (STATS) stats->inst++;
@@ -254,54 +242,6 @@ struct Traverser {
             nodeBase = triBase = idxBase = triOffset = instIdx = 0;
             if (S.start_node < 0) { leafAddr = S.start_node; nodeAddr = CTL_SENTINEL; }
             else { leafAddr = 0; nodeAddr = WIDE ? 0 : S.start_node; }
-        }
-    }
-
-    // Suspended traversal state, parked in LDS ([field][thread] after the
-    // lane stacks, see path_kernel_persistent) while the rest of the wave
-    // shades; the lane's stack entries stay where they are.  Bit-exact resume:
-    // every field that round() reads is stored as is.
-    static constexpr int kSaveFields = SINGLE ? 21 : 40;
-    __device__ __forceinline__ void save(int* area, int tid) const {
-        int f = 0;
-        auto put = [&](int v) { area[(f++) * kStackBlock + tid] = v; };
-        auto putf = [&](float v) { put(__float_as_int(v)); };
-        putf(cur.ox); putf(cur.oy); putf(cur.oz); putf(cur.dx); putf(cur.dy); putf(cur.dz);
-        putf(cur.idx); putf(cur.idy); putf(cur.idz); putf(cur.oodx); putf(cur.oody); putf(cur.oodz);
-        putf(h.t); putf(h.u); putf(h.v); put((int)h.tri); put((int)h.node);
-        put(nodeAddr); put(leafAddr); put(leaf2);
-        put((resumeLeaves ? 1 : 0) | (anyhit ? 2 : 0));
-        if (!SINGLE) {
-            putf(world.ox); putf(world.oy); putf(world.oz); putf(world.dx); putf(world.dy); putf(world.dz);
-            putf(world.idx); putf(world.idy); putf(world.idz); putf(world.oodx); putf(world.oody); putf(world.oodz);
-            put(level); put(meshSent); put((int)nodeBase); put((int)triBase); put((int)idxBase);
-            put((int)triOffset); put((int)instIdx);
-        }
-    }
-    // span_tmin / tri_tmin are the caller's (they do not change during a trace)
-    __device__ __forceinline__ void restore(const DevScene& S, const int* area, int tid, float smin, float tmn) {
-        int f = 0;
-        auto get = [&]() { return area[(f++) * kStackBlock + tid]; };
-        auto getf = [&]() { return __int_as_float(get()); };
-        cur.ox = getf(); cur.oy = getf(); cur.oz = getf(); cur.dx = getf(); cur.dy = getf(); cur.dz = getf();
-        cur.idx = getf(); cur.idy = getf(); cur.idz = getf(); cur.oodx = getf(); cur.oody = getf(); cur.oodz = getf();
-        h.t = getf(); h.u = getf(); h.v = getf(); h.tri = (uint32_t)get(); h.node = (uint32_t)get();
-        nodeAddr = get(); leafAddr = get(); leaf2 = get();
-        const int fl = get();
-        resumeLeaves = (fl & 1) != 0;
-        anyhit = (fl & 2) != 0;
-        done = false;
-        span_tmin = smin; tri_tmin = tmn;
-        if (SINGLE) {
-            level = 1; meshSent = 0;
-            nodeBase = WIDE ? S.s_wnode_base : S.s_node_base;
-            triBase = S.s_tri_base; idxBase = S.s_idx_base; triOffset = S.s_tri_offset;
-            instIdx = ~(uint32_t)S.start_node;
-        } else {
-            world.ox = getf(); world.oy = getf(); world.oz = getf(); world.dx = getf(); world.dy = getf(); world.dz = getf();
-            world.idx = getf(); world.idy = getf(); world.idz = getf(); world.oodx = getf(); world.oody = getf(); world.oodz = getf();
-            level = get(); meshSent = get(); nodeBase = (uint32_t)get(); triBase = (uint32_t)get();
-            idxBase = (uint32_t)get(); triOffset = (uint32_t)get(); instIdx = (uint32_t)get();
         }
     }
 
@@ -398,10 +338,6 @@ struct Traverser {
                 leafAddr = next;
                 next = below;
                 nsp--;
-            } else if (kLeaf2 && next < 0 && leaf2 >= 0) {
-                leaf2 = next;
-                next = below;
-                nsp--;
             }
             nodeAddr = next;
             st.sp = nsp;
@@ -412,9 +348,6 @@ struct Traverser {
             nodeAddr = (k0 != 0x7fffffff) ? c0 : st.pop();
             if (nodeAddr < 0 && leafAddr >= 0) {
                 leafAddr = nodeAddr;
-                nodeAddr = st.pop();
-            } else if (kLeaf2 && nodeAddr < 0 && leaf2 >= 0) {
-                leaf2 = nodeAddr;
                 nodeAddr = st.pop();
             }
         }
@@ -530,7 +463,7 @@ struct Traverser {
 #endif
 #undef CTL_WIDE_CHILD
             wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
-            if (__popcll(__ballot(CTL_LEAF_BREAK_ON_SECOND && kLeaf2 ? leaf2 >= 0 : leafAddr >= 0)) < CTL_LEAF_BREAK) break;
+            if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
@@ -670,11 +603,6 @@ struct Traverser {
                 if (leafAddr != -214783648) {
                     leaf_tris(S, stats);
                     if (done) return;
-                }
-                if (kLeaf2 && leaf2 < 0) {
-                    leafAddr = leaf2;
-                    leaf2 = 0;
-                    continue;
                 }
                 leafAddr = nodeAddr;
                 if (nodeAddr < 0) nodeAddr = st.pop();

@@ -165,8 +165,7 @@ void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32
     const bool single = c->scene.single != 0;
 #define LT(ST, SG, WD, AL)                                                                                      \
     do {                                                                                                        \
-        static int blocks = 0;                                                                                  \
-        if (!blocks) blocks = resident_blocks(c, wf_trace_kernel<MODE, ST, SG, WD, AL>, kStackLdsBytes);        \
+        const int blocks = resident_blocks(c, wf_trace_kernel<MODE, ST, SG, WD, AL>, kStackLdsBytes);           \
         hipLaunchKernelGGL((wf_trace_kernel<MODE, ST, SG, WD, AL>), dim3(blocks), dim3(kBlock), kStackLdsBytes, s, \
                            c->scene, W, queue, cnt, cursor, c->d_counters);                                     \
     } while (0)

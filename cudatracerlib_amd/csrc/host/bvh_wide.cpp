@@ -4,6 +4,7 @@
 #include <cstring>
 #include <limits>
 #include <stdexcept>
+#include <string>
 
 namespace ctl {
 namespace {
@@ -100,4 +101,69 @@ int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_va
     return c.emit(root_value, 0);
 }
 
+namespace {
+// DFS over (child value, stack entries below the node); `kids` yields a node's
+// children, `inner` tells which of them are nodes to descend into.
+template <class KIDS>
+int stack_bound(size_t n_nodes, int32_t root, int cap, KIDS kids) {
+    std::vector<std::pair<int32_t, int>> todo;
+    todo.push_back({root, 1});   // the bottom sentinel
+    size_t visits = 0;
+    int best = 1;
+    while (!todo.empty()) {
+        const auto [v, below] = todo.back();
+        todo.pop_back();
+        if (++visits > n_nodes) throw std::runtime_error("BVH: a node is reached twice (not a tree)");
+        int32_t c[4];
+        const int nk = kids(v, c);
+        int used = 0;
+        for (int i = 0; i < nk; i++) used += c[i] != kSentinel;
+        const int here = below + (used > 0 ? used - 1 : 0);
+        if (here > best) best = here;
+        if (best > cap) return cap + 1;
+        for (int i = 0; i < nk; i++)
+            if (is_inner(c[i])) todo.push_back({c[i], here});
+    }
+    return best;
+}
+}  // namespace
+
+int binary_stack_bound(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, int cap) {
+    if (!is_inner(root_value)) return 1;
+    return stack_bound(n_nodes, root_value, cap, [&](int32_t v, int32_t c[4]) {
+        const size_t i = (size_t)v / 4;
+        if ((v & 3) != 0 || i >= n_nodes) throw std::runtime_error("BVH: child offset out of range");
+        std::memcpy(&c[0], &nodes[i].v[12], 4);
+        std::memcpy(&c[1], &nodes[i].v[13], 4);
+        return 2;
+    });
+}
+
+int wide_stack_bound(const WideNode* nodes, size_t n_nodes, int32_t root, int cap) {
+    if (!is_inner(root)) return 1;
+    return stack_bound(n_nodes, root, cap, [&](int32_t v, int32_t c[4]) {
+        if ((size_t)v >= n_nodes) throw std::runtime_error("wide BVH: child index out of range");
+        for (int k = 0; k < 4; k++) c[k] = nodes[v].child[k];
+        return 4;
+    });
+}
+
 }  // namespace ctl
+
+namespace ctl { void set_host_error(const std::string& s); }
+
+extern "C" CTL_API ctl_status ctl_host_bvh_stack_bound(const ctl_bvh_node* nodes, uint64_t n_nodes,
+                                                       int32_t root_value, int32_t out[2]) {
+    if (!nodes || !out || n_nodes == 0) { ctl::set_host_error("bvh_stack_bound: no nodes"); return CTL_ERR_INVALID; }
+    try {
+        out[0] = ctl::binary_stack_bound(nodes, n_nodes, root_value, 1024);
+        std::vector<ctl::WideNode> w;
+        const int32_t root = ctl::collapse_wide(nodes, n_nodes, root_value, w);
+        out[1] = ctl::wide_stack_bound(w.data(), w.size(), root, 1024);
+    } catch (const std::exception& e) {
+        ctl::set_host_error(std::string("bvh_stack_bound: ") + e.what());
+        return CTL_ERR_INVALID;
+    }
+    return CTL_OK;
+}
+

@@ -41,4 +41,14 @@ static_assert(sizeof(WideNode) == 128, "wide node is 128 B");
 int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out,
                       std::vector<uint32_t>* src = nullptr);
 
+// Worst-case traversal stack of a tree (entries, the bottom sentinel
+// included) for the traversal in device/traverse.h: a node pushes every
+// child but the one it descends into, so the deepest stack is 1 + the largest
+// sum of (children - 1) along a root-to-node path.  Children are counted
+// without sentinel / empty slots; leaves count (a leaf child can be pushed).
+// Throws on a malformed tree (offset out of range, a node reached twice).
+// Stops and returns `cap` + 1 once the bound passes `cap`.
+int binary_stack_bound(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, int cap);
+int wide_stack_bound(const WideNode* nodes, size_t n_nodes, int32_t root, int cap);
+
 }  // namespace ctl

@@ -483,8 +483,22 @@ CTL_API ctl_status ctl_variance_stats(ctl_ctx* ctx, const ctl_pixel_variance* d_
  * batched rays) since the last reset; 64-bit (the reference's counter is a
  * 32-bit atomicInc, Base/Platform.cu:12-21).  Synchronises the device. */
 CTL_API uint64_t ctl_rays_traced(ctl_ctx* ctx);
+/* Zeroes the ray counter and clears a recorded traversal stack overflow. */
 CTL_API ctl_status ctl_reset_rays(ctl_ctx* ctx, void* stream);
+/* The ABI's sync point (the reference's cudaDeviceSynchronize after a pass,
+ * Tracer.h:240, TraceHelper.cu:744): waits for the stream, then returns
+ * CTL_ERR_STATE if any traversal since the last ctl_reset_rays overflowed its
+ * stack (the ray's result is then invalid; the reference would have written
+ * past its int[64] local stack, BVHTraversal.h:14).  The overflow is sticky:
+ * render / intersect calls return CTL_ERR_STATE until ctl_reset_rays.  Scene
+ * upload already refuses a BVH whose worst-case stack could overflow, so this
+ * is a second line of defence. */
 CTL_API ctl_status ctl_sync(ctl_ctx* ctx, void* stream);
+
+/* Worst-case traversal stack (entries per lane) of the uploaded scene over
+ * every traversal it can take; ctl_scene_upload refuses scenes above the
+ * device stack depth (128).  0 without a scene. */
+CTL_API int32_t ctl_scene_stack_bound(const ctl_ctx* ctx);
 
 /* Traversal statistics for the roofline's algorithmic byte count (same kernel
  * compiled with counters; off in the timed path).  out[0]=rays,
@@ -497,6 +511,14 @@ CTL_API ctl_status ctl_render_pass_stats(ctl_ctx* ctx, const ctl_pt_params* para
 /* ------------------------------------------------------------------------ */
 /* Host helpers (no GPU needed): the reference's host-side compile step      */
 /* ------------------------------------------------------------------------ */
+
+/* Worst-case traversal stack of one reference BVH (BVHNodeData tree rooted at
+ * the child value root_value, SplitBVHBuilder.cpp:163-203): out[0] for the
+ * reference's binary order, out[1] for the 4-wide tree the upload collapses it
+ * into.  CTL_ERR_INVALID on a malformed tree (ctl_host_last_error).  Caps at
+ * 1024 (a bound above the cap reads 1025). */
+CTL_API ctl_status ctl_host_bvh_stack_bound(const ctl_bvh_node* nodes, uint64_t n_nodes, int32_t root_value,
+                                            int32_t out[2]);
 
 /* TriIntersectorData::setData (Engine/TriIntersectorData.cu:5-18). */
 CTL_API void ctl_woop_set(const float v0[3], const float v1[3], const float v2[3], ctl_woop_tri* out);

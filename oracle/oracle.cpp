@@ -678,8 +678,10 @@ Spec uniform_sample_one_light(RenderCtx& C, const BRec& bRec, const ctl_material
     return spec_div(estimate_direct(C, bRec, mat, d->lights[idx], pdf), pdf);
 }
 
-// PathTrace<true> restricted to surfaces without media / env map (PathTracer.cu:10-113)
-Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, V3 rXo, V3 rXd, V3 rYo, V3 rYd, int maxPathLength, int rrStartDepth) {
+// PathTrace<DIRECT> restricted to surfaces without media / env map (PathTracer.cu:10-113);
+// DIRECT = false: emission unweighted (:66-67), no UniformSampleOneLight (:82-83)
+Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, V3 rXo, V3 rXd, V3 rYo, V3 rYd, int maxPathLength, int rrStartDepth,
+                bool direct = true) {
     const ctl_scene_desc* d = C.S.d;
     Spec cl = v3s(0.0f), cf = v3s(1.0f);
     int depth = 0;
@@ -710,7 +712,7 @@ Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, V3 rXo, V3 rXd, V3 rYo, V3 rYd, 
             if (li != UINT_MAX) {
                 float misWeight = 1.0f;
                 const ctl_light& L = d->lights[li];
-                if (!(depth == 1 || specularBounce)) {
+                if (!(!direct || depth == 1 || specularBounce)) {
                     DRec dRec;   // DirectSamplingRecFromRay (TraceAlgorithms.cu:33-42)
                     dRec.ref = rori; dRec.refN = last_nor; dRec.p = bRec.dg.P; dRec.n = bRec.dg.n;
                     dRec.d = rdir; dRec.dist = r2.t; dRec.measure = ESolidAngle;
@@ -724,7 +726,7 @@ Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, V3 rXo, V3 rXd, V3 rYo, V3 rYd, 
             }
             Spec f = bsdf_sample(d, mat, bRec, brdf_scattering_pdf, C.rng->randomFloat2());
             last_nor = bRec.dg.sys.n;
-            if ((mat.combined_type & ESmooth) != 0) cl = cl + cf * uniform_sample_one_light(C, bRec, mat);
+            if (direct && (mat.combined_type & ESmooth) != 0) cl = cl + cf * uniform_sample_one_light(C, bRec, mat);
             specularBounce = (bRec.sampledType & EDelta) != 0;
             cf = cf * f;
             rori = bRec.dg.P;
@@ -1357,7 +1359,8 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
                 V3 o, dd, xo, dX, dY;
                 sensor_ray(cam, pX, o, dd);
                 sensor_ray_diff(cam, pX, xo, dX, dY);
-                Spec col = v3s(1.0f) * path_trace(C, o, dd, xo, dX, xo, dY, prm->max_path_length, prm->rr_start_depth);
+                Spec col = v3s(1.0f) * path_trace(C, o, dd, xo, dX, xo, dY, prm->max_path_length, prm->rr_start_depth,
+                                                   prm->direct != 0);
                 smp[lin] = Smp{pX.x, pX.y, col, true};
             }
         }

@@ -112,6 +112,28 @@ def test_render_pass_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, passe
     assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
 
 
+@pytest.mark.parametrize("config,scale,w,h", [(1, 1.0, 64, 64), (2, 0.25, 96, 64), (3, 0.003, 64, 48),
+                                              (5, 0.003, 64, 48)])
+@pytest.mark.parametrize("mode", ["persistent", "wavefront", "megakernel"])
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_render_direct0_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, mode, bvh):
+    """PathTrace<false> (KEY_Direct = 0, PathTracer.h:16): no UniformSampleOneLight,
+    emission unweighted (PathTracer.cu:62-70, 82-83), so no shadow rays at all."""
+    d = select_bvh(scene(ctl, config, scale, w, h), bvh)
+    p = ctl.PTParams(0, 50, 5, 1, 64, 1, 0, {"persistent": 0, "megakernel": ctl.CTL_PT_MEGAKERNEL,
+                                           "wavefront": ctl.CTL_PT_WAVEFRONT}[mode])
+    want, wrays = oracle_render(orc, d, p, 2, w, h)
+    got, grays = render_gpu(ctl, tracer, d, p, 2, w, h, dev)
+    assert grays == wrays
+    assert want[:, :3].max() > 0.0
+    bad = np.nonzero((want.view(np.uint32) != got.view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
+    # fewer rays than Direct=1: no NEE shadow rays
+    p1 = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, p.flags)
+    _, wrays1 = oracle_render(orc, d, p1, 1, w, h)
+    assert wrays < 2 * wrays1
+
+
 @pytest.mark.parametrize("mpl,rr", [(1, 5), (3, 1), (8, 2)])
 def test_render_short_paths_and_rr(ctl, orc, tracer, dev, mpl, rr):
     """MaxPathLength / RRStartDepth edge values (PathTracer.h:16-19)."""
