@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--shadow-any-hit", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wpt-passes", type=int, default=3, help="WavefrontPathTracer leg passes (0: skip)")
+    ap.add_argument("--closest-shadow-passes", type=int, default=4,
+                    help="passes of the leg with the reference's closest-hit Occluded shadow rays (0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--schedule", default="persistent", choices=["persistent", "megakernel", "wavefront"])
@@ -67,6 +69,72 @@ def parse():
     ap.add_argument("--bvh", default="wide", choices=["wide", "wideq", "binary"],
                     help="device traversal: 4-wide collapsed BVH, or the reference's binary order")
     return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+PEAK_HBM = 8000.0    # GB/s, MI355X_MICROARCH.md (HBM3E spec)
+PEAK_L2 = 34500.0    # GB/s, aggregate L2 rate, MI355X_MICROARCH.md (L2)
+
+
+def pmc_profile():
+    """Newest committed rocprofv3 counter summary (profiles/rNN_pmc.json,
+    tools_pmc.sh + tools_pmc_summary.py) and whether it was measured on the
+    libctl_trace.so this run loads."""
+    import glob
+    import hashlib
+    here = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(here, "profiles", "r[0-9][0-9]*_pmc.json")))
+    if not files:
+        return None, None, False
+    j = json.load(open(files[-1]))
+    lib = os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_trace.so")
+    match = hashlib.sha256(open(lib, "rb").read()).hexdigest() == j.get("lib_sha256")
+    return j, os.path.relpath(files[-1], here), match
+
+
+def roofline(prof, fam, ms, alg_bytes, kernel):
+    """Roofline of one kernel: physical HBM bytes (PMC counters of the same
+    binary) over its live per-launch time against the HBM peak, plus the L2 and
+    vector-memory-address-unit fractions that actually bind it.  The
+    algorithmic-byte model of SURVEY 8(d) is reported beside it as a model: the
+    4-wide tree and the caches serve those bytes, so it is not a fraction of
+    any hardware limit."""
+    j, path, match = prof
+    k = (j or {}).get("kernels", {}).get(fam, {})
+    hbm = k.get("hbm_bytes")
+    r = {"bound": "hbm", "achieved": None, "peak": PEAK_HBM, "unit": "GB/s", "frac": None, "traffic": hbm,
+         "kernel": kernel, "per_launch_ms": round(ms, 4)}
+    if hbm:
+        ach = hbm / (ms * 1e-3) / 1e9
+        r["achieved"] = round(ach, 2)
+        r["frac"] = r["frac_hbm"] = round(ach / PEAK_HBM, 4)
+    if k.get("l2_read_bytes"):
+        r["frac_l2"] = round(k["l2_read_bytes"] / (ms * 1e-3) / 1e9 / PEAK_L2, 4)
+    if k.get("ta_busy") is not None:
+        r["frac_ta"] = round(k["ta_busy"], 4)
+        r["binding_unit"] = ("vector-memory address unit (TA)" if k["ta_busy"] > 0.5 else
+                             "latency / issue (no unit above 50 %)")
+    for key in ("l2_hit_rate", "ta_cycles_per_vmem_wave_inst", "valu_lane_util"):
+        if key in k:
+            r[key] = round(k[key], 4)
+    if k.get("counters_per_launch", {}).get("SQ_INSTS_VMEM_RD") is not None:
+        r["vmem_rd_wave_insts_per_launch"] = k["counters_per_launch"]["SQ_INSTS_VMEM_RD"]
+    r["profile"] = path
+    r["profile_matches_binary"] = match
+    r["alg_model"] = {"bytes_per_launch": int(alg_bytes), "gbs": round(alg_bytes / (ms * 1e-3) / 1e9, 2),
+                      "note": "SURVEY 8(d) model: 64 B per inner node, 52 B per triangle test, 108 B per "
+                              "instance entry of the reference's binary traversal of the same rays; L2-served, "
+                              "not a bound"}
+    return r
 
 
 def cpu_baseline(desc, params, seconds, threads):
@@ -95,12 +163,14 @@ def cpu_baseline(desc, params, seconds, threads):
         "kind": "port",
         "sample": f"oracle PathTrace<true> on the same scene, every 4th pixel of {passes} pass(es), "
                   f"{rays} rays in {el:.1f} s",
+        "cpu_model": cpu_model(),
+        "nproc": os.cpu_count(),
         "ref_nodes_per_ray": round(float(stats[1]) / max(1, float(stats[0])), 3),
         "ref_tris_per_ray": round(float(stats[2]) / max(1, float(stats[0])), 3),
     }
 
 
-def primary_ray_leg(pt, dev, stream, sptr, torch, pass_index, launches=10):
+def primary_ray_leg(pt, dev, stream, sptr, torch, pass_index, prof, launches=10):
     """Primary-ray traversal through the batch C-ABI (ctl_camera_rays ->
     ctl_intersect): SURVEY §8(d)'s "C3 primary rays" roofline.  Algorithmic
     bytes per launch = 64*inner visits + 52*tri tests + 108*instance entries
@@ -124,18 +194,46 @@ def primary_ray_leg(pt, dev, stream, sptr, torch, pass_index, launches=10):
         ev.append((e0, e1))
     torch.cuda.synchronize(dev)
     ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / launches
-    achieved = alg / (ms * 1e-3) / 1e9
+    kname = "intersect_kernel<closest,single,wide> (ctl_intersect over ctl_camera_rays)"
+    rl = roofline(prof, "primary_intersect", ms, alg, kname)
+    rl["alg_model"].update({"inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3])})
     return {
-        "kernel": "intersect_kernel<closest,single> (ctl_intersect over ctl_camera_rays)",
-        "note": "coherent camera rays reuse the top BVH levels from L2/MALL, so the algorithmic-byte "
-                "model exceeds the HBM traffic here and frac > 1; the path kernel's roofline is the bound",
+        "kernel": kname,
         "rays_per_launch": int(n),
         "ms_per_launch": round(ms, 4),
         "mrays_s": round(n / ms / 1e3, 2),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
-                     "frac": round(achieved / 8000.0, 4), "alg_bytes_per_launch": int(alg),
-                     "inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3])},
+        "roofline": rl,
     }
+
+
+def closest_shadow_leg(pt, fb, stream, sptr, torch, pass_index, passes):
+    """The same pass with the reference's own KernelDynamicScene::Occluded
+    (a closest-hit shadow traversal tested against the light distance,
+    KernelDynamicScene.cu:70-80) instead of any-hit shadow rays: the image is
+    identical, the traversal work is not."""
+    old = pt.params.shadow_any_hit
+    pt.params.shadow_any_hit = 0
+    try:
+        pt.generate_samples(pass_index, sptr)
+        pt.render_pass(fb.data_ptr(), sptr)   # warm-up
+        torch.cuda.synchronize()
+        pt.reset_rays(sptr)
+        ev = []
+        for k in range(passes):
+            pt.generate_samples(pass_index + 1 + k, sptr)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            pt.render_pass(fb.data_ptr(), sptr)
+            e1.record(stream)
+            ev.append((e0, e1))
+        pt.sync(sptr)
+        ms = sum(e0.elapsed_time(e1) for e0, e1 in ev)
+        rays = pt.rays_traced()
+    finally:
+        pt.params.shadow_any_hit = old
+    return {"shadow_rays": "closest hit + distance test (reference Occluded)", "passes": passes,
+            "ms_per_pass": round(ms / passes, 3), "mrays_s": round(rays / (ms * 1e-3) / 1e6, 2)}
 
 
 def wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_index, passes):
@@ -278,11 +376,19 @@ def main():
     elapsed = time.perf_counter() - t0
     step_ms = ev0.elapsed_time(ev1)
     kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in kev)
+    pt.sync(sptr)   # raises if any traversal of the timed region overflowed its stack
 
     rays = pt.rays_traced()
-    prim = primary_ray_leg(pt, dev, stream, sptr, torch, pass_base + a.steps * shards) if rank == 0 else None
-    wpt = (wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_base + a.steps * shards + 1, a.wpt_passes)
+    prof = pmc_profile()
+    nxt = pass_base + a.steps * shards
+    prim = primary_ray_leg(pt, dev, stream, sptr, torch, nxt, prof) if rank == 0 else None
+    wpt = (wpt_leg(ctl, pt, dev, sptr, torch, W, H, nxt + 1, a.wpt_passes)
            if rank == 0 and a.wpt_passes > 0 else None)
+    closest = None
+    if rank == 0 and a.closest_shadow_passes > 0 and shards == 1:
+        scratch = torch.zeros_like(fb)
+        closest = closest_shadow_leg(pt, scratch, stream, sptr, torch, nxt + 10, a.closest_shadow_passes)
+        del scratch
     red = dev if a.backend == "nccl" else torch.device("cpu")
     tt = torch.tensor([elapsed], dtype=torch.float64, device=red)
     rr = torch.tensor([rays], dtype=torch.int64, device=red)
@@ -299,16 +405,17 @@ def main():
         launches = len(kev)   # path-kernel launches on this rank in the timed region
         per_launch_ms = kernel_ms / launches
         passes_per_launch = shards   # one ctl_render_passes launch per step when sharded
-        achieved = alg_bytes_per_pass * passes_per_launch / (per_launch_ms * 1e-3) / 1e9
-        traffic = None
-        tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
-        if os.path.exists(tf):
-            try:
-                j = json.load(open(tf))
-                if j.get("config") == [a.config, a.scale, W, H] and world == 1:
-                    traffic = j.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        fam = "path_kernel_full" if a.config == 5 else "path_kernel"
+        same_workload = (prof[0] or {}).get("config") == [a.config, a.scale, W, H] and passes_per_launch == 1
+        rl = roofline(prof if same_workload else (None, None, False), fam, per_launch_ms,
+                      alg_bytes_per_pass * passes_per_launch, KERNEL_NAME[a.schedule])
+        rl.update({"launches_timed": launches, "gpu_step_ms": round(step_ms / a.steps, 3),
+                   "passes_per_launch": passes_per_launch,
+                   "visits_per_launch": {"inner_nodes": int(st[1]), "tri_tests": int(st[2]),
+                                         "instances": int(st[3]), "rays": int(st[0])}})
+        if passes_per_launch > 1:
+            rl["launch"] = ("ctl_render_passes: the step's sampler tables, one path-kernel launch over all its "
+                            "passes, slice fold (all inside the bracket)")
         out = {
             "metric": "Mrays/s (primary+secondary) at 1920x1080, San-Miguel-scale BVH",
             "value": round(total_rays / elapsed / 1e6, 3),
@@ -339,29 +446,9 @@ def main():
                 "total_rays": total_rays,
                 **({"emulated_ranks": shards} if shards != world else {}),
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": 8000.0,
-                "unit": "GB/s",
-                "frac": round(achieved / 8000.0, 4),
-                "traffic": traffic,
-                "kernel": KERNEL_NAME[a.schedule],
-                "note": "achieved = algorithmic bytes of the reference's binary traversal of the same rays "
-                        "(64 B/inner node, 52 B/triangle test, 108 B/instance entry; SURVEY 8d) / kernel time; "
-                        "the 4-wide tree and L2 residency (97.9 % hits) serve them, so frac can pass 1; "
-                        "physical HBM bytes per launch are in `traffic`",
-                "launches_timed": launches,
-                "gpu_step_ms": round(step_ms / a.steps, 3),
-                "alg_bytes_per_launch": int(alg_bytes_per_pass * passes_per_launch),
-                "passes_per_launch": passes_per_launch,
-                **({"launch": "ctl_render_passes: the step's sampler tables, one path-kernel launch over all "
-                              "its passes, slice fold (all inside the bracket)"} if passes_per_launch > 1 else {}),
-                "per_launch_ms": round(per_launch_ms, 3),
-                "visits_per_launch": {"inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3]),
-                                      "rays": int(st[0])},
-            },
+            "roofline": rl,
             "primary_rays": prim,
+            "closest_hit_shadows": closest,
             "wavefront_tracer": wpt,
             "image_weight_sum": wsum,
             "scene_build_s": round(t_build, 2),

@@ -1,59 +1,81 @@
-"""Summarise rocprofv3 --pmc csv output per kernel family (sum over dispatches)
-and write profiles/traffic.json for bench.py's roofline "traffic" field.
+"""Summarise rocprofv3 --pmc csv output (tools_pmc.sh) per kernel family and
+write gpurun_out/pmc/pmc.json, which bench.py reads (copied to
+profiles/rNN_pmc.json) for the roofline fractions of the same binary:
 
-HBM bytes per launch of the timed pass kernel = (2 x FETCH_SIZE + WRITE_SIZE)
-x 1024 / launches: FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
-reports half the bytes of 16-B-per-lane reads (MI355X_MICROARCH.md, HBM
-section), hence the factor 2 on the read side."""
+  hbm_bytes      (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per launch; FETCH_SIZE /
+                 WRITE_SIZE are KiB, and on gfx950 FETCH_SIZE reports half the
+                 bytes of 16-B-per-lane reads (MI355X_MICROARCH.md, HBM)
+  l2_read_bytes  TCP_TCC_READ_REQ x 128 B per launch (an upper bound: a request
+                 moves at most one 128-B line)
+  ta_busy        TA_TA_BUSY_sum / (256 TAs x GRBM_GUI_ACTIVE / 8 XCDs): the
+                 fraction of the kernel's cycles the vector-memory address
+                 unit of a CU is busy
+  cycles         GRBM_GUI_ACTIVE / 8 per launch (kernel cycles of one XCD)
+"""
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
+import subprocess
 import sys
 
 root = sys.argv[1]
-FAMILIES = ["path_kernel_persistent<false", "path_kernel_persistent<true", "path_kernel<false", "path_kernel<true",
-            "wf_trace_kernel<0", "wf_trace_kernel<1", "wf_trace_kernel<2", "wf_shade_kernel", "wf_resolve_kernel",
-            "wf_gen_kernel", "sampler_kernel"]
+FAMILIES = {
+    "path_kernel": "path_kernel_persistent<false, true, true, false>",
+    "path_kernel_full": "path_kernel_persistent<false, true, true, true>",
+    "primary_intersect": "intersect_kernel<false, false, true, true>",
+    "prim_kernel": "prim_kernel<",
+    "fold_samples": "fold_samples_kernel",
+    "sampler": "sampler_kernel",
+}
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(lambda: collections.defaultdict(set))
 for f in sorted(glob.glob(os.path.join(root, "g*", "**", "*counter_collection.csv"), recursive=True)):
     for row in csv.DictReader(open(f)):
         name = row.get("Kernel_Name", "")
-        fam = "other"
-        for key in FAMILIES:
-            if key in name:
-                fam = key
-                break
-        cname = row.get("Counter_Name")
-        agg[fam][cname] += float(row.get("Counter_Value", 0))
-        disp[fam][cname].add((f, row.get("Dispatch_Id")))
-for fam in sorted(agg):
-    print(fam)
-    for k, v in sorted(agg[fam].items()):
-        print(f"   {k:28s} {v:20.6g}   ({len(disp[fam][k])} dispatches)")
-    a = agg[fam]
-    if a.get("TCC_HIT_sum", 0) + a.get("TCC_MISS_sum", 0) > 0:
-        print(f"   L2 hit rate {a['TCC_HIT_sum'] / (a['TCC_HIT_sum'] + a['TCC_MISS_sum']):.4f}")
-    if a.get("SQ_WAVE_CYCLES"):
-        for k in ["SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"]:
-            if k in a:
-                print(f"   {k} / SQ_WAVE_CYCLES = {a[k] / a['SQ_WAVE_CYCLES']:.3f}")
-    if a.get("SQ_ACTIVE_INST_VALU") and a.get("SQ_THREAD_CYCLES_VALU"):
-        print(f"   VALU lane utilisation {a['SQ_THREAD_CYCLES_VALU'] / (64 * a['SQ_ACTIVE_INST_VALU']):.3f}")
+        fam = next((k for k, key in FAMILIES.items() if key in name), None)
+        if fam is None:
+            continue
+        c = row.get("Counter_Name")
+        agg[fam][c] += float(row.get("Counter_Value", 0))
+        disp[fam][c].add((f, row.get("Dispatch_Id")))
 
-main = "path_kernel_persistent<false"
-if main in agg and "FETCH_SIZE" in agg[main] and "WRITE_SIZE" in agg[main]:
-    a = agg[main]
-    launches = len(disp[main]["FETCH_SIZE"])
-    hbm = (2.0 * a["FETCH_SIZE"] + a["WRITE_SIZE"]) * 1024.0 / launches
-    out = {"kernel": main + ",...>", "config": [3, 1.0, 1920, 1080], "launches": launches,
-           "fetch_size_kib": a["FETCH_SIZE"] / launches, "write_size_kib": a["WRITE_SIZE"] / launches,
-           "hbm_bytes_per_launch": hbm,
-           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of "
-                     "`bench.py --steps 1 --warmup 0`; (2*FETCH_SIZE + WRITE_SIZE) KiB per launch "
-                     "(gfx950 FETCH_SIZE half-count correction)"}
-    os.makedirs("profiles", exist_ok=True)
-    json.dump(out, open("gpurun_out/pmc/traffic.json", "w"), indent=1)
-    print("traffic:", json.dumps(out))
+here = os.path.dirname(os.path.abspath(__file__))
+libp = os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_trace.so")
+out = {"method": __doc__.strip(), "lib_sha256": hashlib.sha256(open(libp, "rb").read()).hexdigest(),
+       "config": [3, 1.0, 1920, 1080], "kernels": {}}
+try:
+    out["git_head"] = subprocess.check_output(["git", "rev-parse", "--short", "HEAD"], cwd=here,
+                                              stderr=subprocess.DEVNULL).decode().strip()
+except Exception:
+    out["git_head"] = None
+for fam, a in sorted(agg.items()):
+    n = {c: max(1, len(d)) for c, d in disp[fam].items()}
+    per = {c: v / n[c] for c, v in a.items()}
+    k = {"launches": max(n.values()), "counters_per_launch": {c: round(v, 1) for c, v in sorted(per.items())}}
+    if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+        k["hbm_bytes"] = (2.0 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0
+    if "TCP_TCC_READ_REQ_sum" in per:
+        k["l2_read_bytes"] = per["TCP_TCC_READ_REQ_sum"] * 128.0
+    if "GRBM_GUI_ACTIVE" in per:
+        k["cycles"] = per["GRBM_GUI_ACTIVE"] / 8.0
+        if "TA_TA_BUSY_sum" in per:
+            k["ta_busy"] = per["TA_TA_BUSY_sum"] / (256.0 * k["cycles"])
+    if per.get("TA_FLAT_READ_WAVEFRONTS_sum") and "TA_TA_BUSY_sum" in per:
+        k["ta_cycles_per_vmem_wave_inst"] = per["TA_TA_BUSY_sum"] / per["TA_FLAT_READ_WAVEFRONTS_sum"]
+    if per.get("TCC_HIT_sum", 0) + per.get("TCC_MISS_sum", 0) > 0:
+        k["l2_hit_rate"] = per["TCC_HIT_sum"] / (per["TCC_HIT_sum"] + per["TCC_MISS_sum"])
+    if per.get("SQ_WAVE_CYCLES"):
+        for c in ["SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"]:
+            if c in per:
+                k[c.lower() + "_frac"] = per[c] / per["SQ_WAVE_CYCLES"]
+    if per.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in per:
+        k["valu_lane_util"] = per["SQ_THREAD_CYCLES_VALU"] / (64.0 * per["SQ_ACTIVE_INST_VALU"])
+    out["kernels"][fam] = k
+json.dump(out, open(os.path.join(root, "pmc.json"), "w"), indent=1)
+for fam, k in out["kernels"].items():
+    print(fam, {x: (round(y, 4) if isinstance(y, float) else y) for x, y in k.items() if x != "counters_per_launch"})
+    for c, v in k["counters_per_launch"].items():
+        print(f"    {c:34s} {v:.6g}")
