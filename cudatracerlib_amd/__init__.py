@@ -25,10 +25,10 @@ import os
 import numpy as np
 
 from . import _abi
-from ._abi import (PTParams, WptParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK, CTL_SCENE_BINARY_BVH,
+from ._abi import (PTParams, WptParams, PrimParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK, CTL_SCENE_BINARY_BVH,
                    CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT)
 
-__all__ = ["HostScene", "Tracer", "PathTracer", "WavefrontPathTracer", "WptParams", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
+__all__ = ["HostScene", "Tracer", "PathTracer", "WavefrontPathTracer", "PrimTracer", "PrimParams", "WptParams", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
            "roughdielectric_material", "set_alpha_map",
            "CTL_SCENE_HALF_HOST_QUIRK", "CTL_SCENE_BINARY_BVH", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "lib", "diffuse_material"]
 
@@ -411,3 +411,27 @@ class WavefrontPathTracer(Tracer):
         ms = C.c_float()
         _check(self._L.ctl_last_pass_ms(self._ctx, C.byref(ms)), self._ctx, "ctl_last_pass_ms")
         return ms.value
+
+
+class PrimTracer(Tracer):
+    """PrimTracer (Integrators/PrimTracer.h:11-22): one primary ray per pixel and
+    a first-hit draw mode (default first_f, PrimTracer.cu:246), non-progressive
+    (every pass clears the image, Tracer<false>::DoPass)."""
+
+    def __init__(self, device=0, draw_mode="first_f", max_path_length=7, near=1.0, far=100000.0):
+        super().__init__(device)
+        mode = _abi.PRIM_DRAW_MODES.index(draw_mode) if isinstance(draw_mode, str) else int(draw_mode)
+        self.params = _abi.PrimParams(mode, max_path_length, near, far, 0)
+
+    def do_pass(self, fb_ptr, pass_index, depth_ptr=None, stream=0):
+        """UpdateKernel's sampler regeneration + DoRender into fb (device PixelData[w*h]);
+        depth_ptr: optional device float[w*h] for the D3D-normalised depth image."""
+        self.generate_samples(pass_index, stream)
+        _check(self._L.ctl_prim_pass(self._ctx, C.byref(self.params), fb_ptr, depth_ptr, stream), self._ctx,
+               "ctl_prim_pass")
+
+    def last_pass_ms(self):
+        ms = C.c_float()
+        _check(self._L.ctl_last_pass_ms(self._ctx, C.byref(ms)), self._ctx, "ctl_last_pass_ms")
+        return ms.value
+

@@ -154,6 +154,17 @@ class PTParams(C.Structure):
                 ("rank", C.c_uint32), ("flags", C.c_uint32)]
 
 
+class PrimParams(C.Structure):
+    _fields_ = [("draw_mode", C.c_int32), ("max_path_length", C.c_int32), ("near_depth", C.c_float),
+                ("far_depth", C.c_float), ("flags", C.c_uint32)]
+
+
+# PathTrace_DrawMode (PrimTracer.h:7-9)
+PRIM_DRAW_MODES = ["linear_depth", "D3D_depth", "v_absdot_n_geo", "v_dot_n_geo", "v_dot_n_shade", "n_geo_colored",
+                   "n_shade_colored", "uv", "bary_coords", "first_Le", "first_f", "first_f_direct",
+                   "first_non_delta_Le", "first_non_delta_f", "first_non_delta_f_direct"]
+
+
 class WptParams(C.Structure):
     _fields_ = [("direct", C.c_int32), ("max_path_length", C.c_int32), ("rr_start_depth", C.c_int32),
                 ("passes_done", C.c_uint32), ("flags", C.c_uint32)]
@@ -173,6 +184,7 @@ SYMBOLS = [
     ("ctl_render_pass", C.c_int32, [_vp, C.POINTER(PTParams), _vp, _vp]),
     ("ctl_render_passes", C.c_int32, [_vp, C.POINTER(PTParams), C.c_uint64, C.c_uint32, _vp, _vp]),
     ("ctl_wpt_render_pass", C.c_int32, [_vp, C.POINTER(WptParams), _vp, _vp]),
+    ("ctl_prim_pass", C.c_int32, [_vp, C.POINTER(PrimParams), _vp, _vp, _vp]),
     ("ctl_rays_traced", C.c_uint64, [_vp]),
     ("ctl_reset_rays", C.c_int32, [_vp, _vp]),
     ("ctl_sync", C.c_int32, [_vp, _vp]),

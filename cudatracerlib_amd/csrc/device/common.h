@@ -206,6 +206,50 @@ __device__ __forceinline__ f2 primary_ray(const DevScene& S, SamplerDev& rng, ui
     return pX;
 }
 
+// UniformSampleOneLight up to its occlusion test (TraceAlgorithms.cu:44-73,
+// 92-101; sampleEmitter KernelDynamicScene.cu:25-39; needs S.n_lights > 0):
+// draws the light choice and the light position, and when both the light
+// sample and the BSDF value are non-zero fills the shadow ray and, in sh.add,
+// EstimateDirect(...) / pdf -- the value UniformSampleOneLight returns when the
+// shadow ray is unoccluded (it returns +0 otherwise).
+template <bool FULL>
+__device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, const ctl_material& mat,
+                                           const bsdf_rec& b, const dgeom& dg, const TexView& tex, ShadowReq& sh) {
+    f2 sample = rng.next2();
+    const uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
+    uint32_t first = 0, cnt = nl;   // STL_upper_bound
+    while (cnt > 0) {
+        uint32_t c2 = cnt / 2, mid = first + c2;
+        if (!(sample.x < S.light_cdf[mid])) { first = mid + 1; cnt -= c2 + 1; }
+        else cnt = c2;
+    }
+    const uint32_t lidx = first < nl ? first : nl - 1;
+    const float fU = S.light_cdf[lidx], fL = lidx > 0 ? S.light_cdf[lidx - 1] : 0.0f;
+    sample.x = (sample.x - fL) / (fU - fL);
+    const float lpdf = fU - fL;
+    direct_rec dRec;
+    dRec.p = dg.P; dRec.n = dg.sys.n; dRec.measure = kEArea;
+    dRec.ref = dg.P; dRec.refN = dg.sys.n;
+    spec value = light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, rng.next2());
+    if (!spec_zero(value)) {
+        bsdf_rec b2 = b;
+        b2.wo = to_local(dg.sys, dRec.d);
+        b2.type_mask = kEAll & ~kEDelta;
+        spec bsdfVal = FULL ? bsdf_f(mat, b2, dg, &tex) : diffuse_f(mat, b2);
+        if (!spec_zero(bsdfVal)) {
+            float weight = 1.0f;
+            if (dRec.measure != kEDiscrete)
+                weight = power_heuristic(dRec.pdf * lpdf, FULL ? bsdf_pdf(mat, b2) : diffuse_pdf(mat, b2));
+            spec ret = value * bsdfVal * weight;
+            ret = ret * mk3s(1.0f);
+            sh.valid = true;
+            sh.d = dRec.d;
+            sh.dist = dRec.dist;
+            sh.add = spec_div(ret, lpdf);
+        }
+    }
+}
+
 // One closest hit of PathTrace<DIRECT> (PathTracer.cu:35-96; DIRECT = P.direct): emission with MIS,
 // BSDF sample, UniformSampleOneLight up to its occlusion test
 // (TraceAlgorithms.cu:44-73, 92-101; sampleEmitter KernelDynamicScene.cu:25-39),
@@ -273,39 +317,8 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
     spec f = FULL ? bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex) : diffuse_sample(mat, b, v.brdf_pdf, rng.next2());
     v.last_nor = dg.sys.n;
     if (P.direct && (mat.combined_type & kESmooth) != 0 && S.n_lights) {   // PathTracer.cu:82-83
-        f2 sample = rng.next2();
-        const uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
-        uint32_t first = 0, cnt = nl;   // STL_upper_bound
-        while (cnt > 0) {
-            uint32_t c2 = cnt / 2, mid = first + c2;
-            if (!(sample.x < S.light_cdf[mid])) { first = mid + 1; cnt -= c2 + 1; }
-            else cnt = c2;
-        }
-        const uint32_t lidx = first < nl ? first : nl - 1;
-        const float fU = S.light_cdf[lidx], fL = lidx > 0 ? S.light_cdf[lidx - 1] : 0.0f;
-        sample.x = (sample.x - fL) / (fU - fL);
-        const float lpdf = fU - fL;
-        direct_rec dRec;
-        dRec.p = dg.P; dRec.n = dg.sys.n; dRec.measure = kEArea;
-        dRec.ref = dg.P; dRec.refN = dg.sys.n;
-        spec value = light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, rng.next2());
-        if (!spec_zero(value)) {
-            bsdf_rec b2 = b;
-            b2.wo = to_local(dg.sys, dRec.d);
-            b2.type_mask = kEAll & ~kEDelta;
-            spec bsdfVal = FULL ? bsdf_f(mat, b2, dg, &tex) : diffuse_f(mat, b2);
-            if (!spec_zero(bsdfVal)) {
-                float weight = 1.0f;
-                if (dRec.measure != kEDiscrete)
-                    weight = power_heuristic(dRec.pdf * lpdf, FULL ? bsdf_pdf(mat, b2) : diffuse_pdf(mat, b2));
-                spec ret = value * bsdfVal * weight;
-                ret = ret * mk3s(1.0f);
-                sh.valid = true;
-                sh.d = dRec.d;
-                sh.dist = dRec.dist;
-                sh.add = v.cf * spec_div(ret, lpdf);
-            }
-        }
+        nee_sample<FULL>(S, rng, mat, b, dg, tex, sh);
+        if (sh.valid) sh.add = v.cf * sh.add;
     }
     v.specular = (b.sampled_type & kEDelta) != 0;
     v.cf = v.cf * f;

@@ -417,6 +417,37 @@ enum {
 };
 CTL_API ctl_status ctl_scene_read(ctl_ctx* ctx, uint32_t array, uint64_t first, uint64_t count, void* host_dst);
 
+/* ---- PrimTracer (BASELINE config C1) ------------------------------------- */
+
+/* PathTrace_DrawMode (Integrators/PrimTracer.h:7-9), in the reference's order. */
+enum {
+    CTL_PRIM_LINEAR_DEPTH = 0, CTL_PRIM_D3D_DEPTH = 1, CTL_PRIM_V_ABSDOT_N_GEO = 2, CTL_PRIM_V_DOT_N_GEO = 3,
+    CTL_PRIM_V_DOT_N_SHADE = 4, CTL_PRIM_N_GEO_COLORED = 5, CTL_PRIM_N_SHADE_COLORED = 6, CTL_PRIM_UV = 7,
+    CTL_PRIM_BARY_COORDS = 8, CTL_PRIM_FIRST_LE = 9, CTL_PRIM_FIRST_F = 10, CTL_PRIM_FIRST_F_DIRECT = 11,
+    CTL_PRIM_FIRST_NON_DELTA_LE = 12, CTL_PRIM_FIRST_NON_DELTA_F = 13, CTL_PRIM_FIRST_NON_DELTA_F_DIRECT = 14
+};
+
+/* PrimTracer parameters (PrimTracer.h:15-16, defaults PrimTracer.cu:246-247). */
+typedef struct {
+    int32_t draw_mode;         /* KEY_DrawingMode, default CTL_PRIM_FIRST_F        */
+    int32_t max_path_length;   /* KEY_MaxPathLength, default 7 (the first_non_delta_* */
+                               /* walk through delta BSDFs; the supported BSDFs     */
+                               /* have none, so it is never taken)                 */
+    float near_depth;          /* the sensor's m_fNearFarDepths (Sensor.h:46), for  */
+    float far_depth;           /* the depth modes and the depth image              */
+    uint32_t flags;            /* reserved, 0                                      */
+} ctl_prim_params;
+
+/* PrimTracer::DoRender (Integrators/PrimTracer.cu:214-233) as Tracer<false>::DoPass
+ * runs it: clears d_fb (Image::Clear), then one primary ray per pixel through
+ * the pixel corner (PrimTracer.cu:22) and the draw mode's first-hit value
+ * (computePixel, :19-106) into the pixel's PixelData.  d_depth (optional,
+ * width*height floats) receives DeviceDepthImage::NormalizeDepthD3D of the
+ * hit distance (g_DepthImage2.Store, :104-105).  Uses the sampler tables of the
+ * last ctl_sampler_generate.  Asynchronous; ctl_last_pass_ms times it. */
+CTL_API ctl_status ctl_prim_pass(ctl_ctx* ctx, const ctl_prim_params* params, ctl_pixel* d_fb, float* d_depth,
+                                 void* stream);
+
 /* ---- WavefrontPathTracer over a DoubleRayBuffer -------- */
 
 /* WavefrontPathTracer parameters (Integrators/PseudoRealtime/WavefrontPathTracer.h:27-38). */

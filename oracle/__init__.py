@@ -26,7 +26,7 @@ def load():
         return _lib
     if not os.path.exists(LIB):
         build()
-    from cudatracerlib_amd._abi import SceneDesc, Camera, PTParams, Pixel
+    from cudatracerlib_amd._abi import SceneDesc, Camera, PTParams, Pixel, PrimParams
     L = C.CDLL(LIB)
     vp = C.c_void_p
     sig = {
@@ -45,6 +45,8 @@ def load():
         "oracle_render_pass": (C.c_uint64, [C.POINTER(SceneDesc), C.POINTER(PTParams), C.c_uint64, vp, C.c_int32,
                                             C.c_int32, C.c_uint32, vp]),
         "oracle_camera_rays": (None, [C.POINTER(SceneDesc), C.c_uint64, vp]),
+        "oracle_prim_pass": (C.c_uint64, [C.POINTER(SceneDesc), C.POINTER(PrimParams), C.c_uint64, vp, vp, C.c_int32,
+                                          C.c_int32]),
         "oracle_animate": (None, [C.POINTER(SceneDesc), C.c_uint32, vp, vp, C.c_float, vp, vp, vp, vp, vp, vp]),
         "oracle_wpt_render_pass": (C.c_uint64, [C.POINTER(SceneDesc), C.c_int32, C.c_int32, C.c_int32, C.c_uint32,
                                                 C.c_uint64, vp, C.c_int32, C.c_int32]),

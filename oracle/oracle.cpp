@@ -1377,6 +1377,108 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
     return totalRays;
 }
 
+// PrimTracer::DoRender as Tracer<false>::DoPass runs it (Integrators/PrimTracer.cu:19-106,
+// 181-233; Kernel/Tracer.h:209-224): clear the image, one primary ray per pixel
+// through the pixel corner, the draw mode's first-hit value added at (x, y).
+// The supported BSDFs have no delta component, so first_non_delta_X == first_X.
+static float depth_d3d(float d, float n, float f) {   // DeviceDepthImage::NormalizeDepthD3D (Tracer.h:26-31)
+    float z = omin(omax(d, n), f);
+    return (f / (f - n) * z - f * n / (f - n)) / z;
+}
+
+uint64_t oracle_prim_pass(const ctl_scene_desc* desc, const ctl_prim_params* prm, uint64_t pass_index, ctl_pixel* fb,
+                          float* depth, int32_t tie, int32_t threads) {
+    const uint32_t nseq = 4096, len = 30;
+    std::vector<float> s1((size_t)nseq * len), s2((size_t)nseq * len * 2);
+    sampler_tables(pass_index, nseq, len, s1.data(), s2.data());
+    const ctl_camera& cam = desc->camera;
+    const uint32_t W = cam.width, H = cam.height;
+    std::memset(fb, 0, sizeof(ctl_pixel) * (size_t)W * H);   // Image::Clear
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+    const int mode = prm->draw_mode;
+    const float nd = prm->near_depth, fd = prm->far_depth;
+    std::atomic<int64_t> nextRow{0};
+    std::atomic<uint64_t> totalRays{0};
+    std::vector<Spec> out((size_t)W * H);
+    auto worker = [&]() {
+        // UniformSampleOneLight's Occluded: any hit over (eps, dist - eps) decides as the
+        // reference's closest hit + distance test does
+        RenderCtx C{SceneView{desc}, nullptr, tie, (desc->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0, true};
+        for (;;) {
+            const int64_t y = nextRow.fetch_add(1);
+            if (y >= (int64_t)H) break;
+            for (uint32_t x = 0; x < W; x++) {
+                Sampler rng{s1.data(), s2.data(), nseq, len, (uint32_t)(y * W + x)};
+                C.rng = &rng;
+                const V2 pX = v2((float)x, (float)y);
+                (void)rng.randomFloat2();   // aperture sample
+                V3 o, d, xo, dX, dY;
+                sensor_ray(cam, pX, o, d);
+                sensor_ray_diff(cam, pX, xo, dX, dY);
+                Hit h;
+                C.rays++;
+                trace_ray(C.S, o, d, h, C.tie, &C.st);
+                Spec L = v3s(0.0f);
+                if (h.tri != UINT_MAX) {
+                    if (mode == CTL_PRIM_LINEAR_DEPTH) {
+                        L = v3s((h.t - nd) / (fd - nd));
+                    } else if (mode == CTL_PRIM_D3D_DEPTH) {
+                        L = v3s(depth_d3d(h.t, nd, fd));
+                    } else {
+                        BRec bRec;   // TraceResult::getBsdfSample (TraceResult.cu:16-45)
+                        bRec.sampledType = 0;
+                        bRec.typeMask = EAll;
+                        bRec.dg.P = o + h.t * d;
+                        fill_dg(C.S, v2(h.u, h.v), h.tri, h.node, bRec.dg, C.quirk);
+                        bRec.wi = toLocal(bRec.dg.sys, -d);
+                        const ctl_material& mat = desc->materials[mat_index(C.S, h.tri, h.node)];
+                        if (mat.two_sided && bRec.wi.z < 0) {
+                            bRec.dg.n = -bRec.dg.n;
+                            bRec.dg.sys.n = -bRec.dg.sys.n;
+                            bRec.wi.z *= -1.0f;
+                        }
+                        c5::compute_partials(bRec.dg, xo, dX, xo, dY);
+                        const V3 w = -d;
+                        if (mode == CTL_PRIM_V_ABSDOT_N_GEO) L = v3s(std::fabs(dot(w, bRec.dg.n)));
+                        else if (mode == CTL_PRIM_V_DOT_N_GEO) L = v3s(dot(w, bRec.dg.n));
+                        else if (mode == CTL_PRIM_V_DOT_N_SHADE) L = v3s(dot(w, bRec.dg.sys.n));
+                        else if (mode == CTL_PRIM_N_GEO_COLORED || mode == CTL_PRIM_N_SHADE_COLORED) {
+                            const V3 n = mode == CTL_PRIM_N_GEO_COLORED ? bRec.dg.n : bRec.dg.sys.n;
+                            const V3 c = n + v3s(1.0f);
+                            L = v3(c.x / 2, c.y / 2, c.z / 2);
+                        } else if (mode == CTL_PRIM_UV) L = v3(bRec.dg.uv.x, bRec.dg.uv.y, 0.0f);
+                        else if (mode == CTL_PRIM_BARY_COORDS) L = v3(bRec.dg.bary.x, bRec.dg.bary.y, 0.0f);
+                        else {
+                            bRec.wo = v3(0.0f, 0.0f, 1.0f);
+                            const Spec f_avg = bsdf_f(desc, mat, bRec);
+                            Spec Le = v3s(0.0f);   // TraceResult::Le -> DiffuseLight::eval (Light.cu:67-82)
+                            const uint32_t li = light_index(C.S, h.tri, h.node);
+                            if (li != UINT_MAX) {
+                                const ctl_light& Lt = desc->lights[li];
+                                Le = (dot(bRec.dg.sys.n, w) <= 0) ? v3s(0.0f)
+                                                                  : v3(Lt.radiance[0], Lt.radiance[1], Lt.radiance[2]);
+                            }
+                            const Spec through = v3s(1.0f);   // Transmittance without media
+                            if (mode == CTL_PRIM_FIRST_LE || mode == CTL_PRIM_FIRST_NON_DELTA_LE) L = through * Le;
+                            else if (mode == CTL_PRIM_FIRST_F || mode == CTL_PRIM_FIRST_NON_DELTA_F) L = through * f_avg;
+                            else L = Le + through * (uniform_sample_one_light(C, bRec, mat) + f_avg * 0.5f);
+                        }
+                    }
+                }
+                out[(size_t)y * W + x] = L;
+                if (depth) depth[(size_t)y * W + x] = depth_d3d(h.t, nd, fd);   // g_DepthImage2.Store
+            }
+        }
+        totalRays += C.rays;
+    };
+    std::vector<std::thread> tv;
+    for (int i = 0; i < threads; i++) tv.emplace_back(worker);
+    for (auto& t : tv) t.join();
+    for (uint32_t y = 0; y < H; y++)
+        for (uint32_t x = 0; x < W; x++) add_sample(fb, W, H, (float)x, (float)y, out[(size_t)y * W + x]);
+    return totalRays;
+}
+
 // Primary rays of pass `pass_index` in image order (pixel y*W+x): the first
 // ray path_trace gets in oracle_render_pass (pathKernel2, PathTracer.cu:182-194),
 // as traversalRay {o, eps; d, FLT_MAX}.
