@@ -21,6 +21,11 @@ struct PathParams {
     int32_t shadow_any_hit;
     int32_t direct;   // KEY_Direct: PathTrace<true> (NEE + MIS) or PathTrace<false>
     bool half_quirk;
+    // N > 1 ranks: work items [0, owned_items) are this rank's pixels; then, per
+    // owned tile, apron (2 ts + 1 items: left column, top row, corner) -- the
+    // other ranks' pixels whose jittered sample can land in the tile (ApronItem)
+    uint32_t owned_items;
+    uint32_t apron;   // 2 * tile_size + 1 when num_ranks > 1, else 0
 };
 
 struct SamplerDev {   // SequenceSampler (Kernel/Sampler_device.h:59-113)
@@ -75,7 +80,43 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint64_t v
 
 // work item g -> pixel of the owned tiles (tile_id % num_ranks == rank); each
 // wave covers an 8x8 pixel block so primary rays in a wave are coherent.
+// Work items of one pass: the rank's pixels, then the apron items.
+__host__ __device__ inline uint32_t owned_tiles_of(const PathParams& P) {
+    return P.num_tiles > P.rank ? (P.num_tiles - P.rank + P.num_ranks - 1) / P.num_ranks : 0u;
+}
+__host__ __device__ inline uint64_t pass_items_of(const PathParams& P) {
+    return (uint64_t)P.owned_items + (uint64_t)owned_tiles_of(P) * P.apron;
+}
+
+// Apron items (N > 1 ranks).  A sample lands on floor(pX): its own pixel or,
+// when the jitter rounds up, the right / lower / lower-right neighbour, which
+// may belong to another rank's tile.  So that every pixel's samples are summed
+// by one rank in the 1-GPU order (fold_samples_kernel), the owner of the
+// target tile traces such a foreign pixel's path itself: apron item (tile, i)
+// is the pixel left of / above / above-left of the tile; it is traced only
+// when its sample lands inside that tile (apron_keep), which needs just the
+// first sampler draw, so the duplicated work is a few paths per image.
+__device__ __forceinline__ bool apron_pixel(const PathParams& P, uint64_t a, uint32_t& px, uint32_t& py,
+                                            uint32_t& x0, uint32_t& y0) {
+    const uint32_t ts = P.tile_size;
+    const uint32_t j = (uint32_t)(a / P.apron), i = (uint32_t)(a % P.apron);
+    const uint32_t tile = j * P.num_ranks + P.rank;
+    if (tile >= P.num_tiles) return false;
+    x0 = (tile % P.tiles_x) * ts;
+    y0 = (tile / P.tiles_x) * ts;
+    if (i < ts) { if (x0 == 0) return false; px = x0 - 1; py = y0 + i; }
+    else if (i < 2 * ts) { if (y0 == 0) return false; px = x0 + (i - ts); py = y0 - 1; }
+    else { if (x0 == 0 || y0 == 0) return false; px = x0 - 1; py = y0 - 1; }
+    if (px >= P.width || py >= P.height) return false;
+    const uint32_t t2 = (py / ts) * P.tiles_x + px / ts;
+    return t2 % P.num_ranks != P.rank;   // a pixel of this rank is covered by its own item
+}
+
 __device__ __forceinline__ bool work_pixel(const PathParams& P, uint64_t g, uint32_t& px, uint32_t& py) {
+    if (P.apron && g >= P.owned_items) {
+        uint32_t x0, y0;
+        return apron_pixel(P, g - P.owned_items, px, py, x0, y0);
+    }
     const uint32_t perTile = P.tile_size * P.tile_size;
     const uint32_t j = (uint32_t)(g / perTile), w = (uint32_t)(g % perTile);
     const uint32_t tile = j * P.num_ranks + P.rank;
@@ -138,6 +179,20 @@ __device__ __forceinline__ void store_sample(const PathParams& P, const SampleSl
     S.s[(size_t)ps * S.per_pass + kk] = make_float4(col.x, col.y, col.z, code);
 }
 
+// Apron item g keeps its path only when the sample lands inside its tile.
+__device__ __forceinline__ bool apron_keep(const PathParams& P, uint64_t g, f2 pX) {
+    if (!P.apron || g < P.owned_items) return true;
+    uint32_t px, py, x0, y0;
+    apron_pixel(P, g - P.owned_items, px, py, x0, y0);
+    const float lx = floorf(pX.x), ly = floorf(pX.y);
+    return lx >= (float)x0 && lx < (float)(x0 + P.tile_size) && ly >= (float)y0 && ly < (float)(y0 + P.tile_size);
+}
+
+// Work item of source pixel (sx, sy) for a target pixel of tile (x0, y0) owned
+// by this rank: its own item, or the tile's apron item when another rank owns it.
+__device__ __forceinline__ bool source_item(const PathParams& P, uint32_t sx, uint32_t sy, uint32_t x0, uint32_t y0,
+                                            uint32_t& k);
+
 // inverse of work_pixel: owned pixel -> work item (false when another rank owns it)
 __device__ __forceinline__ bool pixel_work(const PathParams& P, uint32_t x, uint32_t y, uint32_t& k) {
     const uint32_t ts = P.tile_size;
@@ -145,6 +200,20 @@ __device__ __forceinline__ bool pixel_work(const PathParams& P, uint32_t x, uint
     if (tile % P.num_ranks != P.rank) return false;
     const uint32_t xx = x % ts, yy = y % ts;
     k = (tile / P.num_ranks) * ts * ts + ((yy / 8) * (ts / 8) + xx / 8) * 64 + (yy % 8) * 8 + xx % 8;
+    return true;
+}
+
+__device__ __forceinline__ bool source_item(const PathParams& P, uint32_t sx, uint32_t sy, uint32_t x0, uint32_t y0,
+                                            uint32_t& k) {
+    if (pixel_work(P, sx, sy, k)) return true;
+    if (!P.apron) return false;
+    const uint32_t ts = P.tile_size;
+    const uint32_t tile = (y0 / ts) * P.tiles_x + x0 / ts;
+    uint32_t i;
+    if (sx + 1 == x0 && sy + 1 == y0) i = 2 * ts;
+    else if (sx + 1 == x0) i = sy - y0;
+    else i = ts + (sx - x0);
+    k = P.owned_items + (tile / P.num_ranks) * P.apron + i;
     return true;
 }
 

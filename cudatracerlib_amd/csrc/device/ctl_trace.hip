@@ -176,9 +176,13 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
         PathCtx<STATS, SINGLE, WIDE, FULL> C{S, P, rng, st, 0, TraceStats{0, 0, 0}, true, PathVars{}};
         f3 o, dw;
         const f2 pX = primary_ray(S, rng, px, py, o, dw);
-        C.v.begin(pX, o, dw);
-        while (C.bounce()) {}
-        store_sample(P, PS, 0, (uint32_t)g, px, py, pX, mk3s(1.0f) * C.v.cl);
+        if (apron_keep(P, g, pX)) {
+            C.v.begin(pX, o, dw);
+            while (C.bounce()) {}
+            store_sample(P, PS, 0, (uint32_t)g, px, py, pX, mk3s(1.0f) * C.v.cl);
+        } else {
+            PS.s[g] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // apron path landing outside the tile
+        }
         rays = C.rays;
         ts = C.ts;
         ok = C.ok;
@@ -269,7 +273,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                         shadowPhase = false;
                         ending = false;
                         // loop head of PathTrace: `while (depth++ < MaxPathLength)`
-                        if (v.depth++ < P.max_path_length) active = true;
+                        if (!apron_keep(P, kk, pX)) PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        else if (v.depth++ < P.max_path_length) active = true;
                         else store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
                     } else {
                         PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // work item outside the image: no sample
@@ -899,6 +904,14 @@ static ctl_status prepare_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb
     P.shadow_any_hit = p->shadow_any_hit;
     P.direct = p->direct != 0;
     P.half_quirk = c->half_quirk;
+    P.owned_items = 0;
+    P.apron = nr > 1 ? 2 * ts + 1 : 0;
+    const uint64_t own = (uint64_t)owned_tiles_of(P) * ts * ts;
+    if (own + (uint64_t)owned_tiles_of(P) * P.apron >= 0xffffffffull) {
+        c->err = "render_pass: 2^32-1 or more work items per pass";
+        return CTL_ERR_INVALID;
+    }
+    P.owned_items = (uint32_t)own;
     return CTL_OK;
 }
 
@@ -915,8 +928,7 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
     if (r != CTL_OK) return r;
     CTL_HIP(c, hipSetDevice(c->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    uint32_t owned = (P.num_tiles > P.rank) ? (P.num_tiles - P.rank + P.num_ranks - 1) / P.num_ranks : 0;
-    uint64_t threads = (uint64_t)owned * P.tile_size * P.tile_size;
+    const uint64_t threads = pass_items_of(P);   // owned pixels + apron items
     if (threads == 0) return CTL_OK;
     dim3 grid((unsigned)((threads + kBlock - 1) / kBlock));
     const float* s1 = c->d_s1[c->active];
@@ -977,12 +989,17 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
 // (its own and the ones that rounded over from the left / upper / upper-left
 // neighbour) in image order of their pixels, pass by pass -- one sequential
 // AddSample per pixel in image order (Image.cu:22-44), as the oracle adds them.
-// Only this rank's pixels are sources (pixel_work).
+// Only this rank's pixels are targets; a source of another rank is read from
+// the target tile's apron item (source_item), so each pixel is summed by one
+// rank in the 1-GPU order and the N-rank reduce is exact.
 __global__ __launch_bounds__(kBlock) void fold_samples_kernel(PathParams P, const float4* __restrict__ slots,
                                                               uint32_t per_pass, uint32_t n, ctl_pixel* fb) {
     const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (q >= (uint64_t)P.width * P.height) return;
     const uint32_t x = (uint32_t)(q % P.width), y = (uint32_t)(q / P.width);
+    const uint32_t ts = P.tile_size;
+    if (((y / ts) * P.tiles_x + x / ts) % P.num_ranks != P.rank) return;   // the owner sums it (apron items)
+    const uint32_t x0 = x - x % ts, y0 = y - y % ts;
     uint32_t ks[4];
     float codes[4];
     int nc = 0;
@@ -991,7 +1008,7 @@ __global__ __launch_bounds__(kBlock) void fold_samples_kernel(PathParams P, cons
     for (int d = 3; d >= 0; d--) {
         const uint32_t dx = d & 1, dy = d >> 1;
         uint32_t k;
-        if (x >= dx && y >= dy && pixel_work(P, x - dx, y - dy, k)) {
+        if (x >= dx && y >= dy && source_item(P, x - dx, y - dy, x0, y0, k)) {
             ks[nc] = k;
             codes[nc] = (float)(1 + d);
             nc++;
@@ -1057,8 +1074,7 @@ CTL_API ctl_status ctl_render_passes(ctl_ctx* c, const ctl_pt_params* params, ui
     if (r != CTL_OK) return r;
     CTL_HIP(c, hipSetDevice(c->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const uint32_t owned = (P.num_tiles > P.rank) ? (P.num_tiles - P.rank + P.num_ranks - 1) / P.num_ranks : 0;
-    const uint64_t per_pass = (uint64_t)owned * P.tile_size * P.tile_size;
+    const uint64_t per_pass = pass_items_of(P);   // owned pixels + apron items
     if (per_pass == 0) return CTL_OK;
     const uint64_t items = per_pass * n_passes;
     if (items >= 0xffffffffull) { c->err = "render_passes: 2^32-1 or more work items"; return CTL_ERR_INVALID; }
@@ -1130,8 +1146,7 @@ CTL_API ctl_status ctl_camera_rays(ctl_ctx* c, const ctl_pt_params* params, ctl_
     ctl_pixel dummy;
     ctl_status r = prepare_pass(c, params, &dummy, P);
     if (r != CTL_OK) return r;
-    const uint32_t owned = (P.num_tiles > P.rank) ? (P.num_tiles - P.rank + P.num_ranks - 1) / P.num_ranks : 0;
-    const uint64_t items = (uint64_t)owned * P.tile_size * P.tile_size;
+    const uint64_t items = P.owned_items;   // this rank's pixels
     *n_out = (int64_t)items;
     if (items == 0 || !d_rays) return CTL_OK;   // d_rays == NULL: size query
     if (capacity < (int64_t)items) { c->err = "camera_rays: ray buffer too small"; return CTL_ERR_INVALID; }

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S, PathParams P
         const bool inRange = g < n_items;
         if (!__any(inRange)) break;
         uint32_t px = 0, py = 0;
-        const bool valid = inRange && work_pixel(P, g, px, py);
+        bool valid = inRange && work_pixel(P, g, px, py);
         f2 pX = mk2(0, 0);
         f3 o = mk3s(0), d = mk3s(0);
         uint32_t idx = py * P.width + px;
@@ -66,6 +66,7 @@ __global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S, PathParams P
             pX = mk2((float)px, (float)py) + rng.next2();
             (void)rng.next2();   // aperture sample
             sensor_ray(S, pX, o, d);
+            valid = apron_keep(P, g, pX);   // an apron path landing outside the tile: no sample (slot stays 0)
         }
         const bool live = valid && P.max_path_length > 0;
         if (valid && !live) wf_store(P, SS, (uint32_t)g, pX, mk3s(0.0f) + (mk3s(1.0f) * 1.0f) * mk3s(0.0f));
@@ -284,8 +285,7 @@ void wavefront_free(ctl_ctx* c) {
 }
 
 int wavefront_pass(ctl_ctx* c, const PathParams& P, const SampleSlots& SS, bool stats, hipStream_t s) {
-    const uint32_t owned = (P.num_tiles > P.rank) ? (P.num_tiles - P.rank + P.num_ranks - 1) / P.num_ranks : 0;
-    const uint64_t items = (uint64_t)owned * P.tile_size * P.tile_size;
+    const uint64_t items = pass_items_of(P);   // owned pixels + apron items
     if (items == 0) return 0;
     if (items > 0xffffffffull) { c->err = "wavefront: too many paths per pass"; return CTL_ERR_INVALID; }
     WfState& W = c->wf;

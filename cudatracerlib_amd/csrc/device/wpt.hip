@@ -32,7 +32,7 @@ struct WptPay {
     float4 a;   // throughput xyz | bsdf_pdf
     float4 b;   // L xyz | dDist
     float4 c;   // directF xyz | bits: half x (pixel) | half y << 16, stored as the rounded floats' integers
-    uint4 d;    // dIdx | specular_bounce | prev_normal (16-bit spherical code) | unused
+    uint4 d;    // dIdx | specular_bounce | prev_normal (16-bit spherical code) | source pixel (ours)
 };
 static_assert(sizeof(WptPay) == 64, "payload is 64 B");
 
@@ -46,6 +46,8 @@ struct WptBuffers {
     ctl_hit* sec_hits = nullptr;
     uint8_t* flags = nullptr;      // bit 0: continues, bit 1: shadow ray
     uint2* blocks = nullptr;       // per-block counts -> exclusive offsets
+    float4* samples = nullptr;     // images over 2048 px: a finished path's sample per source pixel (L, bounce + 1)
+    size_t sample_capacity = 0;
     uint32_t* totals = nullptr;    // device: {continuations, shadow rays}
     uint32_t* h_totals = nullptr;  // pinned host copy
     std::vector<void*> allocs;
@@ -58,6 +60,7 @@ struct WptArgs {
     int32_t depth, max_path_length, rr_start_depth;
     uint32_t skip;       // rng.skip(iterationIdx + 2), iterationIdx = m_uPassesDone
     bool half_quirk;
+    float4* samples;     // non-null: samples go to per-source slots, folded by wpt_fold_kernel
 };
 
 __device__ __forceinline__ SamplerDev wpt_rng(const float* s1, const float2* s2, const WptArgs& A, uint32_t idx,
@@ -90,7 +93,7 @@ __global__ __launch_bounds__(kBlock) void wpt_create_kernel(DevScene S, WptArgs 
     p.a = make_float4(1.0f, 1.0f, 1.0f, 0.0f);   // throughput = W = Spectrum(1) (Sensor.cu:117)
     p.b = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     p.c = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float((uint32_t)half_round_int(x) | ((uint32_t)half_round_int(y) << 16)));
-    p.d = make_uint4(0xffffffffu, 1u, 0u, 0u);
+    p.d = make_uint4(0xffffffffu, 1u, 0u, i);
     pay[i] = p;
 }
 
@@ -234,10 +237,16 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs
             L = L + (1.0f * tp) * mk3s(0.0f);   // misWeight * throughput * EvalEnvironment (no env map)
         }
         if (terminated) {
-            const uint32_t hx = __float_as_uint(p.c.w) & 0xffffu, hy = __float_as_uint(p.c.w) >> 16;
-            PathParams P{};
-            P.width = A.width; P.height = A.height;
-            add_sample(fb, P, mk2((float)hx, (float)hy), L);
+            if (A.samples) {
+                // the pixel coordinates travel as half: above 2048 several source
+                // pixels share a target, so the sample waits for the ordered fold
+                A.samples[p.d.w] = make_float4(L.x, L.y, L.z, __int_as_float(A.depth + 1));
+            } else {
+                const uint32_t hx = __float_as_uint(p.c.w) & 0xffffu, hy = __float_as_uint(p.c.w) >> 16;
+                PathParams P{};
+                P.width = A.width; P.height = A.height;
+                add_sample(fb, P, mk2((float)hx, (float)hy), L);
+            }
         }
         if (cont) {
             p.a = make_float4(tp.x, tp.y, tp.z, bpdf);
@@ -250,6 +259,52 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs
     }
     const int nc = __syncthreads_count(cont), ns = __syncthreads_count(shadow);
     if (threadIdx.x == 0) blocks[blockIdx.x] = make_uint2((uint32_t)nc, (uint32_t)ns);
+}
+
+// Source range [lo, hi] of pixel coordinate q under the half rounding of the
+// payload (__float2half_rn, round to nearest even): {q} below 2048, up to 33
+// coordinates near 65504; empty when q is not representable.
+__device__ __forceinline__ void half_preimage(uint32_t q, uint32_t n, uint32_t& lo, uint32_t& hi) {
+    lo = 1u; hi = 0u;
+    if (q < 2048u) { lo = hi = q; return; }
+    const uint32_t a = q > 16u ? q - 16u : 0u, b = min(q + 16u, n - 1u);
+    for (uint32_t x = a; x <= b; x++) {
+        if ((uint32_t)half_round_int(x) == q) {
+            if (lo > hi) lo = x;
+            hi = x;
+        }
+    }
+}
+
+// AddSample of the finished paths of a pass on images over 2048 px: per target
+// pixel, its source pixels' samples in (bounce, image order) -- the sequential
+// order of the reference's atomicAdds that the oracle follows -- into PixelData.
+__global__ __launch_bounds__(kBlock) void wpt_fold_kernel(WptArgs A, const float4* __restrict__ samples, ctl_pixel* fb) {
+    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= (uint64_t)A.width * A.height) return;
+    const uint32_t qx = (uint32_t)(q % A.width), qy = (uint32_t)(q / A.width);
+    uint32_t x0, x1, y0, y1;
+    half_preimage(qx, A.width, x0, x1);
+    half_preimage(qy, A.height, y0, y1);
+    if (x0 > x1 || y0 > y1) return;
+    PathParams P{};
+    P.width = A.width; P.height = A.height;
+    int last = 0;   // bounces are visited in increasing order; sources in image order within one
+    for (;;) {
+        int next = 0x7fffffff;
+        for (uint32_t y = y0; y <= y1; y++)
+            for (uint32_t x = x0; x <= x1; x++) {
+                const int b = __float_as_int(samples[(size_t)y * A.width + x].w);
+                if (b > last && b < next) next = b;
+            }
+        if (next == 0x7fffffff) break;
+        for (uint32_t y = y0; y <= y1; y++)
+            for (uint32_t x = x0; x <= x1; x++) {
+                const float4 v = samples[(size_t)y * A.width + x];
+                if (__float_as_int(v.w) == next) add_sample(fb, P, mk2((float)qx, (float)qy), mk3(v.x, v.y, v.z));
+            }
+        last = next;
+    }
 }
 
 // Exclusive scan of the per-block counts in one 1024-thread block.
@@ -365,6 +420,17 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
     A.skip = prm->passes_done + 2u;
     A.half_quirk = c->half_quirk;
     A.depth = 0;
+    A.samples = nullptr;
+    if (cam.width > 2048u || cam.height > 2048u) {
+        if (B->sample_capacity < items) {
+            float4* sm = nullptr;
+            if (!wpt_alloc(B, &sm, items)) { c->err = "wpt: sample slot allocation failed"; return CTL_ERR_NOMEM; }
+            B->samples = sm;
+            B->sample_capacity = items;
+        }
+        A.samples = B->samples;
+        WPT_HIP(hipMemsetAsync(A.samples, 0, items * sizeof(float4), s));   // bounce tag 0: no sample
+    }
     const float* s1 = c->d_s1[c->active];
     const float2* s2 = c->d_s2[c->active];
     const bool nee = prm->direct != 0, full = c->scene.full_shading != 0;
@@ -400,6 +466,10 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
         cur = 1 - cur;
         // while (!m_ray_buf->isEmpty() && ++pass < maxPathLength)
         if (n == 0 || depth + 1 >= prm->max_path_length) break;
+    }
+    if (A.samples) {
+        hipLaunchKernelGGL(wpt_fold_kernel, dim3(nb_max), dim3(kBlock), 0, s, A, (const float4*)A.samples, fb);
+        WPT_HIP(hipGetLastError());
     }
     return count_rays(c, traced, s);
 }

@@ -4,8 +4,12 @@ Rank r of N owns the 64x64 tiles with ``tile_id % N == r`` (interleaved for
 load balance; tile space of IBlockSampler.h:100-108).  A *step* renders N
 progressive passes on every rank, so per-GPU work is fixed (weak scaling) and
 after K steps the job holds the N*K-pass image.  Pixel i always uses sampler
-index y*w+x and the same pass index, so summing the disjoint per-rank
-PixelData framebuffers with one reduce gives exactly the 1-GPU image.
+index y*w+x and the same pass index, so every sample equals the 1-GPU one.
+A jittered sample can round over a tile border onto another rank's pixel
+(AddSample adds at floor(x + u)); the rank that owns the target pixel traces
+that path itself (apron work items, a few per image) and sums each of its
+pixels in the 1-GPU order, so the per-rank PixelData framebuffers are
+disjoint and one reduce gives exactly the 1-GPU image.
 """
 
 
@@ -28,7 +32,8 @@ def owned_tiles(width, height, tile, world, rank):
 
 def reduce_framebuffer(fb, dist, dst=0):
     """Sum the per-rank PixelData framebuffers to `dst` (RCCL over xGMI on GPUs,
-    gloo on CPU).  Ownership is disjoint, so the fp32 sum is exact."""
+    gloo on CPU).  Every pixel is nonzero on its owner rank only, so the fp32
+    sum is exact: x + 0 = x."""
     if fb.is_cuda and dist.get_backend() == "gloo":
         # gloo reduces host tensors only (CPU rehearsals of the N-rank path)
         host = fb.cpu()

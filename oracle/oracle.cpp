@@ -1324,6 +1324,11 @@ void oracle_brute_force(const ctl_scene_desc* d, int64_t n, const ctl_ray* rays,
 // AddSample one by one in image order (pixel y*W+x), the order of a
 // single-threaded pass: a jittered sample can land on the neighbouring pixel
 // (floor(x + u) with u close to 1), so adding from the threads would race.
+// With num_ranks > 1 the rank sums exactly the samples that land on its own
+// pixels, in that order: it also traces another rank's pixel whose sample
+// lands on one of its pixels (the product's apron items), and drops its own
+// samples that land on another rank's pixel, so the ranks' framebuffers sum to
+// the 1-rank framebuffer bit for bit.
 uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm, uint64_t pass_index,
                             ctl_pixel* fb, int32_t tie, int32_t threads, uint32_t pixel_stride, uint64_t* stats) {
     const uint32_t nseq = 4096, len = 30;
@@ -1340,6 +1345,14 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
     uint64_t totalRays = 0, acc[3] = {0, 0, 0};
     struct Smp { float x, y; Spec L; bool set; };
     std::vector<Smp> smp((size_t)W * H);
+    const bool multi = prm->num_ranks > 1;
+    auto owned = [&](uint32_t px, uint32_t py) {
+        return !multi || ((py / ts) * tilesX + px / ts) % prm->num_ranks == prm->rank;
+    };
+    auto lands_owned = [&](V2 pX) {
+        const float lx = std::floor(pX.x), ly = std::floor(pX.y);
+        return lx >= 0.0f && ly >= 0.0f && lx < (float)W && ly < (float)H && owned((uint32_t)lx, (uint32_t)ly);
+    };
     auto worker = [&]() {
         RenderCtx C{SceneView{desc}, nullptr, tie, (desc->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0,
                     prm->shadow_any_hit != 0};
@@ -1349,11 +1362,10 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
             for (uint32_t x = 0; x < W; x++) {
                 uint64_t lin = (uint64_t)y * W + x;
                 if (lin % pixel_stride) continue;
-                uint32_t tile = (uint32_t)(y / ts) * tilesX + x / ts;
-                if (prm->num_ranks > 1 && tile % prm->num_ranks != prm->rank) continue;
                 Sampler rng{s1.data(), s2.data(), nseq, len, (uint32_t)(y * W + x)};
                 C.rng = &rng;
                 V2 pX = v2((float)x, (float)y) + rng.randomFloat2();
+                if (!owned(x, (uint32_t)y) && !lands_owned(pX)) continue;
                 V2 aperture = rng.randomFloat2();
                 (void)aperture;
                 V3 o, dd, xo, dX, dY;
@@ -1372,7 +1384,7 @@ uint64_t oracle_render_pass(const ctl_scene_desc* desc, const ctl_pt_params* prm
     for (int i = 0; i < threads; i++) tv.emplace_back(worker);
     for (auto& t : tv) t.join();
     for (size_t i = 0; i < smp.size(); i++)
-        if (smp[i].set) add_sample(fb, W, H, smp[i].x, smp[i].y, smp[i].L);
+        if (smp[i].set && (!multi || lands_owned(v2(smp[i].x, smp[i].y)))) add_sample(fb, W, H, smp[i].x, smp[i].y, smp[i].L);
     if (stats) { stats[0] = totalRays; stats[1] = acc[0]; stats[2] = acc[1]; stats[3] = acc[2]; }
     return totalRays;
 }

@@ -97,3 +97,31 @@ def oracle_render(orc, desc, params, passes, w, h, threads=0, fb=None, first_pas
         rays += orc.oracle_render_pass(C.byref(desc), C.byref(params), p, oracle.ptr(fb), tie_rule(desc), threads, 1,
                                        None)
     return fb, rays
+
+
+def jitter_landing(orc, pass_index, w, h):
+    """Pixel each pixel's pass sample lands on: floor((x, y) + the first 2-D
+    SequenceSampler draw), as PathTrace / AddSample compute it (fp32)."""
+    nseq, ln = 4096, 30
+    s1 = np.zeros(nseq * ln, np.float32)
+    s2 = np.zeros(nseq * ln * 2, np.float32)
+    orc.oracle_sampler_tables(pass_index, nseq, ln, oracle.ptr(s1), oracle.ptr(s2))
+    t = s2.reshape(ln, nseq, 2)[0]
+    idx = np.arange(w * h, dtype=np.int64)
+    a, b = idx % nseq, (idx // nseq) % nseq
+    u = (np.float32(0) + t[a]) + t[b]          # two fp32 adds, as next2()
+    u = u - np.floor(u)                        # fracf
+    px = (idx % w).astype(np.float32) + u[:, 0]
+    py = (idx // w).astype(np.float32) + u[:, 1]
+    return np.floor(px).astype(np.int64), np.floor(py).astype(np.int64)
+
+
+def cross_rank_strays(orc, pass_index, w, h, ranks, tile=64):
+    """Number of pixels whose pass sample lands on another rank's tile."""
+    lx, ly = jitter_landing(orc, pass_index, w, h)
+    idx = np.arange(w * h, dtype=np.int64)
+    tx = -(-w // tile)
+    own = ((idx // w) // tile * tx + (idx % w) // tile) % ranks
+    inside = (lx < w) & (ly < h)
+    land = ((ly // tile) * tx + lx // tile) % ranks
+    return int(((own != land) & inside).sum())

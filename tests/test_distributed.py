@@ -1,7 +1,10 @@
 """world_size-2 gloo run of the tile-shard + framebuffer-reduce path on CPU.
 Each rank renders its tiles (oracle as the renderer: no GPU here) for the
 pass indices shard.step_pass_indices gives it; the reduced image must equal
-the single-rank render of the same passes bit for bit."""
+the single-rank render of the same passes bit for bit.  The image is 1920
+wide and the passes are ones where a jittered sample rounds over a tile
+border onto the other rank's pixel, so the exchange-free exactness rule
+(the owner of the target pixel sums it; product: apron items) is exercised."""
 import ctypes as C
 import os
 import socket
@@ -20,7 +23,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-W, H, STEPS = 160, 96, 2
+W, H, STEPS, BASE = 1920, 64, 2, 34   # passes 34..37: two cross-rank samples (asserted below)
 
 
 def _render(desc, params, passes):
@@ -46,7 +49,7 @@ def _worker(rank, world, port, out):
         from cudatracerlib_amd import shard
         hs, desc = _scene()
         params = shard.shard_params(ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0), world, rank)
-        passes = [p for s in range(STEPS) for p in shard.step_pass_indices(s, world)]
+        passes = [p for s in range(STEPS) for p in shard.step_pass_indices(s, world, BASE)]
         fb = torch.from_numpy(_render(desc, params, passes))
         shard.reduce_framebuffer(fb, dist)
         if rank == 0:
@@ -64,7 +67,11 @@ def test_two_rank_gloo_shard_reduce_equals_single_rank(tmp_path):
     got = np.load(out)
     hs, desc = _scene()
     params = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
-    want = _render(desc, params, [p for s in range(STEPS) for p in shard.step_pass_indices(s, world)])
+    passes = [p for s in range(STEPS) for p in shard.step_pass_indices(s, world, BASE)]
+    want = _render(desc, params, passes)
+    import oracle
+    from helpers import cross_rank_strays
+    assert sum(cross_rank_strays(oracle.load(), p, W, H, world) for p in passes) >= 2
     assert want[:, 6].sum() > 0.9 * W * H * STEPS * world
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 

@@ -155,6 +155,41 @@ def test_render_half_quirk_mode(ctl, orc, tracer, dev):
     assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
 
 
+def test_tile_sharding_exact_with_cross_rank_samples(ctl, orc, tracer, dev):
+    """1920-wide image, 4 ranks, passes where a jittered sample rounds over a
+    tile border onto another rank's pixel (floor(x + u) = x + 1).  The owner of
+    the target pixel traces that foreign pixel's path (apron item) and sums the
+    pixel in the 1-rank order, so the rank framebuffers sum to the 1-rank
+    framebuffer bit for bit; each rank matches the oracle's rank render."""
+    from helpers import cross_rank_strays
+    w, h, R = 1920, 128, 4
+    passes = [p for p in range(400) if cross_rank_strays(orc, p, w, h, R)][:3]
+    assert len(passes) == 3
+    d = scene(ctl, 2, 0.25, w, h)
+    tracer.upload_scene(d)
+
+    def render(nr, r):
+        tracer.params = ctl.PTParams(1, 50, 5, 1, 64, nr, r, 0)
+        fb = torch.zeros((w * h, 7), dtype=torch.float32, device=dev)
+        for p in passes:
+            tracer.do_pass(fb.data_ptr(), p)
+        torch.cuda.synchronize()
+        return fb.cpu().numpy()
+
+    full = render(1, 0)
+    acc = np.zeros_like(full)
+    for r in range(R):
+        part = render(R, r)
+        acc += part
+        if r == 1:
+            want = np.zeros_like(full)
+            prm = ctl.PTParams(1, 50, 5, 1, 64, R, r, 0)
+            for p in passes:
+                orc.oracle_render_pass(C.byref(d), C.byref(prm), p, oracle.ptr(want), tie_rule(d), 0, 1, None)
+            assert np.array_equal(want.view(np.uint32), part.view(np.uint32))
+    assert np.array_equal(acc.view(np.uint32), full.view(np.uint32))
+
+
 def test_tile_sharding_is_exact(ctl, orc, tracer, dev):
     """Rank r renders tiles with tile_id % R == r; the sum of the
     rank framebuffers equals the single-rank framebuffer bit for bit."""
@@ -467,6 +502,21 @@ def test_wpt_short_paths(ctl, orc, dev, mpl, rr):
     got, grays = wpt_gpu(ctl, d, 1, 2, 96, 64, dev, mpl, rr, first_pass=3)
     assert grays == wrays
     assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
+
+
+@pytest.mark.parametrize("w,h", [(4096, 8), (8, 4200), (2500, 12)])
+def test_wpt_wide_image_shared_targets(ctl, orc, dev, w, h):
+    """Pixel coordinates travel as half (WavefrontPTRayData): above 2048 two or
+    more source pixels round to one target pixel and their samples add into it
+    (the reference's atomicAdd).  The pass is bit-exact against the oracle's
+    sequential adds (bounce, then image order)."""
+    d = scene(ctl, 2, 0.25, w, h)
+    want, wrays = wpt_oracle(orc, d, 1, 2, w, h)
+    got, grays = wpt_gpu(ctl, d, 1, 2, w, h, dev)
+    assert grays == wrays
+    assert want[:, 6].max() >= 4   # shared targets exist
+    bad = np.nonzero((want.view(np.uint32) != got.view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
 
 
 def test_wpt_converges_to_path_tracer(ctl, orc, tracer, dev):
