@@ -26,10 +26,11 @@ import numpy as np
 
 from . import _abi
 from ._abi import (PTParams, WptParams, PrimParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK, CTL_SCENE_BINARY_BVH,
-                   CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT)
+                   CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT, CTL_COMM_ID_BYTES)
 
 __all__ = ["HostScene", "Tracer", "PathTracer", "WavefrontPathTracer", "PrimTracer", "PrimParams", "WptParams", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
-           "roughdielectric_material", "set_alpha_map",
+           "roughdielectric_material", "set_alpha_map", "comm_unique_id", "comm_init_rank", "comm_init_all",
+           "comm_destroy",
            "CTL_SCENE_HALF_HOST_QUIRK", "CTL_SCENE_BINARY_BVH", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "lib", "diffuse_material"]
 
 
@@ -332,6 +333,44 @@ class Tracer:
     def stack_bound(self):
         """Worst-case traversal stack (entries per lane) of the uploaded scene."""
         return int(self._L.ctl_scene_stack_bound(self._ctx))
+
+    def fb_reduce(self, comm, fb_ptr, n_pixels, root=0, stream=0):
+        """Sum every rank's PixelData framebuffer into root's (ctl_fb_reduce over an
+        RCCL communicator from comm_init_all / comm_init_rank or the caller's)."""
+        _check(self._L.ctl_fb_reduce(self._ctx, comm, fb_ptr, int(n_pixels), int(root), stream), self._ctx,
+               "ctl_fb_reduce")
+
+
+def comm_unique_id():
+    """ncclGetUniqueId bytes (ctl_comm_unique_id) for comm_init_rank on every rank."""
+    buf = (C.c_uint8 * CTL_COMM_ID_BYTES)()
+    if lib().ctl_comm_unique_id(buf) != 0:
+        raise CTLError("ctl_comm_unique_id failed")
+    return bytes(buf)
+
+
+def comm_init_rank(nranks, uid, rank, device):
+    """One RCCL communicator of a one-process-per-GPU job (ctl_comm_init_rank)."""
+    out = C.c_void_p()
+    buf = (C.c_uint8 * CTL_COMM_ID_BYTES).from_buffer_copy(uid)
+    if lib().ctl_comm_init_rank(C.byref(out), int(nranks), buf, int(rank), int(device)) != 0:
+        raise CTLError("ctl_comm_init_rank failed")
+    return out.value
+
+
+def comm_init_all(devices):
+    """RCCL communicators of one process driving `devices` (ctl_comm_init_all)."""
+    n = len(devices)
+    out = (C.c_void_p * n)()
+    devs = (C.c_int32 * n)(*devices)
+    if lib().ctl_comm_init_all(out, n, devs) != 0:
+        raise CTLError("ctl_comm_init_all failed")
+    return list(out)
+
+
+def comm_destroy(comm):
+    if lib().ctl_comm_destroy(comm) != 0:
+        raise CTLError("ctl_comm_destroy failed")
 
 
 class PathTracer(Tracer):

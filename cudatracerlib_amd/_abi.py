@@ -16,6 +16,7 @@ CTL_SCENE_BINARY_BVH = 2
 CTL_SCENE_WIDE_QUANT = 4
 CTL_DEFAULT_SPLIT_ALPHA = 0.1875   # include/ctl_trace.h
 CTL_XMSH_MATERIAL_RECORD_SIZE = 148
+CTL_COMM_ID_BYTES = 128
 (CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS,
  CTL_ARRAY_SAMPLES_1D, CTL_ARRAY_SAMPLES_2D) = range(8)
 CTL_BSDF_DIFFUSE = 1
@@ -194,6 +195,12 @@ SYMBOLS = [
     ("ctl_render_pass_stats", C.c_int32, [_vp, C.POINTER(PTParams), _vp, C.POINTER(C.c_uint64), _vp]),
     ("ctl_last_pass_ms", C.c_int32, [_vp, C.POINTER(C.c_float)]),
     ("ctl_camera_rays", C.c_int32, [_vp, C.POINTER(PTParams), _vp, C.c_int64, C.POINTER(C.c_int64), _vp]),
+    ("ctl_comm_unique_id", C.c_int32, [_vp]),
+    ("ctl_comm_init_rank", C.c_int32, [C.POINTER(_vp), C.c_int32, _vp, C.c_int32, C.c_int32]),
+    ("ctl_comm_init_all", C.c_int32, [C.POINTER(_vp), C.c_int32, _vp]),
+    ("ctl_comm_destroy", C.c_int32, [_vp]),
+    ("ctl_fb_reduce", C.c_int32, [_vp, _vp, _vp, C.c_uint64, C.c_int32, _vp]),
+    ("ctl_fb_reduce_all", C.c_int32, [_vp, _vp, _vp, C.c_int32, C.c_uint64, C.c_int32, _vp]),
     ("ctl_image_resolve", C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, C.c_float, _vp, _vp]),
     ("ctl_variance_add_pass", C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, C.c_float, C.c_uint32, _vp, _vp, _vp]),
     ("ctl_variance_stats", C.c_int32, [_vp, _vp, C.c_uint64, _vp, _vp, _vp, _vp]),

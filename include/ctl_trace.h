@@ -384,6 +384,34 @@ CTL_API ctl_status ctl_last_pass_ms(ctl_ctx* ctx, float* ms);
 CTL_API ctl_status ctl_camera_rays(ctl_ctx* ctx, const ctl_pt_params* params, ctl_ray* d_rays, int64_t capacity,
                                    int64_t* n_out, void* stream);
 
+/* ---- multi-GPU: tile shards + one PixelData reduce over RCCL --
+ * The reference renders on one GPU (Tracer<true>::DoPass accumulating into
+ * PixelData, Kernel/Tracer.h:209-248, Engine/Image.h:10-29).  Rank r of N
+ * renders the tiles with tile_id % N == r (ctl_pt_params.num_ranks / rank);
+ * its framebuffer holds exactly the owned pixels' sums, in the 1-GPU order
+ * (samples that round over a tile border are traced by the target's owner),
+ * so one sum-reduce of the N framebuffers is the 1-GPU framebuffer bit for
+ * bit.  A communicator is an RCCL ncclComm_t passed as void*: the caller's own
+ * or one made by these helpers. */
+#define CTL_COMM_ID_BYTES 128u   /* sizeof(ncclUniqueId) */
+/* ncclGetUniqueId: one rank calls it and hands the bytes to the others. */
+CTL_API ctl_status ctl_comm_unique_id(void* id_out);
+/* ncclCommInitRank on `device` (one process per GPU). */
+CTL_API ctl_status ctl_comm_init_rank(void** comm_out, int32_t nranks, const void* id, int32_t rank,
+                                      int32_t device);
+/* ncclCommInitAll: one process driving ndev GPUs; comms_out[i] is rank i on devices[i]. */
+CTL_API ctl_status ctl_comm_init_all(void** comms_out, int32_t ndev, const int32_t* devices);
+CTL_API ctl_status ctl_comm_destroy(void* comm);
+/* Sum the n_pixels PixelData records of every rank's d_fb into root's d_fb
+ * (ncclReduce, fp32 sum, in place).  Every rank calls it with its own ctx and
+ * stream; asynchronous on `stream`. */
+CTL_API ctl_status ctl_fb_reduce(ctl_ctx* ctx, void* comm, ctl_pixel* d_fb, uint64_t n_pixels, int32_t root,
+                                 void* stream);
+/* The same for n contexts of one process (one per GPU, communicators from
+ * ctl_comm_init_all), as one grouped RCCL call. */
+CTL_API ctl_status ctl_fb_reduce_all(ctl_ctx* const* ctxs, void* const* comms, ctl_pixel* const* d_fbs, int32_t n,
+                                     uint64_t n_pixels, int32_t root, void* const* streams);
+
 /* ---- animated meshes: skinning + BVH refit ------------ */
 
 /* AnimatedMesh::k_ComputeState (Engine/AnimatedMesh.cpp:163-184) for animated
