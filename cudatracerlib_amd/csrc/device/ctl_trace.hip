@@ -372,7 +372,16 @@ __attribute__((amdgpu_waves_per_eu(CTL_INTERSECT_WAVES)))
 #endif
 void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            int64_t n2, const ctl_ray* rays2, ctl_hit* hits2,
-                                                           unsigned long long* cursor, unsigned long long* counters) {
+                                                           unsigned long long* cursor, unsigned long long* counters,
+                                                           const uint32_t* dcount) {
+    // dcount: the two segment sizes read from device memory (the WavefrontPathTracer's
+    // queue counts, written by the previous bounce's scan: no host round trip); the
+    // batch is then counted here as traced rays
+    if (dcount) {
+        n = dcount[0];
+        n2 = dcount[1];
+        if (blockIdx.x == 0 && threadIdx.x == 0 && n + n2 > 0) atomicAdd(&counters[0], (unsigned long long)(n + n2));
+    }
     const int64_t total = n + n2;
     CTL_LANE_STACK(st);
     TraceStats ts{0, 0, 0};
@@ -830,9 +839,11 @@ CTL_API ctl_status ctl_sampler_generate(ctl_ctx* c, uint64_t pass_index, void* s
     return CTL_OK;
 }
 
+// dcount != NULL: n and n2 are upper bounds (grid sizing); the kernel reads the
+// segment sizes from dcount[0..1] on the device.
 static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit,
                                    bool stats, void* stream, int64_t n2 = 0, const ctl_ray* rays2 = nullptr,
-                                   ctl_hit* hits2 = nullptr) {
+                                   ctl_hit* hits2 = nullptr, const uint32_t* dcount = nullptr) {
     if (!c || n < 0 || (n > 0 && (!rays || !hits)) || n2 < 0 || (n2 > 0 && (!rays2 || !hits2))) return CTL_ERR_INVALID;
     if (!c->has_scene) { c->err = "intersect: no scene uploaded"; return CTL_ERR_STATE; }
     if (c->overflow_seen) return CTL_ERR_STATE;   // c->err names the overflow (ctl_sync)
@@ -849,7 +860,7 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
         const int nb = resident_blocks(c, intersect_kernel<AN, ST, SG, WD>, kStackLdsBytes);                     \
         hipLaunchKernelGGL((intersect_kernel<AN, ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)),     \
                            dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, n2, rays2, hits2, cursor,  \
-                           c->d_counters);                                                                       \
+                           c->d_counters, dcount);                                                               \
     } while (0)
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;
@@ -1170,8 +1181,8 @@ static ctl_status add_rays(ctl_ctx* c, uint64_t n, hipStream_t s) {
 
 namespace ctl {
 int intersect_launch(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit, hipStream_t s,
-                     int64_t n2, const ctl_ray* rays2, ctl_hit* hits2) {
-    return launch_intersect(c, n, rays, hits, any_hit, false, s, n2, rays2, hits2);
+                     int64_t n2, const ctl_ray* rays2, ctl_hit* hits2, const uint32_t* dcount) {
+    return launch_intersect(c, n, rays, hits, any_hit, false, s, n2, rays2, hits2, dcount);
 }
 int count_rays(ctl_ctx* c, uint64_t n, hipStream_t s) { return add_rays(c, n, s); }
 }  // namespace ctl

@@ -48,10 +48,16 @@ struct WptBuffers {
     uint2* blocks = nullptr;       // per-block counts -> exclusive offsets
     float4* samples = nullptr;     // images over 2048 px: a finished path's sample per source pixel (L, bounce + 1)
     size_t sample_capacity = 0;
-    uint32_t* totals = nullptr;    // device: {continuations, shadow rays}
-    uint32_t* h_totals = nullptr;  // pinned host copy
+    // queue counts per bounce: slot b = {payload rays, shadow rays} traced by bounce
+    // b, written by bounce b-1's scan; kernels read them on the device, the host
+    // reads them back a few bounces late only to stop issuing bounces
+    uint32_t* counts = nullptr;
+    uint32_t* h_counts = nullptr;  // pinned host copy
+    uint32_t count_slots = 0;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<void*> allocs;
 };
+constexpr int kWptLag = 2;   // bounces the host check trails the device by
 
 namespace {
 
@@ -75,8 +81,9 @@ __device__ __forceinline__ SamplerDev wpt_rng(const float* s1, const float2* s2,
 // pathCreateKernelWPT (WavefrontPathTracer.cu:17-49) with one sample per pixel:
 // the payload slot of pixel i is i (rayidx order).
 __global__ __launch_bounds__(kBlock) void wpt_create_kernel(DevScene S, WptArgs A, const float* s1, const float2* s2,
-                                                            uint32_t n, ctl_ray* rays, WptPay* pay) {
+                                                            uint32_t n, ctl_ray* rays, WptPay* pay, uint32_t* count0) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i == 0) { count0[0] = n; count0[1] = 0u; }   // bounce 0: every pixel, no shadow rays
     if (i >= n) return;
     const uint32_t x = i % A.width, y = i / A.width;
     SamplerDev rng = wpt_rng(s1, s2, A, i, 0);
@@ -116,11 +123,13 @@ __device__ __forceinline__ uint32_t sample_emitter(const DevScene& S, f2& sample
 // pathIterateKernel<NEXT_EVENT_EST> body for payload element j (WavefrontPathTracer.cu:56-148).
 template <bool NEE, bool FULL>
 __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs A, const float* s1, const float2* s2,
-                                                             uint32_t n, WptPay* pay, ctl_ray* rays,
+                                                             const uint32_t* __restrict__ cnt, WptPay* pay, ctl_ray* rays,
                                                              const ctl_hit* __restrict__ hits,
                                                              const ctl_hit* __restrict__ sec_hits, ctl_ray* sec_tmp,
                                                              uint8_t* flags, uint2* blocks, ctl_pixel* fb) {
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t n = cnt[0];
+    if (blockIdx.x * kBlock >= n) return;   // grid sized for the largest queue
     bool cont = false, shadow = false;
     if (j < n) {
         WptPay p = pay[j];
@@ -309,9 +318,10 @@ __global__ __launch_bounds__(kBlock) void wpt_fold_kernel(WptArgs A, const float
 
 // Exclusive scan of the per-block counts in one 1024-thread block.
 constexpr int kScanThreads = 1024;
-__global__ __launch_bounds__(kScanThreads) void wpt_scan_kernel(uint2* blocks, uint32_t nb, uint32_t* totals) {
+__global__ __launch_bounds__(kScanThreads) void wpt_scan_kernel(uint2* blocks, const uint32_t* cnt, uint32_t* totals) {
     __shared__ uint32_t sc[kScanThreads], ss[kScanThreads];
     const uint32_t t = threadIdx.x;
+    const uint32_t nb = (cnt[0] + kBlock - 1) / kBlock;
     const uint32_t per = (nb + kScanThreads - 1) / kScanThreads;
     const uint32_t b0 = std::min(nb, t * per), b1 = std::min(nb, b0 + per);
     uint32_t c = 0, s = 0;
@@ -334,13 +344,15 @@ __global__ __launch_bounds__(kScanThreads) void wpt_scan_kernel(uint2* blocks, u
 }
 
 // Stable compaction: slot = block offset + preceding waves + preceding lanes.
-__global__ __launch_bounds__(kBlock) void wpt_scatter_kernel(uint32_t n, const uint8_t* __restrict__ flags,
+__global__ __launch_bounds__(kBlock) void wpt_scatter_kernel(const uint32_t* __restrict__ cnt, const uint8_t* __restrict__ flags,
                                                              const uint2* __restrict__ blocks,
                                                              const WptPay* __restrict__ pay_in,
                                                              const ctl_ray* __restrict__ rays_in,
                                                              const ctl_ray* __restrict__ sec_tmp, WptPay* pay_out,
                                                              ctl_ray* rays_out, ctl_ray* sec_out) {
     __shared__ uint32_t wc[kBlock / 64], ws[kBlock / 64];
+    const uint32_t n = cnt[0];
+    if (blockIdx.x * kBlock >= n) return;
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t f = j < n ? flags[j] : 0u;
     const bool cont = f & 1u, sh = f & 2u;
@@ -382,7 +394,9 @@ void wpt_free(ctl_ctx* c) {
     WptBuffers* B = c->wpt;
     if (!B) return;
     for (void* p : B->allocs) (void)hipFree(p);
-    if (B->h_totals) (void)hipHostFree(B->h_totals);
+    if (B->h_counts) (void)hipHostFree(B->h_counts);
+    for (hipEvent_t e : B->ev)
+        if (e) (void)hipEventDestroy(e);
     delete B;
     c->wpt = nullptr;
 }
@@ -407,8 +421,8 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
         bool ok = wpt_alloc(B, &B->pay[0], n) && wpt_alloc(B, &B->pay[1], n) && wpt_alloc(B, &B->rays[0], n) &&
                   wpt_alloc(B, &B->rays[1], n) && wpt_alloc(B, &B->hits, n) && wpt_alloc(B, &B->sec_tmp, n) &&
                   wpt_alloc(B, &B->sec, n) && wpt_alloc(B, &B->sec_hits, n) && wpt_alloc(B, &B->flags, n) &&
-                  wpt_alloc(B, &B->blocks, nb_max) && wpt_alloc(B, &B->totals, 4) &&
-                  hipHostMalloc((void**)&B->h_totals, 4 * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
+                  wpt_alloc(B, &B->blocks, nb_max);
+        for (hipEvent_t& e : B->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
         if (!ok) { wpt_free(c); c->err = "wpt: buffer allocation failed"; return CTL_ERR_NOMEM; }
         B->capacity = items;
     }
@@ -435,43 +449,72 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
     const float2* s2 = c->d_s2[c->active];
     const bool nee = prm->direct != 0, full = c->scene.full_shading != 0;
 
-    uint32_t n = (uint32_t)items, n_sec = 0;
+    // count slots for every bounce of the pass (+1 for the last scan's output)
+    const uint32_t slots = (uint32_t)prm->max_path_length + 1u;
+    if (B->count_slots < slots) {
+        uint32_t* dc = nullptr;
+        if (!wpt_alloc(B, &dc, 2 * (size_t)slots)) { c->err = "wpt: count allocation failed"; return CTL_ERR_NOMEM; }
+        if (B->h_counts) (void)hipHostFree(B->h_counts);
+        B->h_counts = nullptr;
+        if (hipHostMalloc((void**)&B->h_counts, 2 * (size_t)slots * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+            c->err = "wpt: count allocation failed";
+            return CTL_ERR_NOMEM;
+        }
+        B->counts = dc;
+        B->count_slots = slots;
+    }
+    const uint32_t n0 = (uint32_t)items;
     int cur = 0;
-    uint64_t traced = 0;
-    hipLaunchKernelGGL(wpt_create_kernel, dim3(nb_max), dim3(kBlock), 0, s, c->scene, A, s1, s2, n, B->rays[0],
-                       B->pay[0]);
+    hipLaunchKernelGGL(wpt_create_kernel, dim3(nb_max), dim3(kBlock), 0, s, c->scene, A, s1, s2, n0, B->rays[0],
+                       B->pay[0], B->counts);
     WPT_HIP(hipGetLastError());
+    // The queue sizes stay on the device: every kernel of bounce b reads slot b,
+    // the grids are sized for the largest queue (the pass's pixels) and idle
+    // blocks exit at once.  The host copies each bounce's totals back and waits
+    // only on bounce b - kWptLag's copy, to stop issuing bounces once a queue is
+    // empty (the at most kWptLag bounces already issued after it run empty).
+    // Queues only shrink (a bounce's continuations and shadow rays are at most its
+    // payload), so the last count the host has read back bounds the grids.
+    uint32_t ub = n0;
+    B->h_counts[0] = n0;   // slot 0 is written by wpt_create_kernel; its host copy is known
+    B->h_counts[1] = 0u;
     for (int depth = 0;; depth++) {
+        const uint32_t* cnt = B->counts + 2 * depth;
+        if (depth >= kWptLag) ub = std::min(ub, B->h_counts[2 * (depth - kWptLag)]);
+        const uint32_t nb = (ub + kBlock - 1) / kBlock;
         // FinishIteration: payload rays, then the secondary buffer (closest
-        // hit), as one launch over both batches (one resident grid, one tail)
-        int r = intersect_launch(c, n, B->rays[cur], B->hits, 0, s, n_sec, B->sec, B->sec_hits);
+        // hit), as one launch over both batches (one resident grid, one tail);
+        // the kernel counts the rays it traces
+        int r = intersect_launch(c, ub, B->rays[cur], B->hits, 0, s, depth ? ub : 0, B->sec, B->sec_hits, cnt);
         if (r != CTL_OK) return r;
-        traced += (uint64_t)n + n_sec;
         A.depth = depth;
-        const uint32_t nb = (n + kBlock - 1) / kBlock;
 #define WPT_IT(NE, FU)                                                                                             \
-    hipLaunchKernelGGL((wpt_iterate_kernel<NE, FU>), dim3(nb), dim3(kBlock), 0, s, c->scene, A, s1, s2, n,        \
+    hipLaunchKernelGGL((wpt_iterate_kernel<NE, FU>), dim3(nb), dim3(kBlock), 0, s, c->scene, A, s1, s2, cnt,      \
                        B->pay[cur], B->rays[cur], B->hits, B->sec_hits, B->sec_tmp, B->flags, B->blocks, fb)
         if (nee) { if (full) WPT_IT(true, true); else WPT_IT(true, false); }
         else { if (full) WPT_IT(false, true); else WPT_IT(false, false); }
 #undef WPT_IT
-        hipLaunchKernelGGL(wpt_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, B->blocks, nb, B->totals);
-        hipLaunchKernelGGL(wpt_scatter_kernel, dim3(nb), dim3(kBlock), 0, s, n, B->flags, B->blocks, B->pay[cur],
+        hipLaunchKernelGGL(wpt_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, B->blocks, cnt, B->counts + 2 * (depth + 1));
+        hipLaunchKernelGGL(wpt_scatter_kernel, dim3(nb), dim3(kBlock), 0, s, cnt, B->flags, B->blocks, B->pay[cur],
                            B->rays[cur], B->sec_tmp, B->pay[1 - cur], B->rays[1 - cur], B->sec);
         WPT_HIP(hipGetLastError());
-        WPT_HIP(hipMemcpyAsync(B->h_totals, B->totals, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        WPT_HIP(hipStreamSynchronize(s));
-        n = B->h_totals[0];
-        n_sec = B->h_totals[1];
+        WPT_HIP(hipMemcpyAsync(B->h_counts + 2 * (depth + 1), B->counts + 2 * (depth + 1), 2 * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, s));
+        WPT_HIP(hipEventRecord(B->ev[depth % 4], s));
         cur = 1 - cur;
         // while (!m_ray_buf->isEmpty() && ++pass < maxPathLength)
-        if (n == 0 || depth + 1 >= prm->max_path_length) break;
+        if (depth + 1 >= prm->max_path_length) break;
+        if (depth >= kWptLag) {
+            const int d = depth - kWptLag;
+            WPT_HIP(hipEventSynchronize(B->ev[d % 4]));
+            if (B->h_counts[2 * (d + 1)] == 0) break;   // bounce d left no paths: the later ones are empty
+        }
     }
     if (A.samples) {
         hipLaunchKernelGGL(wpt_fold_kernel, dim3(nb_max), dim3(kBlock), 0, s, A, (const float4*)A.samples, fb);
         WPT_HIP(hipGetLastError());
     }
-    return count_rays(c, traced, s);
+    return CTL_OK;
 }
 
 }  // namespace ctl
