@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--split-depth", type=int, default=8)
     ap.add_argument("--bins", type=int, default=0, help="SAH bins (0: library default)")
     ap.add_argument("--max-leaf", type=int, default=0, help="max leaf size (0: library default)")
+    ap.add_argument("--builder", default="sbvh", choices=["binned", "sbvh"],
+                    help="mesh BVH builder: the reference's SBVH (default) or early split clipping + binned SAH")
+    ap.add_argument("--sbvh-alpha", type=float, default=1.0e-5, help="SBVH splitAlpha (reference 1e-5)")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="diagnostic: one process renders rank 0's share of an N-rank job "
                          "(N passes per step over the tiles with tile %% N == 0), no collective")
@@ -121,8 +124,11 @@ def roofline(prof, fam, ms, alg_bytes, kernel):
         r["frac_l2"] = round(k["l2_read_bytes"] / (ms * 1e-3) / 1e9 / PEAK_L2, 4)
     if k.get("ta_busy") is not None:
         r["frac_ta"] = round(k["ta_busy"], 4)
-        r["binding_unit"] = ("vector-memory address unit (TA)" if k["ta_busy"] > 0.5 else
-                             "latency / issue (no unit above 50 %)")
+        # TA_TA_BUSY counts cycles with requests in flight: on the traversal it reads
+        # high while the dependent node-fetch chain, not the unit's throughput, binds
+        # (probes/ta_probe.hip and the cooperative-fetch experiment)
+        r["binding_unit"] = ("latency of the dependent node-fetch chain (TA busy = requests in flight)"
+                             if k["ta_busy"] > 0.5 else "latency / issue (no unit above 50 %)")
     for key in ("l2_hit_rate", "ta_cycles_per_vmem_wave_inst", "valu_lane_util"):
         if key in k:
             r[key] = round(k[key], 4)
@@ -161,7 +167,7 @@ def cpu_baseline(desc, params, seconds, threads):
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"oracle PathTrace<true> on the same scene, every 4th pixel of {passes} pass(es), "
+        "sample": f"oracle PathTrace<true> on the same triangles, every 4th pixel of {passes} pass(es), "
                   f"{rays} rays in {el:.1f} s",
         "cpu_model": cpu_model(),
         "nproc": os.cpu_count(),
@@ -295,6 +301,7 @@ def main():
     hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
     if a.split_alpha is not None or a.bins or a.max_leaf:
         hs.set_bvh_params(a.split_alpha, a.split_depth, a.bins, a.max_leaf)
+    hs.set_bvh_builder(a.builder, a.sbvh_alpha)
     desc = hs.compile(threads=threads)
     if a.bvh == "binary":
         desc.flags |= ctl.CTL_SCENE_BINARY_BVH
@@ -437,7 +444,7 @@ def main():
                 "triangles": int(desc.n_tri_data),
                 "bvh_inner_nodes": int(desc.n_bvh_nodes),
                 "bvh_refs": int(desc.n_tri_indices),
-                "bvh": a.bvh,
+                "bvh": a.bvh, "builder": a.builder,
                 "resolution": [W, H],
                 "spp": passes,
                 "tile": 64,
@@ -455,7 +462,13 @@ def main():
         }
         if world == 1 and not a.no_cpu_baseline:
             cores = min(16, os.cpu_count() or 1, threads if threads > 1 else 16)
-            out["cpu_baseline"] = cpu_baseline(desc, pt.params, a.cpu_seconds, cores)
+            # the reference's CPU path runs on its own tree: SBVH with leaves <= 8
+            # (SplitBVHBuilder Platform, BVHBuilderHelper.cpp:119), the same triangles
+            ref_hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
+            ref_hs.set_bvh_builder("sbvh", 1.0e-5).set_bvh_params(0.0, 8, 0, 8)
+            ref_desc = ref_hs.compile(threads=threads)
+            out["cpu_baseline"] = cpu_baseline(ref_desc, pt.params, a.cpu_seconds, cores)
+            out["cpu_baseline"]["bvh"] = "SBVH, leaves <= 8 (the reference's SplitBVHBuilder configuration)"
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

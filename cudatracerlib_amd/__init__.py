@@ -233,6 +233,13 @@ class HostScene:
                                                       int(max_leaf)), None, "set_bvh_params")
         return self
 
+    def set_bvh_builder(self, builder="sbvh", split_alpha=1.0e-5):
+        """Mesh BVH builder: "sbvh" (the reference's SplitBVHBuilder with in-build
+        spatial splits, default) or "binned" (early split clipping + binned SAH)."""
+        b = {"binned": _abi.CTL_BVH_BINNED, "sbvh": _abi.CTL_BVH_SBVH}[builder]
+        _check(self._L.ctl_host_scene_set_bvh_builder(self._h, b, float(split_alpha)), None, "set_bvh_builder")
+        return self
+
     def compile(self, threads=0):
         d = SceneDesc()
         _check(self._L.ctl_host_scene_compile(self._h, threads, C.byref(d)), None, "ctl_host_scene_compile")

@@ -17,6 +17,7 @@ CTL_SCENE_WIDE_QUANT = 4
 CTL_DEFAULT_SPLIT_ALPHA = 0.1875   # include/ctl_trace.h
 CTL_XMSH_MATERIAL_RECORD_SIZE = 148
 CTL_COMM_ID_BYTES = 128
+CTL_BVH_BINNED, CTL_BVH_SBVH = 0, 1
 (CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS,
  CTL_ARRAY_SAMPLES_1D, CTL_ARRAY_SAMPLES_2D) = range(8)
 CTL_BSDF_DIFFUSE = 1
@@ -217,6 +218,7 @@ SYMBOLS = [
                                               C.c_uint32, C.c_uint32]),
     ("ctl_host_scene_set_flags", C.c_int32, [_vp, C.c_uint32]),
     ("ctl_host_scene_set_bvh_params", C.c_int32, [_vp, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("ctl_host_scene_set_bvh_builder", C.c_int32, [_vp, C.c_uint32, C.c_float]),
     ("ctl_host_scene_compile", C.c_int32, [_vp, C.c_uint32, C.POINTER(SceneDesc)]),
     ("ctl_host_scene_add_animated_mesh", C.c_int32, [_vp, C.POINTER(AnimVertex), C.c_uint32, _vp, C.c_uint32, _vp,
                                                      _vp, C.POINTER(Material), C.c_uint32]),

@@ -28,6 +28,7 @@ struct BvhOutput {
     std::vector<uint8_t> leaf_last;      // 1 if entry is the last of its leaf
     int32_t start_node = 0x76543210;     // root value (inner: 0, single object w/ leaf_size_one: ~obj)
     uint32_t max_depth = 0;
+    uint64_t duplicates = 0;             // SBVH: references added by spatial splits
     Box root_box;
 };
 
@@ -37,5 +38,21 @@ struct BvhOutput {
 // line/point: sum(size)==max(size)) are dropped like the reference's "Remove
 // degenerates" step (SplitBVHBuilder.cpp:296-303).
 void build_bvh(const Box* boxes, uint32_t n, const BvhBuildParams& p, BvhOutput& out, const uint32_t* ids = nullptr);
+
+// SBVH of the reference's SplitBVHBuilder (SplitBVHBuilder.cpp:232-597) over
+// triangles t = V[9t .. 9t+8]; see bvh_build.cpp.  Platform and BuildParams
+// defaults of the reference: leaves of 1..8 references, splitAlpha 1e-5,
+// MaxSpatialDepth 48, MaxDepth 64, 128 spatial bins (SplitBVHBuilder.hpp:62-67,117,176).
+struct SbvhParams {
+    uint32_t max_leaf = 8;
+    float split_alpha = 1.0e-5f;
+    uint32_t spatial_bins = 128;
+    uint32_t max_spatial_depth = 48;
+    uint32_t max_depth = 64;
+    uint32_t sweep_max = 1u << 14;   // object splits of larger nodes are binned (bins) instead of sorted
+    uint32_t bins = 256;
+    uint32_t threads = 0;
+};
+void build_sbvh(const float* V, uint32_t ntri, const SbvhParams& p, BvhOutput& out);
 
 }  // namespace ctl

@@ -293,6 +293,16 @@ CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_
     return CTL_OK;
 }
 
+CTL_API ctl_status ctl_host_scene_set_bvh_builder(ctl_host_scene* s, uint32_t builder, float split_alpha) {
+    if (!s || builder > CTL_BVH_SBVH || !(split_alpha >= 0.0f)) {
+        set_host_error("set_bvh_builder: invalid argument");
+        return CTL_ERR_INVALID;
+    }
+    s->builder = builder;
+    s->sbvh_alpha = split_alpha;
+    return CTL_OK;
+}
+
 CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, ctl_scene_desc* out) {
     if (!s || !out) return CTL_ERR_INVALID;
     if (!s->has_camera) { set_host_error("compile: no camera"); return CTL_ERR_INVALID; }
@@ -347,7 +357,22 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         bp.bins = s->sah_bins;
         bp.max_leaf = s->max_leaf;
         BvhOutput bo;
-        if (s->split_alpha > 0.0f && s->split_depth > 0 && !M.animated) {
+        if (s->builder == CTL_BVH_SBVH && !M.animated) {
+            // the reference's SplitBVHBuilder (spatial splits inside the build)
+            std::vector<float> tv((size_t)ntri * 9);
+            parallel_for(ntri, threads, [&](uint64_t b, uint64_t e) {
+                for (uint64_t t = b; t < e; t++)
+                    for (int c = 0; c < 3; c++) {
+                        f3 p = V(M.idx[3 * t + c]);
+                        tv[9 * t + 3 * c] = p.x; tv[9 * t + 3 * c + 1] = p.y; tv[9 * t + 3 * c + 2] = p.z;
+                    }
+            });
+            SbvhParams sp;
+            sp.max_leaf = s->max_leaf;
+            sp.split_alpha = s->sbvh_alpha;
+            sp.threads = threads;
+            build_sbvh(tv.data(), ntri, sp, bo);
+        } else if (s->split_alpha > 0.0f && s->split_depth > 0 && !M.animated) {
             // references of large triangles split in space (ref_split.h)
             std::vector<float> tv((size_t)ntri * 9);
             parallel_for(ntri, threads, [&](uint64_t b, uint64_t e) {

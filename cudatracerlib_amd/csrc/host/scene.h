@@ -50,6 +50,8 @@ struct ctl_host_scene {
     uint32_t split_depth = CTL_DEFAULT_SPLIT_DEPTH;
     uint32_t sah_bins = CTL_DEFAULT_SAH_BINS;
     uint32_t max_leaf = CTL_DEFAULT_MAX_LEAF;
+    uint32_t builder = CTL_BVH_SBVH;   // ctl_host_scene_set_bvh_builder (default: the reference's SBVH)
+    float sbvh_alpha = 1.0e-5f;
 
     // compiled arrays (owned)
     std::vector<ctl_triangle_data> tri_data;

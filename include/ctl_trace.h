@@ -638,6 +638,24 @@ CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags);
 #define CTL_DEFAULT_MAX_LEAF 2u
 CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_alpha, uint32_t split_depth,
                                                  uint32_t bins, uint32_t max_leaf);
+/* BVH builder of the compile (mesh trees; the instance tree is always binned):
+ * CTL_BVH_BINNED: early split clipping + binned SAH (set_bvh_params' knobs);
+ * CTL_BVH_SBVH (default): the reference's SplitBVHBuilder algorithm (SplitBVHBuilder.cpp:232-597,
+ *   Stich et al. 2009): object splits by a SAH sweep over sorted references
+ *   (binned above 16k references), spatial splits over 128 planes per axis with
+ *   the triangle clipped at each plane (BVHBuilderHelper.cpp:78-113), reference
+ *   unsplitting, spatial splits only where the object split's children overlap
+ *   by >= split_alpha x the root area (reference 1e-5) and above depth 48; leaves
+ *   of 1 .. max_leaf references (set_bvh_params; the reference's is 8).  Parallel
+ *   over subtrees.  split_alpha is the SBVH's; the binned builder's stays in
+ *   set_bvh_params.  C3 (10M triangles, 1080p PathTracer, 4-wide device
+ *   traversal): binned + splitting (alpha 0.1875, 64 bins, leaf 2, 41.7M
+ *   references) 2250 Mrays/s; SBVH leaf 2: 2618 (26.6M references), leaf 1 / 3
+ *   / 4 / 8: 2566 / 2560 / 2504 / 2345; split_alpha 1e-6 / 1e-4: 2642 / 2456.
+ *   Skinned meshes always take the binned builder without splitting (refit). */
+#define CTL_BVH_BINNED 0u
+#define CTL_BVH_SBVH 1u
+CTL_API ctl_status ctl_host_scene_set_bvh_builder(ctl_host_scene* s, uint32_t builder, float split_alpha);
 CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, ctl_scene_desc* out);
 
 /* Skinned mesh (AnimatedMesh, Engine/AnimatedMesh.h:71-110): compiled in its

@@ -113,7 +113,7 @@ def test_animated_mesh_compiles_like_a_static_mesh(ctl):
     a.set_camera([0, 2, -9], [0, 2, 0], [0, 1, 0], 50, 16, 16)
     da = a.compile()
     b = ctl.HostScene()
-    b.set_bvh_params(0.0, 0)
+    b.set_bvh_builder("binned").set_bvh_params(0.0, 0)
     b.add_mesh(v, tris, mats, normals=n, uvs=uv)
     b.add_node(0)
     b.set_camera([0, 2, -9], [0, 2, 0], [0, 1, 0], 50, 16, 16)

@@ -102,14 +102,19 @@ def test_triangle_data_and_lights_bit_exact(ctl, orc):
 
 
 @pytest.mark.parametrize("config,scale", [(1, 1.0), (2, 1.0), (3, 0.01)])
-@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("split", [False, True, "sbvh"])
 def test_bvh_layout_contract(ctl, config, scale, split):
     """Reference layout contract (SplitBVHBuilder.cpp:163-203): DFS inner nodes
     (child = index*4), leaves = ~first entry, every triangle referenced (exactly
-    once without reference splitting; at least once with it, as the reference's
-    SBVH), leaf <= 8, last-in-leaf flags, depth bounded for the 64-entry stacks."""
+    once without reference splitting; at least once with it and with the SBVH's
+    spatial splits), leaf <= 8, last-in-leaf flags, depth bounded for the
+    64-entry stacks.  split: binned builder without / with early split
+    clipping, or the SBVH builder (leaf <= 8, the reference's Platform)."""
     s = ctl.HostScene().generate(config, scale, 64, 64)
-    s.set_bvh_params(1.0 if split else 0.0, 4 if split else 0, 0, 0)
+    if split == "sbvh":
+        s.set_bvh_builder("sbvh").set_bvh_params(0.0, 0, 0, 8)
+    else:
+        s.set_bvh_builder("binned").set_bvh_params(1.0 if split else 0.0, 4 if split else 0, 0, 0)
     d = s.compile()
     for m in range(d.n_meshes):
         km = d.meshes[m]

@@ -89,6 +89,28 @@ def test_bvh_traversal_equals_brute_force(ctl, orc, config, scale):
     assert np.array_equal(tri, btri)
 
 
+@pytest.mark.parametrize("config,scale", [(1, 1.0), (2, 0.2), (3, 0.003)])
+@pytest.mark.parametrize("max_leaf", [8, 2])
+def test_sbvh_traversal_equals_brute_force(ctl, orc, config, scale, max_leaf):
+    """The SBVH builder (the reference's SplitBVHBuilder: spatial splits with
+    clipped references, unsplitting) yields a valid tree over the same
+    triangles: traversal == exhaustive Woop scan; references were split."""
+    s = ctl.HostScene().generate(config, scale, 64, 64)
+    s.set_bvh_builder("sbvh", 1.0e-5).set_bvh_params(0.0, 8, 0, max_leaf)
+    d = s.compile()
+    rays = random_rays(d, 20000, seed=config + 7)
+    t, u, v, tri, node, st = oracle_trace(orc, d, rays, mode=0)
+    n = rays.shape[0]
+    bt = np.zeros(n, np.float32)
+    btri = np.zeros(n, np.uint32)
+    orc.oracle_brute_force(C.byref(d), n, oracle.ptr(rays), oracle.ptr(bt), oracle.ptr(btri), 0)
+    assert (tri != 0xFFFFFFFF).sum() > n // 10
+    assert np.array_equal(t, bt)
+    assert np.array_equal(tri, btri)
+    if config != 1:
+        assert d.n_woop_tris > d.n_tri_data   # spatial splits duplicated references
+
+
 def test_image_resolve_oracle_matches_numpy(orc):
     """copySamplesToOutput: weight-normalised RGB (+ splat), sRGB curve, clamp,
     truncation to 8 bit (ImagePipeline.cu:8-21, Spectrum.cu:229-234,
