@@ -579,7 +579,7 @@ struct SbvhBuilder {
         const uint32_t n = (uint32_t)refs.size();
         if (n <= 1 || depth >= p.max_depth) { make_leaf(idx, refs, T); return; }
         const float area = box_area(bb);
-        const float leafSAH = area * (float)n, nodeSAH = area * 2.0f;
+        const float leafSAH = area * (float)n, nodeSAH = area * 2.0f * p.node_cost;
         const int par = n > (1u << 18) ? max_threads : 1;
         ObjectSplit os = object_split(refs, nodeSAH);
         SpatialSplit ss;

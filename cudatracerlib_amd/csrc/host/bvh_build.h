@@ -52,6 +52,7 @@ struct SbvhParams {
     uint32_t sweep_max = 1u << 14;   // object splits of larger nodes are binned (bins) instead of sorted
     uint32_t bins = 256;
     uint32_t threads = 0;
+    float node_cost = 1.0f;          // SAH cost of one child visit relative to one triangle test (reference: 1)
 };
 void build_sbvh(const float* V, uint32_t ntri, const SbvhParams& p, BvhOutput& out);
 

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // scene.cpp — host scene compiler (ctl_host_scene_* of include/ctl_trace.h).
 // Produces exactly the arrays the reference's host code hands to the device:
 //   Mesh::CompileMesh / ConstructBVH  (Engine/Mesh.cpp:199-290, BVHBuilderHelper.cpp:129-147)
