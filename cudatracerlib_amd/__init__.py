@@ -223,6 +223,14 @@ class HostScene:
     def set_flags(self, flags):
         _check(self._L.ctl_host_scene_set_flags(self._h, flags), None, "set_flags")
 
+    def set_environment(self, texture, scale=(1.0, 1.0, 1.0)):
+        """DynamicScene::setEnvironementMap: an InfiniteLight over image texture
+        `texture` (an add_texture index) with radiance `scale`; None removes it."""
+        tex = 0xFFFFFFFF if texture is None else int(texture)
+        _check(self._L.ctl_host_scene_set_environment(self._h, tex, (C.c_float * 3)(*scale)), None,
+               "set_environment")
+        return self
+
     def set_bvh_params(self, split_alpha=None, split_depth=8, bins=0, max_leaf=0):
         """BVH build knobs: reference splitting of large triangles (split_alpha = 0
         disables, None = library default), SAH bins per axis and max leaf size

@@ -96,7 +96,18 @@ class LightTri(C.Structure):         # ShapeSet::triData, 64 B
 class Light(C.Structure):
     _fields_ = [("radiance", C.c_float * 3), ("orthogonal", C.c_uint32), ("tri_first", C.c_uint32),
                 ("tri_count", C.c_uint32), ("cdf_first", C.c_uint32), ("sum_area", C.c_float),
-                ("node_idx", C.c_uint32), ("pad", C.c_uint32 * 3)]
+                ("node_idx", C.c_uint32), ("kind", C.c_uint32), ("pad", C.c_uint32 * 2)]
+
+
+CTL_LIGHT_DIFFUSE = 0
+CTL_LIGHT_INFINITE = 1
+
+
+class EnvLight(C.Structure):          # ctl_env_light (InfiniteLight), 72 B
+    _fields_ = [("texture", C.c_uint32), ("scale", C.c_float * 3), ("size", C.c_float * 2),
+                ("pixel_size", C.c_float * 2), ("normalization", C.c_float), ("scene_center", C.c_float * 3),
+                ("scene_radius", C.c_float), ("cdf_cols", C.c_uint32), ("cdf_rows", C.c_uint32),
+                ("row_weights", C.c_uint32), ("pad", C.c_uint32 * 2)]
 
 
 class Camera(C.Structure):
@@ -134,6 +145,8 @@ class SceneDesc(C.Structure):
         ("textures", C.POINTER(Texture)), ("n_textures", C.c_uint32),
         ("tex_data", C.POINTER(C.c_uint32)), ("n_tex_data", C.c_uint64),
         ("env_map_index", C.c_uint32),
+        ("env", C.POINTER(EnvLight)),
+        ("env_data", C.POINTER(C.c_float)), ("n_env_data", C.c_uint64),
         ("box_min", C.c_float * 3), ("box_max", C.c_float * 3),
         ("ray_eps", C.c_float),
         ("camera", Camera),
@@ -217,6 +230,7 @@ SYMBOLS = [
     ("ctl_host_scene_set_camera", C.c_int32, [_vp, _vp, _vp, _vp, C.c_float, C.c_float, C.c_float,
                                               C.c_uint32, C.c_uint32]),
     ("ctl_host_scene_set_flags", C.c_int32, [_vp, C.c_uint32]),
+    ("ctl_host_scene_set_environment", C.c_int32, [_vp, C.c_uint32, _vp]),
     ("ctl_host_scene_set_bvh_params", C.c_int32, [_vp, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("ctl_host_scene_set_bvh_builder", C.c_int32, [_vp, C.c_uint32, C.c_float]),
     ("ctl_host_scene_compile", C.c_int32, [_vp, C.c_uint32, C.POINTER(SceneDesc)]),

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "traverse.h"
+#include "../ctl_env.h"
 
 namespace ctl {
 
@@ -275,13 +276,47 @@ __device__ __forceinline__ f2 primary_ray(const DevScene& S, SamplerDev& rng, ui
     return pX;
 }
 
+// Shading level of the path kernels (template FULL, DevScene::full_shading):
+// lean = constant diffuse materials only; full = C5 materials (ray
+// differentials, partials, the BSDF type switch, alpha tests); env = full plus
+// the environment light.  The environment code lives only in the env
+// instantiation: inlined into the others it costs the hot kernel ~80 spilled
+// VGPRs.  A scene with an environment map always runs the env level (full
+// shading of constant diffuse materials is exact, see shade_hit).
+enum : int { kShadeLean = 0, kShadeFull = 1, kShadeEnv = 2 };
+
+__device__ __forceinline__ EnvView env_view(const DevScene& S) { return EnvView{S.env, S.env_data, S.textures, S.tex_data}; }
+
+// KernelDynamicScene::pdfEmitter (KernelDynamicScene.cu:42-46)
+__device__ __forceinline__ float pdf_emitter(const DevScene& S, uint32_t li) {
+    return S.light_cdf[li] - (li == 0 ? 0.0f : S.light_cdf[li - 1]);
+}
+
+// The escaped-path term of PathTrace (PathTracer.cu:98-111):
+// misWeight * cf * EvalEnvironment(r), with r the last traced ray.  Without an
+// environment map EvalEnvironment is 0 and the sum stays as it was.
+template <int FULL>
+__device__ __forceinline__ spec env_miss(const DevScene& S, const PathParams& P, const PathVars& v) {
+    if (FULL != kShadeEnv || S.env_index == 0xffffffffu) return (v.cf * 1.0f) * mk3s(0.0f);
+    const EnvView E = env_view(S);
+    float misWeight = 1.0f;
+    if (!(!P.direct || v.depth == 1 || v.specular)) {
+        direct_rec dRec;   // DirectSamplingRecFromRay: d = r.dir, solid-angle measure
+        dRec.d = v.rdir; dRec.measure = kESolidAngle;
+        dRec.ref = v.rori; dRec.refN = v.last_nor; dRec.p = mk3s(0.0f); dRec.n = mk3s(0.0f); dRec.dist = 0.0f;
+        const float direct_pdf = env_pdf_direct(E, dRec) * pdf_emitter(S, S.env_index);
+        misWeight = power_heuristic(v.brdf_pdf, direct_pdf);
+    }
+    return (v.cf * misWeight) * env_eval(E, v.rdir);
+}
+
 // UniformSampleOneLight up to its occlusion test (TraceAlgorithms.cu:44-73,
 // 92-101; sampleEmitter KernelDynamicScene.cu:25-39; needs S.n_lights > 0):
 // draws the light choice and the light position, and when both the light
 // sample and the BSDF value are non-zero fills the shadow ray and, in sh.add,
 // EstimateDirect(...) / pdf -- the value UniformSampleOneLight returns when the
 // shadow ray is unoccluded (it returns +0 otherwise).
-template <bool FULL>
+template <int FULL>
 __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, const ctl_material& mat,
                                            const bsdf_rec& b, const dgeom& dg, const TexView& tex, ShadowReq& sh) {
     f2 sample = rng.next2();
@@ -299,7 +334,11 @@ __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, c
     direct_rec dRec;
     dRec.p = dg.P; dRec.n = dg.sys.n; dRec.measure = kEArea;
     dRec.ref = dg.P; dRec.refN = dg.sys.n;
-    spec value = light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, rng.next2());
+    // Light::sampleDirect dispatch: the environment map or a diffuse area light
+    const f2 lsample = rng.next2();
+    spec value = FULL == kShadeEnv && S.lights[lidx].kind == CTL_LIGHT_INFINITE
+                     ? env_sample_direct(env_view(S), dRec, lsample)
+                     : light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, lsample);
     if (!spec_zero(value)) {
         bsdf_rec b2 = b;
         b2.wo = to_local(dg.sys, dRec.d);
@@ -332,7 +371,7 @@ __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, c
 // SINGLE: one-instance scene, so the hit's node is ~start_node for every
 // lane; indexing with that kernel-uniform value turns the node record and its
 // transform into scalar loads.
-template <bool FULL, bool SINGLE = false>
+template <int FULL, bool SINGLE = false>
 __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P, SamplerDev& rng, PathVars& v,
                                           const HitRec& r, ShadowReq& sh) {
     const uint32_t node = SINGLE ? ~(uint32_t)S.start_node : r.node;
@@ -376,7 +415,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
             direct_rec dRec;
             dRec.ref = v.rori; dRec.refN = v.last_nor; dRec.p = dg.P; dRec.n = dg.n;
             dRec.d = v.rdir; dRec.dist = r.t; dRec.measure = kESolidAngle;
-            float direct_pdf = light_pdf_direct(L, dRec) * (S.light_cdf[li] - (li == 0 ? 0.0f : S.light_cdf[li - 1]));
+            float direct_pdf = light_pdf_direct(L, dRec) * pdf_emitter(S, li);
             misWeight = power_heuristic(v.brdf_pdf, direct_pdf);
         }
         f3 w = -v.rdir;

@@ -62,7 +62,7 @@ constexpr size_t persistent_lds_bytes() { return kStackLdsBytes + sizeof(int) * 
 
 // Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
 // traversals inline in the bounce, as the reference's pathKernel2 runs it.
-template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
+template <bool STATS, bool SINGLE, bool WIDE, int FULL>
 struct PathCtx {
     const DevScene& S;
     const PathParams& P;
@@ -79,9 +79,9 @@ struct PathCtx {
         HitRec r2;   // traceRay (TraceHelper.cu:174-180)
         r2.t = FLT_MAX; r2.tri = 0xffffffffu; r2.node = 0xffffffffu; r2.u = r2.v = 0.0f;
         rays++;
-        ok &= trace_one<0, STATS, SINGLE, WIDE, FULL>(S, v.rori, v.rdir, 0.0f, S.ray_eps, r2, st, &ts);
+        ok &= trace_one<0, STATS, SINGLE, WIDE, FULL != 0>(S, v.rori, v.rdir, 0.0f, S.ray_eps, r2, st, &ts);
         if (r2.tri == 0xffffffffu) {
-            v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);   // no environment map
+            v.cl = v.cl + env_miss<FULL>(S, P, v);   // PathTracer.cu:98-111
             return false;
         }
         ShadowReq sh;
@@ -91,8 +91,8 @@ struct PathCtx {
             HitRec h;
             h.t = any ? sh.dist - S.ray_eps : FLT_MAX; h.tri = 0xffffffffu; h.node = 0xffffffffu; h.u = h.v = 0.0f;
             rays++;
-            if (any) ok &= trace_one<1, STATS, SINGLE, WIDE, FULL>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
-            else ok &= trace_one<0, STATS, SINGLE, WIDE, FULL>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            if (any) ok &= trace_one<1, STATS, SINGLE, WIDE, FULL != 0>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            else ok &= trace_one<0, STATS, SINGLE, WIDE, FULL != 0>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
             if (!shadow_occluded(S, any, h, sh.dist)) v.cl = v.cl + sh.add;
         }
         return cont;
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict
 }
 
 // One path per thread (the reference's pathKernel2 launch shape).
-template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
+template <bool STATS, bool SINGLE, bool WIDE, int FULL>
 __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
                                                       ctl_pixel* fb, unsigned long long* counters, SampleSlots PS) {
     CTL_LANE_STACK(st);
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
 //    pending ray are loop-carried, keeping the register peak low.
 // Work items are independent (own sampler index, own sample slot), so the
 // framebuffer is bit-identical to path_kernel's.
-template <bool STATS, bool SINGLE, bool WIDE, bool FULL>
+template <bool STATS, bool SINGLE, bool WIDE, int FULL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? (FULL ? CTL_PERSIST_WAVES_FULL : CTL_PERSIST_WAVES) : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
                                                                  const float2* s2, uint64_t items,
                                                                  unsigned long long* cursor, unsigned long long* counters,
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             const long long pc0 = wall_clock64();
 #endif
             if (S.n_nodes != 0) {
-                Traverser<2, STATS, SINGLE, WIDE, FULL> T;
+                Traverser<2, STATS, SINGLE, WIDE, FULL != 0> T;
                 T.anyhit = shadowPhase && shadowAny;
                 T.init(S, v.rori, shadowPhase ? sh.d : v.rdir, 0.0f, S.ray_eps, h.t, st, &ts);
                 while (!T.done) T.round(S, st, &ts);
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                 shadowPhase = false;
                 cont = !ending && v.depth++ < P.max_path_length;
             } else if (h.tri == 0xffffffffu) {
-                v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);   // no environment map
+                v.cl = v.cl + env_miss<FULL>(S, P, v);   // PathTracer.cu:98-111
                 cont = false;
             } else {
                 ending = !shade_hit<FULL, SINGLE>(S, P, rng, v, h, sh);
@@ -593,10 +593,28 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
 CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     if (!c || !d) return CTL_ERR_INVALID;
     CTL_HIP(c, hipSetDevice(c->device));
-    if (d->env_map_index != 0xffffffffu) { c->err = "scene_upload: environment maps are not supported"; return CTL_ERR_INVALID; }
     if (d->n_lights > CTL_MAX_NUM_LIGHTS) { c->err = "scene_upload: more than 16 lights"; return CTL_ERR_INVALID; }
-    for (uint32_t i = 0; i < d->n_lights; i++)
+    for (uint32_t i = 0; i < d->n_lights; i++) {
         if (d->lights[i].orthogonal) { c->err = "scene_upload: orthogonal DiffuseLight unsupported"; return CTL_ERR_INVALID; }
+        if (d->lights[i].kind > CTL_LIGHT_INFINITE || (d->lights[i].kind == CTL_LIGHT_INFINITE) != (i == d->env_map_index)) {
+            c->err = "scene_upload: the environment light must be the light env_map_index names";
+            return CTL_ERR_INVALID;
+        }
+    }
+    if (d->env_map_index != 0xffffffffu) {   // InfiniteLight: its record, map and tables
+        const ctl_env_light* e = d->env;
+        if (d->env_map_index >= d->n_lights || !e || e->texture >= d->n_textures || !d->env_data) {
+            c->err = "scene_upload: environment light without its record, texture or tables";
+            return CTL_ERR_INVALID;
+        }
+        const uint32_t w = (uint32_t)e->size[0], h = (uint32_t)e->size[1];
+        if (w != d->textures[e->texture].width || h != d->textures[e->texture].height ||
+            (uint64_t)e->cdf_cols + (uint64_t)(w + 1) * h > d->n_env_data || (uint64_t)e->cdf_rows + h + 1 > d->n_env_data ||
+            (uint64_t)e->row_weights + h > d->n_env_data) {
+            c->err = "scene_upload: environment tables do not match the radiance map";
+            return CTL_ERR_INVALID;
+        }
+    }
     for (uint32_t i = 0; i < d->n_materials; i++) {
         const ctl_material& m = d->materials[i];
         if (m.bsdf_type != CTL_BSDF_DIFFUSE && m.bsdf_type != CTL_BSDF_ROUGHDIELECTRIC) {
@@ -664,6 +682,11 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     UP(lut.data(), lut.size(), &S.normal_lut);
     UP(d->textures, d->n_textures, &S.textures);
     UP(d->tex_data, d->n_tex_data, &S.tex_data);
+    S.env_index = d->env_map_index;
+    if (d->env_map_index != 0xffffffffu) {
+        UP(d->env, 1, &S.env);
+        UP(d->env_data, d->n_env_data, &S.env_data);
+    }
     // 4-wide trees for the device traversal (host/bvh_wide.h), unless the
     // caller asks for the reference's binary visit order
     const bool wide = (d->flags & CTL_SCENE_BINARY_BVH) == 0 && d->n_bvh_nodes > 0;
@@ -767,13 +790,14 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
     S.ray_eps = d->ray_eps;
     for (int i = 0; i < CTL_MAX_NUM_LIGHTS; i++) S.light_cdf[i] = d->light_cdf[i];
     S.camera = d->camera;
-    S.full_shading = 0;
+    S.full_shading = kShadeLean;
     S.alpha = 0;
     for (uint32_t i = 0; i < d->n_materials; i++) {
         const ctl_material& m = d->materials[i];
-        if (m.bsdf_type != CTL_BSDF_DIFFUSE || m.texture != 0xffffffffu || m.alpha_state) S.full_shading = 1;
+        if (m.bsdf_type != CTL_BSDF_DIFFUSE || m.texture != 0xffffffffu || m.alpha_state) S.full_shading = kShadeFull;
         if (m.alpha_state) S.alpha = 1;   // DynamicScene.cpp:586 doAlphaMapping
     }
+    if (S.env_index != 0xffffffffu) S.full_shading = kShadeEnv;
     S.single = 0;
     if (d->n_nodes > 0 && d->scene_start_node < 0) {
         uint32_t node = ~(uint32_t)d->scene_start_node;
@@ -963,7 +987,7 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
     const bool single = c->scene.single != 0;
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;
-    const bool full = c->scene.full_shading != 0;
+    const uint32_t full = c->scene.full_shading;
     if (!(p->flags & CTL_PT_MEGAKERNEL)) {
         unsigned long long* cursor = c->d_cursors + 1;
         CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
@@ -976,7 +1000,7 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
                                dim3(kBlock), lds, s, c->scene, P, s1, s2, threads, cursor,                       \
                                c->d_counters, PS, tbl);                                                          \
         } while (0)
-#define PK2(ST, SG, WD) do { if (full) PK(ST, SG, WD, true); else PK(ST, SG, WD, false); } while (0)
+#define PK2(ST, SG, WD) do { if (full == kShadeEnv) PK(ST, SG, WD, kShadeEnv); else if (full) PK(ST, SG, WD, kShadeFull); else PK(ST, SG, WD, kShadeLean); } while (0)
         if (stats) { if (single) PK2(true, true, false); else PK2(true, false, false); }
         else if (wide) { if (single) PK2(false, true, true); else PK2(false, false, true); }
         else { if (single) PK2(false, true, false); else PK2(false, false, false); }
@@ -985,7 +1009,7 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
     } else {
 #define MK(ST, SG, WD, FU) hipLaunchKernelGGL((path_kernel<ST, SG, WD, FU>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, \
                                               P, s1, s2, fb, c->d_counters, PS)
-#define MK2(ST, SG, WD) do { if (full) MK(ST, SG, WD, true); else MK(ST, SG, WD, false); } while (0)
+#define MK2(ST, SG, WD) do { if (full == kShadeEnv) MK(ST, SG, WD, kShadeEnv); else if (full) MK(ST, SG, WD, kShadeFull); else MK(ST, SG, WD, kShadeLean); } while (0)
         if (stats) { if (single) MK2(true, true, false); else MK2(true, false, false); }
         else if (wide) { if (single) MK2(false, true, true); else MK2(false, false, true); }
         else { if (single) MK2(false, true, false); else MK2(false, false, false); }

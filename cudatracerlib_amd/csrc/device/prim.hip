@@ -34,7 +34,7 @@ __device__ __forceinline__ float depth_d3d(float d, float n, float f) {
     return (f / (f - n) * z - f * n / (f - n)) / z;
 }
 
-template <bool SINGLE, bool WIDE, bool FULL>
+template <bool SINGLE, bool WIDE, int FULL>
 __global__ __launch_bounds__(kBlock) void prim_kernel(DevScene S, PathParams P, PrimParams Q, const float* s1,
                                                       const float2* s2, uint64_t items, unsigned long long* cursor,
                                                       unsigned long long* counters, ctl_pixel* fb, float* depth) {
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kBlock) void prim_kernel(DevScene S, PathParams P, 
         HitRec h;
         h.t = FLT_MAX; h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
         rays++;
-        if (S.n_nodes != 0) ok &= trace_one<0, false, SINGLE, WIDE, FULL>(S, o, d, 0.0f, S.ray_eps, h, st, &ts);
+        if (S.n_nodes != 0) ok &= trace_one<0, false, SINGLE, WIDE, FULL != 0>(S, o, d, 0.0f, S.ray_eps, h, st, &ts);
         spec L = mk3s(0.0f);
         if (h.tri != 0xffffffffu) {
             if (Q.mode == CTL_PRIM_LINEAR_DEPTH) {
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void prim_kernel(DevScene S, PathParams P, 
                                 hs.t = sh.dist - S.ray_eps; hs.u = hs.v = 0.0f;
                                 hs.tri = 0xffffffffu; hs.node = 0xffffffffu;
                                 rays++;
-                                ok &= trace_one<1, false, SINGLE, WIDE, FULL>(S, dg.P, sh.d, 0.0f, S.ray_eps, hs, st, &ts);
+                                ok &= trace_one<1, false, SINGLE, WIDE, FULL != 0>(S, dg.P, sh.d, 0.0f, S.ray_eps, hs, st, &ts);
                                 if (!shadow_occluded(S, true, hs, sh.dist)) direct = sh.add;
                             }
                         }
@@ -142,7 +142,13 @@ __global__ __launch_bounds__(kBlock) void prim_kernel(DevScene S, PathParams P, 
                 }
             }
         }
-        // else: EvalEnvironment without an environment map
+        else if (FULL == kShadeEnv && S.env_index != 0xffffffffu) {
+            // L = EvalEnvironment(r, rX, rY) (PrimTracer.cu:102): the map filtered
+            // over the primary ray's differential footprint
+            f3 co, dX, dY;
+            sensor_diff(S, pX, co, dX, dY);
+            L = env_eval_diff(env_view(S), d, dX, dY);
+        }
         add_sample(fb, P, pX, L);   // Image::AddSample((float)x, (float)y, L): the pixel's own entry
         if (Q.write_depth) depth[idx] = depth_d3d(h.t, Q.near_d, Q.far_d);   // g_DepthImage2.Store
     }
@@ -192,7 +198,8 @@ CTL_API ctl_status ctl_prim_pass(ctl_ctx* c, const ctl_prim_params* p, ctl_pixel
     CTL_HIP(c, hipMemsetAsync(d_fb, 0, sizeof(ctl_pixel) * (size_t)cam.width * cam.height, s));
     unsigned long long* cursor = c->d_cursors + 2;
     CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
-    const bool single = c->scene.single != 0, wide = c->scene.wide != 0, full = c->scene.full_shading != 0;
+    const bool single = c->scene.single != 0, wide = c->scene.wide != 0;
+    const uint32_t full = c->scene.full_shading;
     const uint64_t want = (items + kBlock - 1) / kBlock;
 #define PRK(SG, WD, FU)                                                                                          \
     do {                                                                                                         \
@@ -201,7 +208,7 @@ CTL_API ctl_status ctl_prim_pass(ctl_ctx* c, const ctl_prim_params* p, ctl_pixel
                            kStackLdsBytes, s, c->scene, P, Q, c->d_s1[c->active], c->d_s2[c->active], items,     \
                            cursor, c->d_counters, d_fb, d_depth);                                                \
     } while (0)
-#define PRK2(SG, WD) do { if (full) PRK(SG, WD, true); else PRK(SG, WD, false); } while (0)
+#define PRK2(SG, WD) do { if (full == kShadeEnv) PRK(SG, WD, kShadeEnv); else if (full) PRK(SG, WD, kShadeFull); else PRK(SG, WD, kShadeLean); } while (0)
     if (wide) { if (single) PRK2(true, true); else PRK2(false, true); }
     else { if (single) PRK2(true, false); else PRK2(false, false); }
 #undef PRK2

@@ -79,11 +79,15 @@ struct DevScene {
     const float4* scene_wbvh;    // instance-level wide nodes
     const uint32_t* mesh_wbase;  // first wide node of each mesh
     uint32_t wide;               // wide trees present (scene flag CTL_SCENE_BINARY_BVH clear)
-    uint32_t full_shading;       // C5 materials present (shade_hit<true>)
+    uint32_t full_shading;       // shading level of the path kernels: kShadeLean / kShadeFull / kShadeEnv
     uint32_t alpha;              // KernelDynamicScene::doAlphaMapping (some material has an alpha map)
     uint32_t tie_min;            // exact-t ties -> lowest (triangle, node) instead of first found
     uint32_t s_wnode_base;
     uint32_t quant;              // wide trees in the 64-B quantized format (ctl_qnode.h)
+    // InfiniteLight (ctl_env.h): light env_index of lights[], 0xFFFFFFFF without one
+    uint32_t env_index;
+    const ctl_env_light* env;
+    const float* env_data;
 };
 
 struct TraceStats {

@@ -180,7 +180,7 @@ void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32
 #undef LT
 }
 
-template <bool FULL>
+template <int FULL>
 __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
                                                           WfState W, int bounce, SampleSlots SS) {
     const uint32_t count = W.counts[2 * bounce];
@@ -243,8 +243,8 @@ __global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams
                     W.sh_val[i] = make_float4(sh.add.x, sh.add.y, sh.add.z, terminated ? 1.0f : 0.0f);
                 }
             } else {
-                // miss: loop ends; environment term of PathTracer.cu:98-111 (no env map -> 0)
-                v.cl = v.cl + (v.cf * 1.0f) * mk3s(0.0f);
+                // miss: loop ends; environment term of PathTracer.cu:98-111
+                v.cl = v.cl + env_miss<FULL>(S, P, v);
                 wf_store(P, SS, i, v.pX, mk3s(1.0f) * v.cl);
             }
             W.cl[i] = make_float4(v.cl.x, v.cl.y, v.cl.z, v.pX.x);
@@ -321,10 +321,12 @@ int wavefront_pass(ctl_ctx* c, const PathParams& P, const SampleSlots& SS, bool 
     for (int b = 0; b < maxB; b++) {
         const uint32_t* cnt = &W.counts[2 * b];
         launch_trace<0>(c, s, W.q[b & 1], cnt, &cursors[2 * b], stats);
-        if (c->scene.full_shading)
-            hipLaunchKernelGGL((wf_shade_kernel<true>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, SS);
+        if (c->scene.full_shading == kShadeEnv)
+            hipLaunchKernelGGL((wf_shade_kernel<kShadeEnv>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, SS);
+        else if (c->scene.full_shading)
+            hipLaunchKernelGGL((wf_shade_kernel<kShadeFull>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, SS);
         else
-            hipLaunchKernelGGL((wf_shade_kernel<false>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, SS);
+            hipLaunchKernelGGL((wf_shade_kernel<kShadeLean>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, SS);
         const uint32_t* scnt = &W.counts[2 * b + 1];
         if (P.shadow_any_hit) launch_trace<1>(c, s, W.sq, scnt, &cursors[2 * b + 1], stats);
         else launch_trace<2>(c, s, W.sq, scnt, &cursors[2 * b + 1], stats);

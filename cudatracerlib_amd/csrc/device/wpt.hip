@@ -121,7 +121,7 @@ __device__ __forceinline__ uint32_t sample_emitter(const DevScene& S, f2& sample
 }
 
 // pathIterateKernel<NEXT_EVENT_EST> body for payload element j (WavefrontPathTracer.cu:56-148).
-template <bool NEE, bool FULL>
+template <bool NEE, int FULL>
 __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs A, const float* s1, const float2* s2,
                                                              const uint32_t* __restrict__ cnt, WptPay* pay, ctl_ray* rays,
                                                              const ctl_hit* __restrict__ hits,
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs
                     direct_rec dRec;   // DirectSamplingRecFromRay with the stored previous normal
                     dRec.ref = ro; dRec.refN = LutDecode{S.normal_lut}(p.d.z); dRec.p = dg.P; dRec.n = dg.n;
                     dRec.d = rd; dRec.dist = h.dist; dRec.measure = kESolidAngle;
-                    float direct_pdf = light_pdf_direct(Lt, dRec) * (S.light_cdf[li] - (li == 0 ? 0.0f : S.light_cdf[li - 1]));
+                    float direct_pdf = light_pdf_direct(Lt, dRec) * pdf_emitter(S, li);
                     misWeight = power_heuristic(bpdf, direct_pdf);
                 }
                 f3 w = -rd;
@@ -208,7 +208,9 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs
                     float emPdf = 0.0f;
                     if (S.n_lights) {
                     const uint32_t lidx = sample_emitter(S, sample, emPdf);
-                    spec value = light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, sample);
+                    spec value = FULL == kShadeEnv && S.lights[lidx].kind == CTL_LIGHT_INFINITE
+                                     ? env_sample_direct(env_view(S), dRec, sample)
+                                     : light_sample_direct(S.lights[lidx], S.light_tris, S.light_tri_cdf, dRec, sample);
                     if (dRec.pdf != 0) {
                         dRec.pdf *= emPdf;
                         value = spec_div(value, emPdf);
@@ -243,7 +245,20 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs
             }
         } else {
             terminated = true;
-            L = L + (1.0f * tp) * mk3s(0.0f);   // misWeight * throughput * EvalEnvironment (no env map)
+            // misWeight * throughput * EvalEnvironment(ray) (WavefrontPathTracer.cu:144-157)
+            if (FULL == kShadeEnv && S.env_index != 0xffffffffu) {
+                const EnvView E = env_view(S);
+                float misWeight = 1.0f;
+                if (NEE && !(A.depth == 0 || specular)) {
+                    direct_rec dRec;   // DirectSamplingRecFromRay: d = ray dir, solid-angle measure
+                    dRec.ref = ro; dRec.refN = LutDecode{S.normal_lut}(p.d.z); dRec.p = mk3s(0.0f); dRec.n = mk3s(0.0f);
+                    dRec.d = rd; dRec.dist = h.dist; dRec.measure = kESolidAngle;
+                    misWeight = power_heuristic(bpdf, env_pdf_direct(E, dRec) * pdf_emitter(S, S.env_index));
+                }
+                L = L + (misWeight * tp) * env_eval(E, rd);
+            } else {
+                L = L + (1.0f * tp) * mk3s(0.0f);
+            }
         }
         if (terminated) {
             if (A.samples) {
@@ -447,7 +462,8 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
     }
     const float* s1 = c->d_s1[c->active];
     const float2* s2 = c->d_s2[c->active];
-    const bool nee = prm->direct != 0, full = c->scene.full_shading != 0;
+    const bool nee = prm->direct != 0;
+    const uint32_t full = c->scene.full_shading;
 
     // count slots for every bounce of the pass (+1 for the last scan's output)
     const uint32_t slots = (uint32_t)prm->max_path_length + 1u;
@@ -491,8 +507,8 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
 #define WPT_IT(NE, FU)                                                                                             \
     hipLaunchKernelGGL((wpt_iterate_kernel<NE, FU>), dim3(nb), dim3(kBlock), 0, s, c->scene, A, s1, s2, cnt,      \
                        B->pay[cur], B->rays[cur], B->hits, B->sec_hits, B->sec_tmp, B->flags, B->blocks, fb)
-        if (nee) { if (full) WPT_IT(true, true); else WPT_IT(true, false); }
-        else { if (full) WPT_IT(false, true); else WPT_IT(false, false); }
+        if (nee) { if (full == kShadeEnv) WPT_IT(true, kShadeEnv); else if (full) WPT_IT(true, kShadeFull); else WPT_IT(true, kShadeLean); }
+        else { if (full == kShadeEnv) WPT_IT(false, kShadeEnv); else if (full) WPT_IT(false, kShadeFull); else WPT_IT(false, kShadeLean); }
 #undef WPT_IT
         hipLaunchKernelGGL(wpt_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, B->blocks, cnt, B->counts + 2 * (depth + 1));
         hipLaunchKernelGGL(wpt_scatter_kernel, dim3(nb), dim3(kBlock), 0, s, cnt, B->flags, B->blocks, B->pay[cur],

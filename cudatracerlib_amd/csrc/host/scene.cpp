@@ -8,6 +8,7 @@
 //   LightStream::fillDeviceData       (Engine/DynamicScene.cpp:173-196)
 //   getKernelSceneData eps            (Engine/DynamicScene.cpp:587)
 #include "scene.h"
+#include "../ctl_env.h"
 #include "bvh_build.h"
 #include "ref_split.h"
 #include "../ctl_shade.h"
@@ -294,6 +295,14 @@ CTL_API ctl_status ctl_host_scene_set_bvh_params(ctl_host_scene* s, float split_
     return CTL_OK;
 }
 
+CTL_API ctl_status ctl_host_scene_set_environment(ctl_host_scene* s, uint32_t texture, const float scale[3]) {
+    if (!s || (texture != 0xffffffffu && !scale)) { set_host_error("set_environment: invalid argument"); return CTL_ERR_INVALID; }
+    s->env_texture = texture;
+    if (scale)
+        for (int k = 0; k < 3; k++) s->env_scale[k] = scale[k];
+    return CTL_OK;
+}
+
 CTL_API ctl_status ctl_host_scene_set_bvh_builder(ctl_host_scene* s, uint32_t builder, float split_alpha) {
     if (!s || builder > CTL_BVH_SBVH || !(split_alpha >= 0.0f)) {
         set_host_error("set_bvh_builder: invalid argument");
@@ -559,6 +568,31 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         s->light_tri_cdf.insert(s->light_tri_cdf.end(), cdf.begin(), cdf.end());
         s->klights.push_back(kl);
     }
+    // DynamicScene::setEnvironementMap: the InfiniteLight goes after the area lights
+    // (m_uEnvMapIndex); its constructor's tables and Update()'s scene sphere
+    uint32_t envIndex = 0xffffffffu;
+    s->env_tables.clear();
+    if (s->env_texture != 0xffffffffu) {
+        if (s->env_texture >= s->textures.size()) { set_host_error("compile: environment texture index out of range"); return CTL_ERR_INVALID; }
+        if (s->klights.size() >= CTL_MAX_NUM_LIGHTS) { set_host_error("compile: more than 16 lights"); return CTL_ERR_INVALID; }
+        ctl_env_light& L = s->kenv;
+        L = ctl_env_light{};
+        L.texture = s->env_texture;
+        for (int k = 0; k < 3; k++) L.scale[k] = s->env_scale[k];
+        const ctl_texture& t = s->textures[L.texture];
+        s->env_tables.assign(env_table_floats(t.width, t.height), 0.0f);
+        EnvView E{&L, nullptr, s->textures.data(), s->tex_data.data()};
+        env_build_tables(E, L, s->env_tables.data());
+        const f3 lo = mk3(sceneBox.lo[0], sceneBox.lo[1], sceneBox.lo[2]), hi = mk3(sceneBox.hi[0], sceneBox.hi[1], sceneBox.hi[2]);
+        const f3 c = (lo + hi) * 0.5f;   // AABB::Center
+        L.scene_center[0] = c.x; L.scene_center[1] = c.y; L.scene_center[2] = c.z;
+        L.scene_radius = length(hi - lo) / 1.5f;
+        ctl_light kl{};
+        kl.kind = CTL_LIGHT_INFINITE;
+        kl.node_idx = 0xffffffffu;
+        envIndex = (uint32_t)s->klights.size();
+        s->klights.push_back(kl);
+    }
 
     ctl_scene_desc& d = s->desc;
     d = ctl_scene_desc{};
@@ -588,7 +622,10 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
             d.light_cdf[i] = (i > 0 ? d.light_cdf[i - 1] : 0.0f) + pdf;
         }
     }
-    d.env_map_index = 0xffffffffu;
+    d.env_map_index = envIndex;
+    d.env = envIndex != 0xffffffffu ? &s->kenv : nullptr;
+    d.env_data = s->env_tables.data();
+    d.n_env_data = s->env_tables.size();
     d.textures = s->textures.data();
     d.n_textures = (uint32_t)s->textures.size();
     d.tex_data = s->tex_data.data();

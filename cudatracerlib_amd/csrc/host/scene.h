@@ -64,6 +64,11 @@ struct ctl_host_scene {
     std::vector<ctl_bvh_node> scene_bvh;
     std::vector<ctl_float4x4> xf, inv_xf;
     std::vector<ctl_light> klights;
+    // environment (ctl_host_scene_set_environment): InfiniteLight record + its tables
+    uint32_t env_texture = 0xffffffffu;
+    float env_scale[3] = {1.0f, 1.0f, 1.0f};
+    ctl_env_light kenv{};
+    std::vector<float> env_tables;
     std::vector<ctl_light_tri> light_tris;
     std::vector<float> light_tri_cdf;
     std::vector<ctl_texture> textures;   // added by ctl_host_scene_add_texture (kept across compiles)

@@ -201,8 +201,29 @@ typedef struct {
     uint32_t cdf_first;
     float sum_area;              /* ShapeSet::sumArea                            */
     uint32_t node_idx;           /* m_uNodeIdx                                   */
-    uint32_t pad[3];
+    uint32_t kind;               /* CTL_LIGHT_DIFFUSE, or CTL_LIGHT_INFINITE: the
+                                    environment (desc.env; other fields unused) */
+    uint32_t pad[2];
 } ctl_light;
+enum { CTL_LIGHT_DIFFUSE = 0, CTL_LIGHT_INFINITE = 1 };
+
+/* InfiniteLight (SceneTypes/Light.h:294-367, Light.cpp:10-58): a latitude-
+ * longitude radiance map around the scene, identity world transform.  The
+ * radiance map is an image texture (textures[texture], level 0 read; its wrap
+ * mode applies to the bilinear lookups); env_data holds the sampling tables
+ * the constructor builds: cdf_cols ((width + 1) x height), cdf_rows
+ * (height + 1) and row_weights (height) at the given float offsets. */
+typedef struct {
+    uint32_t texture;
+    float scale[3];              /* m_scale                                      */
+    float size[2];               /* m_size = (width, height)                     */
+    float pixel_size[2];         /* m_pixelSize = (2 pi / width, pi / height)    */
+    float normalization;         /* m_normalization                              */
+    float scene_center[3];       /* Update(): scene box centre                   */
+    float scene_radius;          /*           |scene box size| / 1.5             */
+    uint32_t cdf_cols, cdf_rows, row_weights;
+    uint32_t pad[2];
+} ctl_env_light;
 
 /* PerspectiveSensor device state after Update() (SceneTypes/Sensor.cu:76-96). */
 typedef struct {
@@ -279,7 +300,9 @@ typedef struct {
     /* m_sTexData: image textures and their texel data */
     const ctl_texture* textures;        uint32_t n_textures;
     const uint32_t* tex_data;           uint64_t n_tex_data;
-    uint32_t env_map_index;             /* must be 0xFFFFFFFF (no environment)  */
+    uint32_t env_map_index;             /* m_uEnvMapIndex: the CTL_LIGHT_INFINITE light, 0xFFFFFFFF: none */
+    const ctl_env_light* env;           /* that light's record (NULL without one) */
+    const float* env_data;              uint64_t n_env_data;   /* its sampling tables */
     float box_min[3], box_max[3];       /* m_sBox                               */
     float ray_eps;                      /* m_rayTraceEps, DynamicScene.cpp:587  */
     ctl_camera camera;                  /* m_Camera                             */
@@ -621,6 +644,11 @@ CTL_API ctl_status ctl_host_scene_set_camera(ctl_host_scene* s, const float pos[
                                              const float up[3], float fov_deg, float near_clip,
                                              float far_clip, uint32_t width, uint32_t height);
 CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags);
+/* DynamicScene::setEnvironementMap: an InfiniteLight over image texture
+ * `texture` (ctl_host_scene_add_texture) with radiance scale `scale`; the
+ * compile builds its sampling tables (InfiniteLight::InfiniteLight) and adds it
+ * after the area lights (env_map_index).  texture = 0xFFFFFFFF removes it. */
+CTL_API ctl_status ctl_host_scene_set_environment(ctl_host_scene* s, uint32_t texture, const float scale[3]);
 /* Builds BVHs (threads=0: all hardware threads) and fills *out; the arrays
  * stay owned by `s` until it is destroyed or compiled again. */
 /* BVH build quality knobs of the compile (SplitBVHBuilder's splitAlpha /

@@ -56,6 +56,9 @@ def load():
         "oracle_triangle_data_set": (None, [vp, C.c_uint8, vp, vp, vp]),
         "oracle_light_tri": (None, [vp, vp, vp, vp, vp, vp]),
         "oracle_matrix_inverse": (None, [vp, vp]),
+        "oracle_env_tables": (None, [vp, vp, vp, vp]),
+        "oracle_env_sample": (None, [C.POINTER(SceneDesc), C.c_uint64, vp, vp]),
+        "oracle_env_eval": (None, [C.POINTER(SceneDesc), C.c_uint64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

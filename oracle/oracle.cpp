@@ -603,6 +603,104 @@ float light_pdf_direct(const ctl_light& L, const DRec& dRec) {   // Light.cu:137
 float pdf_emitter(const SceneView& S, uint32_t idx) {   // KernelDynamicScene.cu:41-45
     return S.d->light_cdf[idx] - (idx == 0 ? 0.0f : S.d->light_cdf[idx - 1]);
 }
+// ---- InfiniteLight (SceneTypes/Light.h:294-367, Light.cu:350-511,
+// Light.cpp:10-58) with the identity world transform.  The radiance map is
+// S.d->textures[env->texture]; the tables are the desc's env_data.
+const float O_EPSILON = 0.000001f;               // MathFunc.h:21
+const float O_INV_TWOPI = 1.0f / (2.0f * O_PI);  // MathFunc.h:14
+inline float luminance(Spec s) { return s.x * 0.212671f + s.y * 0.715160f + s.z * 0.072169f; }   // Spectrum.cu:174-177
+// KernelMIPMap::Sample(float width = 0, int x, int y) (MIPMap.cu:155-172): log2(1e-8) < 0 -> level 0, clamped x/y
+Spec env_texel(const ctl_scene_desc* d, int x, int y) {
+    const ctl_texture& t = d->textures[d->env->texture];
+    x = omin(omax(x, 0), (int)t.width - 1);
+    y = omin(omax(y, 0), (int)t.height - 1);
+    uint32_t c = d->tex_data[t.offsets[0] + (uint32_t)y * t.width + (uint32_t)x];
+    return v3(float(c & 0xff) / 255.0f, float((c >> 8) & 0xff) / 255.0f, float((c >> 16) & 0xff) / 255.0f);
+}
+float interval_to_tent(float sample) {   // Warp::intervalToTent (Math/Warp.h:13-27)
+    float sign = 1;
+    if (sample < 0.5f) sample *= 2;
+    else { sign = -1; sample = 2 * (sample - 0.5f); }
+    return sign * (1 - sqrtf(sample));
+}
+V2 env_latlong(V3 v) {   // atan2(v.x, -v.z) / 2pi, safe_acos(v.y) / pi
+    return v2(cr_atan2(v.x, -v.z) * O_INV_TWOPI, cr_acos(omin(1.0f, omax(-1.0f, v.y))) * O_INV_PI);
+}
+// the two bilinear rows of (xPos, yPos) and the pdf numerator they give
+void env_rows(const ctl_scene_desc* d, int xPos, int yPos, float dx1, float dy1, Spec& value1, Spec& value2, float& pdf) {
+    const ctl_env_light& L = *d->env;
+    const float* rowWeights = d->env_data + L.row_weights;
+    float dx2 = 1.0f - dx1, dy2 = 1.0f - dy1;
+    value1 = env_texel(d, xPos, yPos) * dx2 * dy2 + env_texel(d, xPos + 1, yPos) * dx1 * dy2;
+    value2 = env_texel(d, xPos, yPos + 1) * dx2 * dy1 + env_texel(d, xPos + 1, yPos + 1) * dx1 * dy1;
+    int h = (int)L.size[1];
+    pdf = (luminance(value1) * rowWeights[omin(omax(yPos, 0), h - 1)] +
+           luminance(value2) * rowWeights[omin(omax(yPos + 1, 0), h - 1)]) * L.normalization;
+}
+// InfiniteLight::sampleDirect + internalSampleDirection (Light.cu:350-365, 420-457)
+Spec env_sample_direct(const ctl_scene_desc* d, DRec& dRec, V2 sample) {
+    const ctl_env_light& L = *d->env;
+    float qpdf;
+    uint32_t row = sample_reuse(d->env_data + L.cdf_rows, (uint32_t)L.size[1], sample.y, qpdf);
+    uint32_t col = sample_reuse(d->env_data + L.cdf_cols + row * (uint32_t)(L.size[0] + 1), (uint32_t)L.size[0],
+                                sample.x, qpdf);
+    V2 pos = v2((float)col + interval_to_tent(sample.x), (float)row + interval_to_tent(sample.y));
+    int xPos = omin(omax((int)floorf(pos.x), 0), (int)(L.size[0] - 1));
+    int yPos = omin(omax((int)floorf(pos.y), 0), (int)(L.size[1] - 1));
+    Spec value1, value2;
+    float pdf;
+    env_rows(d, xPos, yPos, pos.x - xPos, pos.y - yPos, value1, value2, pdf);
+    Spec value = (value1 + value2) * v3(L.scale[0], L.scale[1], L.scale[2]);
+    float phi = L.pixel_size[0] * (pos.x + 0.5f), theta = L.pixel_size[1] * (pos.y + 0.5f);
+    float sinTheta = cr_sin(theta);
+    V3 dir = v3(cr_sin(phi) * sinTheta, cr_cos(theta), -cr_cos(phi) * sinTheta);
+    pdf /= omax(std::fabs(sinTheta), O_EPSILON);
+    dRec.pdf = pdf;
+    dRec.p = v3(L.scene_center[0], L.scene_center[1], L.scene_center[2]) + dir * L.scene_radius;
+    dRec.n = -normalize(dir);
+    dRec.dist = L.scene_radius;
+    dRec.d = normalize(dir);
+    dRec.measure = ESolidAngle;
+    return spec_div(value, pdf);
+}
+// InfiniteLight::pdfDirect + internalPdfDirection (Light.cu:367-377, 459-479)
+float env_pdf_direct(const ctl_scene_desc* d, const DRec& dRec) {
+    const ctl_env_light& L = *d->env;
+    V2 uv = env_latlong(dRec.d);
+    float u = uv.x * L.size[0] - 0.5f, v = uv.y * L.size[1] - 0.5f;
+    int xPos = (int)floorf(u), yPos = (int)floorf(v);
+    Spec value1, value2;
+    float pdf;
+    env_rows(d, xPos, yPos, u - xPos, v - yPos, value1, value2, pdf);
+    float sinTheta = sqrtf(omax(0.0f, 1 - dRec.d.y * dRec.d.y));
+    float pdfSA = pdf / omax(std::fabs(sinTheta), O_EPSILON);
+    if (dRec.measure == ESolidAngle) return pdfSA;
+    if (dRec.measure == EArea) return pdfSA * absdot(dRec.d, dRec.n) / (dRec.dist * dRec.dist);
+    return 0.0f;
+}
+// KernelDynamicScene::EvalEnvironment(r) -> InfiniteLight::evalEnvironment: Sample(uv, 0) = triangle(0, uv)
+Spec env_eval(const ctl_scene_desc* d, V3 dir) {
+    if (d->env_map_index == UINT_MAX) return v3s(0.0f);
+    const ctl_env_light& L = *d->env;
+    c5::Mip M{d->textures + L.texture, d->tex_data};
+    return c5::triangle(M, 0, env_latlong(dir)) * v3(L.scale[0], L.scale[1], L.scale[2]);
+}
+// EvalEnvironment(r, rX, rY): the MIP map filtered over the differentials (Light.cu:496-511)
+Spec env_eval_diff(const ctl_scene_desc* d, V3 v, V3 vx, V3 vy) {
+    if (d->env_map_index == UINT_MAX) return v3s(0.0f);
+    const ctl_env_light& L = *d->env;
+    V2 uv = env_latlong(v);
+    V3 dvdx = vx - v, dvdy = vy - v;
+    float t1 = O_INV_TWOPI / (v.x * v.x + v.z * v.z), t2 = -O_INV_PI / omax(sqrtf(omax(0.0f, 1.0f - v.y * v.y)), 1e-4f);
+    V2 dudx = v2(t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y), dudy = v2(t1 * (dvdy.z * v.x - dvdy.x * v.z), t2 * dvdy.y);
+    c5::Mip M{d->textures + L.texture, d->tex_data};
+    return c5::mip_eval(M, uv, dudx, dudy) * v3(L.scale[0], L.scale[1], L.scale[2]);
+}
+// Light::sampleDirect dispatch over the light kinds
+Spec sample_direct(const SceneView& S, const ctl_light& L, DRec& dRec, V2 sample) {
+    if (L.kind == CTL_LIGHT_INFINITE) return env_sample_direct(S.d, dRec, sample);
+    return light_sample_direct(S, L, dRec, sample);
+}
 inline float power_heuristic(float fPdf, float gPdf) {   // MonteCarlo.h:29-33 with nf=ng=1
     float f = 1 * fPdf, g = 1 * gPdf;
     return (f * f) / (f * f + g * g);
@@ -638,7 +736,7 @@ Spec estimate_direct(RenderCtx& C, BRec bRec, const ctl_material& mat, const ctl
     DRec dRec;
     dRec.p = bRec.dg.P; dRec.n = bRec.dg.sys.n; dRec.measure = EArea;
     dRec.ref = bRec.dg.P; dRec.refN = bRec.dg.sys.n;
-    Spec value = light_sample_direct(C.S, light, dRec, C.rng->randomFloat2());
+    Spec value = sample_direct(C.S, light, dRec, C.rng->randomFloat2());
     Spec retVal = v3s(0.0f);
     if (!spec_zero(value)) {
         bRec.wo = toLocal(bRec.dg.sys, dRec.d);
@@ -678,7 +776,7 @@ Spec uniform_sample_one_light(RenderCtx& C, const BRec& bRec, const ctl_material
     return spec_div(estimate_direct(C, bRec, mat, d->lights[idx], pdf), pdf);
 }
 
-// PathTrace<DIRECT> restricted to surfaces without media / env map (PathTracer.cu:10-113);
+// PathTrace<DIRECT> restricted to surfaces without media (PathTracer.cu:10-113);
 // DIRECT = false: emission unweighted (:66-67), no UniformSampleOneLight (:82-83)
 Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, V3 rXo, V3 rXd, V3 rYo, V3 rYd, int maxPathLength, int rrStartDepth,
                 bool direct = true) {
@@ -738,7 +836,16 @@ Spec path_trace(RenderCtx& C, V3 rori, V3 rdir, V3 rXo, V3 rXd, V3 rYo, V3 rYd, 
             cf = spec_div(cf, spec_max(cf));
         }
     }
-    if (r2.tri == UINT_MAX) cl = cl + (cf * 1.0f) * v3s(0.0f);   // EvalEnvironment without env map
+    if (r2.tri == UINT_MAX) {   // PathTracer.cu:98-111
+        float misWeight = 1.0f;
+        if (!(!direct || depth == 1 || specularBounce) && d->env_map_index != UINT_MAX) {
+            DRec dRec;   // DirectSamplingRecFromRay(r, dist, last_nor, 0, 0): solid angle along r
+            dRec.ref = rori; dRec.refN = last_nor; dRec.d = rdir; dRec.dist = r2.t; dRec.measure = ESolidAngle;
+            float direct_pdf = env_pdf_direct(d, dRec) * pdf_emitter(C.S, d->env_map_index);
+            misWeight = power_heuristic(brdf_scattering_pdf, direct_pdf);
+        }
+        cl = cl + (cf * misWeight) * env_eval(d, rdir);
+    }
     return cl;
 }
 
@@ -955,7 +1062,7 @@ uint64_t wpt_render(const ctl_scene_desc* d, bool nee, int maxPathLength, int rr
                             float fU = cdf[idx], fL = idx > 0 ? cdf[idx - 1] : 0.0f;
                             sample.x = (sample.x - fL) / (fU - fL);
                             float emPdf = fU - fL;
-                            value = light_sample_direct(S, d->lights[idx], dRec, sample);
+                            value = sample_direct(S, d->lights[idx], dRec, sample);
                             if (dRec.pdf != 0) {
                                 dRec.pdf *= emPdf;
                                 value = spec_div(value, emPdf);
@@ -985,7 +1092,14 @@ uint64_t wpt_render(const ctl_scene_desc* d, bool nee, int maxPathLength, int rr
                 }
             } else {
                 terminated = true;
-                p.L = p.L + (1.0f * p.throughput) * v3s(0.0f);   // misWeight * throughput * EvalEnvironment
+                float misWeight = 1.0f;   // WavefrontPathTracer.cu:144-157
+                if (nee && !(pass == 0 || p.specular_bounce) && d->env_map_index != UINT_MAX) {
+                    DRec dRec;
+                    dRec.ref = rori; dRec.refN = normal_decode((uint16_t)p.prev_normal); dRec.d = rdir;
+                    dRec.dist = h.dist; dRec.measure = ESolidAngle;
+                    misWeight = power_heuristic(p.bsdf_pdf, env_pdf_direct(d, dRec) * pdf_emitter(S, d->env_map_index));
+                }
+                p.L = p.L + (misWeight * p.throughput) * env_eval(d, rdir);
             }
             if (terminated) add_sample(fb, W, H, p.hx, p.hy, p.L);
         }
@@ -1476,6 +1590,8 @@ uint64_t oracle_prim_pass(const ctl_scene_desc* desc, const ctl_prim_params* prm
                             else L = Le + through * (uniform_sample_one_light(C, bRec, mat) + f_avg * 0.5f);
                         }
                     }
+                } else {
+                    L = env_eval_diff(desc, d, dX, dY);   // PrimTracer.cu:102
                 }
                 out[(size_t)y * W + x] = L;
                 if (depth) depth[(size_t)y * W + x] = depth_d3d(h.t, nd, fd);   // g_DepthImage2.Store
@@ -1585,6 +1701,67 @@ void oracle_light_tri(const float* woop12, const uint32_t* tri_data8, const floa
     for (int i = 0; i < 3; i++) { p9[3 * i] = p[i].x; p9[3 * i + 1] = p[i].y; p9[3 * i + 2] = p[i].z; }
     n3[0] = dg.sys.n.x; n3[1] = dg.sys.n.y; n3[2] = dg.sys.n.z;
     *area = a;
+}
+
+// InfiniteLight::InfiniteLight (Light.cpp:10-58) over texture `t`: the column
+// CDFs ((w + 1) x h), the row CDF (h + 1) and the row weights (h) in out, and
+// (normalization, pixel_size.x, pixel_size.y) in out3
+void oracle_env_tables(const ctl_texture* t, const uint32_t* tex_data, float* out, float* out3) {
+    const uint32_t w = t->width, h = t->height;
+    float* cdfCols = out;
+    float* cdfRows = out + (size_t)(w + 1) * h;
+    float* rowWeights = cdfRows + h + 1;
+    auto lum = [&](uint32_t x, uint32_t y) {   // radianceMap.Sample(0, x, y).getLuminance()
+        uint32_t c = tex_data[t->offsets[0] + y * w + x];
+        Spec v = v3(float(c & 0xff) / 255.0f, float((c >> 8) & 0xff) / 255.0f, float((c >> 16) & 0xff) / 255.0f);
+        return luminance(v);
+    };
+    float rowSum = 0.0f;
+    cdfRows[0] = 0;
+    for (uint32_t y = 0; y < h; ++y) {
+        float* col = cdfCols + (size_t)y * (w + 1);
+        float colSum = 0;
+        col[0] = 0;
+        for (uint32_t x = 0; x < w; ++x) {
+            colSum += lum(x, y);
+            col[x + 1] = colSum;
+        }
+        float norm = 1.0f / colSum;
+        for (uint32_t x = 1; x < w; ++x) col[x] *= norm;   // entries 1 .. w-1; entry w is set to 1
+        col[w] = 1.0f;
+        float weight = cr_sin((y + 0.5f) * O_PI / (float)h);
+        rowWeights[y] = weight;
+        rowSum += colSum * weight;
+        cdfRows[y + 1] = rowSum;
+    }
+    float norm = 1.0f / rowSum;
+    for (uint32_t y = 1; y < h; ++y) cdfRows[y] *= norm;
+    cdfRows[h] = 1.0f;
+    out3[0] = 1.0f / (rowSum * (2 * O_PI / (float)w) * (O_PI / (float)h));
+    out3[1] = 2 * O_PI / (float)w;
+    out3[2] = O_PI / (float)h;
+}
+
+// InfiniteLight::sampleDirect for n 2D samples of the desc's environment light:
+// out7 = (d.xyz, pdf, value/pdf rgb); and pdfDirect / evalEnvironment along n
+// directions: out4 = (pdf, radiance rgb)
+void oracle_env_sample(const ctl_scene_desc* desc, uint64_t n, const float* samples2, float* out7) {
+    for (uint64_t i = 0; i < n; i++) {
+        DRec dRec;
+        Spec v = env_sample_direct(desc, dRec, v2(samples2[2 * i], samples2[2 * i + 1]));
+        float* o = out7 + 7 * i;
+        o[0] = dRec.d.x; o[1] = dRec.d.y; o[2] = dRec.d.z; o[3] = dRec.pdf; o[4] = v.x; o[5] = v.y; o[6] = v.z;
+    }
+}
+void oracle_env_eval(const ctl_scene_desc* desc, uint64_t n, const float* dirs3, float* out4) {
+    for (uint64_t i = 0; i < n; i++) {
+        DRec dRec;
+        dRec.d = v3(dirs3[3 * i], dirs3[3 * i + 1], dirs3[3 * i + 2]);
+        dRec.measure = ESolidAngle;
+        Spec v = env_eval(desc, dRec.d);
+        float* o = out4 + 4 * i;
+        o[0] = env_pdf_direct(desc, dRec); o[1] = v.x; o[2] = v.y; o[3] = v.z;
+    }
 }
 
 void oracle_matrix_inverse(const float* in16, float* out16) {

@@ -4,6 +4,8 @@ import ctypes as C
 import os
 import re
 
+import pytest
+
 import cudatracerlib_amd._abi as abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -40,6 +42,41 @@ def test_reference_layout_sizes():
     assert C.sizeof(abi.Material) == 80       # flattened Material + BSDF parameters
     assert C.sizeof(abi.Texture) == 380       # ImageTexture + KernelMIPMap
     assert C.sizeof(abi.PixelVariance) == 44  # PixelVarianceInfo
+    assert C.sizeof(abi.Light) == 48          # flattened DiffuseLight / InfiniteLight header
+    assert C.sizeof(abi.EnvLight) == 72       # InfiniteLight
+
+
+# ctypes mirror <-> include/ctl_trace.h: every field offset and struct size as
+# the C compiler lays them out (gcc on a generated probe, no GPU needed)
+_LAYOUT_STRUCTS = [("ctl_scene_desc", "SceneDesc"), ("ctl_light", "Light"), ("ctl_env_light", "EnvLight"),
+                   ("ctl_texture", "Texture"), ("ctl_material", "Material"), ("ctl_camera", "Camera")]
+
+
+_C_FIELD = {("ctl_texture", "mapping"): "m11"}   # the mirror packs m11..m23 as one array
+
+
+def test_struct_layouts_match_header(tmp_path):
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ctl_trace.h"', 'int main(void) {']
+    expect = []
+    for cname, pname in _LAYOUT_STRUCTS:
+        py = getattr(abi, pname)
+        lines.append(f'printf("%zu\\n", sizeof({cname}));')
+        expect.append(C.sizeof(py))
+        for f in py._fields_:
+            cfield = _C_FIELD.get((cname, f[0]), f[0])
+            lines.append(f'printf("%zu\\n", offsetof({cname}, {cfield}));')
+            expect.append(getattr(py, f[0]).offset)
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == expect
 
 
 def test_create_without_gpu_fails_cleanly():
