@@ -1,6 +1,7 @@
 // bvh_wide.cpp — see bvh_wide.h.
 #include "bvh_wide.h"
 
+#include <algorithm>
 #include <cstring>
 #include <limits>
 #include <stdexcept>
@@ -47,11 +48,93 @@ struct Collapser {
         return nodes[i];
     }
 
+    // SAH-optimal collapse (the wide-BVH dynamic program of Ylitie, Karras and
+    // Laine, HPG 2017, over fixed leaves): every binary inner node is either a
+    // wide node of its own or opened into its parent's slots.  With the leaves
+    // fixed their intersection cost is the same in every collapse, so the cost
+    // to minimise is the summed surface area of the wide nodes (a wide node is
+    // visited when a ray hits its box).  Per binary node x and slot budget k:
+    //   g(x, 1) = f(x) = A(x) + min_j g(l, j) + g(r, 4 - j)   (x its own node)
+    //   g(x, k) = min(g(x, 1), min_j g(l, j) + g(r, k - j))    (x opened)
+    // and g = 0 for leaves.  choice[] keeps the argmin per (x, k).
+    std::vector<float> g;               // 4 per binary node: g(x, 1..4)
+    std::vector<uint8_t> choice;        // 4 per node: 0 = own node, j = left gets j slots
+    std::vector<uint8_t> fsplit;        // per node: the j of f(x)
+
+    void plan(int32_t root) {
+#ifdef CTL_COLLAPSE_GREEDY
+        (void)root;
+#else
+        g.assign(n_nodes * 4, 0.0f);
+        choice.assign(n_nodes * 4, 0);
+        fsplit.assign(n_nodes, 1);
+        std::vector<std::pair<int32_t, bool>> st;   // post order without recursion
+        st.push_back({root, false});
+        size_t visits = 0;
+        while (!st.empty()) {
+            auto [v, done] = st.back();
+            st.pop_back();
+            const ctl_bvh_node& n = node_of(v);
+            Kid a, b;
+            binary_kids(n, (uint32_t)v >> 2, a, b);
+            if (!done) {
+                if (++visits > n_nodes) throw std::runtime_error("wide BVH: a node is reached twice");
+                st.push_back({v, true});
+                if (is_inner(a.v)) st.push_back({a.v, false});
+                if (is_inner(b.v)) st.push_back({b.v, false});
+                continue;
+            }
+            const size_t x = (size_t)v / 4;
+            auto G = [&](const Kid& c, int k) { return is_inner(c.v) ? g[(size_t)c.v / 4 * 4 + (k - 1)] : 0.0f; };
+            // the node's own box: the union of its children's (the parent's slot holds it)
+            float best = std::numeric_limits<float>::infinity();
+            int bj = 1;
+            for (int j = 1; j <= 3; j++) {
+                const float c = G(a, j) + G(b, 4 - j);
+                if (c < best) { best = c; bj = j; }
+            }
+            fsplit[x] = (uint8_t)bj;
+            Kid u = a;
+            for (int i = 0; i < 3; i++) {
+                u.lo[i] = std::min(a.lo[i], b.lo[i]);
+                u.hi[i] = std::max(a.hi[i], b.hi[i]);
+            }
+            // a sentinel sibling has no box: the node's box is its one real child's
+            const Kid& box = b.v == kSentinel ? a : (a.v == kSentinel ? b : u);
+            const float f = kid_area(box) + best;
+            g[4 * x] = f;
+            choice[4 * x] = 0;
+            for (int k = 2; k <= 4; k++) {
+                float bk = f;
+                int ck = 0;
+                for (int j = 1; j < k; j++) {
+                    const float c = G(a, j) + G(b, k - j);
+                    if (c < bk) { bk = c; ck = j; }
+                }
+                g[4 * x + k - 1] = bk;
+                choice[4 * x + k - 1] = (uint8_t)ck;
+            }
+        }
+#endif
+    }
+
+    // the slots subtree x fills with a budget of k (x's box taken from its parent)
+    void expand(const Kid& x, int k, Kid* out, int& nk) {
+        const int ck = is_inner(x.v) ? choice[(size_t)x.v / 4 * 4 + (k - 1)] : 0;
+        if (ck == 0) { out[nk++] = x; return; }
+        Kid a, b;
+        binary_kids(node_of(x.v), (uint32_t)x.v >> 2, a, b);
+        expand(a, ck, out, nk);
+        expand(b, k - ck, out, nk);
+    }
+
     int32_t emit(int32_t v, int depth) {
         if (depth > 256) throw std::runtime_error("wide BVH: tree too deep");
         Kid k[4];
         int nk = 2;
         binary_kids(node_of(v), (uint32_t)v >> 2, k[0], k[1]);
+#ifdef CTL_COLLAPSE_GREEDY
+        // greedy collapse: open the inner child of largest surface area until four children
         while (nk < 4) {
             int best = -1;
             float bestArea = -1.0f;
@@ -63,6 +146,15 @@ struct Collapser {
             k[best] = a;
             k[nk++] = b;
         }
+#else
+        {
+            const Kid a = k[0], b = k[1];
+            const int j = fsplit[(size_t)v / 4];
+            nk = 0;
+            expand(a, j, k, nk);
+            expand(b, 4 - j, k, nk);
+        }
+#endif
         const size_t me = out.size();
         out.push_back(WideNode{});
         if (src) {
@@ -97,7 +189,8 @@ int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_va
                       std::vector<uint32_t>* src) {
     if (!is_inner(root_value) || n_nodes == 0) throw std::runtime_error("wide BVH: root is not an inner node");
     if (src) src->clear();
-    Collapser c{nodes, n_nodes, out, out.size(), src};
+    Collapser c{nodes, n_nodes, out, out.size(), src, {}, {}, {}};
+    c.plan(root_value);
     return c.emit(root_value, 0);
 }
 
