@@ -69,6 +69,11 @@ def parse():
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="diagnostic: one process renders rank 0's share of an N-rank job "
                          "(N passes per step over the tiles with tile %% N == 0), no collective")
+    ap.add_argument("--steps-per-launch", type=int, default=4,
+                    help="steps whose passes go through one ctl_render_passes launch (1: one ctl_render_pass "
+                         "launch per pass, the reference's DoPass granularity)")
+    ap.add_argument("--one-pass-leg", type=int, default=8,
+                    help="passes of the one-launch-per-pass comparison leg (0: skip)")
     ap.add_argument("--bvh", default="wide", choices=["wide", "wideq", "binary"],
                     help="device traversal: 4-wide collapsed BVH, or the reference's binary order")
     return ap.parse_args()
@@ -212,6 +217,29 @@ def primary_ray_leg(pt, dev, stream, sptr, torch, pass_index, prof, launches=10)
     }
 
 
+def single_pass_leg(pt, fb, stream, sptr, torch, pass_index, passes):
+    """The same pass at the reference's DoPass granularity: one ctl_render_pass
+    launch per pass (sampler tables generated before each), bracketed like the
+    headline."""
+    pt.generate_samples(pass_index, sptr)
+    pt.render_pass(fb.data_ptr(), sptr)   # warm-up
+    torch.cuda.synchronize()
+    pt.reset_rays(sptr)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for k in range(passes):
+        pt.generate_samples(pass_index + 1 + k, sptr)
+        pt.render_pass(fb.data_ptr(), sptr)
+    e1.record(stream)
+    pt.sync(sptr)
+    ms = e0.elapsed_time(e1)
+    rays = pt.rays_traced()
+    return {"passes": passes, "ms_per_pass": round(ms / passes, 3), "mrays_s": round(rays / ms / 1e3, 1),
+            "note": "one ctl_render_pass launch per pass (reference DoPass granularity); the headline batches "
+                    "--steps-per-launch steps per ctl_render_passes launch"}
+
+
 def closest_shadow_leg(pt, fb, stream, sptr, torch, pass_index, passes):
     """The same pass with the reference's own KernelDynamicScene::Occluded
     (a closest-hit shadow traversal tested against the light distance,
@@ -335,11 +363,16 @@ def main():
     # kernel of each pass stays outside the brackets but inside the step time.
     kev = []
 
-    # One shard's N passes of a step go through one ctl_render_passes launch
-    # (same framebuffer as N sequential passes), so a rank owning 1/N of the
-    # tiles keeps the resident grid as busy as a full-image pass does.
-    def step(s, timed=False):
-        pidx = shard.step_pass_indices(s, shards, pass_base)
+    # The passes of G = --steps-per-launch consecutive steps (each step: this
+    # rank's tiles of N passes when sharded, one full-image pass otherwise) go
+    # through one ctl_render_passes launch: the same framebuffer as sequential
+    # passes (bit-exact, tests/test_gpu_parity.py), with the next pass's paths
+    # filling the CUs while the previous pass's longest paths finish (a
+    # one-pass launch idles ~10 % of its time in that tail).
+    G = max(1, a.steps_per_launch)
+
+    def step(s, timed=False, nsteps=1):
+        pidx = [p for k in range(nsteps) for p in shard.step_pass_indices(s + k, shards, pass_base)]
         if timed:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
@@ -356,8 +389,8 @@ def main():
             e1.record(stream)
             kev.append((e0, e1))
 
-    for s in range(a.warmup):
-        step(s)
+    for s in range(0, a.warmup, G):
+        step(s, nsteps=min(G, a.warmup - s))
     steps_done = a.warmup
     torch.cuda.synchronize(dev)
     fb.zero_()
@@ -371,8 +404,8 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for s in range(a.steps):
-        step(s, timed=True)
+    for s in range(0, a.steps, G):
+        step(s, timed=True, nsteps=min(G, a.steps - s))
     ev1.record(stream)
     if world > 1:
         shard.reduce_framebuffer(fb, dist)   # RCCL over xGMI
@@ -391,6 +424,9 @@ def main():
     prim = primary_ray_leg(pt, dev, stream, sptr, torch, nxt, prof) if rank == 0 else None
     wpt = (wpt_leg(ctl, pt, dev, sptr, torch, W, H, nxt + 1, a.wpt_passes)
            if rank == 0 and a.wpt_passes > 0 else None)
+    single = None
+    if rank == 0 and shards == 1 and G > 1 and a.one_pass_leg > 0:
+        single = single_pass_leg(pt, fb, stream, sptr, torch, nxt + 40, a.one_pass_leg)
     closest = None
     if rank == 0 and a.closest_shadow_passes > 0 and shards == 1:
         scratch = torch.zeros_like(fb)
@@ -411,9 +447,9 @@ def main():
         wsum = float(img[..., 6].sum().item())
         launches = len(kev)   # path-kernel launches on this rank in the timed region
         per_launch_ms = kernel_ms / launches
-        passes_per_launch = shards   # one ctl_render_passes launch per step when sharded
+        passes_per_launch = passes / launches   # this rank's passes (tiles of them when sharded) per launch
         fam = "path_kernel_full" if a.config == 5 else "path_kernel"
-        same_workload = (prof[0] or {}).get("config") == [a.config, a.scale, W, H] and passes_per_launch == 1
+        same_workload = (prof[0] or {}).get("config") == [a.config, a.scale, W, H, passes_per_launch]
         rl = roofline(prof if same_workload else (None, None, False), fam, per_launch_ms,
                       alg_bytes_per_pass * passes_per_launch, KERNEL_NAME[a.schedule])
         rl.update({"launches_timed": launches, "gpu_step_ms": round(step_ms / a.steps, 3),
@@ -421,7 +457,7 @@ def main():
                    "visits_per_launch": {"inner_nodes": int(st[1]), "tri_tests": int(st[2]),
                                          "instances": int(st[3]), "rays": int(st[0])}})
         if passes_per_launch > 1:
-            rl["launch"] = ("ctl_render_passes: the step's sampler tables, one path-kernel launch over all its "
+            rl["launch"] = ("ctl_render_passes: the launch's sampler tables, one path-kernel launch over all its "
                             "passes, slice fold (all inside the bracket)")
         out = {
             "metric": "Mrays/s (primary+secondary) at 1920x1080, San-Miguel-scale BVH",
@@ -455,6 +491,7 @@ def main():
             },
             "roofline": rl,
             "primary_rays": prim,
+            "one_pass_launches": single,
             "closest_hit_shadows": closest,
             "wavefront_tracer": wpt,
             "image_weight_sum": wsum,
