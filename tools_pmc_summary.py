@@ -23,8 +23,8 @@ import sys
 
 root = sys.argv[1]
 FAMILIES = {
-    "path_kernel": "path_kernel_persistent<false, true, true, false>",
-    "path_kernel_full": "path_kernel_persistent<false, true, true, true>",
+    "path_kernel": "path_kernel_persistent<false, true, true, 0>",
+    "path_kernel_full": "path_kernel_persistent<false, true, true, 1>",
     "primary_intersect": "intersect_kernel<false, false, true, true>",
     "prim_kernel": "prim_kernel<",
     "fold_samples": "fold_samples_kernel",
