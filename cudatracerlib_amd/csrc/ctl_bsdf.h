@@ -605,11 +605,15 @@ CTL_HD spec diffuse_reflectance(const ctl_material& m, const dgeom& dg, const Te
 }
 
 // BSDFALL::sample/f/pdf (BSDF.h:140-208): two-sided flip of wi around the
-// lobe, then the type switch.  `tex` = the scene's texture table.
-CTL_HD spec bsdf_sample(const ctl_material& m, bsdf_rec& b, float& pdf, f2 sample, const dgeom& dg, const TexView* tex) {
+// lobe, then the type switch.  `tex` = the scene's texture table.  `R`: the
+// diffuse reflectance at dg when the caller already evaluated it (a textured
+// diffuse hit samples and evaluates the same texture at the same dg for the
+// BSDF sample and for next-event estimation: one lookup serves both).
+CTL_HD spec bsdf_sample(const ctl_material& m, bsdf_rec& b, float& pdf, f2 sample, const dgeom& dg, const TexView* tex,
+                        const spec* R = nullptr) {
     if (m.bsdf_type == CTL_BSDF_DIFFUSE) {
         if (!diffuse_sample_dir(m, b, pdf, sample)) return mk3s(0.0f);
-        return diffuse_reflectance(m, dg, tex) * 1.0f;
+        return (R ? *R : diffuse_reflectance(m, dg, tex)) * 1.0f;
     }
     const bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
@@ -618,10 +622,10 @@ CTL_HD spec bsdf_sample(const ctl_material& m, bsdf_rec& b, float& pdf, f2 sampl
     return res;
 }
 
-CTL_HD spec bsdf_f(const ctl_material& m, bsdf_rec& b, const dgeom& dg, const TexView* tex) {
+CTL_HD spec bsdf_f(const ctl_material& m, bsdf_rec& b, const dgeom& dg, const TexView* tex, const spec* R = nullptr) {
     if (m.bsdf_type == CTL_BSDF_DIFFUSE) {
         if (!(b.type_mask & m.combined_type)) return mk3s(0.0f);
-        return diffuse_f_refl(m, b, diffuse_reflectance(m, dg, tex));
+        return diffuse_f_refl(m, b, R ? *R : diffuse_reflectance(m, dg, tex));
     }
     const bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;

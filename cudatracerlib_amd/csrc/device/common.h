@@ -284,6 +284,11 @@ __device__ __forceinline__ f2 primary_ray(const DevScene& S, SamplerDev& rng, ui
 // VGPRs.  A scene with an environment map always runs the env level (full
 // shading of constant diffuse materials is exact, see shade_hit).
 enum : int { kShadeLean = 0, kShadeFull = 1, kShadeEnv = 2 };
+#ifdef CTL_NO_ALPHA_TRACE   // measurement builds only: traversal without the alpha test
+#define CTL_ALPHA_OF(F) false
+#else
+#define CTL_ALPHA_OF(F) ((F) != 0)
+#endif
 
 __device__ __forceinline__ EnvView env_view(const DevScene& S) { return EnvView{S.env, S.env_data, S.textures, S.tex_data}; }
 
@@ -318,7 +323,8 @@ __device__ __forceinline__ spec env_miss(const DevScene& S, const PathParams& P,
 // shadow ray is unoccluded (it returns +0 otherwise).
 template <int FULL>
 __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, const ctl_material& mat,
-                                           const bsdf_rec& b, const dgeom& dg, const TexView& tex, ShadowReq& sh) {
+                                           const bsdf_rec& b, const dgeom& dg, const TexView& tex, ShadowReq& sh,
+                                           const spec* R = nullptr) {
     f2 sample = rng.next2();
     const uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
     uint32_t first = 0, cnt = nl;   // STL_upper_bound
@@ -343,7 +349,7 @@ __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, c
         bsdf_rec b2 = b;
         b2.wo = to_local(dg.sys, dRec.d);
         b2.type_mask = kEAll & ~kEDelta;
-        spec bsdfVal = FULL ? bsdf_f(mat, b2, dg, &tex) : diffuse_f(mat, b2);
+        spec bsdfVal = FULL ? bsdf_f(mat, b2, dg, &tex, R) : diffuse_f(mat, b2);
         if (!spec_zero(bsdfVal)) {
             float weight = 1.0f;
             if (dRec.measure != kEDiscrete)
@@ -422,10 +428,16 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
         spec Le = (dot(dg.sys.n, w) <= 0) ? mk3s(0.0f) : mk3(L.radiance[0], L.radiance[1], L.radiance[2]);
         v.cl = v.cl + (v.cf * misWeight) * Le;
     }
-    spec f = FULL ? bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex) : diffuse_sample(mat, b, v.brdf_pdf, rng.next2());
+    // a textured diffuse hit: one texture lookup for the BSDF sample and the NEE evaluation
+    const bool texd = FULL && mat.bsdf_type == CTL_BSDF_DIFFUSE && mat.texture != 0xffffffffu;
+    spec Rtex = mk3s(0.0f);
+    if (texd) Rtex = diffuse_reflectance(mat, dg, &tex);
+    const spec* Rp = texd ? &Rtex : nullptr;
+    spec f = FULL ? bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex, Rp)
+                  : diffuse_sample(mat, b, v.brdf_pdf, rng.next2());
     v.last_nor = dg.sys.n;
     if (P.direct && (mat.combined_type & kESmooth) != 0 && S.n_lights) {   // PathTracer.cu:82-83
-        nee_sample<FULL>(S, rng, mat, b, dg, tex, sh);
+        nee_sample<FULL>(S, rng, mat, b, dg, tex, sh, Rp);
         if (sh.valid) sh.add = v.cf * sh.add;
     }
     v.specular = (b.sampled_type & kEDelta) != 0;

@@ -79,7 +79,7 @@ struct PathCtx {
         HitRec r2;   // traceRay (TraceHelper.cu:174-180)
         r2.t = FLT_MAX; r2.tri = 0xffffffffu; r2.node = 0xffffffffu; r2.u = r2.v = 0.0f;
         rays++;
-        ok &= trace_one<0, STATS, SINGLE, WIDE, FULL != 0>(S, v.rori, v.rdir, 0.0f, S.ray_eps, r2, st, &ts);
+        ok &= trace_one<0, STATS, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, v.rori, v.rdir, 0.0f, S.ray_eps, r2, st, &ts);
         if (r2.tri == 0xffffffffu) {
             v.cl = v.cl + env_miss<FULL>(S, P, v);   // PathTracer.cu:98-111
             return false;
@@ -91,8 +91,8 @@ struct PathCtx {
             HitRec h;
             h.t = any ? sh.dist - S.ray_eps : FLT_MAX; h.tri = 0xffffffffu; h.node = 0xffffffffu; h.u = h.v = 0.0f;
             rays++;
-            if (any) ok &= trace_one<1, STATS, SINGLE, WIDE, FULL != 0>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
-            else ok &= trace_one<0, STATS, SINGLE, WIDE, FULL != 0>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            if (any) ok &= trace_one<1, STATS, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            else ok &= trace_one<0, STATS, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
             if (!shadow_occluded(S, any, h, sh.dist)) v.cl = v.cl + sh.add;
         }
         return cont;
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             const long long pc0 = wall_clock64();
 #endif
             if (S.n_nodes != 0) {
-                Traverser<2, STATS, SINGLE, WIDE, FULL != 0> T;
+                Traverser<2, STATS, SINGLE, WIDE, CTL_ALPHA_OF(FULL)> T;
                 T.anyhit = shadowPhase && shadowAny;
                 T.init(S, v.rori, shadowPhase ? sh.d : v.rdir, 0.0f, S.ray_eps, h.t, st, &ts);
                 while (!T.done) T.round(S, st, &ts);

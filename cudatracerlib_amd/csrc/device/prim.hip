@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kBlock) void prim_kernel(DevScene S, PathParams P, 
         HitRec h;
         h.t = FLT_MAX; h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
         rays++;
-        if (S.n_nodes != 0) ok &= trace_one<0, false, SINGLE, WIDE, FULL != 0>(S, o, d, 0.0f, S.ray_eps, h, st, &ts);
+        if (S.n_nodes != 0) ok &= trace_one<0, false, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, o, d, 0.0f, S.ray_eps, h, st, &ts);
         spec L = mk3s(0.0f);
         if (h.tri != 0xffffffffu) {
             if (Q.mode == CTL_PRIM_LINEAR_DEPTH) {
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void prim_kernel(DevScene S, PathParams P, 
                                 hs.t = sh.dist - S.ray_eps; hs.u = hs.v = 0.0f;
                                 hs.tri = 0xffffffffu; hs.node = 0xffffffffu;
                                 rays++;
-                                ok &= trace_one<1, false, SINGLE, WIDE, FULL != 0>(S, dg.P, sh.d, 0.0f, S.ray_eps, hs, st, &ts);
+                                ok &= trace_one<1, false, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, dg.P, sh.d, 0.0f, S.ray_eps, hs, st, &ts);
                                 if (!shadow_occluded(S, true, hs, sh.dist)) direct = sh.add;
                             }
                         }

@@ -194,7 +194,12 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs
                 else surviveRR = false;
             }
             if (A.depth + 1 != A.max_path_length && surviveRR) {
-                spec f = FULL ? bsdf_sample(mat, b, bpdf, rng.next2(), dg, &tex)
+                // textured diffuse: one texture lookup for the BSDF sample and the NEE evaluation
+                const bool texd = FULL && mat.bsdf_type == CTL_BSDF_DIFFUSE && mat.texture != 0xffffffffu;
+                spec Rtex = mk3s(0.0f);
+                if (texd) Rtex = diffuse_reflectance(mat, dg, &tex);
+                const spec* Rp = texd ? &Rtex : nullptr;
+                spec f = FULL ? bsdf_sample(mat, b, bpdf, rng.next2(), dg, &tex, Rp)
                               : diffuse_sample(mat, b, bpdf, rng.next2());
                 specular = (b.sampled_type & kEDelta) != 0;
                 const f3 out = to_world(dg.sys, b.wo);
@@ -220,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs
                     if (!spec_zero(value)) {
                         b.type_mask = kEAll & ~kEDelta;
                         b.wo = to_local(dg.sys, dRec.d);
-                        spec bsdfVal = FULL ? bsdf_f(mat, b, dg, &tex) : diffuse_f(mat, b);
+                        spec bsdfVal = FULL ? bsdf_f(mat, b, dg, &tex, Rp) : diffuse_f(mat, b);
                         const float bsdfPdf = FULL ? bsdf_pdf(mat, b) : diffuse_pdf(mat, b);
                         const float directPdf = dRec.pdf;   // measure is ESolidAngle after sampleDirect
                         const float weight = power_heuristic(directPdf, bsdfPdf);
