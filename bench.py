@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="diagnostic: one process renders rank 0's share of an N-rank job "
                          "(N passes per step over the tiles with tile %% N == 0), no collective")
-    ap.add_argument("--steps-per-launch", type=int, default=4,
+    ap.add_argument("--steps-per-launch", type=int, default=8,
                     help="steps whose passes go through one ctl_render_passes launch (1: one ctl_render_pass "
                          "launch per pass, the reference's DoPass granularity)")
     ap.add_argument("--one-pass-leg", type=int, default=8,

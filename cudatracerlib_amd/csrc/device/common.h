@@ -278,17 +278,18 @@ __device__ __forceinline__ f2 primary_ray(const DevScene& S, SamplerDev& rng, ui
 
 // Shading level of the path kernels (template FULL, DevScene::full_shading):
 // lean = constant diffuse materials only; full = C5 materials (ray
-// differentials, partials, the BSDF type switch, alpha tests); env = full plus
-// the environment light.  The environment code lives only in the env
+// differentials, partials, the BSDF type switch); alpha = full plus
+// alpha-tested traversal (scenes with alpha maps); env = alpha plus the
+// environment light.  The alpha test stays out of scenes without alpha maps:
+// its code in the leaf loop costs the full kernel 2 % on C5.  The environment code lives only in the env
 // instantiation: inlined into the others it costs the hot kernel ~80 spilled
 // VGPRs.  A scene with an environment map always runs the env level (full
 // shading of constant diffuse materials is exact, see shade_hit).
-enum : int { kShadeLean = 0, kShadeFull = 1, kShadeEnv = 2 };
-#ifdef CTL_NO_ALPHA_TRACE   // measurement builds only: traversal without the alpha test
-#define CTL_ALPHA_OF(F) false
-#else
-#define CTL_ALPHA_OF(F) ((F) != 0)
-#endif
+enum : int { kShadeLean = 0, kShadeFull = 1, kShadeEnv = 2, kShadeAlpha = 3 };
+// the traversal's ALPHA flag of a shading level
+#define CTL_ALPHA_OF(F) ((F) == kShadeEnv || (F) == kShadeAlpha)
+// kernels that never trace (wavefront shade, WPT iterate) share the full instantiation
+#define CTL_NO_TRACE_LEVEL(F) ((F) == kShadeAlpha ? kShadeFull : (F))
 
 __device__ __forceinline__ EnvView env_view(const DevScene& S) { return EnvView{S.env, S.env_data, S.textures, S.tex_data}; }
 

@@ -797,6 +797,7 @@ CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
         if (m.bsdf_type != CTL_BSDF_DIFFUSE || m.texture != 0xffffffffu || m.alpha_state) S.full_shading = kShadeFull;
         if (m.alpha_state) S.alpha = 1;   // DynamicScene.cpp:586 doAlphaMapping
     }
+    if (S.alpha) S.full_shading = kShadeAlpha;
     if (S.env_index != 0xffffffffu) S.full_shading = kShadeEnv;
     S.single = 0;
     if (d->n_nodes > 0 && d->scene_start_node < 0) {
@@ -1000,7 +1001,8 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
                                dim3(kBlock), lds, s, c->scene, P, s1, s2, threads, cursor,                       \
                                c->d_counters, PS, tbl);                                                          \
         } while (0)
-#define PK2(ST, SG, WD) do { if (full == kShadeEnv) PK(ST, SG, WD, kShadeEnv); else if (full) PK(ST, SG, WD, kShadeFull); else PK(ST, SG, WD, kShadeLean); } while (0)
+#define PK2(ST, SG, WD) do { if (full == kShadeEnv) PK(ST, SG, WD, kShadeEnv); else if (full == kShadeAlpha) PK(ST, SG, WD, kShadeAlpha); \
+                              else if (full) PK(ST, SG, WD, kShadeFull); else PK(ST, SG, WD, kShadeLean); } while (0)
         if (stats) { if (single) PK2(true, true, false); else PK2(true, false, false); }
         else if (wide) { if (single) PK2(false, true, true); else PK2(false, false, true); }
         else { if (single) PK2(false, true, false); else PK2(false, false, false); }
@@ -1009,7 +1011,8 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
     } else {
 #define MK(ST, SG, WD, FU) hipLaunchKernelGGL((path_kernel<ST, SG, WD, FU>), grid, dim3(kBlock), kStackLdsBytes, s, c->scene, \
                                               P, s1, s2, fb, c->d_counters, PS)
-#define MK2(ST, SG, WD) do { if (full == kShadeEnv) MK(ST, SG, WD, kShadeEnv); else if (full) MK(ST, SG, WD, kShadeFull); else MK(ST, SG, WD, kShadeLean); } while (0)
+#define MK2(ST, SG, WD) do { if (full == kShadeEnv) MK(ST, SG, WD, kShadeEnv); else if (full == kShadeAlpha) MK(ST, SG, WD, kShadeAlpha); \
+                              else if (full) MK(ST, SG, WD, kShadeFull); else MK(ST, SG, WD, kShadeLean); } while (0)
         if (stats) { if (single) MK2(true, true, false); else MK2(true, false, false); }
         else if (wide) { if (single) MK2(false, true, true); else MK2(false, false, true); }
         else { if (single) MK2(false, true, false); else MK2(false, false, false); }

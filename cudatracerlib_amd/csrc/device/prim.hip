@@ -208,7 +208,8 @@ CTL_API ctl_status ctl_prim_pass(ctl_ctx* c, const ctl_prim_params* p, ctl_pixel
                            kStackLdsBytes, s, c->scene, P, Q, c->d_s1[c->active], c->d_s2[c->active], items,     \
                            cursor, c->d_counters, d_fb, d_depth);                                                \
     } while (0)
-#define PRK2(SG, WD) do { if (full == kShadeEnv) PRK(SG, WD, kShadeEnv); else if (full) PRK(SG, WD, kShadeFull); else PRK(SG, WD, kShadeLean); } while (0)
+#define PRK2(SG, WD) do { if (full == kShadeEnv) PRK(SG, WD, kShadeEnv); else if (full == kShadeAlpha) PRK(SG, WD, kShadeAlpha); \
+                           else if (full) PRK(SG, WD, kShadeFull); else PRK(SG, WD, kShadeLean); } while (0)
     if (wide) { if (single) PRK2(true, true); else PRK2(false, true); }
     else { if (single) PRK2(true, false); else PRK2(false, false); }
 #undef PRK2

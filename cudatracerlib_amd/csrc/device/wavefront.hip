@@ -321,7 +321,7 @@ int wavefront_pass(ctl_ctx* c, const PathParams& P, const SampleSlots& SS, bool 
     for (int b = 0; b < maxB; b++) {
         const uint32_t* cnt = &W.counts[2 * b];
         launch_trace<0>(c, s, W.q[b & 1], cnt, &cursors[2 * b], stats);
-        if (c->scene.full_shading == kShadeEnv)
+        if (CTL_NO_TRACE_LEVEL(c->scene.full_shading) == kShadeEnv)
             hipLaunchKernelGGL((wf_shade_kernel<kShadeEnv>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, SS);
         else if (c->scene.full_shading)
             hipLaunchKernelGGL((wf_shade_kernel<kShadeFull>), dim3(persist), dim3(kBlock), 0, s, c->scene, P, s1, s2, W, b, SS);

@@ -468,7 +468,7 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
     const float* s1 = c->d_s1[c->active];
     const float2* s2 = c->d_s2[c->active];
     const bool nee = prm->direct != 0;
-    const uint32_t full = c->scene.full_shading;
+    const uint32_t full = CTL_NO_TRACE_LEVEL(c->scene.full_shading);
 
     // count slots for every bounce of the pass (+1 for the last scan's output)
     const uint32_t slots = (uint32_t)prm->max_path_length + 1u;

@@ -45,7 +45,7 @@ for f in sorted(glob.glob(os.path.join(root, "g*", "**", "*counter_collection.cs
 here = os.path.dirname(os.path.abspath(__file__))
 libp = os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_trace.so")
 out = {"method": __doc__.strip(), "lib_sha256": hashlib.sha256(open(libp, "rb").read()).hexdigest(),
-       "config": [3, 1.0, 1920, 1080, 4], "kernels": {}}
+       "config": [3, 1.0, 1920, 1080, 8], "kernels": {}}
 try:
     out["git_head"] = subprocess.check_output(["git", "rev-parse", "--short", "HEAD"], cwd=here,
                                               stderr=subprocess.DEVNULL).decode().strip()
