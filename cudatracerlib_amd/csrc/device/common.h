@@ -566,6 +566,6 @@ void wpt_free(ctl_ctx* c);
 // (rays, hits)[0, n) and, in the same launch, (rays2, hits2)[0, n2)
 int intersect_launch(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit, hipStream_t s,
                      int64_t n2 = 0, const ctl_ray* rays2 = nullptr, ctl_hit* hits2 = nullptr,
-                     const uint32_t* dcount = nullptr);
+                     const uint32_t* dcount = nullptr, uint32_t band_w = 0);
 int count_rays(ctl_ctx* c, uint64_t n, hipStream_t s);
 }

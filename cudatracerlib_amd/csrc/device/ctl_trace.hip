@@ -373,7 +373,7 @@ __attribute__((amdgpu_waves_per_eu(CTL_INTERSECT_WAVES)))
 void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            int64_t n2, const ctl_ray* rays2, ctl_hit* hits2,
                                                            unsigned long long* cursor, unsigned long long* counters,
-                                                           const uint32_t* dcount) {
+                                                           const uint32_t* dcount, uint32_t band_w) {
     // dcount: the two segment sizes read from device memory (the WavefrontPathTracer's
     // queue counts, written by the previous bounce's scan: no host round trip); the
     // batch is then counted here as traced rays
@@ -411,8 +411,17 @@ void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
             if (lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
             base = __shfl(base, leader);
             if (need) {
-                const int64_t k = (int64_t)base + __popcll(mask & ((1ull << lane) - 1ull));
+                int64_t k = (int64_t)base + __popcll(mask & ((1ull << lane) - 1ull));
                 if (k < total) {
+                    // band_w: the first segment is a row-major image of that width (the
+                    // WavefrontPathTracer's camera rays); trace it in 8-row bands, column by
+                    // column, so a wave's 64 rays form an 8 x 8 block (hits go to their own
+                    // slots, so the results are those of row order)
+                    if (band_w && k < n) {
+                        const int64_t bw = 8 * (int64_t)band_w, band = k / bw, h = n / band_w;
+                        const int64_t bh = h - 8 * band < 8 ? h - 8 * band : 8, r = k - band * bw;
+                        k = (8 * band + r % bh) * band_w + r / bh;
+                    }
                     ray = k;
                     haveRay = true;
                     const float4* r4 = reinterpret_cast<const float4*>(k < n ? rays + k : rays2 + (k - n));
@@ -868,7 +877,7 @@ CTL_API ctl_status ctl_sampler_generate(ctl_ctx* c, uint64_t pass_index, void* s
 // segment sizes from dcount[0..1] on the device.
 static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit,
                                    bool stats, void* stream, int64_t n2 = 0, const ctl_ray* rays2 = nullptr,
-                                   ctl_hit* hits2 = nullptr, const uint32_t* dcount = nullptr) {
+                                   ctl_hit* hits2 = nullptr, const uint32_t* dcount = nullptr, uint32_t band_w = 0) {
     if (!c || n < 0 || (n > 0 && (!rays || !hits)) || n2 < 0 || (n2 > 0 && (!rays2 || !hits2))) return CTL_ERR_INVALID;
     if (!c->has_scene) { c->err = "intersect: no scene uploaded"; return CTL_ERR_STATE; }
     if (c->overflow_seen) return CTL_ERR_STATE;   // c->err names the overflow (ctl_sync)
@@ -885,7 +894,7 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
         const int nb = resident_blocks(c, intersect_kernel<AN, ST, SG, WD>, kStackLdsBytes);                     \
         hipLaunchKernelGGL((intersect_kernel<AN, ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)),     \
                            dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, n2, rays2, hits2, cursor,  \
-                           c->d_counters, dcount);                                                               \
+                           c->d_counters, dcount, band_w);                                                       \
     } while (0)
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;
@@ -1208,8 +1217,8 @@ static ctl_status add_rays(ctl_ctx* c, uint64_t n, hipStream_t s) {
 
 namespace ctl {
 int intersect_launch(ctl_ctx* c, int64_t n, const ctl_ray* rays, ctl_hit* hits, int32_t any_hit, hipStream_t s,
-                     int64_t n2, const ctl_ray* rays2, ctl_hit* hits2, const uint32_t* dcount) {
-    return launch_intersect(c, n, rays, hits, any_hit, false, s, n2, rays2, hits2, dcount);
+                     int64_t n2, const ctl_ray* rays2, ctl_hit* hits2, const uint32_t* dcount, uint32_t band_w) {
+    return launch_intersect(c, n, rays, hits, any_hit, false, s, n2, rays2, hits2, dcount, band_w);
 }
 int count_rays(ctl_ctx* c, uint64_t n, hipStream_t s) { return add_rays(c, n, s); }
 }  // namespace ctl

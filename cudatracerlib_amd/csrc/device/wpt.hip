@@ -506,7 +506,9 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
         // FinishIteration: payload rays, then the secondary buffer (closest
         // hit), as one launch over both batches (one resident grid, one tail);
         // the kernel counts the rays it traces
-        int r = intersect_launch(c, ub, B->rays[cur], B->hits, 0, s, depth ? ub : 0, B->sec, B->sec_hits, cnt);
+        // bounce 0: the camera rays, one per pixel in row order, traced in 8 x 8 blocks
+        int r = intersect_launch(c, ub, B->rays[cur], B->hits, 0, s, depth ? ub : 0, B->sec, B->sec_hits, cnt,
+                                 depth == 0 && (uint64_t)n0 == (uint64_t)A.width * A.height ? A.width : 0u);
         if (r != CTL_OK) return r;
         A.depth = depth;
 #define WPT_IT(NE, FU)                                                                                             \
