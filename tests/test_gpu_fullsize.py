@@ -78,6 +78,29 @@ def test_full_size_c3_closest_hit_shadows(ctl, orc, dev, c3):
     check(*full_pass(ctl, orc, d, dev, p)[:4])
 
 
+def test_full_size_c3_batched_passes_equal_sequential(ctl, dev, c3):
+    """The bench's launch shape: 8 passes in one ctl_render_passes launch give
+    the framebuffer and ray count of 8 ctl_render_pass calls, bit for bit."""
+    _, d = c3
+    pt = ctl.PathTracer(0)
+    try:
+        pt.upload_scene(d)
+        seq = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
+        pt.reset_rays()
+        for k in range(8):
+            pt.do_pass(seq.data_ptr(), 20 + k)
+        pt.sync()
+        seq_rays = pt.rays_traced()
+        bat = torch.zeros_like(seq)
+        pt.reset_rays()
+        pt.render_passes(bat.data_ptr(), 20, 8)
+        pt.sync()
+        assert pt.rays_traced() == seq_rays > 8 * 2 * W * H
+        assert torch.equal(seq.view(torch.int32), bat.view(torch.int32))
+    finally:
+        pt.close()
+
+
 def test_full_size_c5_pass_bit_exact(ctl, orc, dev, c3):
     c3[0].close()                      # free the C3 host arrays first
     hs = ctl.HostScene().generate(5, 1.0, W, H)
