@@ -281,10 +281,11 @@ __device__ __forceinline__ f2 primary_ray(const DevScene& S, SamplerDev& rng, ui
 // differentials, partials, the BSDF type switch); alpha = full plus
 // alpha-tested traversal (scenes with alpha maps); env = alpha plus the
 // environment light.  The alpha test stays out of scenes without alpha maps:
-// its code in the leaf loop costs the full kernel 2 % on C5.  The environment code lives only in the env
-// instantiation: inlined into the others it costs the hot kernel ~80 spilled
-// VGPRs.  A scene with an environment map always runs the env level (full
-// shading of constant diffuse materials is exact, see shade_hit).
+// its code in the leaf loop costs the full kernel 2 % on C5.  The environment
+// code lives only in the env instantiation: inlined into the others it costs
+// the hot kernel ~80 spilled VGPRs.  A scene with an environment map always
+// runs the env level (full shading of constant diffuse materials is exact, see
+// shade_hit).
 enum : int { kShadeLean = 0, kShadeFull = 1, kShadeEnv = 2, kShadeAlpha = 3 };
 // the traversal's ALPHA flag of a shading level
 #define CTL_ALPHA_OF(F) ((F) == kShadeEnv || (F) == kShadeAlpha)
