@@ -131,3 +131,16 @@ def test_image_resolve_oracle_matches_numpy(orc):
     c = (np.clip(srgb, 0, 1).astype(np.float32) * np.float32(255)).astype(np.uint32)
     want = c[:, 0] | (c[:, 1] << 8) | (c[:, 2] << 16) | (255 << 24)
     assert np.array_equal(out, want.astype(np.uint32))
+
+
+def test_oracle_regression_fixtures():
+    """The oracle's own outputs against committed digests (tests/golden/
+    make_oracle_regression.py): a regression guard on the restatement, not a
+    reference fixture."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_oracle_regression",
+                                                  os.path.join(GOLDEN, "make_oracle_regression.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    want = json.load(open(os.path.join(GOLDEN, "oracle_regression.json")))
+    assert mod.compute() == want
