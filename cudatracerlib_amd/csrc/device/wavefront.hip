@@ -287,7 +287,13 @@ void wavefront_free(ctl_ctx* c) {
 int wavefront_pass(ctl_ctx* c, const PathParams& P, const SampleSlots& SS, bool stats, hipStream_t s) {
     const uint64_t items = pass_items_of(P);   // owned pixels + apron items
     if (items == 0) return 0;
-    if (items > 0xffffffffull) { c->err = "wavefront: too many paths per pass"; return CTL_ERR_INVALID; }
+    // the 32-bit queue cursors take at most one extra fetch per resident lane after a queue runs
+    // dry (at most 2048 lanes per CU): leave that much headroom so a cursor cannot wrap onto live work
+    const int persist = c->cu_count * 8;
+    if (items > 0xffffffffull - (uint64_t)c->cu_count * 2048u) {
+        c->err = "wavefront: too many paths per pass";
+        return CTL_ERR_INVALID;
+    }
     WfState& W = c->wf;
     if (W.capacity < items) {
         (void)hipStreamSynchronize(s);
@@ -308,7 +314,6 @@ int wavefront_pass(ctl_ctx* c, const PathParams& P, const SampleSlots& SS, bool 
     }
     const float* s1 = c->d_s1[c->active];
     const float2* s2 = c->d_s2[c->active];
-    const int persist = c->cu_count * 8;
     const unsigned genBlocks = (unsigned)std::min<uint64_t>((items + kBlock - 1) / kBlock, (uint64_t)persist);
     // a path cut off by kMaxBounces stores nothing: its slot must read "no sample"
     if (hipMemsetAsync(SS.s, 0, items * sizeof(float4), s) != hipSuccess) {
