@@ -106,6 +106,11 @@ def pmc_profile():
     j = json.load(open(files[-1]))
     lib = os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_trace.so")
     match = hashlib.sha256(open(lib, "rb").read()).hexdigest() == j.get("lib_sha256")
+    if not match and j.get("src_sha256"):
+        # hipcc builds are not byte-reproducible: a rebuild of the profiled sources
+        # matches through the source fingerprint (buildid.py)
+        from buildid import source_fingerprint
+        match = "sources" if source_fingerprint(here) == j["src_sha256"] else False
     return j, os.path.relpath(files[-1], here), match
 
 

@@ -43,9 +43,11 @@ for f in sorted(glob.glob(os.path.join(root, "g*", "**", "*counter_collection.cs
         disp[fam][c].add((f, row.get("Dispatch_Id")))
 
 here = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, here)
+from buildid import source_fingerprint  # noqa: E402
 libp = os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_trace.so")
 out = {"method": __doc__.strip(), "lib_sha256": hashlib.sha256(open(libp, "rb").read()).hexdigest(),
-       "config": [3, 1.0, 1920, 1080, 8], "kernels": {}}
+       "src_sha256": source_fingerprint(here), "config": [3, 1.0, 1920, 1080, 8], "kernels": {}}
 try:
     out["git_head"] = subprocess.check_output(["git", "rev-parse", "--short", "HEAD"], cwd=here,
                                               stderr=subprocess.DEVNULL).decode().strip()
