@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--wpt-passes", type=int, default=3, help="WavefrontPathTracer leg passes (0: skip)")
     ap.add_argument("--closest-shadow-passes", type=int, default=4,
                     help="passes of the leg with the reference's closest-hit Occluded shadow rays (0: skip)")
+    ap.add_argument("--prim-passes", type=int, default=16, help="C1 PrimTracer leg passes (0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--schedule", default="persistent", choices=["persistent", "megakernel", "wavefront"])
@@ -299,6 +300,32 @@ def wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_index, passes):
             "mrays_s": round(sum(rays) / (sum(ms) * 1e-3) / 1e6, 2)}
 
 
+def c1_prim_leg(ctl, dev, torch, passes):
+    """BASELINE configs[0]: PrimTracer (first_f) on the Cornell box at 256x256, 1 spp
+    per pass, through ctl_prim_pass on its own context (Integrators/PrimTracer.cu:181-232).
+    Per-pass device time from ctl_last_pass_ms; the first two passes are warmup."""
+    hs = ctl.HostScene().generate(1, 1.0, 256, 256)
+    d = hs.compile()
+    pt = ctl.PrimTracer(dev.index or 0)
+    try:
+        pt.upload_scene(d)
+        fb = torch.zeros((256 * 256, 7), dtype=torch.float32, device=dev)
+        ms, rays = [], []
+        for k in range(passes + 2):
+            pt.reset_rays()
+            pt.do_pass(fb.data_ptr(), k)
+            pt.sync()
+            if k >= 2:
+                ms.append(pt.last_pass_ms())
+                rays.append(pt.rays_traced())
+    finally:
+        pt.close()
+    return {"integrator": "PrimTracer first_f (C1 Cornell box, 256x256, 1 spp)", "passes": passes,
+            "ms_per_pass": round(sum(ms) / len(ms), 4), "rays_per_pass": int(sum(rays) / len(rays)),
+            "mrays_s": round(sum(rays) / (sum(ms) * 1e-3) / 1e6, 2),
+            "note": "plumbing config: 65 k rays per pass, launch-latency bound"}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -429,6 +456,12 @@ def main():
     prim = primary_ray_leg(pt, dev, stream, sptr, torch, nxt, prof) if rank == 0 else None
     wpt = (wpt_leg(ctl, pt, dev, sptr, torch, W, H, nxt + 1, a.wpt_passes)
            if rank == 0 and a.wpt_passes > 0 else None)
+    c1 = None
+    if rank == 0 and a.prim_passes > 0:
+        try:   # a side leg: its failure is reported in the line, not fatal to the headline
+            c1 = c1_prim_leg(ctl, dev, torch, a.prim_passes)
+        except Exception as e:
+            c1 = {"error": f"{type(e).__name__}: {e}"}
     single = None
     if rank == 0 and shards == 1 and G > 1 and a.one_pass_leg > 0:
         single = single_pass_leg(pt, fb, stream, sptr, torch, nxt + 40, a.one_pass_leg)
@@ -499,6 +532,7 @@ def main():
             "one_pass_launches": single,
             "closest_hit_shadows": closest,
             "wavefront_tracer": wpt,
+            "prim_tracer_c1": c1,
             "image_weight_sum": wsum,
             "scene_build_s": round(t_build, 2),
         }
