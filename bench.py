@@ -15,13 +15,17 @@ After the last step the PixelData framebuffers are summed to rank 0 with one
 RCCL reduce over xGMI (inside the timed region).  Rays counted exactly as the
 reference's k_getNumRaysTraced (every traceRay incl. NEE shadow rays).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
-torch.distributed.run (one process per GPU, RCCL backend).
+Launch: python bench.py [--gpus N --steps K --warmup W].  For N>1 under
+torch.distributed.run (one process per GPU, RCCL backend); started as a plain
+`python bench.py --gpus N` the process starts that launcher as a child (before
+any GPU call, never an exec of itself) and exits with its status.
 """
 import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,7 +44,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64)
@@ -77,7 +81,48 @@ def parse():
                     help="passes of the one-launch-per-pass comparison leg (0: skip)")
     ap.add_argument("--bvh", default="wide", choices=["wide", "wideq", "binary"],
                     help="device traversal: 4-wide collapsed BVH, or the reference's binary order")
-    return ap.parse_args()
+    ap.add_argument("--dopass-leg", type=int, default=8,
+                    help="passes of the reference DoPass leg (ctl_scene_update + sampler tables + one "
+                         "ctl_render_pass per pass; 0: skip)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher rehearsal: the ranks join the process group and count themselves; no GPU, "
+                         "no scene (tests/test_bench_launch.py)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, gpus, port):
+    """The child command that runs this script once per GPU: torch.distributed.run
+    with one process per GPU over 127.0.0.1 (the contract's multi-GPU launch)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_plan(a, env):
+    """What a process started as `bench.py --gpus N` does: "run" (it is a rank, or
+    N = 1), "spawn" (no launcher around it and N > 1: start one), or an error
+    message (a launcher with a different world size)."""
+    world = env.get("WORLD_SIZE")
+    if world is None:
+        return "spawn" if a.gpus > 1 else "run"
+    if int(world) != a.gpus:
+        return f"--gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks"
+    return "run"
+
+
+def launch_groups(steps, per_launch):
+    """Split `steps` into ceil(steps / per_launch) launches of near-equal size
+    (sizes differ by at most one), e.g. 20 at 8 -> 7, 7, 6."""
+    if steps <= 0:
+        return []
+    n = -(-steps // max(1, per_launch))
+    base, extra = divmod(steps, n)
+    return [base + (1 if i < extra else 0) for i in range(n)]
 
 
 def cpu_model():
@@ -115,24 +160,36 @@ def pmc_profile():
     return j, os.path.relpath(files[-1], here), match
 
 
-def roofline(prof, fam, ms, alg_bytes, kernel):
+def roofline(prof, fam, ms, alg_bytes, kernel, units=None):
     """Roofline of one kernel: physical HBM bytes (PMC counters of the same
     binary) over its live per-launch time against the HBM peak, plus the L2 and
     vector-memory-address-unit fractions that actually bind it.  The
     algorithmic-byte model of SURVEY 8(d) is reported beside it as a model: the
     4-wide tree and the caches serve those bytes, so it is not a fraction of
-    any hardware limit."""
+    any hardware limit.
+
+    units: the work units (render passes) of one timed launch.  A profile that
+    records its counters per unit ("per_unit", tools_pmc_summary.py) is scaled
+    to this launch shape, so any --steps / launch grouping gets its bytes;
+    otherwise the profile's per-launch counters apply as they are."""
     j, path, match = prof
     k = (j or {}).get("kernels", {}).get(fam, {})
+    scale = 1.0
+    if units is not None and k.get("units_per_launch"):
+        scale = units / k["units_per_launch"]
     hbm = k.get("hbm_bytes")
+    hbm = hbm * scale if hbm else hbm
     r = {"bound": "hbm", "achieved": None, "peak": PEAK_HBM, "unit": "GB/s", "frac": None, "traffic": hbm,
          "kernel": kernel, "per_launch_ms": round(ms, 4)}
+    if units is not None and k.get("units_per_launch"):
+        r["traffic_per_unit"] = k["hbm_bytes"] / k["units_per_launch"] if k.get("hbm_bytes") else None
+        r["profile_units_per_launch"] = k["units_per_launch"]
     if hbm:
         ach = hbm / (ms * 1e-3) / 1e9
         r["achieved"] = round(ach, 2)
         r["frac"] = r["frac_hbm"] = round(ach / PEAK_HBM, 4)
     if k.get("l2_read_bytes"):
-        r["frac_l2"] = round(k["l2_read_bytes"] / (ms * 1e-3) / 1e9 / PEAK_L2, 4)
+        r["frac_l2"] = round(k["l2_read_bytes"] * scale / (ms * 1e-3) / 1e9 / PEAK_L2, 4)
     if k.get("ta_busy") is not None:
         r["frac_ta"] = round(k["ta_busy"], 4)
         # TA_TA_BUSY counts cycles with requests in flight: on the traversal it reads
@@ -144,7 +201,7 @@ def roofline(prof, fam, ms, alg_bytes, kernel):
         if key in k:
             r[key] = round(k[key], 4)
     if k.get("counters_per_launch", {}).get("SQ_INSTS_VMEM_RD") is not None:
-        r["vmem_rd_wave_insts_per_launch"] = k["counters_per_launch"]["SQ_INSTS_VMEM_RD"]
+        r["vmem_rd_wave_insts_per_launch"] = round(k["counters_per_launch"]["SQ_INSTS_VMEM_RD"] * scale, 1)
     r["profile"] = path
     r["profile_matches_binary"] = match
     r["alg_model"] = {"bytes_per_launch": int(alg_bytes), "gbs": round(alg_bytes / (ms * 1e-3) / 1e9, 2),
@@ -152,6 +209,31 @@ def roofline(prof, fam, ms, alg_bytes, kernel):
                               "instance entry of the reference's binary traversal of the same rays; L2-served, "
                               "not a bound"}
     return r
+
+
+def cpu_cores():
+    """Host CPUs of this process: its affinity set, a cgroup CPU quota when there
+    is one, and the job's stated CPU share (OMP_NUM_THREADS: a GPU box shares its
+    256-thread host between 16 GPUs' jobs and sets it to 16).  The baseline runs
+    on min(affinity, quota, share) threads and reports all of them."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    share = None
+    try:
+        share = int(os.environ["OMP_NUM_THREADS"])
+    except (KeyError, ValueError):
+        pass
+    use = min(x for x in (aff, quota, share) if x)
+    return {"threads": max(1, use), "affinity_cpus": aff, "cgroup_cpu_quota": quota, "job_cpu_share": share}
 
 
 def cpu_baseline(desc, params, seconds, threads):
@@ -180,6 +262,7 @@ def cpu_baseline(desc, params, seconds, threads):
         "kind": "port",
         "sample": f"oracle PathTrace<true> on the same triangles, every 4th pixel of {passes} pass(es), "
                   f"{rays} rays in {el:.1f} s",
+        "per_thread_mrays_s": round(rays / el / 1e6 / threads, 4),
         "cpu_model": cpu_model(),
         "nproc": os.cpu_count(),
         "ref_nodes_per_ray": round(float(stats[1]) / max(1, float(stats[0])), 3),
@@ -326,17 +409,51 @@ def c1_prim_leg(ctl, dev, torch, passes):
             "note": "plumbing config: 65 k rays per pass, launch-latency bound"}
 
 
-def main():
-    a = parse()
+def launch_check(a, world, rank):
+    """--launch-check: every rank joins the process group (gloo) and the ranks
+    count themselves; rank 0 prints the line shape the bench prints, with
+    n_gpus = the ranks that reported."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.ones(1, dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": "launch-check", "n_gpus": int(t.item()), "world_size": world,
+                          "gpus_requested": a.gpus}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    plan = launch_plan(a, os.environ)
+    if plan == "spawn":
+        # No launcher around this process: start one rank per GPU as a child
+        # (nothing here has touched the GPU) and report its status.
+        cmd = launcher_cmd(argv, a.gpus, _free_port())
+        log("bench: --gpus %d without a launcher; starting %s" % (a.gpus, " ".join(cmd)))
+        return subprocess.call(cmd)
+    if plan != "run":
+        log("bench: " + plan)
+        return 2
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        log(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if a.launch_check:
+        launch_check(a, world, rank)
+        return 0
     # image-tile shards: one per rank, or N emulated ranks in this one process
     shards = a.emulate_ranks if (world == 1 and a.emulate_ranks > 1) else world
     import torch
     import torch.distributed as dist
+    if world > 1 and a.backend == "nccl" and torch.cuda.device_count() < world:
+        log(f"bench: {world} RCCL ranks but {torch.cuda.device_count()} visible GPUs")
+        return 2
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import cudatracerlib_amd as ctl
     from cudatracerlib_amd import shard
@@ -421,8 +538,11 @@ def main():
             e1.record(stream)
             kev.append((e0, e1))
 
-    for s in range(0, a.warmup, G):
-        step(s, nsteps=min(G, a.warmup - s))
+    # launches of near-equal size (--steps 20 at 8 per launch: 7 + 7 + 6 steps)
+    s = 0
+    for g in launch_groups(a.warmup, G):
+        step(s, nsteps=g)
+        s += g
     steps_done = a.warmup
     torch.cuda.synchronize(dev)
     fb.zero_()
@@ -436,8 +556,10 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for s in range(0, a.steps, G):
-        step(s, timed=True, nsteps=min(G, a.steps - s))
+    s = 0
+    for g in launch_groups(a.steps, G):
+        step(s, timed=True, nsteps=g)
+        s += g
     ev1.record(stream)
     if world > 1:
         shard.reduce_framebuffer(fb, dist)   # RCCL over xGMI
@@ -472,12 +594,15 @@ def main():
         del scratch
     red = dev if a.backend == "nccl" else torch.device("cpu")
     tt = torch.tensor([elapsed], dtype=torch.float64, device=red)
-    rr = torch.tensor([rays], dtype=torch.int64, device=red)
+    rr = torch.tensor([rays, 1], dtype=torch.int64, device=red)   # rays, ranks that rendered
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dist.all_reduce(rr, op=dist.ReduceOp.SUM)
     elapsed = float(tt.item())
-    total_rays = int(rr.item())
+    total_rays = int(rr[0].item())
+    ranks_rendered = int(rr[1].item())
+    if ranks_rendered != world:
+        raise RuntimeError(f"{ranks_rendered} of {world} ranks rendered")
 
     if rank == 0:
         passes = a.steps * shards
@@ -487,11 +612,16 @@ def main():
         per_launch_ms = kernel_ms / launches
         passes_per_launch = passes / launches   # this rank's passes (tiles of them when sharded) per launch
         fam = "path_kernel_full" if a.config == 5 else "path_kernel"
-        same_workload = (prof[0] or {}).get("config") == [a.config, a.scale, W, H, passes_per_launch]
+        # the profile's counters are per pass (units_per_launch), so they scale to this
+        # run's launch shape; only the workload (scene, resolution, schedule, shards) must match
+        pj = prof[0] or {}
+        same_workload = ("passes_per_launch" in pj and list(pj.get("config", []))[:4] == [a.config, a.scale, W, H]
+                         and pj.get("shards", 1) == shards and a.schedule == "persistent" and a.bvh == "wide")
         rl = roofline(prof if same_workload else (None, None, False), fam, per_launch_ms,
-                      alg_bytes_per_pass * passes_per_launch, KERNEL_NAME[a.schedule])
+                      alg_bytes_per_pass * passes_per_launch, KERNEL_NAME[a.schedule], units=passes_per_launch)
         rl.update({"launches_timed": launches, "gpu_step_ms": round(step_ms / a.steps, 3),
-                   "passes_per_launch": passes_per_launch,
+                   "passes_per_launch": round(passes_per_launch, 4),
+                   "steps_per_launch": launch_groups(a.steps, G),
                    "visits_per_launch": {"inner_nodes": int(st[1]), "tri_tests": int(st[2]),
                                          "instances": int(st[3]), "rays": int(st[0])}})
         if passes_per_launch > 1:
@@ -501,7 +631,7 @@ def main():
             "metric": "Mrays/s (primary+secondary) at 1920x1080, San-Miguel-scale BVH",
             "value": round(total_rays / elapsed / 1e6, 3),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": ranks_rendered,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
@@ -537,20 +667,25 @@ def main():
             "scene_build_s": round(t_build, 2),
         }
         if world == 1 and not a.no_cpu_baseline:
-            cores = min(16, os.cpu_count() or 1, threads if threads > 1 else 16)
+            cc = cpu_cores()
             # the reference's CPU path runs on its own tree: SBVH with leaves <= 8
             # (SplitBVHBuilder Platform, BVHBuilderHelper.cpp:119), the same triangles
             ref_hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
             ref_hs.set_bvh_builder("sbvh", 1.0e-5).set_bvh_params(0.0, 8, 0, 8)
             ref_desc = ref_hs.compile(threads=threads)
-            out["cpu_baseline"] = cpu_baseline(ref_desc, pt.params, a.cpu_seconds, cores)
+            out["cpu_baseline"] = cpu_baseline(ref_desc, pt.params, a.cpu_seconds, cc["threads"])
+            out["cpu_baseline"].update({k: v for k, v in cc.items() if k != "threads"})
             out["cpu_baseline"]["bvh"] = "SBVH, leaves <= 8 (the reference's SplitBVHBuilder configuration)"
+            out["cpu_baseline"]["note"] = (
+                "threads = min(affinity set, cgroup quota, the job's CPU share OMP_NUM_THREADS); the oracle's "
+                "rays are independent, so the rate scales about linearly with threads (per_thread_mrays_s)")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     pt.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1,0 +1,53 @@
+"""bench.py's launch contract on CPU (no GPU): `python bench.py --gpus N` without
+a launcher starts N ranks itself (a torch.distributed.run child, never an exec
+of itself), and the line's n_gpus is the number of ranks that reported; a
+launcher with another world size is refused.  The ranks here run the
+--launch-check rehearsal (gloo process group, ranks count themselves)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_n_without_launcher_spawns_n_ranks(n):
+    r = _run(["--gpus", str(n), "--launch-check", "--backend", "gloo"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout   # one line, from rank 0
+    assert lines[0]["n_gpus"] == n and lines[0]["world_size"] == n
+
+
+def test_single_gpu_runs_in_process():
+    r = _run(["--gpus", "1", "--launch-check"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+
+
+def test_mismatched_launcher_world_size_fails():
+    r = _run(["--gpus", "4", "--launch-check"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_launch_groups_near_equal():
+    assert bench.launch_groups(20, 8) == [7, 7, 6]
+    assert bench.launch_groups(64, 8) == [8] * 8
+    assert bench.launch_groups(5, 8) == [5]
+    for steps in range(1, 70):
+        g = bench.launch_groups(steps, 8)
+        assert sum(g) == steps and max(g) - min(g) <= 1 and max(g) <= 8

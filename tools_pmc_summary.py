@@ -11,6 +11,11 @@ profiles/rNN_pmc.json) for the roofline fractions of the same binary:
                  fraction of the kernel's cycles the vector-memory address
                  unit of a CU is busy
   cycles         GRBM_GUI_ACTIVE / 8 per launch (kernel cycles of one XCD)
+
+The path-kernel families also carry units_per_launch (render passes per
+profiled launch; tools_pmc.sh profiles one 8-pass ctl_render_passes launch), so
+bench.py scales the counters to whatever launch shape it times.
+Usage: tools_pmc_summary.py <dir> [passes per profiled path-kernel launch]
 """
 import collections
 import csv
@@ -22,6 +27,7 @@ import subprocess
 import sys
 
 root = sys.argv[1]
+PASSES = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 FAMILIES = {
     "path_kernel": "path_kernel_persistent<false, true, true, 0>",
     "path_kernel_full": "path_kernel_persistent<false, true, true, 1>",
@@ -47,7 +53,8 @@ sys.path.insert(0, here)
 from buildid import source_fingerprint  # noqa: E402
 libp = os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_trace.so")
 out = {"method": __doc__.strip(), "lib_sha256": hashlib.sha256(open(libp, "rb").read()).hexdigest(),
-       "src_sha256": source_fingerprint(here), "config": [3, 1.0, 1920, 1080, 8], "kernels": {}}
+       "src_sha256": source_fingerprint(here), "config": [3, 1.0, 1920, 1080], "shards": 1,
+       "passes_per_launch": PASSES, "kernels": {}}
 try:
     out["git_head"] = subprocess.check_output(["git", "rev-parse", "--short", "HEAD"], cwd=here,
                                               stderr=subprocess.DEVNULL).decode().strip()
@@ -57,6 +64,8 @@ for fam, a in sorted(agg.items()):
     n = {c: max(1, len(d)) for c, d in disp[fam].items()}
     per = {c: v / n[c] for c, v in a.items()}
     k = {"launches": max(n.values()), "counters_per_launch": {c: round(v, 1) for c, v in sorted(per.items())}}
+    if fam.startswith("path_kernel"):
+        k["units_per_launch"] = PASSES
     if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
         k["hbm_bytes"] = (2.0 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0
     if "TCP_TCC_READ_REQ_sum" in per:
