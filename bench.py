@@ -547,6 +547,7 @@ def main(argv=None):
     torch.cuda.synchronize(dev)
     fb.zero_()
     pass_base = steps_done * shards   # fresh passes for the timed image
+    image = torch.empty_like(fb) if world > 1 else fb   # the reduced image (rank 0)
     pt.reset_rays(sptr)
     if world > 1:
         dist.barrier()
@@ -562,7 +563,7 @@ def main(argv=None):
         s += g
     ev1.record(stream)
     if world > 1:
-        shard.reduce_framebuffer(fb, dist)   # RCCL over xGMI
+        shard.reduce_framebuffer(fb, dist, out=image)   # RCCL over xGMI, into rank 0's image
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -606,7 +607,7 @@ def main(argv=None):
 
     if rank == 0:
         passes = a.steps * shards
-        img = fb.view(H, W, 7)
+        img = image.view(H, W, 7)
         wsum = float(img[..., 6].sum().item())
         launches = len(kev)   # path-kernel launches on this rank in the timed region
         per_launch_ms = kernel_ms / launches

@@ -349,10 +349,11 @@ class Tracer:
         """Worst-case traversal stack (entries per lane) of the uploaded scene."""
         return int(self._L.ctl_scene_stack_bound(self._ctx))
 
-    def fb_reduce(self, comm, fb_ptr, n_pixels, root=0, stream=0):
-        """Sum every rank's PixelData framebuffer into root's (ctl_fb_reduce over an
-        RCCL communicator from comm_init_all / comm_init_rank or the caller's)."""
-        _check(self._L.ctl_fb_reduce(self._ctx, comm, fb_ptr, int(n_pixels), int(root), stream), self._ctx,
+    def fb_reduce(self, comm, fb_ptr, out_ptr, n_pixels, root=0, stream=0):
+        """Sum every rank's PixelData framebuffer fb into out on the root (ctl_fb_reduce
+        over an RCCL communicator from comm_init_all / comm_init_rank or the caller's);
+        fb is only read, so it may be called after any step."""
+        _check(self._L.ctl_fb_reduce(self._ctx, comm, fb_ptr, out_ptr, int(n_pixels), int(root), stream), self._ctx,
                "ctl_fb_reduce")
 
 

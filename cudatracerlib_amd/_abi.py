@@ -213,8 +213,8 @@ SYMBOLS = [
     ("ctl_comm_init_rank", C.c_int32, [C.POINTER(_vp), C.c_int32, _vp, C.c_int32, C.c_int32]),
     ("ctl_comm_init_all", C.c_int32, [C.POINTER(_vp), C.c_int32, _vp]),
     ("ctl_comm_destroy", C.c_int32, [_vp]),
-    ("ctl_fb_reduce", C.c_int32, [_vp, _vp, _vp, C.c_uint64, C.c_int32, _vp]),
-    ("ctl_fb_reduce_all", C.c_int32, [_vp, _vp, _vp, C.c_int32, C.c_uint64, C.c_int32, _vp]),
+    ("ctl_fb_reduce", C.c_int32, [_vp, _vp, _vp, _vp, C.c_uint64, C.c_int32, _vp]),
+    ("ctl_fb_reduce_all", C.c_int32, [_vp, _vp, _vp, _vp, C.c_int32, C.c_uint64, C.c_int32, _vp]),
     ("ctl_image_resolve", C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, C.c_float, _vp, _vp]),
     ("ctl_variance_add_pass", C.c_int32, [_vp, _vp, C.c_uint32, C.c_uint32, C.c_float, C.c_uint32, _vp, _vp, _vp]),
     ("ctl_variance_stats", C.c_int32, [_vp, _vp, C.c_uint64, _vp, _vp, _vp, _vp]),

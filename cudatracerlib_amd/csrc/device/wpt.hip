@@ -52,9 +52,16 @@ struct WptBuffers {
     // b, written by bounce b-1's scan; kernels read them on the device, the host
     // reads them back a few bounces late only to stop issuing bounces
     uint32_t* counts = nullptr;
-    uint32_t* h_counts = nullptr;  // pinned host copy
     uint32_t count_slots = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // h_counts is double-buffered over passes: done[b] is recorded after the last
+    // count copy of the pass that used buffer b, and the pass two later waits on it
+    // before it writes that buffer, so a late copy of a pass issued on another
+    // stream cannot overwrite the counts a later pass reads
+    uint32_t* h_cnt[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    bool done_pending[2] = {false, false};
+    int cur_buf = 0;
     std::vector<void*> allocs;
 };
 constexpr int kWptLag = 2;   // bounces the host check trails the device by
@@ -414,7 +421,10 @@ void wpt_free(ctl_ctx* c) {
     WptBuffers* B = c->wpt;
     if (!B) return;
     for (void* p : B->allocs) (void)hipFree(p);
-    if (B->h_counts) (void)hipHostFree(B->h_counts);
+    for (int b = 0; b < 2; b++) {
+        if (B->h_cnt[b]) (void)hipHostFree(B->h_cnt[b]);
+        if (B->done[b]) (void)hipEventDestroy(B->done[b]);
+    }
     for (hipEvent_t e : B->ev)
         if (e) (void)hipEventDestroy(e);
     delete B;
@@ -443,6 +453,7 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
                   wpt_alloc(B, &B->sec, n) && wpt_alloc(B, &B->sec_hits, n) && wpt_alloc(B, &B->flags, n) &&
                   wpt_alloc(B, &B->blocks, nb_max);
         for (hipEvent_t& e : B->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+        for (hipEvent_t& e : B->done) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
         if (!ok) { wpt_free(c); c->err = "wpt: buffer allocation failed"; return CTL_ERR_NOMEM; }
         B->capacity = items;
     }
@@ -473,17 +484,30 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
     // count slots for every bounce of the pass (+1 for the last scan's output)
     const uint32_t slots = (uint32_t)prm->max_path_length + 1u;
     if (B->count_slots < slots) {
+        WPT_HIP(hipDeviceSynchronize());   // no count copy of an earlier pass in flight
         uint32_t* dc = nullptr;
         if (!wpt_alloc(B, &dc, 2 * (size_t)slots)) { c->err = "wpt: count allocation failed"; return CTL_ERR_NOMEM; }
-        if (B->h_counts) (void)hipHostFree(B->h_counts);
-        B->h_counts = nullptr;
-        if (hipHostMalloc((void**)&B->h_counts, 2 * (size_t)slots * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
-            c->err = "wpt: count allocation failed";
-            return CTL_ERR_NOMEM;
+        for (int b = 0; b < 2; b++) {
+            if (B->h_cnt[b]) (void)hipHostFree(B->h_cnt[b]);
+            B->h_cnt[b] = nullptr;
+            B->done_pending[b] = false;
+            if (hipHostMalloc((void**)&B->h_cnt[b], 2 * (size_t)slots * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+                c->err = "wpt: count allocation failed";
+                return CTL_ERR_NOMEM;
+            }
         }
         B->counts = dc;
         B->count_slots = slots;
     }
+    // this pass's host count buffer: the pass that used it last (two passes ago)
+    // may still have copies in flight on its stream
+    const int hb = B->cur_buf;
+    B->cur_buf = 1 - hb;
+    if (B->done_pending[hb]) {
+        WPT_HIP(hipEventSynchronize(B->done[hb]));
+        B->done_pending[hb] = false;
+    }
+    uint32_t* const h_counts = B->h_cnt[hb];
     const uint32_t n0 = (uint32_t)items;
     int cur = 0;
     hipLaunchKernelGGL(wpt_create_kernel, dim3(nb_max), dim3(kBlock), 0, s, c->scene, A, s1, s2, n0, B->rays[0],
@@ -497,11 +521,11 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
     // Queues only shrink (a bounce's continuations and shadow rays are at most its
     // payload), so the last count the host has read back bounds the grids.
     uint32_t ub = n0;
-    B->h_counts[0] = n0;   // slot 0 is written by wpt_create_kernel; its host copy is known
-    B->h_counts[1] = 0u;
+    h_counts[0] = n0;   // slot 0 is written by wpt_create_kernel; its host copy is known
+    h_counts[1] = 0u;
     for (int depth = 0;; depth++) {
         const uint32_t* cnt = B->counts + 2 * depth;
-        if (depth >= kWptLag) ub = std::min(ub, B->h_counts[2 * (depth - kWptLag)]);
+        if (depth >= kWptLag) ub = std::min(ub, h_counts[2 * (depth - kWptLag)]);
         const uint32_t nb = (ub + kBlock - 1) / kBlock;
         // FinishIteration: payload rays, then the secondary buffer (closest
         // hit), as one launch over both batches (one resident grid, one tail);
@@ -521,7 +545,7 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
         hipLaunchKernelGGL(wpt_scatter_kernel, dim3(nb), dim3(kBlock), 0, s, cnt, B->flags, B->blocks, B->pay[cur],
                            B->rays[cur], B->sec_tmp, B->pay[1 - cur], B->rays[1 - cur], B->sec);
         WPT_HIP(hipGetLastError());
-        WPT_HIP(hipMemcpyAsync(B->h_counts + 2 * (depth + 1), B->counts + 2 * (depth + 1), 2 * sizeof(uint32_t),
+        WPT_HIP(hipMemcpyAsync(h_counts + 2 * (depth + 1), B->counts + 2 * (depth + 1), 2 * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, s));
         WPT_HIP(hipEventRecord(B->ev[depth % 4], s));
         cur = 1 - cur;
@@ -530,13 +554,15 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
         if (depth >= kWptLag) {
             const int d = depth - kWptLag;
             WPT_HIP(hipEventSynchronize(B->ev[d % 4]));
-            if (B->h_counts[2 * (d + 1)] == 0) break;   // bounce d left no paths: the later ones are empty
+            if (h_counts[2 * (d + 1)] == 0) break;   // bounce d left no paths: the later ones are empty
         }
     }
     if (A.samples) {
         hipLaunchKernelGGL(wpt_fold_kernel, dim3(nb_max), dim3(kBlock), 0, s, A, (const float4*)A.samples, fb);
         WPT_HIP(hipGetLastError());
     }
+    WPT_HIP(hipEventRecord(B->done[hb], s));
+    B->done_pending[hb] = true;
     return CTL_OK;
 }
 

@@ -5,11 +5,13 @@
 //   compile, a framebuffer; every step renders N progressive passes of the
 //   rank's tiles (ctl_render_passes, num_ranks = N, rank = i; weak scaling:
 //   per-GPU work is fixed); after the last step one grouped RCCL reduce
-//   (ctl_fb_reduce_all) sums the rank framebuffers into GPU 0's.  The result
-//   is the 1-GPU framebuffer of the same passes bit for bit.
+//   (ctl_fb_reduce_all) sums the rank framebuffers into an image buffer on
+//   GPU 0.  The result is the 1-GPU framebuffer of the same passes bit for bit.
+//   --reduce-every 1 reduces after every step instead (a progressive preview;
+//   the rank framebuffers are only read, so the last reduce is the same image).
 //
 // usage: mgpu_render [--config C] [--scale S] [--width W] [--height H]
-//                    [--steps K] [--devices N] [--out file]
+//                    [--steps K] [--devices N] [--reduce-every R] [--out file]
 // Prints one line: devices, passes, rays, seconds, Mrays/s.  --out writes
 // GPU 0's reduced PixelData framebuffer (W*H*7 floats).
 #include <hip/hip_runtime.h>
@@ -41,7 +43,7 @@
     } while (0)
 
 int main(int argc, char** argv) {
-    int config = 2, steps = 2, ndev = 0;
+    int config = 2, steps = 2, ndev = 0, reduce_every = 0;
     double scale = 0.25;
     uint32_t width = 320, height = 180;
     std::string out;
@@ -53,6 +55,7 @@ int main(int argc, char** argv) {
         else if (a == "--height") height = (uint32_t)std::atoi(argv[i + 1]);
         else if (a == "--steps") steps = std::atoi(argv[i + 1]);
         else if (a == "--devices") ndev = std::atoi(argv[i + 1]);
+        else if (a == "--reduce-every") reduce_every = std::atoi(argv[i + 1]);
         else if (a == "--out") out = argv[i + 1];
         else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
     }
@@ -83,10 +86,15 @@ int main(int argc, char** argv) {
         CHECK_HIP(hipMemsetAsync(fb[(size_t)i], 0, npx * sizeof(ctl_pixel), stream[(size_t)i]));
         CHECK_CTL(ctx[(size_t)i], ctl_reset_rays(ctx[(size_t)i], stream[(size_t)i]));
     }
+    ctl_pixel* image = nullptr;   // the reduced image, on GPU 0
+    CHECK_HIP(hipSetDevice(0));
+    CHECK_HIP(hipMalloc(&image, npx * sizeof(ctl_pixel)));
     std::vector<void*> comm((size_t)ndev, nullptr);
     if (ctl_comm_init_all(comm.data(), ndev, nullptr) != CTL_OK) { std::fprintf(stderr, "ctl_comm_init_all failed\n"); return 1; }
     for (int i = 0; i < ndev; i++) CHECK_CTL(ctx[(size_t)i], ctl_sync(ctx[(size_t)i], stream[(size_t)i]));
 
+    std::vector<void*> sv(stream.begin(), stream.end());
+    std::vector<const ctl_pixel*> cfb(fb.begin(), fb.end());
     const auto t0 = std::chrono::steady_clock::now();
     for (int s = 0; s < steps; s++) {
         for (int i = 0; i < ndev; i++) {   // asynchronous: all GPUs render at once
@@ -97,11 +105,12 @@ int main(int argc, char** argv) {
             CHECK_CTL(ctx[(size_t)i], ctl_render_passes(ctx[(size_t)i], &p, (uint64_t)s * ndev, (uint32_t)ndev,
                                                         fb[(size_t)i], stream[(size_t)i]));
         }
-    }
-    std::vector<void*> sv(stream.begin(), stream.end());
-    if (ctl_fb_reduce_all(ctx.data(), comm.data(), fb.data(), ndev, npx, 0, sv.data()) != CTL_OK) {
-        std::fprintf(stderr, "ctl_fb_reduce_all: %s\n", ctl_last_error(ctx[0]));
-        return 1;
+        if ((reduce_every > 0 && (s + 1) % reduce_every == 0) || s + 1 == steps) {
+            if (ctl_fb_reduce_all(ctx.data(), comm.data(), cfb.data(), image, ndev, npx, 0, sv.data()) != CTL_OK) {
+                std::fprintf(stderr, "ctl_fb_reduce_all: %s\n", ctl_last_error(ctx[0]));
+                return 1;
+            }
+        }
     }
     uint64_t rays = 0;
     for (int i = 0; i < ndev; i++) {
@@ -114,7 +123,7 @@ int main(int argc, char** argv) {
     if (!out.empty()) {
         std::vector<ctl_pixel> h(npx);
         CHECK_HIP(hipSetDevice(0));
-        CHECK_HIP(hipMemcpy(h.data(), fb[0], npx * sizeof(ctl_pixel), hipMemcpyDeviceToHost));
+        CHECK_HIP(hipMemcpy(h.data(), image, npx * sizeof(ctl_pixel), hipMemcpyDeviceToHost));
         FILE* f = std::fopen(out.c_str(), "wb");
         if (!f || std::fwrite(h.data(), sizeof(ctl_pixel), npx, f) != npx) { std::fprintf(stderr, "write %s failed\n", out.c_str()); return 1; }
         std::fclose(f);
@@ -126,6 +135,8 @@ int main(int argc, char** argv) {
         (void)hipStreamDestroy(stream[(size_t)i]);
         ctl_destroy(ctx[(size_t)i]);
     }
+    (void)hipSetDevice(0);
+    (void)hipFree(image);
     ctl_host_scene_destroy(hs);
     return 0;
 }

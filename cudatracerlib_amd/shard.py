@@ -30,16 +30,25 @@ def owned_tiles(width, height, tile, world, rank):
     return [t for t in range(tiles) if t % world == rank]
 
 
-def reduce_framebuffer(fb, dist, dst=0):
-    """Sum the per-rank PixelData framebuffers to `dst` (RCCL over xGMI on GPUs,
-    gloo on CPU).  Every pixel is nonzero on its owner rank only, so the fp32
-    sum is exact: x + 0 = x."""
+def reduce_framebuffer(fb, dist, dst=0, out=None):
+    """Sum the per-rank PixelData framebuffers into a separate image on `dst`
+    (RCCL over xGMI on GPUs, gloo on CPU) and return it (on `dst`; other ranks
+    get their send copy back).  Every pixel is nonzero on its owner rank only,
+    so the fp32 sum is exact: x + 0 = x.  `fb` itself is never written: each rank
+    keeps accumulating its own pixels, so this may run after any step (a
+    reduce in place would fold the other ranks' totals into dst's accumulator
+    and count them again at the next reduce)."""
     if fb.is_cuda and dist.get_backend() == "gloo":
         # gloo reduces host tensors only (CPU rehearsals of the N-rank path)
         host = fb.cpu()
         dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM)
-        if dist.get_rank() == dst:
-            fb.copy_(host)
-        return fb
-    dist.reduce(fb, dst=dst, op=dist.ReduceOp.SUM)
-    return fb
+        if out is None:
+            return host.to(fb.device)
+        out.copy_(host)
+        return out
+    if out is None:
+        out = fb.clone()
+    else:
+        out.copy_(fb)
+    dist.reduce(out, dst=dst, op=dist.ReduceOp.SUM)
+    return out

@@ -425,15 +425,20 @@ CTL_API ctl_status ctl_comm_init_rank(void** comm_out, int32_t nranks, const voi
 /* ncclCommInitAll: one process driving ndev GPUs; comms_out[i] is rank i on devices[i]. */
 CTL_API ctl_status ctl_comm_init_all(void** comms_out, int32_t ndev, const int32_t* devices);
 CTL_API ctl_status ctl_comm_destroy(void* comm);
-/* Sum the n_pixels PixelData records of every rank's d_fb into root's d_fb
- * (ncclReduce, fp32 sum, in place).  Every rank calls it with its own ctx and
- * stream; asynchronous on `stream`. */
-CTL_API ctl_status ctl_fb_reduce(ctl_ctx* ctx, void* comm, ctl_pixel* d_fb, uint64_t n_pixels, int32_t root,
-                                 void* stream);
+/* Sum the n_pixels PixelData records of every rank's d_fb into d_out on the
+ * root (ncclReduce, fp32 sum).  d_fb is only read: each rank keeps
+ * accumulating its own pixels into it, so the reduce may run after any step and
+ * any number of times (d_out then holds the image of all passes so far; it must
+ * not alias d_fb, and is ignored on the other ranks).  Every rank calls it with
+ * its own ctx and stream; asynchronous on `stream`.  RCCL is loaded on first
+ * use (CTL_ERR_NODEVICE when it cannot be). */
+CTL_API ctl_status ctl_fb_reduce(ctl_ctx* ctx, void* comm, const ctl_pixel* d_fb, ctl_pixel* d_out,
+                                 uint64_t n_pixels, int32_t root, void* stream);
 /* The same for n contexts of one process (one per GPU, communicators from
- * ctl_comm_init_all), as one grouped RCCL call. */
-CTL_API ctl_status ctl_fb_reduce_all(ctl_ctx* const* ctxs, void* const* comms, ctl_pixel* const* d_fbs, int32_t n,
-                                     uint64_t n_pixels, int32_t root, void* const* streams);
+ * ctl_comm_init_all), as one grouped RCCL call; d_out lives on ctxs[root]'s GPU. */
+CTL_API ctl_status ctl_fb_reduce_all(ctl_ctx* const* ctxs, void* const* comms, const ctl_pixel* const* d_fbs,
+                                     ctl_pixel* d_out, int32_t n, uint64_t n_pixels, int32_t root,
+                                     void* const* streams);
 
 /* ---- animated meshes: skinning + BVH refit ------------ */
 

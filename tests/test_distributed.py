@@ -26,10 +26,10 @@ def _free_port():
 W, H, STEPS, BASE = 1920, 64, 2, 34   # passes 34..37: two cross-rank samples (asserted below)
 
 
-def _render(desc, params, passes):
+def _render(desc, params, passes, fb=None):
     import oracle
     O = oracle.load()
-    fb = np.zeros((W * H, 7), np.float32)
+    fb = np.zeros((W * H, 7), np.float32) if fb is None else fb
     for p in passes:
         O.oracle_render_pass(C.byref(desc), C.byref(params), p, oracle.ptr(fb), 0, 2, 1, None)
     return fb
@@ -49,11 +49,15 @@ def _worker(rank, world, port, out):
         from cudatracerlib_amd import shard
         hs, desc = _scene()
         params = shard.shard_params(ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0), world, rank)
-        passes = [p for s in range(STEPS) for p in shard.step_pass_indices(s, world, BASE)]
-        fb = torch.from_numpy(_render(desc, params, passes))
-        shard.reduce_framebuffer(fb, dist)
+        # a progressive job: the rank framebuffer accumulates step by step and the
+        # image is reduced after every step; the last reduce must be the whole image
+        fb = np.zeros((W * H, 7), np.float32)
+        img = None
+        for s in range(STEPS):
+            _render(desc, params, shard.step_pass_indices(s, world, BASE), fb)
+            img = shard.reduce_framebuffer(torch.from_numpy(fb), dist)
         if rank == 0:
-            np.save(out, fb.numpy())
+            np.save(out, img.numpy())
     finally:
         dist.destroy_process_group()
 
