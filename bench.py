@@ -329,6 +329,36 @@ def single_pass_leg(pt, fb, stream, sptr, torch, pass_index, passes):
                     "--steps-per-launch steps per ctl_render_passes launch"}
 
 
+def reference_dopass_leg(pt, desc, fb, stream, sptr, torch, pass_index, passes):
+    """The reference's own pass loop as a drop-in drives it: Tracer::DoPass =
+    UpdateKernel (ctl_scene_update on the unchanged scene: constants only, no
+    copy, no sync) + the sampler tables + one render pass
+    (Kernel/Tracer.h:209-248, TraceHelper.cu:182-217).  Device time of the loop
+    between HIP events on the pass stream, and the host time of the update calls."""
+    pt.generate_samples(pass_index, sptr)
+    pt.render_pass(fb.data_ptr(), sptr)   # warm-up
+    torch.cuda.synchronize()
+    pt.reset_rays(sptr)
+    upd = 0.0
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for k in range(passes):
+        t0 = time.perf_counter()
+        pt.update_scene(desc, 0, sptr)
+        upd += time.perf_counter() - t0
+        pt.generate_samples(pass_index + 1 + k, sptr)
+        pt.render_pass(fb.data_ptr(), sptr)
+    e1.record(stream)
+    pt.sync(sptr)
+    ms = e0.elapsed_time(e1)
+    rays = pt.rays_traced()
+    return {"passes": passes, "ms_per_pass": round(ms / passes, 3), "mrays_s": round(rays / ms / 1e3, 1),
+            "update_host_ms_per_call": round(upd * 1e3 / passes, 4),
+            "note": "per pass: ctl_scene_update(dirty=0) + ctl_sampler_generate + ctl_render_pass (reference "
+                    "DoPass: UpdateKernel + DoRender)"}
+
+
 def closest_shadow_leg(pt, fb, stream, sptr, torch, pass_index, passes):
     """The same pass with the reference's own KernelDynamicScene::Occluded
     (a closest-hit shadow traversal tested against the light distance,
@@ -588,6 +618,9 @@ def main(argv=None):
     single = None
     if rank == 0 and shards == 1 and G > 1 and a.one_pass_leg > 0:
         single = single_pass_leg(pt, fb, stream, sptr, torch, nxt + 40, a.one_pass_leg)
+    dopass = None
+    if rank == 0 and shards == 1 and a.dopass_leg > 0:
+        dopass = reference_dopass_leg(pt, desc, fb, stream, sptr, torch, nxt + 60, a.dopass_leg)
     closest = None
     if rank == 0 and a.closest_shadow_passes > 0 and shards == 1:
         scratch = torch.zeros_like(fb)
@@ -661,6 +694,7 @@ def main(argv=None):
             "roofline": rl,
             "primary_rays": prim,
             "one_pass_launches": single,
+            "reference_dopass": dopass,
             "closest_hit_shadows": closest,
             "wavefront_tracer": wpt,
             "prim_tracer_c1": c1,

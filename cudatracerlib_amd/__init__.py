@@ -231,6 +231,13 @@ class HostScene:
                "set_environment")
         return self
 
+    def set_environment_transform(self, rot):
+        """InfiniteLight::m_worldTransform (Light.h:307): a 3x3 rotation, world = rot @ local."""
+        r = np.ascontiguousarray(rot, dtype=np.float32).reshape(9)
+        _check(self._L.ctl_host_scene_set_environment_transform(self._h, (C.c_float * 9)(*r.tolist())), None,
+               "set_environment_transform")
+        return self
+
     def set_bvh_params(self, split_alpha=None, split_depth=8, bins=0, max_leaf=0):
         """BVH build knobs: reference splitting of large triangles (split_alpha = 0
         disables, None = library default), SAH bins per axis and max leaf size
@@ -289,6 +296,19 @@ class Tracer:
 
     def upload_scene(self, desc):
         _check(self._L.ctl_scene_upload(self._ctx, C.byref(desc)), self._ctx, "ctl_scene_upload")
+
+    def update_scene(self, desc, dirty=0, stream=0):
+        """UpdateKernel / DynamicScene::UpdateScene (ctl_scene_update): the scene constants
+        always, plus the array groups in `dirty` (_abi.CTL_DIRTY_*)."""
+        _check(self._L.ctl_scene_update(self._ctx, C.byref(desc), int(dirty), stream), self._ctx, "ctl_scene_update")
+
+    def set_transform(self, node, xf16, stream=0):
+        """DynamicScene::SetNodeTransform on the device (ctl_scene_set_transform):
+        xf16 = row-major object->world 4x4."""
+        m = _abi.Float4x4()
+        m.m[:] = [float(x) for x in np.asarray(xf16, dtype=np.float32).reshape(16)]
+        _check(self._L.ctl_scene_set_transform(self._ctx, int(node), C.byref(m), stream), self._ctx,
+               "ctl_scene_set_transform")
 
     def generate_samples(self, pass_index, stream=0):
         _check(self._L.ctl_sampler_generate(self._ctx, int(pass_index), stream), self._ctx, "ctl_sampler_generate")

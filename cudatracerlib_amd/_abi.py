@@ -32,6 +32,14 @@ CTL_WRAP_REPEAT, CTL_WRAP_CLAMP, CTL_WRAP_MIRROR, CTL_WRAP_BLACK = 0, 1, 2, 3
 CTL_MAX_NUM_LIGHTS = 16
 CTL_PT_MEGAKERNEL = 1
 CTL_PT_WAVEFRONT = 2
+# ctl_scene_update dirty groups (DynamicScene streams)
+CTL_DIRTY_TRI_DATA, CTL_DIRTY_WOOP, CTL_DIRTY_BVH, CTL_DIRTY_TRI_INDICES = 1, 2, 4, 8
+CTL_DIRTY_MATERIALS, CTL_DIRTY_MESHES, CTL_DIRTY_NODES, CTL_DIRTY_LIGHTS = 16, 32, 64, 128
+CTL_DIRTY_TEXTURES, CTL_DIRTY_ENV, CTL_DIRTY_ALL = 256, 512, 1023
+# ctl_scene_read arrays
+(CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS,
+ CTL_ARRAY_SAMPLES_1D, CTL_ARRAY_SAMPLES_2D, CTL_ARRAY_NODE_XF, CTL_ARRAY_NODE_INV_XF, CTL_ARRAY_LIGHTS,
+ CTL_ARRAY_LIGHT_TRIS, CTL_ARRAY_LIGHT_CDF, CTL_ARRAY_SCENE_BOX, CTL_ARRAY_ENV) = range(15)
 
 
 class BVHNode(C.Structure):          # BVHNodeData, 64 B
@@ -103,11 +111,11 @@ CTL_LIGHT_DIFFUSE = 0
 CTL_LIGHT_INFINITE = 1
 
 
-class EnvLight(C.Structure):          # ctl_env_light (InfiniteLight), 72 B
+class EnvLight(C.Structure):          # ctl_env_light (InfiniteLight), 112 B
     _fields_ = [("texture", C.c_uint32), ("scale", C.c_float * 3), ("size", C.c_float * 2),
                 ("pixel_size", C.c_float * 2), ("normalization", C.c_float), ("scene_center", C.c_float * 3),
                 ("scene_radius", C.c_float), ("cdf_cols", C.c_uint32), ("cdf_rows", C.c_uint32),
-                ("row_weights", C.c_uint32), ("pad", C.c_uint32 * 2)]
+                ("row_weights", C.c_uint32), ("world", (C.c_float * 3) * 3), ("pad", C.c_uint32 * 3)]
 
 
 class Camera(C.Structure):
@@ -193,6 +201,8 @@ SYMBOLS = [
     ("ctl_destroy", None, [_vp]),
     ("ctl_last_error", C.c_char_p, [_vp]),
     ("ctl_scene_upload", C.c_int32, [_vp, C.POINTER(SceneDesc)]),
+    ("ctl_scene_update", C.c_int32, [_vp, C.POINTER(SceneDesc), C.c_uint32, _vp]),
+    ("ctl_scene_set_transform", C.c_int32, [_vp, C.c_uint32, _vp, _vp]),
     ("ctl_sampler_generate", C.c_int32, [_vp, C.c_uint64, _vp]),
     ("ctl_sampler_upload", C.c_int32, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
     ("ctl_intersect", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, _vp]),
@@ -231,6 +241,7 @@ SYMBOLS = [
                                               C.c_uint32, C.c_uint32]),
     ("ctl_host_scene_set_flags", C.c_int32, [_vp, C.c_uint32]),
     ("ctl_host_scene_set_environment", C.c_int32, [_vp, C.c_uint32, _vp]),
+    ("ctl_host_scene_set_environment_transform", C.c_int32, [_vp, _vp]),
     ("ctl_host_scene_set_bvh_params", C.c_int32, [_vp, C.c_float, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("ctl_host_scene_set_bvh_builder", C.c_int32, [_vp, C.c_uint32, C.c_float]),
     ("ctl_host_scene_compile", C.c_int32, [_vp, C.c_uint32, C.POINTER(SceneDesc)]),

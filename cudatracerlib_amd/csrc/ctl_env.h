@@ -3,7 +3,7 @@
 // kernels: importance sampling of the latitude-longitude radiance map through
 // its row / column CDFs with a tent offset, the matching solid-angle pdf, and
 // the radiance seen along a ray (bilinear at level 0, or filtered with ray
-// differentials for the PrimTracer).  Identity world transform.
+// differentials for the PrimTracer), under m_worldTransform's rotation.
 //
 //   env_sample_direct  InfiniteLight::sampleDirect + internalSampleDirection (Light.cu:350-365, 420-457)
 //   env_pdf_direct     InfiniteLight::pdfDirect + internalPdfDirection      (Light.cu:367-377, 459-479)
@@ -26,6 +26,22 @@ struct EnvView {
     CTL_HD TexView map() const { return TexView{tex + e->texture, texels}; }
 };
 
+
+// m_worldTransform (Light.h:307, an OrthogonalAffineMap with zero translation):
+// TransformDirection = float4x4::TransformDirection (float4x4.h:404-408),
+// TransformDirectionTranspose = (dot(d, col0), dot(d, col1), dot(d, col2)) (float4x4.h:424-427)
+CTL_HD m44 env_world(const ctl_env_light& L) {
+    m44 m = m44_zero();
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) m.at(i, j) = L.world[i][j];
+    m.at(3, 3) = 1.0f;
+    return m;
+}
+CTL_HD f3 env_to_world(const ctl_env_light& L, f3 d) { return xform_dir(env_world(L), d); }
+CTL_HD f3 env_to_local(const ctl_env_light& L, f3 d) {
+    const m44 m = env_world(L);
+    return mk3(dot(d, xyz(m.col(0))), dot(d, xyz(m.col(1))), dot(d, xyz(m.col(2))));
+}
 
 CTL_HD float luminance(spec s) { return s.x * 0.212671f + s.y * 0.715160f + s.z * 0.072169f; }   // Spectrum.cu:174-177
 
@@ -96,6 +112,7 @@ CTL_HD spec env_sample_direct(const EnvView& E, direct_rec& dRec, f2 sample) {
     f3 d;
     float pdf;
     env_internal_sample(E, sample, d, value, pdf);
+    d = env_to_world(L, d);   // d = m_worldTransform.TransformDirection(d) (Light.cu:355)
     dRec.pdf = pdf;
     dRec.p = mk3(L.scene_center[0], L.scene_center[1], L.scene_center[2]) + d * L.scene_radius;
     dRec.n = -normalize(d);
@@ -106,7 +123,7 @@ CTL_HD spec env_sample_direct(const EnvView& E, direct_rec& dRec, f2 sample) {
 }
 
 CTL_HD float env_pdf_direct(const EnvView& E, const direct_rec& dRec) {
-    const float pdfSA = env_internal_pdf(E, dRec.d);
+    const float pdfSA = env_internal_pdf(E, env_to_local(*E.e, dRec.d));   // Light.cu:369
     if (dRec.measure == kESolidAngle) return pdfSA;
     if (dRec.measure == kEArea) return pdfSA * absdot(dRec.d, dRec.n) / (dRec.dist * dRec.dist);
     return 0.0f;
@@ -118,14 +135,16 @@ CTL_HD f2 env_uv(f3 v) {
 
 // evalEnvironment(ray): KernelMIPMap::Sample(uv, 0) = the bilinear lookup of level 0 (MIPMap.cu:140-153)
 CTL_HD spec env_eval(const EnvView& E, f3 dir) {
-    const spec value = tex_triangle(E.map(), 0, env_uv(dir));
+    const spec value = tex_triangle(E.map(), 0, env_uv(env_to_local(*E.e, dir)));   // Light.cu:483
     return value * mk3(E.e->scale[0], E.e->scale[1], E.e->scale[2]);
 }
 
 // evalEnvironment(ray, rX, rY): the map filtered over the ray differentials' footprint
-CTL_HD spec env_eval_diff(const EnvView& E, f3 v, f3 vx, f3 vy) {
+// (rd, rxd, ryd: the world directions of ray, rX, rY; Light.cu:496-511)
+CTL_HD spec env_eval_diff(const EnvView& E, f3 rd, f3 rxd, f3 ryd) {
+    const f3 v = env_to_local(*E.e, rd);
     const f2 uv = env_uv(v);
-    const f3 dvdx = vx - v, dvdy = vy - v;
+    const f3 dvdx = env_to_local(*E.e, rxd) - v, dvdy = env_to_local(*E.e, ryd) - v;
     const float t1 = CTL_INV_TWOPI / (v.x * v.x + v.z * v.z);
     const float t2 = -CTL_INV_PI / tmax(sqrtf(tmax(0.0f, 1.0f - v.y * v.y)), 1e-4f);
     const f2 dudx = mk2(t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y);

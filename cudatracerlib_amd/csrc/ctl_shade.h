@@ -61,6 +61,58 @@ CTL_HD void fill_dg(const ctl_triangle_data& td, const m44& L2W, f2 bary, bool h
     if (dot(dg.n, dg.sys.n) < 0.0f) dg.n = -dg.n;
 }
 
+// The spherical-normal decode without a table (Uchar2ToNormalizedFloat3,
+// Compression.h:20-31); the device LUT holds the same values.
+struct NormalDecodeRef {
+#if defined(__HIP__)
+    __host__ __device__
+#endif
+    f3 operator()(uint32_t c) const { return normal_decode16(c); }
+};
+
+// TriIntersectorData::getData (Engine/TriIntersectorData.cu:20-32): the three
+// vertices back from the Woop record (inverse of the unit-triangle transform).
+CTL_HD void woop_get_hd(const float v[12], f3& v0, f3& v1, f3& v2) {
+    m44 m = m44_identity();
+    m.set_row(0, mk4(v[4], v[5], v[6], v[7]));
+    m.set_row(1, mk4(v[8], v[9], v[10], v[11]));
+    m.set_row(2, mk4(v[0], v[1], v[2], v[3]));
+    m.at(2, 3) *= -1.0f;
+    m = inverse(m);
+    f3 e02 = xyz(m.col(0)), e12 = xyz(m.col(1));
+    v2 = xyz(m.col(3));
+    v0 = v2 + e02;
+    v1 = v2 + e12;
+}
+
+// ShapeSet::triData::Recalculate (Engine/ShapeSet.cu:11-22) for a light triangle
+// whose i_dat / t_dat are set: world-space vertices under the node transform, the
+// shading normal at the centroid (fillDG on the host: the half quirk decode) and
+// the area.  Shared by the scene compile (DynamicScene::CreateShape) and the
+// device update of a moved node (DynamicScene::SetNodeTransform -> RecomputeShape,
+// DynamicScene.cpp:433-443).
+CTL_HD void light_tri_recalc(const float woop[12], const ctl_triangle_data& td, const m44& mxf, ctl_light_tri& lt) {
+    f3 p[3];
+    woop_get_hd(woop, p[0], p[1], p[2]);
+    dgeom dg;
+    fill_dg(td, mxf, mk2(1.0f / 3.0f, 1.0f / 3.0f), true, NormalDecodeRef{}, dg);
+    for (int i = 0; i < 3; i++) p[i] = xform_point(mxf, p[i]);
+    const float area = 0.5f * length(cross(p[2] - p[0], p[1] - p[0]));
+    for (int i = 0; i < 3; i++) { lt.p[i][0] = p[i].x; lt.p[i][1] = p[i].y; lt.p[i][2] = p[i].z; }
+    lt.n[0] = dg.sys.n.x; lt.n[1] = dg.sys.n.y; lt.n[2] = dg.sys.n.z;
+    lt.area = area;
+}
+
+// ShapeSet::Recalculate's area distribution (Engine/ShapeSet.cpp:39-57): the CDF
+// over the light's triangles in order, normalised by the summed area.
+CTL_HD float shapeset_cdf(const ctl_light_tri* tris, uint32_t n, float* cdf) {
+    float sumArea = 0;
+    cdf[0] = 0.0f;
+    for (uint32_t i = 0; i < n; i++) { sumArea += tris[i].area; cdf[i + 1] = cdf[i] + tris[i].area; }
+    for (uint32_t i = 0; i <= n; i++) cdf[i] = cdf[i] / sumArea;
+    return sumArea;
+}
+
 // DifferentialGeometry::computePartials (Engine/DifferentialGeometry.cu:5-84)
 // with AlgebraHelper::solveLinearSystem2x2 (Math/AlgebraHelper.h:11-24).
 CTL_HD bool solve2x2_ref(const float a[2][2], const float b[2], float x[2]) {

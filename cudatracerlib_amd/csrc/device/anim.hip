@@ -22,10 +22,12 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cmath>
 #include <cstring>
 
 #include "common.h"
 #include "../ctl_anim.h"
+#include "../ctl_shade.h"
 #include "../host/bvh_wide.h"
 
 namespace ctl {
@@ -256,14 +258,47 @@ __global__ __launch_bounds__(kAB) void inst_box_kernel(const ctl_node* __restric
     instance_box(m, mb, mb + 3, out + 6 * i, out + 6 * i + 3);
 }
 
-// scene box = union of the instance boxes; eps = 1e-4 * |size| (DynamicScene.cpp:587)
-__global__ void scene_eps_kernel(const float* inst, uint32_t n, float* out) {
+// scene box = union of the instance boxes; eps = 1e-4 * |size| (DynamicScene.cpp:587);
+// the environment light's scene sphere follows the box (UpdateScene re-runs
+// InfiniteLight::Update, DynamicScene.cpp:540-542, Light.h:316-323)
+__global__ void scene_eps_kernel(const float* inst, uint32_t n, float* out, ctl_env_light* env) {
     float lo[3], hi[3];
     box_empty(lo, hi);
     for (uint32_t i = 0; i < n; i++) box_extend(lo, hi, inst + 6 * i, inst + 6 * i + 3);
     for (int k = 0; k < 3; k++) { out[k] = lo[k]; out[3 + k] = hi[k]; }
     const f3 size = mk3(hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]);
     out[6] = 1e-4f * length(size);
+    if (env) {
+        const f3 l = mk3(lo[0], lo[1], lo[2]), h = mk3(hi[0], hi[1], hi[2]);
+        const f3 c = (l + h) * 0.5f;   // AABB::Center
+        env->scene_center[0] = c.x; env->scene_center[1] = c.y; env->scene_center[2] = c.z;
+        env->scene_radius = length(h - l) / 1.5f;
+    }
+}
+
+// DynamicScene::SetNodeTransform -> RecomputeShape (DynamicScene.cpp:433-443,
+// ShapeSet.cpp:39-57): the ShapeSet of every diffuse light on `node`, one thread
+// per light, its triangles in order (the area CDF is a sequential sum).
+__global__ void light_recalc_kernel(ctl_light* lights, uint32_t n_lights, ctl_light_tri* tris, float* cdf,
+                                    const float4* __restrict__ woop, const ctl_triangle_data* __restrict__ td,
+                                    const float4* __restrict__ xf, uint32_t node) {
+    const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= n_lights) return;
+    ctl_light& L = lights[li];
+    if (L.kind != CTL_LIGHT_DIFFUSE || L.node_idx != node) return;
+    m44 m;
+    for (int k = 0; k < 4; k++) {
+        const float4 r = xf[4 * node + k];
+        m.d[4 * k] = r.x; m.d[4 * k + 1] = r.y; m.d[4 * k + 2] = r.z; m.d[4 * k + 3] = r.w;
+    }
+    for (uint32_t i = 0; i < L.tri_count; i++) {
+        ctl_light_tri& t = tris[L.tri_first + i];
+        const float4* w4 = woop + 3 * (size_t)t.i_dat;
+        float w[12];
+        for (int k = 0; k < 3; k++) { const float4 q = w4[k]; w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w; }
+        light_tri_recalc(w, td[t.t_dat], m, t);
+    }
+    L.sum_area = shapeset_cdf(tris + L.tri_first, L.tri_count, cdf + L.cdf_first);
 }
 
 template <class T>
@@ -390,11 +425,21 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
         !anim_alloc(A, &A->d_inst_boxes, 6ull * std::max(1u, d->n_nodes)) || !anim_alloc(A, &A->d_eps, 8) ||
         hipHostMalloc((void**)&A->h_eps, 8 * sizeof(float), hipHostMallocDefault) != hipSuccess)
         return fail("animation state allocation failed");
+    const bool wide = !wn.empty() || !sw.empty();
+    // the instance tree's refit plan: animated meshes and moved nodes (ctl_scene_set_transform)
+    if (d->n_nodes > 0 && d->scene_start_node >= 0 && d->n_scene_bvh_nodes > 0) {
+        if (!plan_binary(A, A->scene_bin, d->scene_bvh_nodes, d->n_scene_bvh_nodes, 0,
+                         (uint32_t)d->scene_start_node >> 2, err))
+            return fail(err);
+        if (wide && !sw.empty()) {
+            if (ssrc.size() != 4 * sw.size()) return fail("wide source map missing");
+            if (!plan_gather(A, A->scene_wide, ssrc.data(), (uint32_t)sw.size(), 0, err)) return fail(err);
+        }
+    }
     if (d->n_anim_meshes == 0) return CTL_OK;
     if (!anim_upload(A, (ctl_anim_vertex**)&A->d_verts, d->anim_vertices, d->n_anim_vertices) ||
         !anim_upload(A, (uint32_t**)&A->d_tris, d->anim_triangles, 3ull * d->n_anim_triangles))
         return fail("animation upload failed");
-    const bool wide = !wn.empty();
     size_t tmp = 0, etmp = 0;
     for (uint32_t a = 0; a < d->n_anim_meshes; a++) {
         AnimMeshPlan P;
@@ -427,15 +472,6 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
         tmp = std::max<size_t>(tmp, P.am.vertex_count);
         etmp = std::max<size_t>(etmp, P.n_entries);
         A->meshes.push_back(std::move(P));
-    }
-    if (d->n_nodes > 0 && d->scene_start_node >= 0 && d->n_scene_bvh_nodes > 0) {
-        if (!plan_binary(A, A->scene_bin, d->scene_bvh_nodes, d->n_scene_bvh_nodes, 0,
-                         (uint32_t)d->scene_start_node >> 2, err))
-            return fail(err);
-        if (wide && !sw.empty()) {
-            if (ssrc.size() != 4 * sw.size()) return fail("wide source map missing");
-            if (!plan_gather(A, A->scene_wide, ssrc.data(), (uint32_t)sw.size(), 0, err)) return fail(err);
-        }
     }
     if (!anim_alloc(A, &A->d_P, tmp) || !anim_alloc(A, &A->d_N, tmp) || !anim_alloc(A, &A->d_ebox, 2 * etmp))
         return fail("animation buffers allocation failed");
@@ -498,15 +534,65 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         float* sbin = reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh));
         if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
         launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);
-        hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps);
+        hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps,
+                           const_cast<ctl_env_light*>(S.env));
         if (hipMemcpyAsync(A->h_eps, A->d_eps, 7 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {
             c->err = "scene_animate: epsilon readback failed";
             return CTL_ERR_HIP;
         }
         S.ray_eps = A->h_eps[6];
+        c->device_eps = true;
     }
     if (hipGetLastError() != hipSuccess) { c->err = "scene_animate: launch failed"; return CTL_ERR_HIP; }
+    return CTL_OK;
+}
+
+CTL_API ctl_status ctl_scene_set_transform(ctl_ctx* c, uint32_t node, const ctl_float4x4* xf, void* stream) {
+    if (!c || !xf) return CTL_ERR_INVALID;
+    if (!c->has_scene || !c->anim) { c->err = "scene_set_transform: no scene uploaded"; return CTL_ERR_STATE; }
+    AnimState* A = c->anim;
+    DevScene& S = c->scene;
+    if (node >= S.n_nodes) { c->err = "scene_set_transform: node index out of range"; return CTL_ERR_INVALID; }
+    if (S.wide && S.quant && A->scene_bin.valid) {
+        c->err = "scene_set_transform: 64-B quantized trees are not refit (upload without CTL_SCENE_WIDE_QUANT)";
+        return CTL_ERR_STATE;
+    }
+    for (int k = 0; k < 16; k++)
+        if (!std::isfinite(xf->m[k])) { c->err = "scene_set_transform: non-finite transform"; return CTL_ERR_INVALID; }
+    if (hipSetDevice(c->device) != hipSuccess) { c->err = "scene_set_transform: hipSetDevice failed"; return CTL_ERR_HIP; }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // SceneBVH::setTransform (SceneBVH.cpp:77-89): the matrix and its inverse, on the host
+    m44 M;
+    std::memcpy(M.d, xf->m, 64);
+    const m44 inv = inverse(M);
+    float* dxf = reinterpret_cast<float*>(const_cast<float4*>(S.xf)) + 16 * (size_t)node;
+    float* dixf = reinterpret_cast<float*>(const_cast<float4*>(S.inv_xf)) + 16 * (size_t)node;
+    if (hipMemcpyAsync(dxf, M.d, 64, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(dixf, inv.d, 64, hipMemcpyHostToDevice, s) != hipSuccess) {
+        c->err = "scene_set_transform: transform upload failed";
+        return CTL_ERR_HIP;
+    }
+    if (S.n_lights)
+        hipLaunchKernelGGL(light_recalc_kernel, dim3(1), dim3(64), 0, s, const_cast<ctl_light*>(S.lights), S.n_lights,
+                           const_cast<ctl_light_tri*>(S.light_tris), const_cast<float*>(S.light_tri_cdf), S.woop,
+                           S.tri_data, S.xf, node);
+    hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf, A->n_nodes,
+                       A->d_mesh_boxes, A->d_inst_boxes);
+    LeafCtx LS{nullptr, nullptr, A->d_inst_boxes};
+    float* sbin = reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh));
+    if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
+    if (S.wide) launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);
+    hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps,
+                       const_cast<ctl_env_light*>(S.env));
+    if (hipGetLastError() != hipSuccess) { c->err = "scene_set_transform: launch failed"; return CTL_ERR_HIP; }
+    if (hipMemcpyAsync(A->h_eps, A->d_eps, 7 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        c->err = "scene_set_transform: epsilon readback failed";
+        return CTL_ERR_HIP;
+    }
+    S.ray_eps = A->h_eps[6];
+    c->device_eps = true;
     return CTL_OK;
 }
 
@@ -539,6 +625,17 @@ CTL_API ctl_status ctl_scene_read(ctl_ctx* c, uint32_t array, uint64_t first, ui
             else { src = c->d_s2[c->active]; elem = sizeof(float2); }
             n = (uint64_t)c->nseq * c->len;
             break;
+        case CTL_ARRAY_NODE_XF: src = S.xf; elem = sizeof(ctl_float4x4); n = S.n_nodes; break;
+        case CTL_ARRAY_NODE_INV_XF: src = S.inv_xf; elem = sizeof(ctl_float4x4); n = S.n_nodes; break;
+        case CTL_ARRAY_LIGHTS: src = S.lights; elem = sizeof(ctl_light); n = c->sarr[SA_LIGHTS].bytes / elem; break;
+        case CTL_ARRAY_LIGHT_TRIS: src = S.light_tris; elem = sizeof(ctl_light_tri); n = c->sarr[SA_LTRIS].bytes / elem; break;
+        case CTL_ARRAY_LIGHT_CDF: src = S.light_tri_cdf; elem = sizeof(float); n = c->sarr[SA_LCDF].bytes / elem; break;
+        case CTL_ARRAY_SCENE_BOX:
+            if (!c->anim || !c->device_eps) { c->err = "scene_read: the scene box is derived by set_transform / animate"; return CTL_ERR_STATE; }
+            src = c->anim->d_eps; elem = 6 * sizeof(float); n = 1; break;
+        case CTL_ARRAY_ENV:
+            if (!S.env) { c->err = "scene_read: no environment light"; return CTL_ERR_STATE; }
+            src = S.env; elem = sizeof(ctl_env_light); n = 1; break;
         default: c->err = "scene_read: unknown array"; return CTL_ERR_INVALID;
     }
     if (first > n || count > n - first) { c->err = "scene_read: range out of bounds"; return CTL_ERR_INVALID; }

@@ -488,12 +488,30 @@ struct WfState {
 struct WptBuffers;
 struct AnimState;
 
+// Device arrays of an uploaded scene (scene_dev.hip): one allocation per
+// KernelDynamicScene stream, reused by ctl_scene_update while it fits.
+enum SceneArr : int {
+    SA_BVH, SA_WOOP, SA_IDX, SA_TRI, SA_MATS, SA_MESHES, SA_NODES, SA_SBVH, SA_XF, SA_IXF, SA_LIGHTS, SA_LTRIS,
+    SA_LCDF, SA_LUT, SA_TEX, SA_TEXDATA, SA_ENV, SA_ENVDATA, SA_WBVH, SA_SWBVH, SA_WBASE, SA_COUNT
+};
+struct SceneArray {
+    void* p = nullptr;
+    size_t bytes = 0;   // bytes of the current contents
+    size_t cap = 0;     // allocated
+};
+
 }  // namespace ctl
 
 struct ctl_ctx {
     int device = 0;
     std::string err;
-    std::vector<void*> scene_allocs;
+    ctl::SceneArray sarr[ctl::SA_COUNT];
+    std::vector<uint32_t> h_wbase;              // host copy of the mesh wide-tree bases
+    int stack_mesh_bin = 0, stack_mesh_wide = 0;// worst-case mesh-level stacks (bvh_wide.h)
+    int stack_top_bin = -1, stack_top_wide = -1;// top level (-1: no instance tree)
+    uint32_t tree_flags = 0;                    // CTL_SCENE_BINARY_BVH / WIDE_QUANT the trees were built for
+    uint32_t n_anim_meshes = 0;
+    bool device_eps = false;                    // ray_eps derived on the device (set_transform / animate)
     ctl::DevScene scene{};
     bool has_scene = false;
     bool half_quirk = false;
@@ -552,6 +570,8 @@ int resident_blocks(ctl_ctx* c, K kernel, size_t lds) {
     return nb;
 }
 
+// scene_dev.hip: drops the device scene
+void free_scene(ctl_ctx* c);
 // wavefront.hip
 int wavefront_pass(ctl_ctx* c, const PathParams& P, const SampleSlots& SS, bool stats, hipStream_t s);
 void wavefront_free(ctl_ctx* c);

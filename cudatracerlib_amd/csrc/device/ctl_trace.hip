@@ -483,32 +483,6 @@ static std::string g_create_err;
         }                                                                                  \
     } while (0)
 
-static void free_scene(ctl_ctx* c) {
-    for (void* p : c->scene_allocs) (void)hipFree(p);
-    c->scene_allocs.clear();
-    ctl::anim_free(c);
-    c->has_scene = false;
-}
-
-template <class T>
-static ctl_status upload(ctl_ctx* c, const T* src, size_t count, const T** dst, size_t pad = 0) {
-    size_t bytes = count * sizeof(T);
-    void* p = nullptr;
-    hipError_t e = hipMalloc(&p, bytes + pad * sizeof(T) ? bytes + pad * sizeof(T) : 16);
-    if (e != hipSuccess) { c->err = std::string("hipMalloc: ") + hipGetErrorString(e); return CTL_ERR_NOMEM; }
-    c->scene_allocs.push_back(p);
-    if (pad) {
-        e = hipMemset(static_cast<char*>(p) + bytes, 0, pad * sizeof(T));
-        if (e != hipSuccess) { c->err = std::string("hipMemset: ") + hipGetErrorString(e); return CTL_ERR_HIP; }
-    }
-    if (bytes) {
-        e = hipMemcpy(p, src, bytes, hipMemcpyHostToDevice);
-        if (e != hipSuccess) { c->err = std::string("hipMemcpy: ") + hipGetErrorString(e); return CTL_ERR_HIP; }
-    }
-    *dst = reinterpret_cast<const T*>(p);
-    return CTL_OK;
-}
-
 extern "C" {
 
 CTL_API int32_t ctl_abi_version(void) { return CTL_ABI_VERSION; }
@@ -597,244 +571,6 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
         if (c->pass_ev[i]) (void)hipEventDestroy(c->pass_ev[i]);
     if (c->d_powers) (void)hipFree(c->d_powers);
     delete c;
-}
-
-CTL_API ctl_status ctl_scene_upload(ctl_ctx* c, const ctl_scene_desc* d) {
-    if (!c || !d) return CTL_ERR_INVALID;
-    CTL_HIP(c, hipSetDevice(c->device));
-    if (d->n_lights > CTL_MAX_NUM_LIGHTS) { c->err = "scene_upload: more than 16 lights"; return CTL_ERR_INVALID; }
-    for (uint32_t i = 0; i < d->n_lights; i++) {
-        if (d->lights[i].orthogonal) { c->err = "scene_upload: orthogonal DiffuseLight unsupported"; return CTL_ERR_INVALID; }
-        if (d->lights[i].kind > CTL_LIGHT_INFINITE || (d->lights[i].kind == CTL_LIGHT_INFINITE) != (i == d->env_map_index)) {
-            c->err = "scene_upload: the environment light must be the light env_map_index names";
-            return CTL_ERR_INVALID;
-        }
-    }
-    if (d->env_map_index != 0xffffffffu) {   // InfiniteLight: its record, map and tables
-        const ctl_env_light* e = d->env;
-        if (d->env_map_index >= d->n_lights || !e || e->texture >= d->n_textures || !d->env_data) {
-            c->err = "scene_upload: environment light without its record, texture or tables";
-            return CTL_ERR_INVALID;
-        }
-        const uint32_t w = (uint32_t)e->size[0], h = (uint32_t)e->size[1];
-        if (w != d->textures[e->texture].width || h != d->textures[e->texture].height ||
-            (uint64_t)e->cdf_cols + (uint64_t)(w + 1) * h > d->n_env_data || (uint64_t)e->cdf_rows + h + 1 > d->n_env_data ||
-            (uint64_t)e->row_weights + h > d->n_env_data) {
-            c->err = "scene_upload: environment tables do not match the radiance map";
-            return CTL_ERR_INVALID;
-        }
-    }
-    for (uint32_t i = 0; i < d->n_materials; i++) {
-        const ctl_material& m = d->materials[i];
-        if (m.bsdf_type != CTL_BSDF_DIFFUSE && m.bsdf_type != CTL_BSDF_ROUGHDIELECTRIC) {
-            c->err = "scene_upload: only diffuse and roughdielectric BSDFs are supported";
-            return CTL_ERR_INVALID;
-        }
-        if (m.bsdf_type == CTL_BSDF_ROUGHDIELECTRIC && (m.distribution > CTL_MICROFACET_GGX || !m.sample_visible)) {
-            c->err = "scene_upload: roughdielectric needs a Beckmann/GGX distribution with visible-normal sampling";
-            return CTL_ERR_INVALID;
-        }
-        if (m.bsdf_type == CTL_BSDF_DIFFUSE && m.texture != 0xffffffffu && m.texture >= d->n_textures) {
-            c->err = "scene_upload: material texture index out of range";
-            return CTL_ERR_INVALID;
-        }
-        if (m.alpha_state) {
-            const uint32_t st = m.alpha_state;
-            if (st != 1 && st != 2 && st != 5 && st != 6) {
-                c->err = "scene_upload: alpha state must be 0, 1, 2, 5 or 6 (color compare unsupported)";
-                return CTL_ERR_INVALID;
-            }
-            if (st < 4 && (m.alpha_texture == 0xffffffffu || m.alpha_texture >= d->n_textures)) {
-                c->err = "scene_upload: alpha map texture index out of range";
-                return CTL_ERR_INVALID;
-            }
-            if (m.bsdf_type != CTL_BSDF_DIFFUSE && st >= 4) {
-                c->err = "scene_upload: reflectance-map alpha needs a diffuse material";
-                return CTL_ERR_INVALID;
-            }
-        }
-    }
-    for (uint32_t i = 0; i < d->n_textures; i++) {
-        const ctl_texture& t = d->textures[i];
-        if (t.levels == 0 || t.levels > 16 || t.width < 2 || t.height < 2 || t.set_id != 0 ||
-            (uint64_t)t.offsets[t.levels - 1] + (uint64_t)(t.width >> (t.levels - 1)) * (t.height >> (t.levels - 1)) > d->n_tex_data) {
-            c->err = "scene_upload: invalid texture record";
-            return CTL_ERR_INVALID;
-        }
-    }
-    CTL_HIP(c, hipDeviceSynchronize());
-    free_scene(c);
-    DevScene S{};
-    ctl_status r;
-#define UP(src, cnt, dst, ...)                                    \
-    if ((r = upload(c, src, cnt, dst, ##__VA_ARGS__)) != CTL_OK) { free_scene(c); return r; }
-    const ctl_bvh_node* bvh; UP(d->bvh_nodes, d->n_bvh_nodes, &bvh);
-    // one zeroed entry past the end: the leaf loop loads entry i+1 while it tests entry i
-    const ctl_woop_tri* woop; UP(d->woop_tris, d->n_woop_tris, &woop, 1);
-    UP(d->tri_indices, d->n_tri_indices, &S.tri_idx, 1);
-    UP(d->tri_data, d->n_tri_data, &S.tri_data);
-    UP(d->materials, d->n_materials, &S.mats);
-    UP(d->meshes, d->n_meshes, &S.meshes);
-    UP(d->nodes, d->n_nodes, &S.nodes);
-    const ctl_bvh_node* sb; UP(d->scene_bvh_nodes, d->n_scene_bvh_nodes, &sb);
-    const ctl_float4x4* xf; UP(d->node_xf, d->n_nodes, &xf);
-    const ctl_float4x4* ixf; UP(d->node_inv_xf, d->n_nodes, &ixf);
-    UP(d->lights, d->n_lights, &S.lights);
-    UP(d->light_tris, d->n_light_tris, &S.light_tris);
-    UP(d->light_tri_cdf, d->n_light_tri_cdf, &S.light_tri_cdf);
-    // decoded spherical-normal table (Uchar2ToNormalizedFloat3, Compression.h:20-31)
-    std::vector<float4> lut(65536);
-    for (uint32_t code = 0; code < 65536; code++) {
-        f3 v = normal_decode16(code);
-        lut[code] = make_float4(v.x, v.y, v.z, 0.0f);
-    }
-    UP(lut.data(), lut.size(), &S.normal_lut);
-    UP(d->textures, d->n_textures, &S.textures);
-    UP(d->tex_data, d->n_tex_data, &S.tex_data);
-    S.env_index = d->env_map_index;
-    if (d->env_map_index != 0xffffffffu) {
-        UP(d->env, 1, &S.env);
-        UP(d->env_data, d->n_env_data, &S.env_data);
-    }
-    // 4-wide trees for the device traversal (host/bvh_wide.h), unless the
-    // caller asks for the reference's binary visit order
-    const bool wide = (d->flags & CTL_SCENE_BINARY_BVH) == 0 && d->n_bvh_nodes > 0;
-    std::vector<WideNode> wn, sw;
-    std::vector<uint32_t> wbase, wsrc, ssrc;   // src maps: only for the refit of animated scenes
-    const bool want_src = d->n_anim_meshes > 0;
-    if (wide) {
-        wbase.assign(d->n_meshes, 0);
-        try {
-            std::vector<uint32_t> ms;
-            for (uint32_t m = 0; m < d->n_meshes; m++) {
-                const size_t first = d->meshes[m].bvh_node_offset / 4;
-                if (first >= d->n_bvh_nodes) throw std::runtime_error("mesh BVH offset out of range");
-                wbase[m] = (uint32_t)wn.size();
-                collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn, want_src ? &ms : nullptr);
-                if (want_src) wsrc.insert(wsrc.end(), ms.begin(), ms.end());
-            }
-            if (d->n_nodes > 0 && d->scene_start_node >= 0)
-                collapse_wide(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, sw,
-                              want_src ? &ssrc : nullptr);
-        } catch (const std::exception& e) {
-            free_scene(c);
-            c->err = std::string("scene_upload: ") + e.what();
-            return CTL_ERR_INVALID;
-        }
-        // 64-B quantized nodes on request (not when the refit will rewrite float nodes)
-        bool quant = (d->flags & CTL_SCENE_WIDE_QUANT) != 0 && !want_src;
-        std::vector<QWideNode> qn, qs;
-        auto encode = [](const std::vector<WideNode>& in, std::vector<QWideNode>& out) {
-            out.resize(in.size());
-            for (size_t i = 0; i < in.size(); i++) {
-                const WideNode& w = in[i];
-                const float lo[3][4] = {{w.lo_x[0], w.lo_x[1], w.lo_x[2], w.lo_x[3]},
-                                        {w.lo_y[0], w.lo_y[1], w.lo_y[2], w.lo_y[3]},
-                                        {w.lo_z[0], w.lo_z[1], w.lo_z[2], w.lo_z[3]}};
-                const float hi[3][4] = {{w.hi_x[0], w.hi_x[1], w.hi_x[2], w.hi_x[3]},
-                                        {w.hi_y[0], w.hi_y[1], w.hi_y[2], w.hi_y[3]},
-                                        {w.hi_z[0], w.hi_z[1], w.hi_z[2], w.hi_z[3]}};
-                if (!quantize_wide(lo, hi, w.child, out[i])) return false;
-            }
-            return true;
-        };
-        if (quant) quant = encode(wn, qn) && encode(sw, qs);
-        if (quant) {
-            const QWideNode* qd; UP(qn.data(), qn.size(), &qd);
-            const QWideNode* sqd; UP(qs.data(), qs.size(), &sqd);
-            S.wbvh = reinterpret_cast<const float4*>(qd);
-            S.scene_wbvh = reinterpret_cast<const float4*>(sqd);
-        } else {
-            const WideNode* wd; UP(wn.data(), wn.size(), &wd);
-            const WideNode* swd; UP(sw.data(), sw.size(), &swd);
-            S.wbvh = reinterpret_cast<const float4*>(wd);
-            S.scene_wbvh = reinterpret_cast<const float4*>(swd);
-        }
-        S.quant = quant ? 1 : 0;
-        UP(wbase.data(), wbase.size(), &S.mesh_wbase);
-        S.wide = 1;
-        S.tie_min = 1;
-        c->wide_nodes = wn.size();
-    }
-#undef UP
-    // Worst-case traversal stack (host/bvh_wide.h), for every traversal the
-    // scene can take (the 4-wide trees, and the binary trees of stats launches
-    // and CTL_SCENE_BINARY_BVH): a scene that could overflow the kStackMax
-    // entries of a lane is refused here, so no ray can end early on a full
-    // stack.  Two levels: top-level stack + the pending top-level entry + the
-    // mesh stack (its sentinel included).
-    try {
-        int mesh_bin = 0, mesh_wide = 0;
-        for (uint32_t m = 0; m < d->n_meshes && d->n_bvh_nodes > 0; m++) {
-            const size_t first = d->meshes[m].bvh_node_offset / 4;
-            mesh_bin = std::max(mesh_bin, binary_stack_bound(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, kStackMax));
-            if (wide) mesh_wide = std::max(mesh_wide, wide_stack_bound(wn.data() + wbase[m], wn.size() - wbase[m], 0, kStackMax));
-        }
-        int bound = std::max(mesh_bin, mesh_wide);
-        if (d->n_nodes > 0 && d->scene_start_node >= 0) {
-            const int top_bin = binary_stack_bound(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, kStackMax);
-            const int top_wide = wide ? wide_stack_bound(sw.data(), sw.size(), 0, kStackMax) : 0;
-            bound = std::max(top_bin + 1 + mesh_bin, wide ? top_wide + 1 + mesh_wide : 0);
-        }
-        if (bound > kStackMax) {
-            free_scene(c);
-            c->err = "scene_upload: the BVH needs a deeper traversal stack than " + std::to_string(kStackMax) + " entries";
-            return CTL_ERR_INVALID;
-        }
-        c->stack_bound = bound;
-    } catch (const std::exception& e) {
-        free_scene(c);
-        c->err = std::string("scene_upload: ") + e.what();
-        return CTL_ERR_INVALID;
-    }
-    S.bvh = reinterpret_cast<const float4*>(bvh);
-    S.woop = reinterpret_cast<const float4*>(woop);
-    S.scene_bvh = reinterpret_cast<const float4*>(sb);
-    S.xf = reinterpret_cast<const float4*>(xf);
-    S.inv_xf = reinterpret_cast<const float4*>(ixf);
-    S.n_nodes = d->n_nodes;
-    S.start_node = d->scene_start_node;
-    S.n_lights = d->n_lights;
-    S.flags = d->flags;
-    S.ray_eps = d->ray_eps;
-    for (int i = 0; i < CTL_MAX_NUM_LIGHTS; i++) S.light_cdf[i] = d->light_cdf[i];
-    S.camera = d->camera;
-    S.full_shading = kShadeLean;
-    S.alpha = 0;
-    for (uint32_t i = 0; i < d->n_materials; i++) {
-        const ctl_material& m = d->materials[i];
-        if (m.bsdf_type != CTL_BSDF_DIFFUSE || m.texture != 0xffffffffu || m.alpha_state) S.full_shading = kShadeFull;
-        if (m.alpha_state) S.alpha = 1;   // DynamicScene.cpp:586 doAlphaMapping
-    }
-    if (S.alpha) S.full_shading = kShadeAlpha;
-    if (S.env_index != 0xffffffffu) S.full_shading = kShadeEnv;
-    S.single = 0;
-    if (d->n_nodes > 0 && d->scene_start_node < 0) {
-        uint32_t node = ~(uint32_t)d->scene_start_node;
-        if (node >= d->n_nodes) { free_scene(c); c->err = "scene_upload: start node out of range"; return CTL_ERR_INVALID; }
-        const ctl_kernel_mesh& M = d->meshes[d->nodes[node].mesh_index];
-        S.single = 1;
-        S.s_node_base = M.bvh_node_offset;
-        S.s_tri_base = M.bvh_triangle_offset;
-        S.s_idx_base = M.bvh_indices_offset;
-        S.s_tri_offset = M.triangle_offset;
-        if (S.wide) {
-            // host copy of the wide base of that mesh
-            uint32_t mi = d->nodes[node].mesh_index, base = 0;
-            CTL_HIP(c, hipMemcpy(&base, S.mesh_wbase + mi, 4, hipMemcpyDeviceToHost));
-            S.s_wnode_base = base;
-        }
-    }
-    c->scene = S;
-    c->half_quirk = (d->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
-    c->n_tri_data = d->n_tri_data;
-    c->n_woop = d->n_woop_tris;
-    c->n_bvh_nodes = d->n_bvh_nodes;
-    c->n_scene_bvh = d->n_scene_bvh_nodes;
-    int ar = ctl::anim_setup(c, d, wn, wbase, sw, wsrc, ssrc);
-    if (ar != CTL_OK) { free_scene(c); return (ctl_status)ar; }
-    c->has_scene = true;
-    return CTL_OK;
 }
 
 CTL_API ctl_status ctl_sampler_upload(ctl_ctx* c, const float* seq1d, const float* seq2d, uint32_t nseq, uint32_t len,

@@ -27,18 +27,7 @@ void set_host_error(const std::string& s) { g_host_error = s; }
 
 void woop_set(f3 a, f3 b, f3 c, ctl_woop_tri& out) { woop_set_hd(a, b, c, out.v); }
 
-void woop_get(const ctl_woop_tri& in, f3& v0, f3& v1, f3& v2) {
-    m44 m = m44_identity();
-    m.set_row(0, mk4(in.v[4], in.v[5], in.v[6], in.v[7]));
-    m.set_row(1, mk4(in.v[8], in.v[9], in.v[10], in.v[11]));
-    m.set_row(2, mk4(in.v[0], in.v[1], in.v[2], in.v[3]));
-    m.at(2, 3) *= -1.0f;
-    m = inverse(m);
-    f3 e02 = xyz(m.col(0)), e12 = xyz(m.col(1));
-    v2 = xyz(m.col(3));
-    v0 = v2 + e02;
-    v1 = v2 + e12;
-}
+void woop_get(const ctl_woop_tri& in, f3& v0, f3& v1, f3& v2) { woop_get_hd(in.v, v0, v1, v2); }
 
 void camera_setup(const float pos[3], const float tar[3], const float up[3], float fov_deg, float nearc, float farc,
                   uint32_t w, uint32_t h, ctl_camera& out) {
@@ -97,10 +86,6 @@ void parallel_for(uint64_t n, uint32_t threads, F f) {
     }
     for (auto& t : ts) t.join();
 }
-
-struct NormalDecodeHost {
-    f3 operator()(uint32_t c) const { return normal_decode16(c); }
-};
 
 }  // namespace
 bool scene_add_light(ctl_host_scene* s, uint32_t node, uint32_t local_mat, const float L[3]) {
@@ -300,6 +285,12 @@ CTL_API ctl_status ctl_host_scene_set_environment(ctl_host_scene* s, uint32_t te
     s->env_texture = texture;
     if (scale)
         for (int k = 0; k < 3; k++) s->env_scale[k] = scale[k];
+    return CTL_OK;
+}
+
+CTL_API ctl_status ctl_host_scene_set_environment_transform(ctl_host_scene* s, const float rot9[9]) {
+    if (!s || !rot9) { set_host_error("set_environment_transform: invalid argument"); return CTL_ERR_INVALID; }
+    for (int k = 0; k < 9; k++) s->env_rot[k] = rot9[k];
     return CTL_OK;
 }
 
@@ -507,7 +498,6 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
     }
 
     // --- lights (CreateLight -> CreateShape -> ShapeSet)
-    NormalDecodeHost ndec;
     for (size_t li = 0; li < s->lights.size(); li++) {
         const auto& L = s->lights[li];
         if (s->meshes[s->nodes[L.node].mesh].animated) {
@@ -536,35 +526,21 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         std::vector<uint32_t> seen;
         std::vector<char> used(ntri, 0);
         m44 mxf = s->nodes[L.node].xf;
-        float sumArea = 0;
-        std::vector<float> areas;
         for (uint64_t e = e0; e < e1; e++) {
             uint32_t i2 = s->tri_indices[e] >> 1;
             const ctl_triangle_data& td = s->tri_data[km.triangle_offset + i2];
             if (((td.w[1] >> 16) & 0xff) != L.local_mat || used[i2]) continue;
             used[i2] = 1;
             ctl_light_tri lt{};
-            f3 p[3];
-            woop_get(s->woop[e], p[0], p[1], p[2]);
-            dgeom dg;
-            fill_dg(td, mxf, mk2(1.0f / 3.0f, 1.0f / 3.0f), true, ndec, dg);   // host fillDG
-            for (int i = 0; i < 3; i++) p[i] = xform_point(mxf, p[i]);
-            float area = 0.5f * length(cross(p[2] - p[0], p[1] - p[0]));
-            for (int i = 0; i < 3; i++) { lt.p[i][0] = p[i].x; lt.p[i][1] = p[i].y; lt.p[i][2] = p[i].z; }
-            lt.n[0] = dg.sys.n.x; lt.n[1] = dg.sys.n.y; lt.n[2] = dg.sys.n.z;
-            lt.area = area;
+            light_tri_recalc(s->woop[e].v, td, mxf, lt);   // ShapeSet::triData::Recalculate (host fillDG)
             lt.i_dat = (uint32_t)e;
             lt.t_dat = km.triangle_offset + i2;
             s->light_tris.push_back(lt);
-            areas.push_back(area);
         }
-        kl.tri_count = (uint32_t)areas.size();
+        kl.tri_count = (uint32_t)(s->light_tris.size() - kl.tri_first);
         if (kl.tri_count == 0) { set_host_error("compile: area light material has no triangles"); return CTL_ERR_INVALID; }
         std::vector<float> cdf(kl.tri_count + 1);
-        cdf[0] = 0.0f;
-        for (uint32_t i = 0; i < kl.tri_count; i++) { sumArea += areas[i]; cdf[i + 1] = cdf[i] + areas[i]; }
-        for (uint32_t i = 0; i <= kl.tri_count; i++) cdf[i] = cdf[i] / sumArea;
-        kl.sum_area = sumArea;
+        kl.sum_area = shapeset_cdf(s->light_tris.data() + kl.tri_first, kl.tri_count, cdf.data());
         s->light_tri_cdf.insert(s->light_tri_cdf.end(), cdf.begin(), cdf.end());
         s->klights.push_back(kl);
     }
@@ -579,6 +555,7 @@ CTL_API ctl_status ctl_host_scene_compile(ctl_host_scene* s, uint32_t threads, c
         L = ctl_env_light{};
         L.texture = s->env_texture;
         for (int k = 0; k < 3; k++) L.scale[k] = s->env_scale[k];
+        for (int k = 0; k < 9; k++) L.world[k / 3][k % 3] = s->env_rot[k];   // m_worldTransform
         const ctl_texture& t = s->textures[L.texture];
         s->env_tables.assign(env_table_floats(t.width, t.height), 0.0f);
         EnvView E{&L, nullptr, s->textures.data(), s->tex_data.data()};

@@ -67,6 +67,7 @@ struct ctl_host_scene {
     // environment (ctl_host_scene_set_environment): InfiniteLight record + its tables
     uint32_t env_texture = 0xffffffffu;
     float env_scale[3] = {1.0f, 1.0f, 1.0f};
+    float env_rot[9] = {1.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 1.0f};   // InfiniteLight::m_worldTransform
     ctl_env_light kenv{};
     std::vector<float> env_tables;
     std::vector<ctl_light_tri> light_tris;

@@ -208,11 +208,17 @@ typedef struct {
 enum { CTL_LIGHT_DIFFUSE = 0, CTL_LIGHT_INFINITE = 1 };
 
 /* InfiniteLight (SceneTypes/Light.h:294-367, Light.cpp:10-58): a latitude-
- * longitude radiance map around the scene, identity world transform.  The
- * radiance map is an image texture (textures[texture], level 0 read; its wrap
- * mode applies to the bilinear lookups); env_data holds the sampling tables
- * the constructor builds: cdf_cols ((width + 1) x height), cdf_rows
- * (height + 1) and row_weights (height) at the given float offsets. */
+ * longitude radiance map around the scene.  The radiance map is an image
+ * texture (textures[texture], level 0 read; its wrap mode applies to the
+ * bilinear lookups); env_data holds the sampling tables the constructor builds:
+ * cdf_cols ((width + 1) x height), cdf_rows (height + 1) and row_weights
+ * (height) at the given float offsets.  world = the rotation part of
+ * m_worldTransform (NormalizedT<OrthogonalAffineMap>, Light.h:307), row-major:
+ * directions are mapped world = world * local (TransformDirection) and back
+ * with its transpose (TransformDirectionTranspose, Light.cu:342-510); the
+ * reference's constructor sets the identity, which ctl_host_scene compiles
+ * unless ctl_host_scene_set_environment_transform says otherwise.  Upload
+ * refuses a matrix whose rows are not orthonormal. */
 typedef struct {
     uint32_t texture;
     float scale[3];              /* m_scale                                      */
@@ -222,7 +228,8 @@ typedef struct {
     float scene_center[3];       /* Update(): scene box centre                   */
     float scene_radius;          /*           |scene box size| / 1.5             */
     uint32_t cdf_cols, cdf_rows, row_weights;
-    uint32_t pad[2];
+    float world[3][3];           /* m_worldTransform rotation, row-major          */
+    uint32_t pad[3];
 } ctl_env_light;
 
 /* PerspectiveSensor device state after Update() (SceneTypes/Sensor.cu:76-96). */
@@ -357,6 +364,56 @@ CTL_API const char* ctl_last_error(const ctl_ctx* ctx);
 /* Copies the scene to the device (synchronous).  Replaces any previous scene. */
 CTL_API ctl_status ctl_scene_upload(ctl_ctx* ctx, const ctl_scene_desc* desc);
 
+/* The arrays of a ctl_scene_desc grouped as the reference's DynamicScene
+ * streams that UpdateScene re-uploads when invalidated
+ * (Engine/DynamicScene.cpp:480-554, Base/Buffer.h:257-291). */
+enum {
+    CTL_DIRTY_TRI_DATA = 1u << 0,     /* tri_data        (m_pTriDataStream)          */
+    CTL_DIRTY_WOOP = 1u << 1,         /* woop_tris       (m_pTriIntStream)           */
+    CTL_DIRTY_BVH = 1u << 2,          /* bvh_nodes       (m_pBVHStream); the 4-wide  */
+                                      /*   mesh trees are rebuilt from them           */
+    CTL_DIRTY_TRI_INDICES = 1u << 3,  /* tri_indices     (m_pBVHIndicesStream)       */
+    CTL_DIRTY_MATERIALS = 1u << 4,    /* materials       (m_pMaterialBuffer)         */
+    CTL_DIRTY_MESHES = 1u << 5,       /* meshes + mesh_boxes (m_pMeshBuffer)         */
+    CTL_DIRTY_NODES = 1u << 6,        /* nodes, node_xf / node_inv_xf, scene_bvh_nodes,
+                                         scene_start_node (m_pNodeStream + SceneBVH) */
+    CTL_DIRTY_LIGHTS = 1u << 7,       /* lights, light_tris, light_tri_cdf
+                                         (m_pLightStream + the ShapeSet data)        */
+    CTL_DIRTY_TEXTURES = 1u << 8,     /* textures, tex_data (m_pTextureBuffer)       */
+    CTL_DIRTY_ENV = 1u << 9,          /* env_map_index, env, env_data                */
+    CTL_DIRTY_ALL = (1u << 10) - 1u
+};
+
+/* UpdateKernel(DynamicScene*) (Kernel/TraceHelper.cu:182-217), called by the
+ * reference at the start of every Tracer::DoPass (Kernel/Tracer.h:229), plus
+ * the incremental DynamicScene::UpdateScene.  Refreshes the scene constants
+ * every time (camera, ray_eps, box, light_cdf, flags: KernelDynamicScene's
+ * non-array members) and copies only the array groups in `dirty` (CTL_DIRTY_*),
+ * stream-ordered on `stream`; clean arrays must keep their counts (else
+ * CTL_ERR_INVALID, the uploaded scene unchanged).  With dirty = 0 it costs no
+ * copy and no device synchronisation.  An array whose size grows is
+ * reallocated after the device drains; a dirty tree array rebuilds the 4-wide
+ * copies on the host.  ray_eps: after ctl_scene_set_transform or
+ * ctl_scene_animate the device's own epsilon (from the moved scene box) stays
+ * until the instances are uploaded again (CTL_DIRTY_NODES).  Those two calls
+ * edit device arrays only: marking such an array dirty uploads the desc's
+ * version again.  Without an uploaded scene this is ctl_scene_upload. */
+CTL_API ctl_status ctl_scene_update(ctl_ctx* ctx, const ctl_scene_desc* desc, uint32_t dirty, void* stream);
+
+/* DynamicScene::SetNodeTransform (Engine/DynamicScene.cpp:433-443) +
+ * SceneBVH::setTransform (Engine/SceneBVH.cpp:77-89) on the device: writes the
+ * node's object->world transform (row-major 4x4) and its inverse
+ * (float4x4::inverse, computed on the host as the reference does), recomputes
+ * the ShapeSet of every area light on the node (RecomputeShape,
+ * ShapeSet.cpp:39-57: world triangles, normals, areas, CDF, sumArea), refits
+ * the instance boxes and the scene BVH (binary and 4-wide; the reference's
+ * BVHRebuilder also rotates the tree, which traversal does not observe), and
+ * derives the scene box, ray epsilon (DynamicScene.cpp:583-587) and the
+ * environment light's scene sphere (InfiniteLight::Update) from it.
+ * Synchronises `stream` once (the epsilon is a kernel argument).  The caller's
+ * desc is not changed. */
+CTL_API ctl_status ctl_scene_set_transform(ctl_ctx* ctx, uint32_t node, const ctl_float4x4* xf, void* stream);
+
 /* Generates the SequenceSamplerData tables of render pass `pass_index` (the
  * pass-th UpdateKernel call, Kernel/Sampler.h:36-55 + 63-85) on the device,
  * asynchronously on `stream` (double-buffered; safe to call while the
@@ -469,7 +526,14 @@ enum {
     CTL_ARRAY_RAY_EPS = 5,     /* 1 float             */
     CTL_ARRAY_SAMPLES_1D = 6,  /* float, element-major [len][num_sequences]: the tables of the last
                                   ctl_sampler_generate / ctl_sampler_upload */
-    CTL_ARRAY_SAMPLES_2D = 7   /* float2, same layout */
+    CTL_ARRAY_SAMPLES_2D = 7,  /* float2, same layout */
+    CTL_ARRAY_NODE_XF = 8,     /* ctl_float4x4 per node */
+    CTL_ARRAY_NODE_INV_XF = 9, /* ctl_float4x4 per node */
+    CTL_ARRAY_LIGHTS = 10,     /* ctl_light           */
+    CTL_ARRAY_LIGHT_TRIS = 11, /* ctl_light_tri       */
+    CTL_ARRAY_LIGHT_CDF = 12,  /* float               */
+    CTL_ARRAY_SCENE_BOX = 13,  /* 6 floats: min xyz, max xyz (after set_transform / animate) */
+    CTL_ARRAY_ENV = 14         /* ctl_env_light       */
 };
 CTL_API ctl_status ctl_scene_read(ctl_ctx* ctx, uint32_t array, uint64_t first, uint64_t count, void* host_dst);
 
@@ -654,6 +718,9 @@ CTL_API ctl_status ctl_host_scene_set_flags(ctl_host_scene* s, uint32_t flags);
  * compile builds its sampling tables (InfiniteLight::InfiniteLight) and adds it
  * after the area lights (env_map_index).  texture = 0xFFFFFFFF removes it. */
 CTL_API ctl_status ctl_host_scene_set_environment(ctl_host_scene* s, uint32_t texture, const float scale[3]);
+/* The environment light's m_worldTransform rotation (row-major 3x3, world =
+ * R * local); the reference's constructor sets the identity (Light.cpp:58). */
+CTL_API ctl_status ctl_host_scene_set_environment_transform(ctl_host_scene* s, const float rot9[9]);
 /* Builds BVHs (threads=0: all hardware threads) and fills *out; the arrays
  * stay owned by `s` until it is destroyed or compiled again. */
 /* BVH build quality knobs of the compile (SplitBVHBuilder's splitAlpha /

@@ -604,8 +604,8 @@ float pdf_emitter(const SceneView& S, uint32_t idx) {   // KernelDynamicScene.cu
     return S.d->light_cdf[idx] - (idx == 0 ? 0.0f : S.d->light_cdf[idx - 1]);
 }
 // ---- InfiniteLight (SceneTypes/Light.h:294-367, Light.cu:350-511,
-// Light.cpp:10-58) with the identity world transform.  The radiance map is
-// S.d->textures[env->texture]; the tables are the desc's env_data.
+// Light.cpp:10-58).  The radiance map is S.d->textures[env->texture]; the
+// tables are the desc's env_data; env->world is m_worldTransform's rotation.
 const float O_EPSILON = 0.000001f;               // MathFunc.h:21
 const float O_INV_TWOPI = 1.0f / (2.0f * O_PI);  // MathFunc.h:14
 inline float luminance(Spec s) { return s.x * 0.212671f + s.y * 0.715160f + s.z * 0.072169f; }   // Spectrum.cu:174-177
@@ -622,6 +622,21 @@ float interval_to_tent(float sample) {   // Warp::intervalToTent (Math/Warp.h:13
     if (sample < 0.5f) sample *= 2;
     else { sign = -1; sample = 2 * (sample - 0.5f); }
     return sign * (1 - sqrtf(sample));
+}
+// m_worldTransform (Light.h:307, an OrthogonalAffineMap with zero translation):
+// TransformDirection = float4x4::TransformDirection (float4x4.h:404-408),
+// TransformDirectionTranspose = (dot(d, col0), dot(d, col1), dot(d, col2)) (float4x4.h:424-427)
+M44 env_world(const ctl_env_light& L) {
+    M44 m = M44::zeros();
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) m(i, j) = L.world[i][j];
+    m(3, 3) = 1.0f;
+    return m;
+}
+V3 env_to_world(const ctl_env_light& L, V3 d) { return transformDirection(env_world(L), d); }
+V3 env_to_local(const ctl_env_light& L, V3 d) {
+    const M44 m = env_world(L);
+    return v3(dot(d, xyz(m.col(0))), dot(d, xyz(m.col(1))), dot(d, xyz(m.col(2))));
 }
 V2 env_latlong(V3 v) {   // atan2(v.x, -v.z) / 2pi, safe_acos(v.y) / pi
     return v2(cr_atan2(v.x, -v.z) * O_INV_TWOPI, cr_acos(omin(1.0f, omax(-1.0f, v.y))) * O_INV_PI);
@@ -655,6 +670,7 @@ Spec env_sample_direct(const ctl_scene_desc* d, DRec& dRec, V2 sample) {
     float sinTheta = cr_sin(theta);
     V3 dir = v3(cr_sin(phi) * sinTheta, cr_cos(theta), -cr_cos(phi) * sinTheta);
     pdf /= omax(std::fabs(sinTheta), O_EPSILON);
+    dir = env_to_world(L, dir);   // d = m_worldTransform.TransformDirection(d) (Light.cu:355)
     dRec.pdf = pdf;
     dRec.p = v3(L.scene_center[0], L.scene_center[1], L.scene_center[2]) + dir * L.scene_radius;
     dRec.n = -normalize(dir);
@@ -666,13 +682,14 @@ Spec env_sample_direct(const ctl_scene_desc* d, DRec& dRec, V2 sample) {
 // InfiniteLight::pdfDirect + internalPdfDirection (Light.cu:367-377, 459-479)
 float env_pdf_direct(const ctl_scene_desc* d, const DRec& dRec) {
     const ctl_env_light& L = *d->env;
-    V2 uv = env_latlong(dRec.d);
+    const V3 ld = env_to_local(L, dRec.d);   // internalPdfDirection(TransformDirectionTranspose(dRec.d)) (Light.cu:369)
+    V2 uv = env_latlong(ld);
     float u = uv.x * L.size[0] - 0.5f, v = uv.y * L.size[1] - 0.5f;
     int xPos = (int)floorf(u), yPos = (int)floorf(v);
     Spec value1, value2;
     float pdf;
     env_rows(d, xPos, yPos, u - xPos, v - yPos, value1, value2, pdf);
-    float sinTheta = sqrtf(omax(0.0f, 1 - dRec.d.y * dRec.d.y));
+    float sinTheta = sqrtf(omax(0.0f, 1 - ld.y * ld.y));
     float pdfSA = pdf / omax(std::fabs(sinTheta), O_EPSILON);
     if (dRec.measure == ESolidAngle) return pdfSA;
     if (dRec.measure == EArea) return pdfSA * absdot(dRec.d, dRec.n) / (dRec.dist * dRec.dist);
@@ -683,14 +700,15 @@ Spec env_eval(const ctl_scene_desc* d, V3 dir) {
     if (d->env_map_index == UINT_MAX) return v3s(0.0f);
     const ctl_env_light& L = *d->env;
     c5::Mip M{d->textures + L.texture, d->tex_data};
-    return c5::triangle(M, 0, env_latlong(dir)) * v3(L.scale[0], L.scale[1], L.scale[2]);
+    return c5::triangle(M, 0, env_latlong(env_to_local(L, dir))) * v3(L.scale[0], L.scale[1], L.scale[2]);
 }
 // EvalEnvironment(r, rX, rY): the MIP map filtered over the differentials (Light.cu:496-511)
-Spec env_eval_diff(const ctl_scene_desc* d, V3 v, V3 vx, V3 vy) {
+Spec env_eval_diff(const ctl_scene_desc* d, V3 rd, V3 rxd, V3 ryd) {
     if (d->env_map_index == UINT_MAX) return v3s(0.0f);
     const ctl_env_light& L = *d->env;
+    const V3 v = env_to_local(L, rd);
     V2 uv = env_latlong(v);
-    V3 dvdx = vx - v, dvdy = vy - v;
+    V3 dvdx = env_to_local(L, rxd) - v, dvdy = env_to_local(L, ryd) - v;
     float t1 = O_INV_TWOPI / (v.x * v.x + v.z * v.z), t2 = -O_INV_PI / omax(sqrtf(omax(0.0f, 1.0f - v.y * v.y)), 1e-4f);
     V2 dudx = v2(t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y), dudy = v2(t1 * (dvdy.z * v.x - dvdy.x * v.z), t2 * dvdy.y);
     c5::Mip M{d->textures + L.texture, d->tex_data};

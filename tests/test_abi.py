@@ -43,7 +43,7 @@ def test_reference_layout_sizes():
     assert C.sizeof(abi.Texture) == 380       # ImageTexture + KernelMIPMap
     assert C.sizeof(abi.PixelVariance) == 44  # PixelVarianceInfo
     assert C.sizeof(abi.Light) == 48          # flattened DiffuseLight / InfiniteLight header
-    assert C.sizeof(abi.EnvLight) == 72       # InfiniteLight
+    assert C.sizeof(abi.EnvLight) == 112      # InfiniteLight (+ m_worldTransform rotation)
 
 
 # ctypes mirror <-> include/ctl_trace.h: every field offset and struct size as

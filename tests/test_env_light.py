@@ -33,7 +33,19 @@ def env_image(w=32, h=16, seed=5):
             (np.clip(b, 0, 255).astype(np.uint32) << 16) | (255 << 24)).astype(np.uint32)
 
 
-def env_scene(ctl, textured=False, w=64, h=48, env_filter=None, with_area_light=True, scale=(2.0, 1.8, 1.6)):
+def rotation(axis, angle):
+    a = np.asarray(axis, np.float64)
+    a /= np.linalg.norm(a)
+    c, s = np.cos(angle), np.sin(angle)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    return (np.eye(3) * c + s * K + (1 - c) * np.outer(a, a)).astype(np.float32)
+
+
+ROT = rotation((0.3, 1.0, -0.2), 1.1)   # m_worldTransform of the rotated-map cases
+
+
+def env_scene(ctl, textured=False, w=64, h=48, env_filter=None, with_area_light=True, scale=(2.0, 1.8, 1.6),
+              rot=None):
     """An open scene: ground plane, two boxes (one rough glass or textured when
     `textured`), an area light; the camera sees the sky above the horizon."""
     s = ctl.HostScene()
@@ -73,6 +85,8 @@ def env_scene(ctl, textured=False, w=64, h=48, env_filter=None, with_area_light=
     if with_area_light:
         s.add_area_light(node, 2, (12.0, 12.0, 12.0))
     s.set_environment(env_tex, scale)
+    if rot is not None:
+        s.set_environment_transform(rot)
     s.set_camera((0.5, 1.6, -6.0), (0.0, 1.2, 0.0), (0, 1, 0), 60.0, w, h)
     return s, s.compile()
 
@@ -161,6 +175,39 @@ def test_env_sampling_is_a_normalized_density(ctl, orc):
     assert sun.mean() > 2 * (16 / (32 * 16))
 
 
+def test_env_world_transform_rotates_the_map(ctl, orc):
+    """m_worldTransform (Light.h:307; TransformDirection / TransformDirectionTranspose,
+    Light.cu:342-510): with rotation R the radiance and pdf seen along R v are
+    those of the identity map along v, and the sampled directions are R times
+    the identity's (up to fp32 rounding of the rotation)."""
+    s0, d0 = env_scene(ctl)
+    s1, d1 = env_scene(ctl, rot=ROT)
+    e0, e1 = d0.env.contents, d1.env.contents
+    assert np.array_equal(np.array(e0.world, np.float32), np.eye(3, dtype=np.float32))
+    assert np.array_equal(np.array(e1.world, np.float32), ROT)
+    rng = np.random.default_rng(3)
+    n = 50_000
+    v = rng.normal(size=(n, 3)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    rv = np.ascontiguousarray((v.astype(np.float64) @ ROT.T.astype(np.float64)).astype(np.float32))
+    o0 = np.zeros((n, 4), np.float32)
+    o1 = np.zeros((n, 4), np.float32)
+    orc.oracle_env_eval(C.byref(d0), n, oracle.ptr(np.ascontiguousarray(v)), oracle.ptr(o0))
+    orc.oracle_env_eval(C.byref(d1), n, oracle.ptr(rv), oracle.ptr(o1))
+    # away from the lat-long seam and the poles the lookups agree to rounding
+    keep = (np.abs(v[:, 0]) > 0.02) & (np.abs(v[:, 1]) < 0.98)
+    rel = np.abs(o1[keep] - o0[keep]) / np.maximum(np.abs(o0[keep]), 1e-6)
+    assert np.quantile(rel, 0.99) < 2e-2 and np.median(rel) < 1e-4
+    m = 5000
+    smp = rng.random((m, 2), dtype=np.float32)
+    s0o = np.zeros((m, 7), np.float32)
+    s1o = np.zeros((m, 7), np.float32)
+    orc.oracle_env_sample(C.byref(d0), m, oracle.ptr(smp), oracle.ptr(s0o))
+    orc.oracle_env_sample(C.byref(d1), m, oracle.ptr(smp), oracle.ptr(s1o))
+    assert np.allclose(s1o[:, :3], s0o[:, :3] @ ROT.T, atol=1e-5)
+    assert np.array_equal(s1o[:, 3:].view(np.uint32), s0o[:, 3:].view(np.uint32))   # pdf and value: local
+
+
 def test_set_environment_rejects_bad_texture(ctl):
     s = ctl.HostScene()
     v = np.array([(0, 0, 0), (1, 0, 0), (0, 1, 0)], np.float32)
@@ -228,6 +275,38 @@ def test_render_env_bit_exact(ctl, orc, dev, mode, direct, textured):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["persistent", "wavefront", "megakernel"])
+@pytest.mark.parametrize("direct", [1, 0])
+def test_render_env_rotated_bit_exact(ctl, orc, dev, mode, direct):
+    """A rotated environment map (InfiniteLight::m_worldTransform): sampleDirect
+    turns its directions into the world, pdfDirect and evalEnvironment turn the
+    world direction back (Light.cu:355, 369, 483)."""
+    w, h = 64, 48
+    _, d = env_scene(ctl, textured=True, w=w, h=h, rot=ROT)
+    flags = 0 if mode == "persistent" else getattr(ctl, MODES[mode])
+    p = ctl.PTParams(direct, 8, 3, 1, 64, 1, 0, flags)
+    want, wrays = oracle_render(orc, d, p, 2, w, h)
+    got, grays = render_gpu(ctl, d, p, 2, w, h, dev)
+    assert grays == wrays
+    bad = np.nonzero((want.view(np.uint32) != got.view(np.uint32)).any(axis=1))[0]
+    assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
+    _, d0 = env_scene(ctl, textured=True, w=w, h=h)
+    plain, _ = oracle_render(orc, d0, p, 2, w, h)
+    assert not np.array_equal(plain.view(np.uint32), want.view(np.uint32))   # the rotation shows
+
+
+@pytest.mark.gpu
+def test_upload_refuses_non_rotation_env_transform(ctl, dev):
+    s, d = env_scene(ctl, rot=np.diag([2.0, 1.0, 1.0]).astype(np.float32))
+    pt = ctl.PathTracer(0)
+    try:
+        with pytest.raises(ctl.CTLError, match="rotation"):
+            pt.upload_scene(d)
+    finally:
+        pt.close()
+
+
+@pytest.mark.gpu
 def test_render_env_only_light(ctl, orc, dev):
     """The environment as the only emitter (light CDF = [1]): every NEE sample
     goes to the map."""
@@ -243,12 +322,13 @@ def test_render_env_only_light(ctl, orc, dev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("direct", [1, 0])
-def test_wpt_env_bit_exact(ctl, orc, dev, direct):
+@pytest.mark.parametrize("rotated", [False, True])
+def test_wpt_env_bit_exact(ctl, orc, dev, direct, rotated):
     """WavefrontPathTracer (WavefrontPathTracer.cu:51-157) with the environment:
     sampleEmitterDirect over both lights, the escaped-ray term with its
     pathDepth / prev_normal MIS."""
     w, h = 64, 48
-    _, d = env_scene(ctl, textured=True, w=w, h=h)
+    _, d = env_scene(ctl, textured=True, w=w, h=h, rot=ROT if rotated else None)
     wt = ctl.WavefrontPathTracer(0, direct=direct, max_path_length=8, rr_start_depth=3)
     try:
         wt.upload_scene(d)
@@ -271,11 +351,12 @@ def test_wpt_env_bit_exact(ctl, orc, dev, direct):
 @pytest.mark.gpu
 @pytest.mark.parametrize("env_filter", ["CTL_TEX_BILINEAR", "CTL_TEX_TRILINEAR", "CTL_TEX_EWA"])
 @pytest.mark.parametrize("mode", ["first_f_direct", "uv"])
-def test_prim_env_bit_exact(ctl, orc, dev, env_filter, mode):
+@pytest.mark.parametrize("rotated", [False, True])
+def test_prim_env_bit_exact(ctl, orc, dev, env_filter, mode, rotated):
     """PrimTracer misses: EvalEnvironment(r, rX, rY), the map filtered over the
     primary ray differentials' footprint; first_f_direct also samples the
     environment for its UniformSampleOneLight."""
-    _, d = env_scene(ctl, w=64, h=48, env_filter=getattr(ctl._abi, env_filter))
+    _, d = env_scene(ctl, w=64, h=48, env_filter=getattr(ctl._abi, env_filter), rot=ROT if rotated else None)
     mi = ctl._abi.PRIM_DRAW_MODES.index(mode)
     pt = ctl.PrimTracer(0, draw_mode=mi)
     try:

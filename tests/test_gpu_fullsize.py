@@ -4,6 +4,9 @@ the scratch part of the lane stack), 1920x1080.  One PathTracer pass on the
 GPU, the same pass by the oracle over the whole image: every pixel's
 PixelData bit-exact, the traversed-ray count equal, no stack overflow
 (ctl_sync), the scene's worst-case stack within the device stack."""
+import ctypes as C
+import time
+
 import numpy as np
 import pytest
 
@@ -99,6 +102,107 @@ def test_full_size_c3_batched_passes_equal_sequential(ctl, dev, c3):
         assert torch.equal(seq.view(torch.int32), bat.view(torch.int32))
     finally:
         pt.close()
+
+
+def test_full_size_c3_reference_dopass_loop(ctl, dev, c3):
+    """The reference's pass loop as a drop-in would drive it: Tracer::DoPass calls
+    UpdateKernel, then renders (Kernel/Tracer.h:209-248).  The first of ten
+    rounds uploads the scene (ctl_scene_upload); rounds 2..10 call
+    ctl_scene_update on the unchanged desc, which must take under 1 ms each (no
+    copy, no device sync) and leave the image of ten plain passes."""
+    _, d = c3
+    pt = ctl.PathTracer(0)
+    try:
+        fb = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
+        up = []
+        pt.reset_rays()
+        for k in range(10):
+            t0 = time.perf_counter()
+            if k == 0:
+                pt.upload_scene(d)
+            else:
+                pt.update_scene(d, 0)
+            up.append(time.perf_counter() - t0)
+            pt.do_pass(fb.data_ptr(), 40 + k)
+        pt.sync()
+        loop_rays = pt.rays_traced()
+        ref = torch.zeros_like(fb)
+        pt.reset_rays()
+        pt.render_passes(ref.data_ptr(), 40, 10)
+        pt.sync()
+        assert pt.rays_traced() == loop_rays
+        assert torch.equal(fb.view(torch.int32), ref.view(torch.int32))
+    finally:
+        pt.close()
+    assert up[0] > 0.1                       # the upload copies ~3.5 GB and collapses the trees
+    assert max(up[1:]) < 1e-3, up
+
+
+def test_full_size_c4_eight_rank_shards(ctl, orc, dev, c3):
+    """BASELINE configs[3] (C4) on one GPU: the 10M-triangle C3 scene at 1080p
+    sharded over 8 ranks (tile % 8 == rank, IBlockSampler.h:100-108), each
+    rank's 8 passes in one ctl_render_passes launch (the bench's N = 8 step).
+    The 8 rank framebuffers sum bit for bit to the 1-rank framebuffer of the same
+    passes (every pixel has one owner, Image.cu:22-44 adds in the 1-GPU order);
+    rank 0's framebuffer equals the oracle's rank-0 render on every 97th pixel;
+    the ranks' rays add up to the 1-rank count plus the few apron paths a rank
+    traces for its neighbours; no stack overflow (ctl_sync)."""
+    _, d = c3
+    N, first = 8, 64
+    pt = ctl.PathTracer(0)
+    try:
+        pt.upload_scene(d)
+        fbs, rays = [], []
+        for r in range(N):
+            pt.params = ctl.PTParams(1, 50, 5, 1, 64, N, r, 0)
+            fb = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
+            pt.reset_rays()
+            pt.render_passes(fb.data_ptr(), first, N)
+            pt.sync()
+            rays.append(pt.rays_traced())
+            fbs.append(fb)
+        total = fbs[0].clone()
+        for fb in fbs[1:]:
+            total += fb
+        pt.params = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
+        one = torch.zeros_like(total)
+        pt.reset_rays()
+        pt.render_passes(one.data_ptr(), first, N)
+        pt.sync()
+        one_rays = pt.rays_traced()
+        assert torch.equal(total.view(torch.int32), one.view(torch.int32))
+        # each pixel is written by exactly one rank
+        nz = torch.stack([(fb[:, 6] > 0) for fb in fbs]).sum(0)
+        assert int(nz.max()) == 1 and float((nz == 1).float().mean()) > 0.999
+        rank0 = fbs[0].cpu().numpy()
+    finally:
+        pt.close()
+    assert one_rays <= sum(rays) <= one_rays * 1.001, (one_rays, sum(rays))
+    # rank 0 against the oracle's rank mode, every 97th pixel (sources), on the
+    # pixels that received exactly their own sample in every pass
+    import oracle
+    from helpers import jitter_landing
+    want = np.zeros((W * H, 7), np.float32)
+    p0 = ctl.PTParams(1, 50, 5, 1, 64, N, 0, 0)
+    for p in range(first, first + N):
+        orc.oracle_render_pass(C.byref(d), C.byref(p0), p, oracle.ptr(want), 1, ORACLE_THREADS, 97, None)
+    lin = np.arange(W * H)
+    ok = lin % 97 == 0
+    for p in range(first, first + N):
+        lx, ly = jitter_landing(orc, p, W, H)
+        self_land = (lx == lin % W) & (ly == lin // W)
+        ok &= self_land
+        # no neighbour's sample lands on a checked pixel
+        for dx, dy in ((1, 0), (0, 1), (1, 1)):
+            src = lin - dx - dy * W
+            valid = (src >= 0) & (lin % W >= dx)
+            s = np.clip(src, 0, W * H - 1)
+            ok &= ~(valid & (lx[s] == lin % W) & (ly[s] == lin // W))
+    tiles_x = -(-W // 64)
+    owned = (((lin // W) // 64) * tiles_x + (lin % W) // 64) % N == 0
+    ok &= owned
+    assert ok.sum() > 2000
+    assert np.array_equal(rank0[ok].view(np.uint32), want[ok].view(np.uint32))
 
 
 def test_full_size_c5_pass_bit_exact(ctl, orc, dev, c3):
