@@ -602,6 +602,7 @@ def main(argv=None):
     step_ms = ev0.elapsed_time(ev1)
     kernel_ms = sum(e0.elapsed_time(e1) for e0, e1 in kev)
     pt.sync(sptr)   # raises if any traversal of the timed region overflowed its stack
+    wsum = float(image[:, 6].sum().item()) if rank == 0 else 0.0   # the timed passes' image (before the legs)
 
     rays = pt.rays_traced()
     prof = pmc_profile()
@@ -640,8 +641,6 @@ def main(argv=None):
 
     if rank == 0:
         passes = a.steps * shards
-        img = image.view(H, W, 7)
-        wsum = float(img[..., 6].sum().item())
         launches = len(kev)   # path-kernel launches on this rank in the timed region
         per_launch_ms = kernel_ms / launches
         passes_per_launch = passes / launches   # this rank's passes (tiles of them when sharded) per launch
