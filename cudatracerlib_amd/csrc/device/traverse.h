@@ -506,7 +506,10 @@ struct Traverser {
             const uint32_t nyw = negy ? why : wly, fyw = negy ? wly : why;
             const uint32_t nzw = negz ? whz : wlz, fzw = negz ? wlz : whz;
 #define CTL_QB(W, K) ((float)(((W) >> (8 * (K))) & 0xffu))
-#define CTL_QPAIR(W, P, SC, K0, K1) (v2f{(P), (P)} + v2f{CTL_QB(W, K0), CTL_QB(W, K1)} * v2f{(SC), (SC)})
+            // p + q * s in one fused op: q * s is exact (q < 256, s a power of two), so the
+            // fused result is the encoder's p + q * s (mul, then add) bit for bit
+#define CTL_QPAIR(W, P, SC, K0, K1) \
+    __builtin_elementwise_fma(v2f{CTL_QB(W, K0), CTL_QB(W, K1)}, v2f{(SC), (SC)}, v2f{(P), (P)})
             const v2f nx01 = CTL_QPAIR(nxw, qa.x, qa.w, 0, 1) * ix - ox, nx23 = CTL_QPAIR(nxw, qa.x, qa.w, 2, 3) * ix - ox;
             const v2f fx01 = CTL_QPAIR(fxw, qa.x, qa.w, 0, 1) * ix - ox, fx23 = CTL_QPAIR(fxw, qa.x, qa.w, 2, 3) * ix - ox;
             const v2f ny01 = CTL_QPAIR(nyw, qa.y, qb.x, 0, 1) * iy - oy, ny23 = CTL_QPAIR(nyw, qa.y, qb.x, 2, 3) * iy - oy;

@@ -13,8 +13,10 @@
  *   --------------------------------------------------- --------------------------------
  *   InitializeKernel / DeinitializeKernel               ctl_create / ctl_destroy
  *     Kernel/TraceHelper.h:41-42, TraceHelper.cu:253-272
- *   UpdateKernel(DynamicScene*, ISamplingSeq...&)       ctl_scene_upload + ctl_sampler_generate
- *     Kernel/TraceHelper.h:44, TraceHelper.cu:182-217
+ *   UpdateKernel(DynamicScene*, ISamplingSeq...&)       ctl_scene_update + ctl_sampler_generate
+ *     Kernel/TraceHelper.h:44, TraceHelper.cu:182-217     (first call / full replace: ctl_scene_upload)
+ *   DynamicScene::UpdateScene (DynamicScene.cpp:480-554) ctl_scene_update's dirty groups
+ *   DynamicScene::SetNodeTransform (:433-443)           ctl_scene_set_transform
  *   __internal__IntersectBuffers(N, rays, res, skip, any_hit)
  *     Kernel/TraceHelper.h:71, TraceHelper.cu:736-746  ctl_intersect
  *   PathTracer::RenderBlock / pathKernel2 per pass      ctl_render_pass
