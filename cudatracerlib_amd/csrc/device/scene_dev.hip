@@ -282,7 +282,12 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
                 mesh_bin = std::max(mesh_bin, binary_stack_bound(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, kStackMax));
                 if (!wide) continue;
                 c->h_wbase[m] = (uint32_t)wn.size();
-                collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn, want_src ? &ms : nullptr);
+                // the mesh's entries: [bvh_indices_offset, the next mesh's) -- leaf children carry counts
+                const uint64_t e0 = d->meshes[m].bvh_indices_offset;
+                const uint64_t e1 = m + 1 < d->n_meshes ? d->meshes[m + 1].bvh_indices_offset : d->n_tri_indices;
+                if (e0 > d->n_tri_indices || e1 < e0 || e1 > d->n_tri_indices) throw std::runtime_error("mesh entry range out of range");
+                collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn, want_src ? &ms : nullptr,
+                              d->tri_indices + e0, (size_t)(e1 - e0));
                 if (want_src) wsrc.insert(wsrc.end(), ms.begin(), ms.end());
                 mesh_wide = std::max(mesh_wide, wide_stack_bound(wn.data() + c->h_wbase[m], wn.size() - c->h_wbase[m], 0, kStackMax));
             }

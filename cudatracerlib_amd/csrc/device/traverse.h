@@ -309,6 +309,83 @@ struct Traverser {
         }
     }
 
+    // One Woop test of a counted leaf's entry (t, u, v exactly as leaf_tris);
+    // the entry's TriIntersectorData2 word, only needed for the triangle index,
+    // is loaded once the entry passes the geometric test (a candidate hit).
+    __device__ __forceinline__ bool test_entry(const DevScene& S, float4 v00, float4 v11, float4 v22, uint32_t entry,
+                                               uint32_t index, TraceStats* stats) {
+        CTL_PROF_COUNT(stats, leaf_lanes, leaf_waves);
+        if (STATS) stats->tris++;
+        float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
+        float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
+        float t = Oz * invDz;
+        if (t > tri_tmin && (t < h.t || (S.tie_min && t == h.t && h.tri != 0xffffffffu))) {
+            float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
+            float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
+            float u = Ox + t * Dx;
+            if (u >= 0.0f) {
+                float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
+                float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
+                float v = Oy + t * Dy;
+                if (v >= 0.0f && u + v <= 1.0f) {
+#ifdef CTL_LEAF_IDX_LAZY
+                    const uint32_t gtri = (S.tri_idx[idxBase + entry] >> 1) + triOffset;
+#else
+                    (void)entry;
+                    const uint32_t gtri = (index >> 1) + triOffset;
+#endif
+                    if ((t < h.t || gtri < h.tri || (gtri == h.tri && instIdx < h.node)) &&
+                        (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v))) {
+                        h.node = instIdx;
+                        h.tri = gtri;
+                        h.u = u;
+                        h.v = v;
+                        h.t = t;
+                        if (ANY == 1 || (ANY == 2 && anyhit)) { done = true; return true; }
+                    }
+                }
+            }
+        }
+        return false;
+    }
+
+    // A leaf child of a 4-wide mesh tree carries its entry count
+    // (host/bvh_wide.h: ~((first << 3) | count), count 1..7, 0 = 8 or more):
+    // the entries' Woop records are loaded two at a time up front, with no
+    // look-ahead past the leaf and no TriIntersectorData2 load per test.  The
+    // entries are tested in the reference's order; a long leaf walks its
+    // last-in-leaf flags as leaf_tris does.
+    __device__ __forceinline__ void leaf_counted(const DevScene& S, TraceStats* stats) {
+        const uint32_t code = (uint32_t)(~leafAddr);
+        const uint32_t first = code >> 3, cnt = code & 7u;
+        if (first == 214783647u) return;   // the reference's -214783648 leaf value (BVHTraversal.h:109,221)
+        if (cnt == 0) {
+            leafAddr = ~(int)first;
+            leaf_tris(S, stats);
+            return;
+        }
+        const float4* tv = S.woop + triBase + first * 3u;
+        const uint32_t* ti = S.tri_idx + idxBase + first;
+        for (uint32_t i = 0; i < cnt; i += 2) {
+            const float4 a0 = tv[3 * i], a1 = tv[3 * i + 1], a2 = tv[3 * i + 2];
+#ifdef CTL_LEAF_IDX_LAZY
+            const uint32_t ia = 0, ib = 0;
+#else
+            const uint32_t ia = ti[i];
+            uint32_t ib = ia;
+#endif
+            float4 b0 = a0, b1 = a1, b2 = a2;
+            if (i + 1 < cnt) {
+                b0 = tv[3 * i + 3]; b1 = tv[3 * i + 4]; b2 = tv[3 * i + 5];
+#ifndef CTL_LEAF_IDX_LAZY
+                ib = ti[i + 1];
+#endif
+            }
+            if (test_entry(S, a0, a1, a2, first + i, ia, stats)) return;
+            if (i + 1 < cnt && test_entry(S, b0, b1, b2, first + i + 1, ib, stats)) return;
+        }
+    }
+
     // Sort the hit children near-first (5-comparator network on the entry
     // distances; misses carry 0x7fffffff and sort last), take the nearest,
     // push the others far-to-near, postpone a leaf.  Shared by the float and
@@ -607,7 +684,10 @@ struct Traverser {
 #endif
         while (leafAddr < 0) {
             if (SINGLE || level == 1) {
-                if (leafAddr != -214783648) {
+                if (WIDE) {
+                    leaf_counted(S, stats);
+                    if (done) return;
+                } else if (leafAddr != -214783648) {
                     leaf_tris(S, stats);
                     if (done) return;
                 }

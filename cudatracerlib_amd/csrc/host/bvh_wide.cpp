@@ -41,6 +41,19 @@ struct Collapser {
     std::vector<WideNode>& out;
     size_t base;
     std::vector<uint32_t>* src;
+    const ctl_tri_index* idx;   // counted leaves (mesh trees), or null
+    size_t n_idx;
+
+    // a leaf value as the wide node stores it (bvh_wide.h: wide_leaf_code)
+    int32_t leaf_value(int32_t v) const {
+        if (!idx || v == kSentinel || v >= 0) return v;
+        const uint32_t first = (uint32_t)~v;
+        if (first >= kWideLeafMaxEntry || first >= n_idx) throw std::runtime_error("wide BVH: leaf entry out of range");
+        uint32_t cnt = 1;
+        for (size_t e = first; e < n_idx && !(idx[e] & 1u) && cnt < 8; e++) cnt++;
+        if (cnt < 8 && first + cnt > n_idx) throw std::runtime_error("wide BVH: leaf runs past the entries");
+        return wide_leaf_code(first, cnt);
+    }
 
     const ctl_bvh_node& node_of(int32_t v) const {
         size_t i = (size_t)v / 4;
@@ -165,7 +178,7 @@ struct Collapser {
         int32_t child[4];
         for (int i = 0; i < 4; i++) {
             if (i >= nk) { child[i] = kSentinel; continue; }
-            child[i] = is_inner(k[i].v) ? emit(k[i].v, depth + 1) : k[i].v;
+            child[i] = is_inner(k[i].v) ? emit(k[i].v, depth + 1) : leaf_value(k[i].v);
         }
         WideNode& w = out[me];
         // empty slots and sentinel children (the right child of a single-leaf
@@ -186,10 +199,10 @@ struct Collapser {
 }  // namespace
 
 int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out,
-                      std::vector<uint32_t>* src) {
+                      std::vector<uint32_t>* src, const ctl_tri_index* idx, size_t n_idx) {
     if (!is_inner(root_value) || n_nodes == 0) throw std::runtime_error("wide BVH: root is not an inner node");
     if (src) src->clear();
-    Collapser c{nodes, n_nodes, out, out.size(), src, {}, {}, {}};
+    Collapser c{nodes, n_nodes, out, out.size(), src, idx, n_idx, {}, {}, {}};
     c.plan(root_value);
     return c.emit(root_value, 0);
 }

@@ -41,8 +41,21 @@ static_assert(sizeof(WideNode) == 128, "wide node is 128 B");
 // child slot the slot's box was taken from (0xFFFFFFFF for empty / sentinel slots),
 // indexed like the appended nodes — what a refit of the binary tree needs to
 // refresh the wide boxes with one gather.
+// idx (optional, mesh trees): the tree's TriIntersectorData2 entries (n_idx of
+// them, indexed by the leaf values).  With it, every leaf child carries its
+// entry count: child = ~((first_entry << 3) | count) with count 1..7, or 0 for
+// a leaf of 8 or more entries (the traversal then walks the last-in-leaf
+// flags, as the reference does); see wide_leaf_code.  Without it (the
+// instance tree) leaf children stay ~first value.
 int32_t collapse_wide(const ctl_bvh_node* nodes, size_t n_nodes, int32_t root_value, std::vector<WideNode>& out,
-                      std::vector<uint32_t>* src = nullptr);
+                      std::vector<uint32_t>* src = nullptr, const ctl_tri_index* idx = nullptr, size_t n_idx = 0);
+
+// Leaf child of a counted mesh tree: ~((first << 3) | count), count 1..7 or 0 (>= 8).
+// Entries are < 2^28 (the upload refuses larger meshes in this mode).
+inline int32_t wide_leaf_code(uint32_t first, uint32_t count) {
+    return ~(int32_t)((first << 3) | (count <= 7 ? count : 0u));
+}
+constexpr uint32_t kWideLeafMaxEntry = 1u << 28;
 
 // Worst-case traversal stack of a tree (entries, the bottom sentinel
 // included) for the traversal in device/traverse.h: a node pushes every
