@@ -36,16 +36,25 @@ CTL_HD float copysign_ref(float a, float b) {                            // Math
 }
 CTL_HD float fracf_ref(float f) { return f - floorf(f); }                 // MathFunc.h:138-141
 
-CTL_HD float cr_sin(float x) { return (float)sin((double)x); }
-CTL_HD float cr_cos(float x) { return (float)cos((double)x); }
-CTL_HD float cr_tan(float x) { return (float)tan((double)x); }
-CTL_HD float cr_acos(float x) { return (float)acos((double)x); }
-CTL_HD float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
-CTL_HD float cr_atan(float x) { return (float)atan((double)x); }
-CTL_HD float cr_exp(float x) { return (float)exp((double)x); }
-CTL_HD float cr_log(float x) { return (float)log((double)x); }
-CTL_HD float cr_log2(float x) { return (float)log2((double)x); }
-CTL_HD float cr_pow(float a, float b) { return (float)pow((double)a, (double)b); }
+// On the device the fp64 library bodies are large (range reduction, ~30-60
+// fp64 ops and their register pairs); each one stays out of line so a caller's
+// register peak does not include them (rough_sample: 148 -> 69 VGPRs, which is
+// what lets the C5 path kernel run at 4 waves/SIMD).  -DCTL_CR_INLINE inlines them.
+#if defined(__HIP__) && !defined(CTL_CR_INLINE)
+#define CTL_CR static __host__ __device__ __noinline__
+#else
+#define CTL_CR CTL_HD
+#endif
+CTL_CR float cr_sin(float x) { return (float)sin((double)x); }
+CTL_CR float cr_cos(float x) { return (float)cos((double)x); }
+CTL_CR float cr_tan(float x) { return (float)tan((double)x); }
+CTL_CR float cr_acos(float x) { return (float)acos((double)x); }
+CTL_CR float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+CTL_CR float cr_atan(float x) { return (float)atan((double)x); }
+CTL_CR float cr_exp(float x) { return (float)exp((double)x); }
+CTL_CR float cr_log(float x) { return (float)log((double)x); }
+CTL_CR float cr_log2(float x) { return (float)log2((double)x); }
+CTL_CR float cr_pow(float a, float b) { return (float)pow((double)a, (double)b); }
 
 struct f2 { float x, y; };
 struct f3 { float x, y, z; };

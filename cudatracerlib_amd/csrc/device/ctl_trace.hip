@@ -48,7 +48,8 @@ static_assert(sizeof(ctl_texture) == 380, "ctl_texture is 380 B");
 static_assert(sizeof(ctl_pixel_variance) == 44, "PixelVarianceInfo is 44 B");
 
 #ifndef CTL_PERSIST_WAVES_FULL
-#define CTL_PERSIST_WAVES_FULL 3   // ... with the C5 shading (out-of-line texture / microfacet calls)
+#define CTL_PERSIST_WAVES_FULL 4   // ... with the C5 shading (out-of-line texture / microfacet / fp64 math
+                                   // calls; path state parked in LDS): C5 3 waves 1480, 4 waves 1658 Mrays/s
 #endif
 #ifndef CTL_PERSIST_WAVES
 #define CTL_PERSIST_WAVES 4   // waves/SIMD for the persistent path kernel, measured on C3 with the packed
@@ -57,8 +58,59 @@ static_assert(sizeof(ctl_pixel_variance) == 44, "PixelVarianceInfo is 44 B");
 
 namespace {
 
-// dynamic LDS of path_kernel_persistent: lane stacks + the work item word per lane
-constexpr size_t persistent_lds_bytes() { return kStackLdsBytes + sizeof(int) * kStackBlock; }
+// Path state of path_kernel_persistent parked in LDS while the lane's ray is
+// traced: everything the shading needs and the traversal does not (throughput,
+// radiance, last normal, wo, pixel position, BSDF pdf, depth and specular flag,
+// the pending shadow ray's contribution, the sampler's sequence offsets and
+// draw counters) -- 23 words per lane in [word][thread] layout (conflict-free
+// ds_read/ds_write_b32).  Only the ray (origin, both directions, shadow
+// distance) and a few flags stay in VGPRs across the traversal loop, so the
+// traversal's register peak no longer stacks on top of the shading state.
+// 16 KB stacks + 1 KB work words + 23 KB parked state = 40 KB per 256-thread
+// block: 4 blocks per CU, i.e. the 4 waves/SIMD the VGPR budget targets.
+// Lean kernel VGPR spills 36 -> 11; C3 2983 -> 3219 Mrays/s (same box, -DCTL_PARK=0 A/B).
+#ifndef CTL_PARK
+#define CTL_PARK 1
+#endif
+constexpr int kParkWords = CTL_PARK ? 23 : 0;
+struct Park {
+    int tid;
+    __device__ __forceinline__ void put(int w, float x) const {
+        ctl_lds_stack[kExtraLdsOff + w * kStackBlock + tid] = __float_as_int(x);
+    }
+    __device__ __forceinline__ void puti(int w, uint32_t x) const {
+        ctl_lds_stack[kExtraLdsOff + w * kStackBlock + tid] = (int)x;
+    }
+    __device__ __forceinline__ float get(int w) const {
+        return __int_as_float(ctl_lds_stack[kExtraLdsOff + w * kStackBlock + tid]);
+    }
+    __device__ __forceinline__ uint32_t geti(int w) const {
+        return (uint32_t)ctl_lds_stack[kExtraLdsOff + w * kStackBlock + tid];
+    }
+    __device__ __forceinline__ void put3(int w, f3 x) const { put(w, x.x); put(w + 1, x.y); put(w + 2, x.z); }
+    __device__ __forceinline__ f3 get3(int w) const { return mk3(get(w), get(w + 1), get(w + 2)); }
+    __device__ __forceinline__ void store(const PathVars& v, const ShadowReq& sh, const SamplerDev& rng) const {
+        put3(0, v.cl); put3(3, v.cf); put3(6, v.last_nor); put3(9, v.wo);
+        put(12, v.pX.x); put(13, v.pX.y); put(14, v.brdf_pdf);
+        puti(15, ((uint32_t)v.depth << 1) | (v.specular ? 1u : 0u));
+        put3(16, sh.add);
+        puti(19, rng.a); puti(20, rng.b); puti(21, rng.d1); puti(22, rng.d2);
+    }
+    __device__ __forceinline__ void load(PathVars& v, ShadowReq& sh, SamplerDev& rng) const {
+        v.cl = get3(0); v.cf = get3(3); v.last_nor = get3(6); v.wo = get3(9);
+        v.pX.x = get(12); v.pX.y = get(13); v.brdf_pdf = get(14);
+        const uint32_t ds = geti(15);
+        v.depth = (int)(ds >> 1); v.specular = (ds & 1u) != 0;
+        sh.add = get3(16);
+        rng.a = geti(19); rng.b = geti(20); rng.d1 = geti(21); rng.d2 = geti(22);
+    }
+};
+
+// dynamic LDS of path_kernel_persistent: lane stacks + the work item word per
+// lane + the parked path state
+constexpr size_t persistent_lds_bytes() {
+    return kStackLdsBytes + sizeof(int) * kStackBlock * (1 + kParkWords);
+}
 
 // Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
 // traversals inline in the bounce, as the reference's pathKernel2 runs it.
@@ -226,6 +278,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
     // work item of the lane's path (pass slot * PS.per_pass + item), parked in
     // LDS for the path's lifetime instead of holding a VGPR through the traces
     int* pkw = ctl_lds_stack + kPathWordOff + threadIdx.x;
+    const Park park{(int)threadIdx.x};
     // k -> (pass slot, item of the pass): a few subtractions (slots <= passes per launch)
     auto split = [&](uint32_t k, uint32_t& ps, uint32_t& kk) {
         ps = 0; kk = k;
@@ -276,6 +329,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                         if (!apron_keep(P, kk, pX)) PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                         else if (v.depth++ < P.max_path_length) active = true;
                         else store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
+                        if (CTL_PARK && active) park.store(v, sh, rng);
                     } else {
                         PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // work item outside the image: no sample
                     }
@@ -305,6 +359,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
 #ifdef CTL_PROFILE_TRACE
             prof_trace += wall_clock64() - pc0;
 #endif
+            if (CTL_PARK) park.load(v, sh, rng);
             bool cont;
             if (shadowPhase) {
                 if (!shadow_occluded(S, shadowAny, h, sh.dist)) v.cl = v.cl + sh.add;
@@ -324,6 +379,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                 work_pixel(P, kk, px, py);
                 store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
                 active = false;
+            } else if (CTL_PARK) {
+                park.store(v, sh, rng);
             }
         }
     }
