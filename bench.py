@@ -84,6 +84,8 @@ def parse(argv=None):
     ap.add_argument("--dopass-leg", type=int, default=8,
                     help="passes of the reference DoPass leg (ctl_scene_update + sampler tables + one "
                          "ctl_render_pass per pass; 0: skip)")
+    ap.add_argument("--c5-passes", type=int, default=16,
+                    help="C5 (textured scene, full-shading kernel) leg passes (0: skip; skipped when --config 5)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal: the ranks join the process group and count themselves; no GPU, "
                          "no scene (tests/test_bench_launch.py)")
@@ -439,6 +441,49 @@ def c1_prim_leg(ctl, dev, torch, passes):
             "note": "plumbing config: 65 k rays per pass, launch-latency bound"}
 
 
+def c5_leg(ctl, dev, torch, stream, sptr, a, threads):
+    """BASELINE configs[4] (C5, the textured / rough-material scene) on its own
+    context: the full-shading path kernel (path_kernel_persistent FULL=1) at the
+    headline's resolution, path length and launch shape.  One untimed launch,
+    then --c5-passes passes in launches of --steps-per-launch, bracketed with
+    HIP events on the launch stream."""
+    t0 = time.perf_counter()
+    hs = ctl.HostScene().generate(5, 1.0, a.width, a.height)
+    hs.set_bvh_builder(a.builder, a.sbvh_alpha)
+    d = hs.compile(threads=threads)
+    t_build = time.perf_counter() - t0
+    pt = ctl.PathTracer(dev.index or 0, max_path_length=a.max_path_length, rr_start_depth=a.rr_start,
+                        shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, schedule="persistent")
+    try:
+        pt.upload_scene(d)
+        fb = torch.zeros((a.width * a.height, 7), dtype=torch.float32, device=dev)
+        G = max(1, a.steps_per_launch)
+        pt.render_passes(fb.data_ptr(), 0, G, sptr)
+        torch.cuda.synchronize(dev)
+        pt.reset_rays(sptr)
+        ev = []
+        p = G
+        for g in launch_groups(a.c5_passes, G):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            pt.render_passes(fb.data_ptr(), p, g, sptr)
+            e1.record(stream)
+            ev.append((e0, e1))
+            p += g
+        torch.cuda.synchronize(dev)
+        pt.sync(sptr)
+        ms = sum(e0.elapsed_time(e1) for e0, e1 in ev)
+        rays = pt.rays_traced()
+    finally:
+        pt.close()
+    return {"workload": f"PathTracer C5 (BASELINE.json configs[4]): {d.n_tri_data} tris, {a.width}x{a.height}, "
+                        f"{a.c5_passes} spp, textured + rough materials (path_kernel_persistent FULL=1)",
+            "passes": a.c5_passes, "launches": len(ev), "ms_per_pass": round(ms / a.c5_passes, 3),
+            "rays_per_pass": int(rays / a.c5_passes), "mrays_s": round(rays / (ms * 1e-3) / 1e6, 2),
+            "scene_build_s": round(t_build, 1)}
+
+
 def launch_check(a, world, rank):
     """--launch-check: every rank joins the process group (gloo) and the ranks
     count themselves; rank 0 prints the line shape the bench prints, with
@@ -627,6 +672,12 @@ def main(argv=None):
         scratch = torch.zeros_like(fb)
         closest = closest_shadow_leg(pt, scratch, stream, sptr, torch, nxt + 10, a.closest_shadow_passes)
         del scratch
+    c5 = None
+    if rank == 0 and shards == 1 and a.c5_passes > 0 and a.config != 5:
+        try:   # a side leg, like C1: reported in the line, not fatal to the headline
+            c5 = c5_leg(ctl, dev, torch, stream, sptr, a, threads)
+        except Exception as e:
+            c5 = {"error": f"{type(e).__name__}: {e}"}
     red = dev if a.backend == "nccl" else torch.device("cpu")
     tt = torch.tensor([elapsed], dtype=torch.float64, device=red)
     rr = torch.tensor([rays, 1], dtype=torch.int64, device=red)   # rays, ranks that rendered
@@ -697,6 +748,7 @@ def main(argv=None):
             "closest_hit_shadows": closest,
             "wavefront_tracer": wpt,
             "prim_tracer_c1": c1,
+            "path_tracer_c5": c5,
             "image_weight_sum": wsum,
             "scene_build_s": round(t_build, 2),
         }

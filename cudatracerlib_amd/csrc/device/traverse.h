@@ -43,9 +43,34 @@ constexpr int kStackMax = 128;
 // lanes of the wave still look for a leaf (1 = the reference's rule: none;
 // C3 sweep: 1 -> 2098, 2 -> 2164, 4 -> 2225, 6 -> 2237, 8 -> 2216, 16 -> 2146 Mrays/s;
 // later, with the current kernel, 5 / 6 / 7 agree within run-to-run noise, ~2250).
+// CTL_LEAF_SPECULATE 0: a lane that holds a postponed leaf stops visiting
+// nodes until the leaf phase tests it, so every ray visits nodes and leaves in
+// the same order whatever the rest of its wave does.
+#ifndef CTL_LEAF_SPECULATE
+#define CTL_LEAF_SPECULATE 1
+#endif
 #ifndef CTL_LEAF_BREAK
 #define CTL_LEAF_BREAK 5
 #endif
+
+// Order-independent culling of the 4-wide traversal (the tie_min scenes): a
+// box is culled only when its entry lies more than kCullSlack ulps (~0.2 %)
+// beyond the closest hit so far.  Without the slack a box whose slab entry
+// rounds a few ulps past the Woop t of a triangle inside it is culled or
+// visited depending on which hits were found first -- and with leaves
+// postponed per wave, that order depends on the other rays of the wave, so a
+// handful of rays per 10^7 changed their hit from launch to launch.  With it,
+// the closest (t, triangle, node) is always tested, in any order: the result is
+// a function of the ray alone, the same as the oracle's binary-order
+// traversal under the same rule (oracle/oracle.cpp trace_two_level).
+#ifndef CTL_CULL_SLACK
+#define CTL_CULL_SLACK (1 << 14)
+#endif
+constexpr int kCullSlack = CTL_CULL_SLACK;
+__device__ __forceinline__ int cull_bits(float t) {
+    const int b = __float_as_int(t);
+    return b >= 0 ? min(b + kCullSlack, 0x7f800000) : b;
+}
 
 struct DevScene {
     const float4* bvh;          // mesh BVHNodeData, float4 units
@@ -477,14 +502,14 @@ struct Traverser {
         // opaque to the optimiser: otherwise it splits off + (16 - s) into two ops per load
         asm volatile("" : "+v"(onx), "+v"(ofx), "+v"(ony), "+v"(ofy), "+v"(onz), "+v"(ofz));
 #endif
-        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (CTL_LEAF_SPECULATE || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
             const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
             CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
             if (STATS) stats->nodes++;
-            const int tBits = __float_as_int(h.t);
+            const int tBits = cull_bits(h.t);
             int k0, k1, k2, k3;
 #ifndef CTL_WIDE_MINMAX
             const uint32_t off = (nodeBase + (uint32_t)nodeAddr) << 7;
@@ -562,14 +587,14 @@ struct Traverser {
         const int tminBits = __float_as_int(span_tmin);
         const bool negx = __float_as_int(cur.idx) < 0, negy = __float_as_int(cur.idy) < 0;
         const bool negz = __float_as_int(cur.idz) < 0;
-        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (CTL_LEAF_SPECULATE || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
             const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
             CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
             if (STATS) stats->nodes++;
-            const int tBits = __float_as_int(h.t);
+            const int tBits = cull_bits(h.t);
             const uint32_t off = (nodeBase + (uint32_t)nodeAddr) << 6;
             const float4 qa = *reinterpret_cast<const float4*>(nbytes + off);
             const float4 qb = *reinterpret_cast<const float4*>(nbytes + off + 16u);

@@ -85,9 +85,17 @@ struct Stats { uint64_t nodes = 0, tris = 0, inst = 0; };
 
 // TracerayTemplate, pointer overload (BVHTraversal.h:122-232).  spanTmin is 0
 // for traceRay and the ray's tmin for the batch kernel (TraceHelper.cu:469).
+// cullSlack > 0 (TIE_MIN_INDEX, the wide-BVH device rule): boxes are culled
+// against rayT plus that many ulps, so the closest hit is tested in any visit
+// order (device/traverse.h cull_bits); 0 keeps the reference's culling.
+constexpr int kCullSlack = 1 << 14;
+inline float cull_t(float t, int slack) {
+    const int b = as_int(t);
+    return b >= 0 ? as_float(std::min(b + slack, 0x7f800000)) : t;
+}
 template <class CLB>
 bool traceray_template(V3 ori, V3 dir, float& rayT, float spanTmin, const CLB& clb, const float* nodes4,
-                       int bvhNodesOffset, int startNode, Stats* st) {
+                       int bvhNodesOffset, int startNode, Stats* st, int cullSlack = 0) {
     if (startNode < 0) return clb(~startNode);
     bool found = false;
     // index 1 holds the sentinel; index 0 only absorbs the pop of an already
@@ -108,6 +116,7 @@ bool traceray_template(V3 ori, V3 dir, float& rayT, float spanTmin, const CLB& c
         while ((unsigned int)nodeAddr < (unsigned int)EntrypointSentinel) {
             const float* n = nodes4 + 4 * (size_t)(bvhNodesOffset + nodeAddr);
             if (st) st->nodes++;
+            const float tc = cull_t(rayT, cullSlack);
             int c0i, c1i;
             std::memcpy(&c0i, n + 12, 4);
             std::memcpy(&c1i, n + 13, 4);
@@ -120,13 +129,13 @@ bool traceray_template(V3 ori, V3 dir, float& rayT, float spanTmin, const CLB& c
             const float c1loz = n[10] * idirz - oodz;
             const float c1hiz = n[11] * idirz - oodz;
             const float c0min = spanBegin(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, spanTmin);
-            const float c0max = spanEnd(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, rayT);
+            const float c0max = spanEnd(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, tc);
             const float c1lox = n[4] * idirx - oodx;
             const float c1hix = n[5] * idirx - oodx;
             const float c1loy = n[6] * idiry - oody;
             const float c1hiy = n[7] * idiry - oody;
             const float c1min = spanBegin(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, spanTmin);
-            const float c1max = spanEnd(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, rayT);
+            const float c1max = spanEnd(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, tc);
             bool swp = (c1min < c0min);
             bool traverseChild0 = (c0max >= c0min);
             bool traverseChild1 = (c1max >= c1min);
@@ -191,6 +200,7 @@ bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float t
     const float* meshNodes = reinterpret_cast<const float*>(d->bvh_nodes);
     const float* tris = reinterpret_cast<const float*>(d->woop_tris);
     bool done = false;   // any-hit termination
+    const int slack = tie == TIE_MIN_INDEX ? kCullSlack : 0;
     auto instClb = [&](int nodeIdx) -> bool {
         if (done) return false;
         if (st) st->inst++;
@@ -236,9 +246,9 @@ bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float t
             }
             return found;
         };
-        return traceray_template(ol, dl, h.t, spanTmin, triClb, meshNodes, (int)mesh.bvh_node_offset, 0, st);
+        return traceray_template(ol, dl, h.t, spanTmin, triClb, meshNodes, (int)mesh.bvh_node_offset, 0, st, slack);
     };
-    return traceray_template(ori, dir, h.t, spanTmin, instClb, sceneNodes, 0, d->scene_start_node, st);
+    return traceray_template(ori, dir, h.t, spanTmin, instClb, sceneNodes, 0, d->scene_start_node, st, slack);
 }
 
 // traceRay(dir, ori, TraceResult*) (TraceHelper.cu:174-180) on an Init()'ed result
