@@ -42,7 +42,8 @@ constexpr int kStackMax = 128;
 // The wide inner-node loop hands over to the leaves once fewer than this many
 // lanes of the wave still look for a leaf (1 = the reference's rule: none;
 // C3 sweep: 1 -> 2098, 2 -> 2164, 4 -> 2225, 6 -> 2237, 8 -> 2216, 16 -> 2146 Mrays/s;
-// later, with the current kernel, 5 / 6 / 7 agree within run-to-run noise, ~2250).
+// later, with the current kernel, 5 / 6 / 7 agree within run-to-run noise, ~2250;
+// round 3 with the LDS-parked path state: 3 / 4 / 5 / 7 -> 3185 / 3187 / 3170 / 3151).
 // CTL_LEAF_SPECULATE 0: a lane that holds a postponed leaf stops visiting
 // nodes until the leaf phase tests it, so every ray visits nodes and leaves in
 // the same order whatever the rest of its wave does.
@@ -50,7 +51,7 @@ constexpr int kStackMax = 128;
 #define CTL_LEAF_SPECULATE 1
 #endif
 #ifndef CTL_LEAF_BREAK
-#define CTL_LEAF_BREAK 5
+#define CTL_LEAF_BREAK 4
 #endif
 
 // Order-independent culling of the 4-wide traversal (the tie_min scenes): a
