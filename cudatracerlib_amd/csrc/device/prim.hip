@@ -34,8 +34,15 @@ __device__ __forceinline__ float depth_d3d(float d, float n, float f) {
     return (f / (f - n) * z - f * n / (f - n)) / z;
 }
 
+#ifndef CTL_PRIM_WAVES
+#define CTL_PRIM_WAVES 0   // waves/SIMD hint for prim_kernel (0: the compiler's choice)
+#endif
 template <bool SINGLE, bool WIDE, int FULL>
-__global__ __launch_bounds__(kBlock) void prim_kernel(DevScene S, PathParams P, PrimParams Q, const float* s1,
+__global__ __launch_bounds__(kBlock)
+#if CTL_PRIM_WAVES
+__attribute__((amdgpu_waves_per_eu(CTL_PRIM_WAVES)))
+#endif
+void prim_kernel(DevScene S, PathParams P, PrimParams Q, const float* s1,
                                                       const float2* s2, uint64_t items, unsigned long long* cursor,
                                                       unsigned long long* counters, ctl_pixel* fb, float* depth) {
     CTL_LANE_STACK(st);
