@@ -166,7 +166,19 @@ __device__ __forceinline__ void add_sample(ctl_pixel* fb, const PathParams& P, f
 struct SampleSlots {
     float4* s;            // [pass slot][work item]
     uint32_t per_pass;    // work items of one pass
+    uint32_t inv;         // min(floor(2^32 / per_pass), 2^32 - 1): k / per_pass in one mul_hi (split)
+    // k -> (pass slot, work item of the pass): the mul_hi quotient is exact or
+    // one short (k < 2^32), fixed by one compare
+    __device__ __forceinline__ void split(uint32_t k, uint32_t& ps, uint32_t& kk) const {
+        ps = __umulhi(k, inv);
+        kk = k - ps * per_pass;
+        if (kk >= per_pass) { kk -= per_pass; ps++; }
+    }
 };
+inline SampleSlots make_slots(float4* s, uint32_t per_pass) {
+    const uint64_t q = per_pass ? (1ull << 32) / per_pass : 0;
+    return SampleSlots{s, per_pass, (uint32_t)(q > 0xffffffffull ? 0xffffffffull : q)};
+}
 __device__ __forceinline__ void store_sample(const PathParams& P, const SampleSlots& S, uint32_t ps, uint32_t kk,
                                              uint32_t px, uint32_t py, f2 pX, spec col) {
     col.x = tmax(0.0f, col.x); col.y = tmax(0.0f, col.y); col.z = tmax(0.0f, col.z);

@@ -279,11 +279,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
     // LDS for the path's lifetime instead of holding a VGPR through the traces
     int* pkw = ctl_lds_stack + kPathWordOff + threadIdx.x;
     const Park park{(int)threadIdx.x};
-    // k -> (pass slot, item of the pass): a few subtractions (slots <= passes per launch)
-    auto split = [&](uint32_t k, uint32_t& ps, uint32_t& kk) {
-        ps = 0; kk = k;
-        while (kk >= PS.per_pass) { kk -= PS.per_pass; ps++; }
-    };
+    auto split = [&](uint32_t k, uint32_t& ps, uint32_t& kk) { PS.split(k, ps, kk); };
     PathVars v;
     ShadowReq sh;
     sh.valid = false;
@@ -755,7 +751,7 @@ static ctl_status prepare_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb
 
 static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const PathParams& P, ctl_pixel* fb, bool stats,
                                   hipStream_t s, uint64_t threads, dim3 grid, const float* s1, const float2* s2,
-                                  SampleSlots PS = SampleSlots{nullptr, 0}, uint32_t tbl = 0);
+                                  SampleSlots PS = make_slots(nullptr, 0), uint32_t tbl = 0);
 
 static ctl_status prepare_slots(ctl_ctx* c, uint64_t items, hipStream_t s);
 static void launch_fold(ctl_ctx* c, const PathParams& P, uint32_t per_pass, uint32_t n, ctl_pixel* fb, hipStream_t s);
@@ -775,7 +771,7 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
     ctl_status r1 = prepare_slots(c, threads, s);   // every schedule stores samples per work item
     if (r1 != CTL_OK) return r1;
     ctl_status r2 = launch_schedule(c, p, P, fb, stats, s, threads, grid, s1, s2,
-                                    SampleSlots{c->d_slices, (uint32_t)threads}, 0);
+                                    make_slots(c->d_slices, (uint32_t)threads), 0);
     if (r2 != CTL_OK) return r2;
     launch_fold(c, P, (uint32_t)threads, 1, fb, s);
     CTL_HIP(c, hipEventRecord(c->pass_ev[1], s));
@@ -941,7 +937,7 @@ CTL_API ctl_status ctl_render_passes(ctl_ctx* c, const ctl_pt_params* params, ui
     r = prepare_slots(c, items, s);
     if (r != CTL_OK) return r;
     r = launch_schedule(c, params, P, d_fb, false, s, items, dim3(1), c->d_mt1, c->d_mt2,
-                        SampleSlots{c->d_slices, (uint32_t)per_pass}, (uint32_t)tbl);
+                        make_slots(c->d_slices, (uint32_t)per_pass), (uint32_t)tbl);
     if (r != CTL_OK) return r;
     launch_fold(c, P, (uint32_t)per_pass, n_passes, d_fb, s);
     CTL_HIP(c, hipGetLastError());
