@@ -163,6 +163,27 @@ __device__ __forceinline__ void add_sample(ctl_pixel* fb, const PathParams& P, f
 // additions and their order of one sequential AddSample per work item.
 // code: 0 = no sample (dropped as AddSample drops it), 1 + dx + 2 dy = landed
 // on (px + dx, py + dy).
+// A kernel's by-value record argument read in place from the kernel-argument
+// segment (device pass; `arg` itself on the host pass, which never runs it).
+// off = the argument's byte offset among the explicit arguments, laid out in
+// order at their natural alignment (kernarg_next).  -DCTL_KERNARG_BYVALUE
+// keeps the by-value copies for A/B runs.
+template <class T>
+__device__ __forceinline__ const T& kernarg_ref(const T& arg, size_t off) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(CTL_KERNARG_BYVALUE)
+    (void)arg;
+    return *reinterpret_cast<const T*>((const char*)__builtin_amdgcn_kernarg_segment_ptr() + off);
+#else
+    (void)off;
+    return arg;
+#endif
+}
+// offset of the argument of type B that follows an argument of type A at offset off
+template <class A, class B>
+constexpr size_t kernarg_next(size_t off) {
+    return (off + sizeof(A) + alignof(B) - 1) / alignof(B) * alignof(B);
+}
+
 struct SampleSlots {
     float4* s;            // [pass slot][work item]
     uint32_t per_pass;    // work items of one pass

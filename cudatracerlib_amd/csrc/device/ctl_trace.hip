@@ -214,8 +214,10 @@ __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict
 
 // One path per thread (the reference's pathKernel2 launch shape).
 template <bool STATS, bool SINGLE, bool WIDE, int FULL>
-__global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
+__global__ __launch_bounds__(kBlock) void path_kernel(DevScene S_arg, PathParams P_arg, const float* s1, const float2* s2,
                                                       ctl_pixel* fb, unsigned long long* counters, SampleSlots PS) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
+    const PathParams& P = kernarg_ref<PathParams>(P_arg, kernarg_next<DevScene, PathParams>(0));
     CTL_LANE_STACK(st);
     const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     uint32_t rays = 0;
@@ -266,13 +268,20 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S, PathParams P, 
 // Work items are independent (own sampler index, own sample slot), so the
 // framebuffer is bit-identical to path_kernel's.
 template <bool STATS, bool SINGLE, bool WIDE, int FULL>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? (FULL ? CTL_PERSIST_WAVES_FULL : CTL_PERSIST_WAVES) : 2))) void path_kernel_persistent(DevScene S, PathParams P, const float* s1,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? (FULL ? CTL_PERSIST_WAVES_FULL : CTL_PERSIST_WAVES) : 2))) void path_kernel_persistent(DevScene S_arg, PathParams P_arg, const float* s1,
                                                                  const float2* s2, uint64_t items,
                                                                  unsigned long long* cursor, unsigned long long* counters,
                                                                  SampleSlots PS, uint32_t tbl) {
     // Work item k renders pass slot k / PS.per_pass (sampler tables at
     // s1/s2 + slot * tbl) of work item k % PS.per_pass; every finished sample
     // goes to its own slot, folded into the framebuffer afterwards (store_sample).
+    // The scene and pass records are read in place from the kernel-argument
+    // segment (scalar loads at their uses) rather than held in SGPRs for the
+    // kernel's lifetime: 100+ live SGPRs spilled into VGPR lanes and from
+    // there to scratch.  C3 3184 -> 3310, C5 1662 -> 1772 Mrays/s; VGPR spills
+    // lean 10 -> 0, full 98 -> 40 (profiles/r03_park_slack_ab.txt).
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);
+    const PathParams& P = kernarg_ref<PathParams>(P_arg, kernarg_next<DevScene, PathParams>(0));
     CTL_LANE_STACK(st);
     SamplerDev rng{s1, s2, P.nseq, P.len, 0, 0, 0, 0};
     // work item of the lane's path (pass slot * PS.per_pass + item), parked in
@@ -423,10 +432,11 @@ __global__ __launch_bounds__(kBlock)
 #if CTL_INTERSECT_WAVES
 __attribute__((amdgpu_waves_per_eu(CTL_INTERSECT_WAVES)))
 #endif
-void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
+void intersect_kernel(DevScene S_arg, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            int64_t n2, const ctl_ray* rays2, ctl_hit* hits2,
                                                            unsigned long long* cursor, unsigned long long* counters,
                                                            const uint32_t* dcount, uint32_t band_w) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
     // dcount: the two segment sizes read from device memory (the WavefrontPathTracer's
     // queue counts, written by the previous bounce's scan: no host round trip); the
     // batch is then counted here as traced rays
@@ -500,8 +510,10 @@ void intersect_kernel(DevScene S, int64_t n, const ctl_ray* rays, ctl_hit* hits,
 // jitter + aperture draw + PerspectiveSensor, Sensor.cu:130-144), as a
 // traversalRay batch: tmin = scene eps, tmax = FLT_MAX.  Work items outside
 // the image get an empty interval (tmax = 0).
-__global__ __launch_bounds__(kBlock) void camera_ray_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
+__global__ __launch_bounds__(kBlock) void camera_ray_kernel(DevScene S_arg, PathParams P_arg, const float* s1, const float2* s2,
                                                             uint64_t items, ctl_ray* rays) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
+    const PathParams& P = kernarg_ref<PathParams>(P_arg, kernarg_next<DevScene, PathParams>(0));
     const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (g >= items) return;
     uint32_t px, py;

@@ -42,9 +42,11 @@ __global__ __launch_bounds__(kBlock)
 #if CTL_PRIM_WAVES
 __attribute__((amdgpu_waves_per_eu(CTL_PRIM_WAVES)))
 #endif
-void prim_kernel(DevScene S, PathParams P, PrimParams Q, const float* s1,
+void prim_kernel(DevScene S_arg, PathParams P_arg, PrimParams Q, const float* s1,
                                                       const float2* s2, uint64_t items, unsigned long long* cursor,
                                                       unsigned long long* counters, ctl_pixel* fb, float* depth) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
+    const PathParams& P = kernarg_ref<PathParams>(P_arg, kernarg_next<DevScene, PathParams>(0));
     CTL_LANE_STACK(st);
     const int lane = threadIdx.x & 63;
     uint32_t rays = 0;

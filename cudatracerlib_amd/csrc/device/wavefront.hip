@@ -49,8 +49,10 @@ __device__ __forceinline__ void wf_store(const PathParams& P, const SampleSlots&
     store_sample(P, SS, 0, i, px, py, pX, col);
 }
 
-__global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
+__global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S_arg, PathParams P_arg, const float* s1, const float2* s2,
                                                         WfState W, uint64_t n_items, SampleSlots SS) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
+    const PathParams& P = kernarg_ref<PathParams>(P_arg, kernarg_next<DevScene, PathParams>(0));
     for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;; g += (uint64_t)gridDim.x * kBlock) {
         // keep whole waves in the loop so the ballot in queue_push sees every lane
         const bool inRange = g < n_items;
@@ -96,9 +98,10 @@ __global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S, PathParams P
 #endif
 constexpr int kWfRefillMin = CTL_WF_REFILL_MIN;
 template <int MODE, bool STATS, bool SINGLE, bool WIDE, bool ALPHA>
-__global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S, WfState W, const uint32_t* queue,
+__global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S_arg, WfState W, const uint32_t* queue,
                                                           const uint32_t* countp, uint32_t* cursor,
                                                           unsigned long long* counters) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
     CTL_LANE_STACK(st);
     const uint32_t count = *countp;
     if (count == 0) return;
@@ -181,8 +184,10 @@ void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32
 }
 
 template <int FULL>
-__global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S, PathParams P, const float* s1, const float2* s2,
+__global__ __launch_bounds__(kBlock) void wf_shade_kernel(DevScene S_arg, PathParams P_arg, const float* s1, const float2* s2,
                                                           WfState W, int bounce, SampleSlots SS) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
+    const PathParams& P = kernarg_ref<PathParams>(P_arg, kernarg_next<DevScene, PathParams>(0));
     const uint32_t count = W.counts[2 * bounce];
     const uint32_t* qin = W.q[bounce & 1];
     uint32_t* qout = W.q[(bounce + 1) & 1];

@@ -87,8 +87,9 @@ __device__ __forceinline__ SamplerDev wpt_rng(const float* s1, const float2* s2,
 
 // pathCreateKernelWPT (WavefrontPathTracer.cu:17-49) with one sample per pixel:
 // the payload slot of pixel i is i (rayidx order).
-__global__ __launch_bounds__(kBlock) void wpt_create_kernel(DevScene S, WptArgs A, const float* s1, const float2* s2,
+__global__ __launch_bounds__(kBlock) void wpt_create_kernel(DevScene S_arg, WptArgs A, const float* s1, const float2* s2,
                                                             uint32_t n, ctl_ray* rays, WptPay* pay, uint32_t* count0) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i == 0) { count0[0] = n; count0[1] = 0u; }   // bounce 0: every pixel, no shadow rays
     if (i >= n) return;
@@ -129,11 +130,12 @@ __device__ __forceinline__ uint32_t sample_emitter(const DevScene& S, f2& sample
 
 // pathIterateKernel<NEXT_EVENT_EST> body for payload element j (WavefrontPathTracer.cu:56-148).
 template <bool NEE, int FULL>
-__global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S, WptArgs A, const float* s1, const float2* s2,
+__global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S_arg, WptArgs A, const float* s1, const float2* s2,
                                                              const uint32_t* __restrict__ cnt, WptPay* pay, ctl_ray* rays,
                                                              const ctl_hit* __restrict__ hits,
                                                              const ctl_hit* __restrict__ sec_hits, ctl_ray* sec_tmp,
                                                              uint8_t* flags, uint2* blocks, ctl_pixel* fb) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t n = cnt[0];
     if (blockIdx.x * kBlock >= n) return;   // grid sized for the largest queue
