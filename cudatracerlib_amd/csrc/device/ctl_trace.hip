@@ -690,9 +690,13 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
     CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
     const bool single = c->scene.single != 0;
     const uint64_t want = ((uint64_t)(n + n2) + kBlock - 1) / kBlock;
+#ifndef CTL_INTERSECT_BPC
+#define CTL_INTERSECT_BPC 3   // resident blocks per CU of the batch traversal (0: occupancy limit)
+#endif
 #define IK(AN, ST, SG, WD)                                                                                       \
     do {                                                                                                         \
-        const int nb = resident_blocks(c, intersect_kernel<AN, ST, SG, WD>, kStackLdsBytes);                     \
+        int nb = resident_blocks(c, intersect_kernel<AN, ST, SG, WD>, kStackLdsBytes);                           \
+        if (CTL_INTERSECT_BPC > 0) nb = std::min(nb, CTL_INTERSECT_BPC * c->cu_count);                          \
         hipLaunchKernelGGL((intersect_kernel<AN, ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)),     \
                            dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, n2, rays2, hits2, cursor,  \
                            c->d_counters, dcount, band_w);                                                       \
@@ -803,10 +807,14 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
         unsigned long long* cursor = c->d_cursors + 1;
         CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
         const uint64_t want = (threads + kBlock - 1) / kBlock;
+#ifndef CTL_PERSIST_BPC
+#define CTL_PERSIST_BPC 0   // resident blocks per CU of the persistent path kernel (0: occupancy limit)
+#endif
 #define PK(ST, SG, WD, FU)                                                                                       \
         do {                                                                                                     \
             constexpr size_t lds = persistent_lds_bytes();                                                      \
-            const int nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD, FU>, lds);                      \
+            int nb = resident_blocks(c, path_kernel_persistent<ST, SG, WD, FU>, lds);                            \
+            if (CTL_PERSIST_BPC > 0) nb = std::min(nb, CTL_PERSIST_BPC * c->cu_count);                          \
             hipLaunchKernelGGL((path_kernel_persistent<ST, SG, WD, FU>), dim3((unsigned)std::min<uint64_t>(nb, want)), \
                                dim3(kBlock), lds, s, c->scene, P, s1, s2, threads, cursor,                       \
                                c->d_counters, PS, tbl);                                                          \
