@@ -412,9 +412,13 @@ __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, c
 // SINGLE: one-instance scene, so the hit's node is ~start_node for every
 // lane; indexing with that kernel-uniform value turns the node record and its
 // transform into scalar loads.
+// part: when non-null (persistent kernel), the path's first-hit partials live in
+// this memory slot instead of PathVars, so they hold no VGPRs across the traces;
+// they are read back only for a textured material, the one consumer of the
+// partials.  has_partials is then `depth > 1` (the first hit always computes them).
 template <int FULL, bool SINGLE = false>
 __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P, SamplerDev& rng, PathVars& v,
-                                          const HitRec& r, ShadowReq& sh) {
+                                          const HitRec& r, ShadowReq& sh, float4* part = nullptr) {
     const uint32_t node = SINGLE ? ~(uint32_t)S.start_node : r.node;
     sh.valid = false;
     bsdf_rec b;
@@ -440,8 +444,17 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
             f3 co, dX, dY;
             sensor_diff(S, v.pX, co, dX, dY);
             compute_partials(dg, co, dX, co, dY);
-            v.dudx = dg.dudx; v.dudy = dg.dudy; v.dvdx = dg.dvdx; v.dvdy = dg.dvdy;
-            v.has_partials = true;
+            if (part) {
+                *part = make_float4(dg.dudx, dg.dudy, dg.dvdx, dg.dvdy);
+            } else {
+                v.dudx = dg.dudx; v.dudy = dg.dudy; v.dvdx = dg.dvdx; v.dvdy = dg.dvdy;
+                v.has_partials = true;
+            }
+        } else if (part) {
+            dg.has_partials = true;
+            float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (mat.texture != 0xffffffffu) q = *part;
+            dg.dudx = q.x; dg.dudy = q.y; dg.dvdx = q.z; dg.dvdy = q.w;
         } else {
             dg.dudx = v.dudx; dg.dudy = v.dudy; dg.dvdx = v.dvdx; dg.dvdy = v.dvdy;
             dg.has_partials = v.has_partials;

@@ -73,6 +73,12 @@ namespace {
 #define CTL_PARK 1
 #endif
 constexpr int kParkWords = CTL_PARK ? 23 : 0;
+// The FULL kernel keeps a path's first-hit texture partials in its own sample
+// slot (written only when the path ends) rather than in four VGPRs carried
+// through every trace (shade_hit's `part`).
+#ifndef CTL_PART_SLOT
+#define CTL_PART_SLOT 1
+#endif
 struct Park {
     int tid;
     __device__ __forceinline__ void put(int w, float x) const {
@@ -374,7 +380,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                 v.cl = v.cl + env_miss<FULL>(S, P, v);   // PathTracer.cu:98-111
                 cont = false;
             } else {
-                ending = !shade_hit<FULL, SINGLE>(S, P, rng, v, h, sh);
+                ending = !shade_hit<FULL, SINGLE>(S, P, rng, v, h, sh, CTL_PART_SLOT ? PS.s + *pkw : nullptr);
                 shadowPhase = sh.valid;
                 cont = sh.valid || (!ending && v.depth++ < P.max_path_length);
             }

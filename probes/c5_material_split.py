@@ -44,11 +44,25 @@ def filtered(f):
     return (ctl._abi.Texture * nt)(*out)
 
 
+def with_unused_textured(mats):
+    """the same materials plus one unused textured material: the scene runs the
+    full-shading kernel while every hit shades constant diffuse"""
+    t = ctl.Material.from_buffer_copy(mats[0])
+    t.texture = 0
+    out = [ctl.Material.from_buffer_copy(m) for m in mats] + [t]
+    return (ctl.Material * (n + 1))(*out)
+
+
 for name, kr, kt, flt in (("C5", 1, 1, None), ("rough only", 1, 0, None), ("textures only", 0, 1, None),
                           ("tex trilinear", 0, 1, ctl._abi.CTL_TEX_TRILINEAR), ("tex EWA", 0, 1, ctl._abi.CTL_TEX_EWA),
-                          ("tex bilinear", 0, 1, ctl._abi.CTL_TEX_BILINEAR), ("neither", 0, 0, None)):
+                          ("tex bilinear", 0, 1, ctl._abi.CTL_TEX_BILINEAR), ("neither", 0, 0, None),
+                          ("neither, full", 0, 0, "full")):
     d = type(desc).from_buffer_copy(desc)
     mats = variant(kr, kt)
+    if flt == "full":
+        mats = with_unused_textured(mats)
+        d.n_materials = n + 1
+        flt = None
     d.materials = mats
     tx = filtered(flt)
     d.textures = tx
