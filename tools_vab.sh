@@ -10,6 +10,6 @@ for v in ${VARS:-base}; do
   CTL_LIB=$PWD/$L timeout -k 10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --wpt-passes 0 --dopass-leg 0 --one-pass-leg 0 --closest-shadow-passes 0 --prim-passes 0 ${C5:---c5-passes 16} "$@" > gpurun_out/vab/${i}_$v.json 2> gpurun_out/vab/${i}_$v.err || { echo "BENCH $v FAILED"; tail -20 gpurun_out/vab/${i}_$v.err; exit 1; }
   python3 -c "
 import json; j=json.load(open('gpurun_out/vab/${i}_$v.json')); c5=j.get('path_tracer_c5') or {}
-print('$v C3', j['value'], 'primary', j['primary_rays']['mrays_s'], 'C5', c5.get('mrays_s'), 'wsum', j.get('image_weight_sum'))"
+print('$v C3', j['value'], 'primary', j['primary_rays']['mrays_s'], 'wpt', (j.get('wavefront_tracer') or {}).get('mrays_s'), 'C5', c5.get('mrays_s'), 'wsum', j.get('image_weight_sum'))"
   i=$((i+1))
 done
