@@ -72,8 +72,13 @@ def parse(argv=None):
                     help="mesh BVH builder: the reference's SBVH (default) or early split clipping + binned SAH")
     ap.add_argument("--sbvh-alpha", type=float, default=1.0e-5, help="SBVH splitAlpha (reference 1e-5)")
     ap.add_argument("--emulate-ranks", type=int, default=0,
-                    help="diagnostic: one process renders rank 0's share of an N-rank job "
-                         "(N passes per step over the tiles with tile %% N == 0), no collective")
+                    help="diagnostic: one process renders one rank's share of an N-rank job "
+                         "(N passes per step over the tiles with tile %% N == rank), no collective")
+    ap.add_argument("--emulate-rank", type=int, default=0,
+                    help="the rank whose share --emulate-ranks renders (default 0)")
+    ap.add_argument("--binary-passes", type=int, default=8,
+                    help="passes of the reference-order leg (CTL_SCENE_BINARY_BVH: the reference's own binary "
+                         "visit order, bit-exact to its CPU traversal; 0: skip)")
     ap.add_argument("--steps-per-launch", type=int, default=64,
                     help="steps whose passes go through one ctl_render_passes launch (1: one ctl_render_pass "
                          "launch per pass, the reference's DoPass granularity)")
@@ -391,6 +396,49 @@ def closest_shadow_leg(pt, fb, stream, sptr, torch, pass_index, passes):
             "ms_per_pass": round(ms / passes, 3), "mrays_s": round(rays / (ms * 1e-3) / 1e6, 2)}
 
 
+def binary_leg(ctl, pt, desc, fb, stream, sptr, torch, pass_index, passes):
+    """The reference-exact traversal (CTL_SCENE_BINARY_BVH: the uploaded binary
+    BVH in the reference's own host visit order, so every hit equals the
+    reference CPU traversal's, ties included) on the same context: the scene's
+    trees switched by ctl_scene_update, one untimed launch, then `passes` passes
+    in one ctl_render_passes launch between HIP events."""
+    db = type(desc).from_buffer_copy(desc)
+    db.flags |= ctl.CTL_SCENE_BINARY_BVH
+    pt.update_scene(db, 0, sptr)
+    pt.render_passes(fb.data_ptr(), pass_index, min(passes, 4), sptr)   # warm-up
+    torch.cuda.synchronize()
+    pt.reset_rays(sptr)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    pt.render_passes(fb.data_ptr(), pass_index + 4, passes, sptr)
+    e1.record(stream)
+    pt.sync(sptr)
+    ms = e0.elapsed_time(e1)
+    rays = pt.rays_traced()
+    pt.update_scene(desc, 0, sptr)   # back to the 4-wide trees
+    return {"traversal": "CTL_SCENE_BINARY_BVH: the reference's binary visit order (host branch of "
+                         "BVHTraversal.h:122-232), hits bit-exact to its CPU traversal",
+            "passes": passes, "ms_per_pass": round(ms / passes, 3), "mrays_s": round(rays / (ms * 1e-3) / 1e6, 2)}
+
+
+def reference_order_record():
+    """The newest committed distance of the default 4-wide order from the
+    reference's binary order (profiles/rNN_reference_order.json, written by
+    tests/test_reference_order.py::test_full_size_c3_reference_order_distance)."""
+    import glob
+    here = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(here, "profiles", "r[0-9][0-9]*_reference_order.json")))
+    if not files:
+        return None
+    j = json.load(open(files[-1]))
+    t = j.get("total", {})
+    return {"rays": t.get("rays"), "differing_rays": t.get("differ"), "ties": t.get("ties"),
+            "reference_culled": t.get("ref_culled"), "wide_culled": t.get("other_culled"),
+            "pixels_over_1e-4_rel": (j.get("pass") or {}).get("pixels_over_1e-4_rel"),
+            "pixels": (j.get("pass") or {}).get("pixels"), "source": os.path.relpath(files[-1], here)}
+
+
 def wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_index, passes):
     """WavefrontPathTracer::DoRender (ctl_wpt_render_pass) on the same context and
     scene: the batch traversal's second caller.  The first
@@ -525,6 +573,12 @@ def main(argv=None):
         return 0
     # image-tile shards: one per rank, or N emulated ranks in this one process
     shards = a.emulate_ranks if (world == 1 and a.emulate_ranks > 1) else world
+    tile_rank = rank   # the tile shard this process renders
+    if shards != world:
+        if not 0 <= a.emulate_rank < shards:
+            log(f"bench: --emulate-rank {a.emulate_rank} outside 0..{shards - 1}")
+            return 2
+        tile_rank = a.emulate_rank
     import torch
     import torch.distributed as dist
     if world > 1 and a.backend == "nccl" and torch.cuda.device_count() < world:
@@ -565,7 +619,7 @@ def main(argv=None):
         f"built in {t_build:.1f}s with {threads} threads")
 
     pt = ctl.PathTracer(local, max_path_length=a.max_path_length, rr_start_depth=a.rr_start,
-                        shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, num_ranks=shards, rank=rank,
+                        shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, num_ranks=shards, rank=tile_rank,
                         schedule=a.schedule)
     pt.upload_scene(desc)
     W, H = a.width, a.height
@@ -673,6 +727,14 @@ def main(argv=None):
         scratch = torch.zeros_like(fb)
         closest = closest_shadow_leg(pt, scratch, stream, sptr, torch, nxt + 10, a.closest_shadow_passes)
         del scratch
+    binary = None
+    if rank == 0 and shards == 1 and a.binary_passes > 0 and a.bvh == "wide":
+        try:   # a side leg: reported in the line, not fatal to the headline
+            scratch = torch.zeros_like(fb)
+            binary = binary_leg(ctl, pt, desc, scratch, stream, sptr, torch, nxt + 80, a.binary_passes)
+            del scratch
+        except Exception as e:
+            binary = {"error": f"{type(e).__name__}: {e}"}
     c5 = None
     if rank == 0 and shards == 1 and a.c5_passes > 0 and a.config != 5:
         try:   # a side leg, like C1: reported in the line, not fatal to the headline
@@ -740,13 +802,15 @@ def main(argv=None):
                 "parallelism": (f"image-tile shard x{world} + {'RCCL' if a.backend == 'nccl' else a.backend} reduce"
                                 if world > 1 else "single GPU"),
                 "total_rays": total_rays,
-                **({"emulated_ranks": shards} if shards != world else {}),
+                **({"emulated_ranks": shards, "emulated_rank": tile_rank} if shards != world else {}),
             },
             "roofline": rl,
             "primary_rays": prim,
             "one_pass_launches": single,
             "reference_dopass": dopass,
             "closest_hit_shadows": closest,
+            "binary_bvh": binary,
+            "parity_vs_reference_order": reference_order_record(),
             "wavefront_tracer": wpt,
             "prim_tracer_c1": c1,
             "path_tracer_c5": c5,

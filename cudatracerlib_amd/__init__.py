@@ -273,6 +273,24 @@ def bvh_stack_bound(nodes, root_value=0):
     return out[0], out[1]
 
 
+def host_wide_trees(desc):
+    """The 4-wide trees ctl_scene_upload builds from desc (ctl_host_wide_trees):
+    (mesh nodes (n, 32) float32, per-mesh first node (n_meshes,) uint32,
+    instance-tree nodes (m, 32) float32), 128-B WideNode records as float32 rows
+    (the child / pad words keep their int bits)."""
+    L = lib()
+    nm, ns = C.c_uint64(0), C.c_uint64(0)
+    _check(L.ctl_host_wide_trees(C.byref(desc), None, 0, C.byref(nm), None, None, 0, C.byref(ns)), None,
+           "ctl_host_wide_trees: " + (L.ctl_host_last_error() or b"").decode())
+    mesh = np.zeros((nm.value, 32), np.float32)
+    wbase = np.zeros(desc.n_meshes, np.uint32)
+    scene = np.zeros((ns.value, 32), np.float32)
+    _check(L.ctl_host_wide_trees(C.byref(desc), mesh.ctypes.data, nm.value, C.byref(nm), wbase.ctypes.data,
+                                 scene.ctypes.data, ns.value, C.byref(ns)), None,
+           "ctl_host_wide_trees: " + (L.ctl_host_last_error() or b"").decode())
+    return mesh, wbase, scene
+
+
 class Tracer:
     """Per-GPU traversal context (InitializeKernel/UpdateKernel/IntersectBuffers)."""
 
@@ -338,6 +356,18 @@ class Tracer:
         _check(self._L.ctl_scene_read(self._ctx, int(which), int(first), int(count), out.ctypes.data), self._ctx,
                "ctl_scene_read")
         return out
+
+    def wide_trees(self, desc):
+        """The uploaded scene's 4-wide trees as the device holds them (after any
+        refit by animate / set_transform), in host_wide_trees' layout; float
+        nodes only (not CTL_SCENE_WIDE_QUANT)."""
+        if desc.flags & _abi.CTL_SCENE_WIDE_QUANT:
+            raise ValueError("wide_trees: quantized trees are read as host_wide_trees' decoded boxes")
+        mesh0, wbase0, scene0 = host_wide_trees(desc)
+        mesh = self.read_array(_abi.CTL_ARRAY_WIDE_BVH, 0, mesh0.shape[0], np.float32, 32)
+        wbase = self.read_array(_abi.CTL_ARRAY_MESH_WIDE_BASE, 0, wbase0.size, np.uint32, 1).reshape(-1)
+        scene = self.read_array(_abi.CTL_ARRAY_SCENE_WIDE_BVH, 0, scene0.shape[0], np.float32, 32)
+        return mesh, wbase, scene
 
     def rays_traced(self):
         return int(self._L.ctl_rays_traced(self._ctx))

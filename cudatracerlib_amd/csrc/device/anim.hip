@@ -29,6 +29,7 @@
 #include "../ctl_anim.h"
 #include "../ctl_shade.h"
 #include "../host/bvh_wide.h"
+#include "../ctl_qnode.h"
 
 namespace ctl {
 
@@ -544,6 +545,7 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         S.ray_eps = A->h_eps[6];
         c->device_eps = true;
     }
+    c->device_edited = true;
     if (hipGetLastError() != hipSuccess) { c->err = "scene_animate: launch failed"; return CTL_ERR_HIP; }
     return CTL_OK;
 }
@@ -593,6 +595,7 @@ CTL_API ctl_status ctl_scene_set_transform(ctl_ctx* c, uint32_t node, const ctl_
     }
     S.ray_eps = A->h_eps[6];
     c->device_eps = true;
+    c->device_edited = true;
     return CTL_OK;
 }
 
@@ -636,6 +639,15 @@ CTL_API ctl_status ctl_scene_read(ctl_ctx* c, uint32_t array, uint64_t first, ui
         case CTL_ARRAY_ENV:
             if (!S.env) { c->err = "scene_read: no environment light"; return CTL_ERR_STATE; }
             src = S.env; elem = sizeof(ctl_env_light); n = 1; break;
+        case CTL_ARRAY_WIDE_BVH:
+        case CTL_ARRAY_SCENE_WIDE_BVH:
+        case CTL_ARRAY_MESH_WIDE_BASE:
+            if (!S.wide) { c->err = "scene_read: the scene has no 4-wide trees (CTL_SCENE_BINARY_BVH)"; return CTL_ERR_STATE; }
+            elem = array == CTL_ARRAY_MESH_WIDE_BASE ? sizeof(uint32_t) : (S.quant ? sizeof(QWideNode) : sizeof(WideNode));
+            src = array == CTL_ARRAY_WIDE_BVH ? (const void*)S.wbvh
+                  : array == CTL_ARRAY_SCENE_WIDE_BVH ? (const void*)S.scene_wbvh : (const void*)S.mesh_wbase;
+            n = c->sarr[array == CTL_ARRAY_WIDE_BVH ? SA_WBVH : array == CTL_ARRAY_SCENE_WIDE_BVH ? SA_SWBVH : SA_WBASE].bytes / elem;
+            break;
         default: c->err = "scene_read: unknown array"; return CTL_ERR_INVALID;
     }
     if (first > n || count > n - first) { c->err = "scene_read: range out of bounds"; return CTL_ERR_INVALID; }

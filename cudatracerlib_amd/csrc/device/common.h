@@ -562,6 +562,7 @@ struct ctl_ctx {
     uint32_t tree_flags = 0;                    // CTL_SCENE_BINARY_BVH / WIDE_QUANT the trees were built for
     uint32_t n_anim_meshes = 0;
     bool device_eps = false;                    // ray_eps derived on the device (set_transform / animate)
+    bool device_edited = false;                 // set_transform / animate rewrote device arrays since the upload
     ctl::DevScene scene{};
     bool has_scene = false;
     bool half_quirk = false;

@@ -35,6 +35,7 @@ struct Rccl {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommUserRank) user_rank = nullptr;   // optional: checks d_out on the root
     std::string err;
     bool ok = false;
 };
@@ -61,6 +62,7 @@ const Rccl& rccl() {
         sym(R.group_end, "ncclGroupEnd");
         sym(R.error_string, "ncclGetErrorString");
         if (!all) { R.err = "RCCL: missing entry points"; return; }
+        R.user_rank = reinterpret_cast<decltype(&ncclCommUserRank)>(dlsym(h, "ncclCommUserRank"));
         R.ok = true;
     });
     return R;
@@ -126,6 +128,13 @@ CTL_API ctl_status ctl_fb_reduce(ctl_ctx* c, void* comm, const ctl_pixel* d_fb, 
     if (!c || !comm || (!d_fb && n_pixels)) return CTL_ERR_INVALID;
     if (d_out && d_out == d_fb) { c->err = "fb_reduce: d_out must not alias d_fb"; return CTL_ERR_INVALID; }
     if (!have_rccl(c)) return CTL_ERR_NODEVICE;
+    if (!d_out && n_pixels) {   // the root needs a receive buffer (RCCL would get a null recvbuff)
+        int me = -1;
+        if (!rccl().user_rank || rccl().user_rank(reinterpret_cast<ncclComm_t>(comm), &me) != ncclSuccess || me == root) {
+            c->err = "fb_reduce: d_out is required on the root rank";
+            return CTL_ERR_INVALID;
+        }
+    }
     if (hipSetDevice(c->device) != hipSuccess) { c->err = "fb_reduce: hipSetDevice failed"; return CTL_ERR_HIP; }
     const size_t count = (size_t)n_pixels * (sizeof(ctl_pixel) / sizeof(float));
     return nccl_status(c, rccl().reduce(d_fb, d_out, count, ncclFloat, ncclSum, root,
@@ -138,6 +147,7 @@ CTL_API ctl_status ctl_fb_reduce_all(ctl_ctx* const* ctxs, void* const* comms, c
                                      void* const* streams) {
     if (!ctxs || !comms || !d_fbs || n < 1 || root < 0 || root >= n) return CTL_ERR_INVALID;
     if (!have_rccl(ctxs[0])) return CTL_ERR_NODEVICE;
+    if (!d_out && n_pixels) { ctxs[0]->err = "fb_reduce_all: d_out (on the root's GPU) is required"; return CTL_ERR_INVALID; }
     if (d_out && d_out == d_fbs[root]) { ctxs[0]->err = "fb_reduce_all: d_out must not alias d_fbs[root]"; return CTL_ERR_INVALID; }
     const size_t count = (size_t)n_pixels * (sizeof(ctl_pixel) / sizeof(float));
     if (rccl().group_start() != ncclSuccess) return CTL_ERR_HIP;

@@ -224,6 +224,12 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
         dirty |= kDirtyTrees | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES;
     // the refit plans (anim_setup) are rebuilt with the instance tree's wide copy
     if (dirty & (kDirtyTrees | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES)) dirty |= CTL_DIRTY_NODES;
+    // after set_transform / animate, re-uploading any tree group returns every
+    // device-edited array to the desc (geometry, instances, their area lights,
+    // the environment's scene sphere), never a mix of moved and unmoved state
+    if (c->device_edited && (dirty & (kDirtyTrees | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES)))
+        dirty |= kDirtyTrees | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES | CTL_DIRTY_TRI_DATA | CTL_DIRTY_WOOP |
+                 CTL_DIRTY_LIGHTS | CTL_DIRTY_ENV;
     ctl_status r;
     if ((r = validate(c, d, dirty)) != CTL_OK) return r;
     if ((r = check_clean(c, d, dirty)) != CTL_OK) return r;
@@ -269,7 +275,9 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
     const bool want_src = d->n_anim_meshes > 0;
     std::vector<WideNode> wn, sw;
     std::vector<uint32_t> wsrc, ssrc;
-    const bool mesh_trees = (dirty & CTL_DIRTY_BVH) != 0;
+    // the 4-wide mesh trees read the binary nodes, the leaf entries' last-in-leaf
+    // flags (counted leaves) and the per-mesh offsets
+    const bool mesh_trees = (dirty & (CTL_DIRTY_BVH | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES)) != 0;
     const bool top_tree = (dirty & CTL_DIRTY_NODES) != 0;
     try {
         if (mesh_trees) {
@@ -282,12 +290,12 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
                 mesh_bin = std::max(mesh_bin, binary_stack_bound(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, kStackMax));
                 if (!wide) continue;
                 c->h_wbase[m] = (uint32_t)wn.size();
-                // the mesh's entries: [bvh_indices_offset, the next mesh's) -- leaf children carry counts
+                // the mesh's entries start at bvh_indices_offset (meshes may be stored in any
+                // order); leaf children carry counts, each leaf bounded by its last-in-leaf flag
                 const uint64_t e0 = d->meshes[m].bvh_indices_offset;
-                const uint64_t e1 = m + 1 < d->n_meshes ? d->meshes[m + 1].bvh_indices_offset : d->n_tri_indices;
-                if (e0 > d->n_tri_indices || e1 < e0 || e1 > d->n_tri_indices) throw std::runtime_error("mesh entry range out of range");
+                if (e0 > d->n_tri_indices) throw std::runtime_error("mesh entry offset out of range");
                 collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn, want_src ? &ms : nullptr,
-                              d->tri_indices + e0, (size_t)(e1 - e0));
+                              d->tri_indices + e0, (size_t)(d->n_tri_indices - e0));
                 if (want_src) wsrc.insert(wsrc.end(), ms.begin(), ms.end());
                 mesh_wide = std::max(mesh_wide, wide_stack_bound(wn.data() + c->h_wbase[m], wn.size() - c->h_wbase[m], 0, kStackMax));
             }
@@ -361,7 +369,6 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
     }
     if (mesh_trees || top_tree) {
         S.wide = wide ? 1 : 0;
-        S.tie_min = wide ? 1 : 0;
         c->tree_flags = d->flags & tree_bits;
     }
     S.bvh = dptr<float4>(c, SA_BVH);
@@ -429,6 +436,7 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
         SD_HIP(c, hipStreamSynchronize(s));
     }
     c->n_anim_meshes = d->n_anim_meshes;
+    if (dirty & CTL_DIRTY_NODES) c->device_edited = false;
     return CTL_OK;
 }
 
@@ -442,6 +450,7 @@ void free_scene(ctl_ctx* c) {
     c->h_wbase.clear();
     c->tree_flags = 0xffffffffu;
     c->device_eps = false;
+    c->device_edited = false;
     c->scene = DevScene{};
     c->scene.env_index = 0xffffffffu;
 }

@@ -44,34 +44,34 @@ constexpr int kStackMax = 128;
 // C3 sweep: 1 -> 2098, 2 -> 2164, 4 -> 2225, 6 -> 2237, 8 -> 2216, 16 -> 2146 Mrays/s;
 // later, with the current kernel, 5 / 6 / 7 agree within run-to-run noise, ~2250;
 // round 3 with the LDS-parked path state: 3 / 4 / 5 / 7 -> 3185 / 3187 / 3170 / 3151).
-// CTL_LEAF_SPECULATE 0: a lane that holds a postponed leaf stops visiting
-// nodes until the leaf phase tests it, so every ray visits nodes and leaves in
-// the same order whatever the rest of its wave does.
-#ifndef CTL_LEAF_SPECULATE
-#define CTL_LEAF_SPECULATE 1
-#endif
 #ifndef CTL_LEAF_BREAK
 #define CTL_LEAF_BREAK 4
 #endif
-
-// Order-independent culling of the 4-wide traversal (the tie_min scenes): a
-// box is culled only when its entry lies more than kCullSlack ulps (~0.2 %)
-// beyond the closest hit so far.  Without the slack a box whose slab entry
-// rounds a few ulps past the Woop t of a triangle inside it is culled or
-// visited depending on which hits were found first -- and with leaves
-// postponed per wave, that order depends on the other rays of the wave, so a
-// handful of rays per 10^7 changed their hit from launch to launch.  With it,
-// the closest (t, triangle, node) is always tested, in any order: the result is
-// a function of the ray alone, the same as the oracle's binary-order
-// traversal under the same rule (oracle/oracle.cpp trace_two_level).
-#ifndef CTL_CULL_SLACK
-#define CTL_CULL_SLACK (1 << 14)
+// CTL_LEAF_SPECULATE 1 (default): in the 4-wide mesh trees a lane that holds a
+// postponed leaf keeps visiting nodes (with the cull distance it had when it
+// postponed) until it reaches its next leaf; 0: it waits for the leaf phase.
+#ifndef CTL_LEAF_SPECULATE
+#define CTL_LEAF_SPECULATE 1
 #endif
-constexpr int kCullSlack = CTL_CULL_SLACK;
-__device__ __forceinline__ int cull_bits(float t) {
-    const int b = __float_as_int(t);
-    return b >= 0 ? min(b + kCullSlack, 0x7f800000) : b;
-}
+
+// Per-ray visit order (round 4).  Every traversal is a function of its ray
+// alone, never of the other rays of its wave:
+//  * binary trees (CTL_SCENE_BINARY_BVH, stats launches) run the reference's
+//    host order exactly (BVHTraversal.h:214: the vote mask of a lone lane), so
+//    a lane stops at its first postponed leaf; results equal the reference's
+//    CPU traversal bit for bit, ties included;
+//  * 4-wide mesh trees speculate: after postponing leaf L1 the lane walks on to
+//    its next leaf L2 with the cull distance of before L1 (`tcull`), then tests
+//    L1, L2 (and the leaves stacked right behind) and takes the new distance.
+//    A wave may end its node loop while such a lane is still walking (every
+//    lane holds a leaf, or CTL_LEAF_BREAK); the lane then tests L1, keeps
+//    `tcull`, and resumes holding a phantom leaf (kPhantomLeaf, skipped by the
+//    leaf test) so it stops at L2 exactly as if it had never been interrupted.
+//  Culling is the reference's (`far >= entry` against tcull), ties first-found.
+// The oracle restates the same order over the same 4-wide arrays
+// (oracle/oracle.cpp trace_two_level_wide).
+constexpr int kPhantomLeaf = ~(int)(214783647u << 3);   // counted-leaf code of the reference's skipped
+                                                        // leaf value -214783648 (BVHTraversal.h:109,221)
 
 struct DevScene {
     const float4* bvh;          // mesh BVHNodeData, float4 units
@@ -107,7 +107,6 @@ struct DevScene {
     uint32_t wide;               // wide trees present (scene flag CTL_SCENE_BINARY_BVH clear)
     uint32_t full_shading;       // shading level of the path kernels: kShadeLean / kShadeFull / kShadeEnv
     uint32_t alpha;              // KernelDynamicScene::doAlphaMapping (some material has an alpha map)
-    uint32_t tie_min;            // exact-t ties -> lowest (triangle, node) instead of first found
     uint32_t s_wnode_base;
     uint32_t quant;              // wide trees in the 64-B quantized format (ctl_qnode.h)
     // InfiniteLight (ctl_env.h): light env_index of lights[], 0xFFFFFFFF without one
@@ -234,6 +233,7 @@ struct Traverser {
     RayLocal world;   // unused when SINGLE
     HitRec h;
     float span_tmin, tri_tmin;
+    float tcull;   // cull distance of the 4-wide node loops (h.t, or its value before a phantom leaf)
     int nodeAddr, leafAddr, level, meshSent;
     uint32_t nodeBase, triBase, idxBase, triOffset, instIdx;
     bool done, resumeLeaves;
@@ -249,6 +249,7 @@ struct Traverser {
     __device__ __forceinline__ void init(const DevScene& S, f3 o, f3 d, float smin, float tmn, float tmaxv,
                                          LaneStack& st, TraceStats* stats) {
         h.t = tmaxv; h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
+        tcull = tmaxv;
         span_tmin = smin; tri_tmin = tmn;
         st.sp = 0;
         st.overflow = false;
@@ -307,9 +308,7 @@ struct Traverser {
             float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
             float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
             float t = Oz * invDz;
-            // exact-t tie under tie_min: lower (triangle, node) wins, in any
-            // visit order; a hit at exactly the initial tmax stays rejected
-            if (t > tri_tmin && (t < h.t || (S.tie_min && t == h.t && h.tri != 0xffffffffu))) {
+            if (t > tri_tmin && t < h.t) {   // TraceHelper.cu:121 (first found wins a tie)
                 float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
                 float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
                 float u = Ox + t * Dx;
@@ -318,9 +317,7 @@ struct Traverser {
                     float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
                     float v = Oy + t * Dy;
                     const uint32_t gtri = (index >> 1) + triOffset;
-                    if (v >= 0.0f && u + v <= 1.0f &&
-                        (t < h.t || gtri < h.tri || (gtri == h.tri && instIdx < h.node)) &&
-                        (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v))) {
+                    if (v >= 0.0f && u + v <= 1.0f && (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v))) {
                         h.node = instIdx;
                         h.tri = gtri;
                         h.u = u;
@@ -345,7 +342,7 @@ struct Traverser {
         float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
         float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
         float t = Oz * invDz;
-        if (t > tri_tmin && (t < h.t || (S.tie_min && t == h.t && h.tri != 0xffffffffu))) {
+        if (t > tri_tmin && t < h.t) {
             float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
             float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
             float u = Ox + t * Dx;
@@ -360,8 +357,7 @@ struct Traverser {
                     (void)entry;
                     const uint32_t gtri = (index >> 1) + triOffset;
 #endif
-                    if ((t < h.t || gtri < h.tri || (gtri == h.tri && instIdx < h.node)) &&
-                        (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v))) {
+                    if (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v)) {
                         h.node = instIdx;
                         h.tri = gtri;
                         h.u = u;
@@ -503,14 +499,16 @@ struct Traverser {
         // opaque to the optimiser: otherwise it splits off + (16 - s) into two ops per load
         asm volatile("" : "+v"(onx), "+v"(ofx), "+v"(ony), "+v"(ofy), "+v"(onz), "+v"(ofz));
 #endif
-        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (CTL_LEAF_SPECULATE || leafAddr >= 0)) {
+        // speculation only inside a mesh (the instance level stops at its first leaf)
+        const bool spec = CTL_LEAF_SPECULATE && (SINGLE || level == 1);
+        const int tBits = __float_as_int(tcull);
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (spec || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
             const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
             CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
             if (STATS) stats->nodes++;
-            const int tBits = cull_bits(h.t);
             int k0, k1, k2, k3;
 #ifndef CTL_WIDE_MINMAX
             const uint32_t off = (nodeBase + (uint32_t)nodeAddr) << 7;
@@ -588,14 +586,16 @@ struct Traverser {
         const int tminBits = __float_as_int(span_tmin);
         const bool negx = __float_as_int(cur.idx) < 0, negy = __float_as_int(cur.idy) < 0;
         const bool negz = __float_as_int(cur.idz) < 0;
-        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (CTL_LEAF_SPECULATE || leafAddr >= 0)) {
+        // speculation only inside a mesh (the instance level stops at its first leaf)
+        const bool spec = CTL_LEAF_SPECULATE && (SINGLE || level == 1);
+        const int tBits = __float_as_int(tcull);
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (spec || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
             const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
             CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
             if (STATS) stats->nodes++;
-            const int tBits = cull_bits(h.t);
             const uint32_t off = (nodeBase + (uint32_t)nodeAddr) << 6;
             const float4 qa = *reinterpret_cast<const float4*>(nbytes + off);
             const float4 qb = *reinterpret_cast<const float4*>(nbytes + off + 16u);
@@ -609,6 +609,20 @@ struct Traverser {
             const uint32_t nyw = negy ? why : wly, fyw = negy ? wly : why;
             const uint32_t nzw = negz ? whz : wlz, fzw = negz ? wlz : whz;
 #define CTL_QB(W, K) ((float)(((W) >> (8 * (K))) & 0xffu))
+#ifdef CTL_QUANT_FUSED
+            // experiment: the decode folded into the slab, (p + q s) idir - ood =
+            // fma(q, s idir, p idir - ood): one cvt + half a packed fma per bound
+            const float axs = qa.w * cur.idx, ays = qb.x * cur.idy, azs = qb.y * cur.idz;
+            const float bxs = qa.x * cur.idx - cur.oodx, bys = qa.y * cur.idy - cur.oody, bzs = qa.z * cur.idz - cur.oodz;
+#define CTL_QPAIR(W, A, B, K0, K1) \
+    __builtin_elementwise_fma(v2f{CTL_QB(W, K0), CTL_QB(W, K1)}, v2f{(A), (A)}, v2f{(B), (B)})
+            const v2f nx01 = CTL_QPAIR(nxw, axs, bxs, 0, 1), nx23 = CTL_QPAIR(nxw, axs, bxs, 2, 3);
+            const v2f fx01 = CTL_QPAIR(fxw, axs, bxs, 0, 1), fx23 = CTL_QPAIR(fxw, axs, bxs, 2, 3);
+            const v2f ny01 = CTL_QPAIR(nyw, ays, bys, 0, 1), ny23 = CTL_QPAIR(nyw, ays, bys, 2, 3);
+            const v2f fy01 = CTL_QPAIR(fyw, ays, bys, 0, 1), fy23 = CTL_QPAIR(fyw, ays, bys, 2, 3);
+            const v2f nz01 = CTL_QPAIR(nzw, azs, bzs, 0, 1), nz23 = CTL_QPAIR(nzw, azs, bzs, 2, 3);
+            const v2f fz01 = CTL_QPAIR(fzw, azs, bzs, 0, 1), fz23 = CTL_QPAIR(fzw, azs, bzs, 2, 3);
+#else
             // p + q * s in one fused op: q * s is exact (q < 256, s a power of two), so the
             // fused result is the encoder's p + q * s (mul, then add) bit for bit
 #define CTL_QPAIR(W, P, SC, K0, K1) \
@@ -619,6 +633,7 @@ struct Traverser {
             const v2f fy01 = CTL_QPAIR(fyw, qa.y, qb.x, 0, 1) * iy - oy, fy23 = CTL_QPAIR(fyw, qa.y, qb.x, 2, 3) * iy - oy;
             const v2f nz01 = CTL_QPAIR(nzw, qa.z, qb.y, 0, 1) * iz - oz, nz23 = CTL_QPAIR(nzw, qa.z, qb.y, 2, 3) * iz - oz;
             const v2f fz01 = CTL_QPAIR(fzw, qa.z, qb.y, 0, 1) * iz - oz, fz23 = CTL_QPAIR(fzw, qa.z, qb.y, 2, 3) * iz - oz;
+#endif
 #undef CTL_QPAIR
 #undef CTL_QB
             int k0, k1, k2, k3, c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
@@ -642,7 +657,9 @@ struct Traverser {
 
     __device__ __forceinline__ void inner_binary(const DevScene& S, LaneStack& st, TraceStats* stats) {
         const float4* nodes = (SINGLE || level) ? S.bvh : S.scene_bvh;
-        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL) {
+        // the reference's host order: the lane stops at its first postponed leaf
+        // (BVHTraversal.h:214, mask = leafAddr >= 0)
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && leafAddr >= 0) {
             const float4* n = nodes + nodeBase + nodeAddr;
             const float4 n0xy = n[0];
             const float4 n1xy = n[1];
@@ -685,7 +702,7 @@ struct Traverser {
                 leafAddr = nodeAddr;
                 nodeAddr = st.pop();
             }
-            if (!__any(leafAddr >= 0)) break;
+            if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
@@ -702,6 +719,9 @@ struct Traverser {
         }
         else inner_binary(S, st, stats);
         resumeLeaves = false;
+        // a speculating lane the wave stopped before it reached its next leaf
+        const bool cut = WIDE && CTL_LEAF_SPECULATE && (SINGLE || level == 1) && leafAddr < 0 &&
+                         (unsigned)nodeAddr < (unsigned)CTL_SENTINEL;
 #ifdef CTL_PROFILE_TRACE
         {
             const uint32_t nl = (uint32_t)__popcll(__ballot(leafAddr < 0));
@@ -737,12 +757,15 @@ struct Traverser {
                     level = 1;
                     nodeAddr = 0;             // mesh root (TraceHelper.cu:170)
                     leafAddr = 0;
+                    tcull = h.t;
                     return;
                 }
                 leafAddr = nodeAddr;
                 if (nodeAddr < 0) nodeAddr = st.pop();
             }
         }
+        if (cut) leafAddr = kPhantomLeaf;   // walk on to the next leaf with the old tcull
+        else tcull = h.t;
         if (nodeAddr == CTL_SENTINEL) {
             if (!SINGLE && level == 1) {
                 // mesh traversal finished (bottom sentinel or a sentinel child)

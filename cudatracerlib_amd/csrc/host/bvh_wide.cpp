@@ -1,5 +1,6 @@
 // bvh_wide.cpp — see bvh_wide.h.
 #include "bvh_wide.h"
+#include "../ctl_qnode.h"
 
 #include <algorithm>
 #include <cstring>
@@ -273,3 +274,66 @@ extern "C" CTL_API ctl_status ctl_host_bvh_stack_bound(const ctl_bvh_node* nodes
     return CTL_OK;
 }
 
+
+// The 4-wide trees ctl_scene_upload builds (device/scene_dev.hip commit): one
+// counted-leaf tree per mesh, then the instance tree.
+extern "C" CTL_API ctl_status ctl_host_wide_trees(const ctl_scene_desc* d, void* mesh_out, uint64_t mesh_capacity,
+                                                  uint64_t* n_mesh_nodes, uint32_t* wbase_out, void* scene_out,
+                                                  uint64_t scene_capacity, uint64_t* n_scene_nodes) {
+    if (!d || !n_mesh_nodes || !n_scene_nodes) { ctl::set_host_error("host_wide_trees: null argument"); return CTL_ERR_INVALID; }
+    try {
+        std::vector<ctl::WideNode> wn, sw;
+        std::vector<uint32_t> wb(d->n_meshes, 0);
+        for (uint32_t m = 0; m < d->n_meshes && d->n_bvh_nodes > 0; m++) {
+            const size_t first = d->meshes[m].bvh_node_offset / 4;
+            if (first >= d->n_bvh_nodes) throw std::runtime_error("mesh BVH offset out of range");
+            const uint64_t e0 = d->meshes[m].bvh_indices_offset;
+            if (e0 > d->n_tri_indices) throw std::runtime_error("mesh entry offset out of range");
+            wb[m] = (uint32_t)wn.size();
+            ctl::collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn, nullptr, d->tri_indices + e0,
+                               (size_t)(d->n_tri_indices - e0));
+        }
+        if (d->n_bvh_nodes > 0 && d->n_nodes > 0 && d->scene_start_node >= 0)
+            ctl::collapse_wide(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, sw);
+        // CTL_SCENE_WIDE_QUANT: the boxes the quantized nodes decode to (what the
+        // device's slab test sees; empty slots NaN), when every node quantizes
+        if ((d->flags & CTL_SCENE_WIDE_QUANT) && d->n_anim_meshes == 0) {
+            std::vector<ctl::WideNode> dq[2] = {wn, sw};
+            bool ok = true;
+            for (auto& tree : dq)
+                for (ctl::WideNode& w : tree) {
+                    const float lo[3][4] = {{w.lo_x[0], w.lo_x[1], w.lo_x[2], w.lo_x[3]},
+                                            {w.lo_y[0], w.lo_y[1], w.lo_y[2], w.lo_y[3]},
+                                            {w.lo_z[0], w.lo_z[1], w.lo_z[2], w.lo_z[3]}};
+                    const float hi[3][4] = {{w.hi_x[0], w.hi_x[1], w.hi_x[2], w.hi_x[3]},
+                                            {w.hi_y[0], w.hi_y[1], w.hi_y[2], w.hi_y[3]},
+                                            {w.hi_z[0], w.hi_z[1], w.hi_z[2], w.hi_z[3]}};
+                    ctl::QWideNode q;
+                    if (!ctl::quantize_wide(lo, hi, w.child, q)) { ok = false; break; }
+                    const float nan = std::numeric_limits<float>::quiet_NaN();
+                    for (int i = 0; i < 4; i++) {
+                        const bool used = w.child[i] != 0x76543210;
+                        auto b = [&](uint32_t word) { return (word >> (8 * i)) & 0xffu; };
+                        w.lo_x[i] = used ? ctl::qdecode(q.px, b(q.lo_x), q.sx) : nan;
+                        w.hi_x[i] = used ? ctl::qdecode(q.px, b(q.hi_x), q.sx) : nan;
+                        w.lo_y[i] = used ? ctl::qdecode(q.py, b(q.lo_y), q.sy) : nan;
+                        w.hi_y[i] = used ? ctl::qdecode(q.py, b(q.hi_y), q.sy) : nan;
+                        w.lo_z[i] = used ? ctl::qdecode(q.pz, b(q.lo_z), q.sz) : nan;
+                        w.hi_z[i] = used ? ctl::qdecode(q.pz, b(q.hi_z), q.sz) : nan;
+                    }
+                }
+            if (ok) { wn = dq[0]; sw = dq[1]; }
+        }
+        *n_mesh_nodes = wn.size();
+        *n_scene_nodes = sw.size();
+        if ((mesh_out && mesh_capacity < wn.size()) || (scene_out && scene_capacity < sw.size()))
+            throw std::runtime_error("output capacity too small");
+        if (mesh_out && !wn.empty()) std::memcpy(mesh_out, wn.data(), wn.size() * sizeof(ctl::WideNode));
+        if (scene_out && !sw.empty()) std::memcpy(scene_out, sw.data(), sw.size() * sizeof(ctl::WideNode));
+        if (wbase_out && !wb.empty()) std::memcpy(wbase_out, wb.data(), wb.size() * sizeof(uint32_t));
+    } catch (const std::exception& e) {
+        ctl::set_host_error(std::string("host_wide_trees: ") + e.what());
+        return CTL_ERR_INVALID;
+    }
+    return CTL_OK;
+}

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define CTL_ABI_VERSION 1
+#define CTL_ABI_VERSION 2   /* 2: round 4 (ctl_env_light 112 B, ctl_fb_reduce d_out, wide-tree reads) */
 
 #if defined(_WIN32)
 #define CTL_API __declspec(dllexport)
@@ -252,11 +252,14 @@ enum {
      * ((h & 0x7fff) << 13) + 0x38000000, i.e. +0 -> 2^-15); off = IEEE decode
      * like its CUDA path (__half2float).  The oracle supports both.          */
     CTL_SCENE_HALF_HOST_QUIRK = 1u << 0,
-    /* traverse the uploaded binary BVH in the reference's visit order, so an
-     * exact-t tie goes to the first triangle found (TraceHelper.cu:121,650).
+    /* traverse the uploaded binary BVH in the reference's own (host) visit
+     * order: every hit, ties included, is the reference CPU traversal's
+     * (BVHTraversal.h:122-232, TraceHelper.cu:88-172).
      * Off (default): the backend collapses each tree into 4-wide 128-B nodes
-     * on upload and resolves exact-t ties to the lowest (triangle, node);
-     * every other hit is identical.                                          */
+     * on upload and traverses them in its own per-ray order:
+     * deterministic (a function of the ray alone), first-found ties; it can
+     * differ from the reference where two triangles tie exactly or a box's
+     * rounded entry lies past the hit inside it (counted in DESIGN.md §5).    */
     CTL_SCENE_BINARY_BVH = 1u << 1,
     /* re-encode the 4-wide trees as 64-B nodes with 8-bit child bounds on a
      * per-node power-of-two grid, rounded outward (csrc/ctl_qnode.h): half the
@@ -399,7 +402,10 @@ enum {
  * ctl_scene_animate the device's own epsilon (from the moved scene box) stays
  * until the instances are uploaded again (CTL_DIRTY_NODES).  Those two calls
  * edit device arrays only: marking such an array dirty uploads the desc's
- * version again.  Without an uploaded scene this is ctl_scene_upload. */
+ * version again, and after them any tree group (BVH, TRI_INDICES, MESHES,
+ * NODES) re-uploads every array they edit (TRI_DATA, WOOP, BVH, NODES,
+ * LIGHTS, ENV), so geometry, instances, lights and the environment's scene
+ * sphere all return to the desc together.  Without an uploaded scene this is ctl_scene_upload. */
 CTL_API ctl_status ctl_scene_update(ctl_ctx* ctx, const ctl_scene_desc* desc, uint32_t dirty, void* stream);
 
 /* DynamicScene::SetNodeTransform (Engine/DynamicScene.cpp:433-443) +
@@ -488,7 +494,8 @@ CTL_API ctl_status ctl_comm_destroy(void* comm);
  * root (ncclReduce, fp32 sum).  d_fb is only read: each rank keeps
  * accumulating its own pixels into it, so the reduce may run after any step and
  * any number of times (d_out then holds the image of all passes so far; it must
- * not alias d_fb, and is ignored on the other ranks).  Every rank calls it with
+ * not alias d_fb; it is required on the root (CTL_ERR_INVALID when NULL there)
+ * and ignored on the other ranks).  Every rank calls it with
  * its own ctx and stream; asynchronous on `stream`.  RCCL is loaded on first
  * use (CTL_ERR_NODEVICE when it cannot be). */
 CTL_API ctl_status ctl_fb_reduce(ctl_ctx* ctx, void* comm, const ctl_pixel* d_fb, ctl_pixel* d_out,
@@ -535,7 +542,16 @@ enum {
     CTL_ARRAY_LIGHT_TRIS = 11, /* ctl_light_tri       */
     CTL_ARRAY_LIGHT_CDF = 12,  /* float               */
     CTL_ARRAY_SCENE_BOX = 13,  /* 6 floats: min xyz, max xyz (after set_transform / animate) */
-    CTL_ARRAY_ENV = 14         /* ctl_env_light       */
+    CTL_ARRAY_ENV = 14,        /* ctl_env_light       */
+    /* the 4-wide trees the default traversal walks (CTL_ERR_STATE under
+     * CTL_SCENE_BINARY_BVH): 128-B nodes {lo_x, hi_x, lo_y, hi_y, lo_z, hi_z}
+     * float[4] each + int32 child[4] + pad[4] (64-B quantized nodes under
+     * CTL_SCENE_WIDE_QUANT, csrc/ctl_qnode.h); child >= 0 a node of the same
+     * tree, < 0 a leaf (mesh trees: ~((first entry << 3) | count 1..7, 0 = 8 or
+     * more); instance tree: ~node), 0x76543210 an empty slot.                */
+    CTL_ARRAY_WIDE_BVH = 15,       /* all mesh trees                          */
+    CTL_ARRAY_SCENE_WIDE_BVH = 16, /* the instance tree (root at node 0)      */
+    CTL_ARRAY_MESH_WIDE_BASE = 17  /* uint32 per mesh: its tree's first node  */
 };
 CTL_API ctl_status ctl_scene_read(ctl_ctx* ctx, uint32_t array, uint64_t first, uint64_t count, void* host_dst);
 
@@ -670,6 +686,16 @@ CTL_API ctl_status ctl_render_pass_stats(ctl_ctx* ctx, const ctl_pt_params* para
  * reference's binary order, out[1] for the 4-wide tree the upload collapses it
  * into.  CTL_ERR_INVALID on a malformed tree (ctl_host_last_error).  Caps at
  * 1024 (a bound above the cap reads 1025). */
+/* The 4-wide trees ctl_scene_upload builds from desc (bvh_nodes, tri_indices,
+ * meshes, scene_bvh_nodes / scene_start_node), in the CTL_ARRAY_WIDE_BVH /
+ * _SCENE_WIDE_BVH / _MESH_WIDE_BASE layouts (float nodes).  Query the sizes
+ * with NULL outputs; *n_mesh_nodes / *n_scene_nodes are always set.
+ * wbase_out holds desc->n_meshes entries.  CTL_ERR_INVALID on a malformed
+ * tree or too small a capacity. */
+CTL_API ctl_status ctl_host_wide_trees(const ctl_scene_desc* desc, void* mesh_out, uint64_t mesh_capacity,
+                                       uint64_t* n_mesh_nodes, uint32_t* wbase_out, void* scene_out,
+                                       uint64_t scene_capacity, uint64_t* n_scene_nodes);
+
 CTL_API ctl_status ctl_host_bvh_stack_bound(const ctl_bvh_node* nodes, uint64_t n_nodes, int32_t root_value,
                                             int32_t out[2]);
 

@@ -12,8 +12,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(_HERE, "_build", "liboracle.so")
 _lib = None
 
-TIE_FIRST_FOUND = 0
-TIE_MIN_INDEX = 1
+TIE_FIRST_FOUND = 0   # the reference's binary visit order (the reference semantics)
+TIE_MIN_INDEX = 1     # round-3 device rule, kept for comparison
+TRAVERSE_WIDE = 2     # the product's 4-wide per-ray order over trees registered with oracle_set_wide
 
 
 def build():
@@ -30,6 +31,7 @@ def load():
     L = C.CDLL(LIB)
     vp = C.c_void_p
     sig = {
+        "oracle_set_wide": (None, [C.POINTER(SceneDesc), vp, C.c_uint64, vp, C.c_uint32, vp, C.c_uint64]),
         "oracle_woop_set": (None, [vp, vp, vp, vp]),
         "oracle_woop_get": (None, [vp, vp, vp, vp]),
         "oracle_xorwow_uniforms": (None, [C.c_uint64, C.c_uint64, C.c_uint64, vp]),

@@ -174,7 +174,13 @@ struct SceneView {
     bool quirk() const { return (d->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0; }
 };
 
-enum TieMode { TIE_FIRST_FOUND = 0, TIE_MIN_INDEX = 1 };
+// Traversal modes: TIE_FIRST_FOUND = the reference's binary visit order
+// (BVHTraversal.h host branch, TraceHelper.cu:121); TIE_MIN_INDEX = that order
+// with the round-3 device rule (exact-t ties to the lowest (triangle, node),
+// boxes culled 2^14 ulps late), kept for the regression digests of round 3;
+// TRAVERSE_WIDE = the product's 4-wide per-ray order (trace_two_level_wide)
+// over the 4-wide trees registered with oracle_set_wide.
+enum TieMode { TIE_FIRST_FOUND = 0, TIE_MIN_INDEX = 1, TRAVERSE_WIDE = 2 };
 
 struct Hit {
     float t; float u, v; uint32_t tri; uint32_t node;
@@ -192,8 +198,12 @@ bool scene_has_alpha(const ctl_scene_desc* d) {   // DynamicScene.cpp:586 doAlph
     return false;
 }
 
+bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
+                          Stats* st, bool alpha);
+
 bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
                      int tie, Stats* st, bool alpha = false) {
+    if (tie == TRAVERSE_WIDE) return trace_two_level_wide(S, ori, dir, spanTmin, triTmin, h, anyHit, st, alpha);
     const ctl_scene_desc* d = S.d;
     if (d->n_nodes == 0) return false;
     const float* sceneNodes = reinterpret_cast<const float*>(d->scene_bvh_nodes);
@@ -249,6 +259,217 @@ bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float t
         return traceray_template(ol, dl, h.t, spanTmin, triClb, meshNodes, (int)mesh.bvh_node_offset, 0, st, slack);
     };
     return traceray_template(ori, dir, h.t, spanTmin, instClb, sceneNodes, 0, d->scene_start_node, st, slack);
+}
+
+// ---------------------------------------------------------------------------
+// The product's 4-wide per-ray order (NOT a reference function).
+//
+// The default device traversal (cudatracerlib_amd/csrc/device/traverse.h,
+// Traverser<..., WIDE>) walks 4-wide trees collapsed from the reference's
+// binary ones (host/bvh_wide.h) in its own order.  This is a sequential
+// statement of that order, so the GPU path can be held to it bit for bit; how
+// far it lands from the reference's binary order (trace_two_level, tie 0) is
+// measured separately (tests/test_reference_order.py).  The trees themselves
+// are inputs, registered per scene with oracle_set_wide (read back from the
+// device or built by the library's host collapse), like the binary arrays.
+//
+// Order: per node the slabs of the four children (near/far plane chosen by the
+// sign of idir), entry/exit spans as kepler_math on the fp32 bits, children
+// whose span is non-empty against `tcull` sorted near-first by a fixed
+// 5-comparator network, the nearest taken, the rest pushed far-to-near, one
+// leaf postponed.  Inside a mesh a lane holding a postponed leaf keeps walking
+// (with the same tcull) until it reaches its next leaf; then the postponed
+// leaf, that leaf and any leaves stacked right behind it are tested, and
+// tcull becomes the closest hit.  The instance level stops at its first leaf.
+// Woop test and first-found ties exactly as TraceHelper.cu:118-161.
+// ---------------------------------------------------------------------------
+struct WideTrees {
+    const void* key_nodes = nullptr;   // the desc arrays the trees were built for
+    const void* key_scene = nullptr;
+    uint64_t key_n = 0;
+    std::vector<float> mesh;           // 32 floats (128 B) per node: lo_x hi_x lo_y hi_y lo_z hi_z child pad
+    std::vector<uint32_t> wbase;       // first node of each mesh's tree
+    std::vector<float> scene;          // the instance tree (root at node 0)
+    bool set = false;
+};
+WideTrees g_wide;
+std::mutex g_wide_mtx;
+
+const WideTrees& wide_trees_for(const ctl_scene_desc* d) {
+    if (!g_wide.set || g_wide.key_nodes != (const void*)d->bvh_nodes || g_wide.key_n != d->n_bvh_nodes ||
+        g_wide.key_scene != (const void*)d->scene_bvh_nodes || g_wide.wbase.size() < d->n_meshes) {
+        std::fprintf(stderr, "oracle: TRAVERSE_WIDE without 4-wide trees registered for this scene (oracle_set_wide)\n");
+        std::abort();
+    }
+    return g_wide;
+}
+
+struct WRay {
+    float ox, oy, oz, dx, dy, dz, idx, idy, idz, oodx, oody, oodz;
+    void set(V3 o, V3 d) {
+        ox = o.x; oy = o.y; oz = o.z; dx = d.x; dy = d.y; dz = d.z;
+        const float ooeps = powf(2.0f, -80.0f);   // TraceHelper.cu:412
+        idx = 1.0f / (fabsf(d.x) > ooeps ? d.x : o_copysign(ooeps, d.x));
+        idy = 1.0f / (fabsf(d.y) > ooeps ? d.y : o_copysign(ooeps, d.y));
+        idz = 1.0f / (fabsf(d.z) > ooeps ? d.z : o_copysign(ooeps, d.z));
+        oodx = ox * idx; oody = oy * idy; oodz = oz * idz;
+    }
+};
+
+bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
+                          Stats* st, bool alpha) {
+    const ctl_scene_desc* d = S.d;
+    if (d->n_nodes == 0) return false;
+    const WideTrees& W = wide_trees_for(d);
+    const float* tris = reinterpret_cast<const float*>(d->woop_tris);
+    const bool single = d->scene_start_node < 0;
+    std::vector<int> stack;
+    stack.reserve(64);
+    stack.push_back(EntrypointSentinel);
+    auto pop = [&]() -> int {
+        if (stack.empty()) return EntrypointSentinel;
+        const int v = stack.back();
+        stack.pop_back();
+        return v;
+    };
+    WRay world, cur;
+    world.set(ori, dir);
+    cur = world;
+    int level = 0, nodeAddr = 0, leafAddr = 0;
+    size_t meshSent = 0;
+    uint32_t wnodeBase = 0, triBase = 0, idxBase = 0, triOffset = 0, inst = 0;
+    float tcull = h.t;
+    const int tminBits = as_int(spanTmin);
+    bool found = false;
+    auto enter = [&](uint32_t node) {   // TraceHelper.cu:91-100
+        if (st) st->inst++;
+        inst = node;
+        const ctl_node& N = d->nodes[node];
+        const ctl_kernel_mesh& M = d->meshes[N.mesh_index];
+        wnodeBase = W.wbase[N.mesh_index];
+        triBase = M.bvh_triangle_offset; idxBase = M.bvh_indices_offset; triOffset = M.triangle_offset;
+        M44 modl = S.inv(node);
+        cur.set(transformPoint(modl, v3(world.ox, world.oy, world.oz)),
+                transformDirection(modl, v3(world.dx, world.dy, world.dz)));
+    };
+    // one Woop test (TraceHelper.cu:118-161); true = any-hit termination
+    auto test = [&](uint32_t e) -> bool {
+        const float* v = tris + 4 * ((size_t)triBase + (size_t)e * 3);
+        const uint32_t index = d->tri_indices[idxBase + e];
+        if (st) st->tris++;
+        float Oz = v[3] - cur.ox * v[0] - cur.oy * v[1] - cur.oz * v[2];
+        float invDz = 1.0f / (cur.dx * v[0] + cur.dy * v[1] + cur.dz * v[2]);
+        float t = Oz * invDz;
+        if (t > triTmin && t < h.t) {
+            float Ox = v[7] + cur.ox * v[4] + cur.oy * v[5] + cur.oz * v[6];
+            float Dx = cur.dx * v[4] + cur.dy * v[5] + cur.dz * v[6];
+            float u = Ox + t * Dx;
+            if (u >= 0.0f) {
+                float Oy = v[11] + cur.ox * v[8] + cur.oy * v[9] + cur.oz * v[10];
+                float Dy = cur.dx * v[8] + cur.dy * v[9] + cur.dz * v[10];
+                float vv = Oy + t * Dy;
+                const uint32_t gtri = (index >> 1) + triOffset;
+                if (vv >= 0.0f && u + vv <= 1.0f && (!alpha || alpha_survives(d, gtri, inst, u, vv))) {
+                    h.node = inst; h.tri = gtri; h.u = u; h.v = vv; h.t = t;
+                    found = true;
+                    if (anyHit) return true;
+                }
+            }
+        }
+        return false;
+    };
+    // a counted leaf child ~((first << 3) | count), count 0 = walk the last-in-leaf flags
+    auto leaf = [&](int value) -> bool {
+        const uint32_t code = (uint32_t)~value;
+        const uint32_t first = code >> 3, cnt = code & 7u;
+        if (first == 214783647u) return false;   // the reference's skipped leaf value (BVHTraversal.h:221)
+        if (cnt == 0) {
+            for (uint32_t e = first;; e++) {
+                if (test(e)) return true;
+                if (d->tri_indices[idxBase + e] & 1u) break;
+            }
+            return false;
+        }
+        for (uint32_t i = 0; i < cnt; i++)
+            if (test(first + i)) return true;
+        return false;
+    };
+    if (single) {
+        enter(~(uint32_t)d->scene_start_node);
+        level = 1;
+    }
+    for (;;) {
+        const bool spec = level == 1;
+        const float* tree = level ? W.mesh.data() + 32 * (size_t)wnodeBase : W.scene.data();
+        const int tBits = as_int(tcull);
+        const bool nx = as_int(cur.idx) < 0, ny = as_int(cur.idy) < 0, nz = as_int(cur.idz) < 0;
+        while ((unsigned)nodeAddr < (unsigned)EntrypointSentinel && (spec || leafAddr >= 0)) {
+            if (st) st->nodes++;
+            const float* n = tree + 32 * (size_t)nodeAddr;
+            int k[4], c[4];
+            for (int i = 0; i < 4; i++) {
+                const float lx = n[i], hx = n[4 + i], ly = n[8 + i], hy = n[12 + i], lz = n[16 + i], hz = n[20 + i];
+                const float nX = (nx ? hx : lx) * cur.idx - cur.oodx, fX = (nx ? lx : hx) * cur.idx - cur.oodx;
+                const float nY = (ny ? hy : ly) * cur.idy - cur.oody, fY = (ny ? ly : hy) * cur.idy - cur.oody;
+                const float nZ = (nz ? hz : lz) * cur.idz - cur.oodz, fZ = (nz ? lz : hz) * cur.idz - cur.oodz;
+                const float cmin = as_float(imax3(as_int(nX), as_int(nY), omax(as_int(nZ), tminBits)));
+                const float cmax = as_float(imin3(as_int(fX), as_int(fY), omin(as_int(fZ), tBits)));
+                k[i] = (cmax >= cmin) ? as_int(cmin) : 0x7fffffff;
+                std::memcpy(&c[i], n + 24 + i, 4);
+            }
+            auto cx = [&](int a, int b) {
+                if (k[b] < k[a]) { std::swap(k[a], k[b]); std::swap(c[a], c[b]); }
+            };
+            cx(0, 1); cx(2, 3); cx(0, 2); cx(1, 3); cx(1, 2);
+            int m = 0;
+            for (int i = 0; i < 4; i++) m += k[i] != 0x7fffffff;
+            for (int i = m - 1; i >= 1; i--) stack.push_back(c[i]);
+            int next = m > 0 ? c[0] : pop();
+            if (next < 0 && leafAddr >= 0) {   // postpone one leaf
+                leafAddr = next;
+                next = pop();
+            }
+            nodeAddr = next;
+        }
+        bool entered = false;
+        while (leafAddr < 0) {
+            if (level == 1) {
+                if (leaf(leafAddr)) return true;
+                leafAddr = nodeAddr;
+                if (nodeAddr < 0) nodeAddr = pop();
+            } else {
+                if (leafAddr != -214783648) {
+                    enter((uint32_t)~leafAddr);
+                    stack.push_back(nodeAddr);   // pending top-level work
+                    meshSent = stack.size();
+                    stack.push_back(EntrypointSentinel);
+                    level = 1;
+                    nodeAddr = 0;
+                    leafAddr = 0;
+                    entered = true;
+                    break;
+                }
+                leafAddr = nodeAddr;
+                if (nodeAddr < 0) nodeAddr = pop();
+            }
+        }
+        tcull = h.t;
+        if (entered) continue;
+        if (nodeAddr == EntrypointSentinel) {
+            if (level == 1 && !single) {
+                stack.resize(meshSent);
+                const int saved = pop();
+                level = 0;
+                cur = world;
+                leafAddr = saved;
+                nodeAddr = saved;
+                if (saved < 0) nodeAddr = pop();
+            } else {
+                break;
+            }
+        }
+    }
+    return found;
 }
 
 // traceRay(dir, ori, TraceResult*) (TraceHelper.cu:174-180) on an Init()'ed result
@@ -1292,6 +1513,23 @@ void animate(const ctl_scene_desc* d, uint32_t anim, const float* b0, const floa
 // C API for tests (ctypes)
 // ===========================================================================
 extern "C" {
+
+// Registers the 4-wide trees of scene d for TRAVERSE_WIDE (128-B WideNode
+// records, host/bvh_wide.h layout; wbase[mesh] = first node of the mesh's tree;
+// the instance tree rooted at node 0).  Replaces the previous registration.
+void oracle_set_wide(const ctl_scene_desc* d, const void* mesh_nodes, uint64_t n_mesh_nodes, const uint32_t* wbase,
+                     uint32_t n_wbase, const void* scene_nodes, uint64_t n_scene_nodes) {
+    std::lock_guard<std::mutex> g(g_wide_mtx);
+    g_wide.key_nodes = d->bvh_nodes;
+    g_wide.key_scene = d->scene_bvh_nodes;
+    g_wide.key_n = d->n_bvh_nodes;
+    const float* m = static_cast<const float*>(mesh_nodes);
+    const float* sc = static_cast<const float*>(scene_nodes);
+    g_wide.mesh.assign(m, m + 32 * n_mesh_nodes);
+    g_wide.wbase.assign(wbase, wbase + n_wbase);
+    g_wide.scene.assign(sc, sc + 32 * n_scene_nodes);
+    g_wide.set = true;
+}
 
 void oracle_woop_set(const float* v0, const float* v1, const float* v2, float* out12) {
     woop_set(v3(v0[0], v0[1], v0[2]), v3(v1[0], v1[1], v1[2]), v3(v2[0], v2[1], v2[2]), out12);

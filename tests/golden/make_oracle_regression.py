@@ -1,6 +1,7 @@
 """Regression fixtures of the oracle itself: SHA-256 digests of small oracle
-renders (C1 PrimTracer first_f, C2 PathTracer Direct 1 / 0, WavefrontPathTracer,
-the environment light's tables).  These are NOT reference outputs (the reference
+renders (C1 PrimTracer first_f, C2 PathTracer Direct 1 / 0, WavefrontPathTracer),
+each in the reference's binary visit order (mode 0) and in the product's 4-wide
+per-ray order (mode 2, tests/helpers.py tie_rule).  These are NOT reference outputs (the reference
 ships none and cannot be built here): they pin the restatement
 against unintended changes, and the GPU parity tests pin the HIP path to it.
 
@@ -20,7 +21,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import cudatracerlib_amd as ctl  # noqa: E402
 import oracle  # noqa: E402
-from helpers import oracle_render, tie_rule  # noqa: E402
+from helpers import tie_rule  # noqa: E402
 
 
 def digest(a):
@@ -32,20 +33,23 @@ def compute():
     out = {}
     hs = ctl.HostScene().generate(1, 1.0, 64, 64)
     d = hs.compile(threads=4)
-    p = ctl.PrimParams(ctl._abi.PRIM_DRAW_MODES.index("first_f"), 7, 1.0, 100000.0, 0)
-    fb = np.zeros((64 * 64, 7), np.float32)
-    depth = np.zeros(64 * 64, np.float32)
-    rays = orc.oracle_prim_pass(C.byref(d), C.byref(p), 0, oracle.ptr(fb), oracle.ptr(depth), tie_rule(d), 4)
-    out["c1_prim_first_f_64"] = {"fb": digest(fb), "depth": digest(depth), "rays": int(rays)}
     hs2 = ctl.HostScene().generate(2, 0.05, 64, 48)
     d2 = hs2.compile(threads=4)
-    for direct in (1, 0):
-        pp = ctl.PTParams(direct, 50, 5, 1, 64, 1, 0, 0)
-        fb2, r2 = oracle_render(orc, d2, pp, 2, 64, 48, threads=4)
-        out[f"c2_path_direct{direct}_64x48x2"] = {"fb": digest(fb2), "rays": int(r2)}
-    fbw = np.zeros((64 * 48, 7), np.float32)
-    rw = orc.oracle_wpt_render_pass(C.byref(d2), 1, 50, 5, 1, 1, oracle.ptr(fbw), tie_rule(d2), 4)
-    out["c2_wpt_direct1_64x48"] = {"fb": digest(fbw), "rays": int(rw)}
+    for name, mode in (("", lambda d: 0), ("_wide", tie_rule)):
+        p = ctl.PrimParams(ctl._abi.PRIM_DRAW_MODES.index("first_f"), 7, 1.0, 100000.0, 0)
+        fb = np.zeros((64 * 64, 7), np.float32)
+        depth = np.zeros(64 * 64, np.float32)
+        rays = orc.oracle_prim_pass(C.byref(d), C.byref(p), 0, oracle.ptr(fb), oracle.ptr(depth), mode(d), 4)
+        out["c1_prim_first_f_64" + name] = {"fb": digest(fb), "depth": digest(depth), "rays": int(rays)}
+        for direct in (1, 0):
+            pp = ctl.PTParams(direct, 50, 5, 1, 64, 1, 0, 0)
+            fb2 = np.zeros((64 * 48, 7), np.float32)
+            r2 = sum(orc.oracle_render_pass(C.byref(d2), C.byref(pp), k, oracle.ptr(fb2), mode(d2), 4, 1, None)
+                     for k in range(2))
+            out[f"c2_path_direct{direct}_64x48x2" + name] = {"fb": digest(fb2), "rays": int(r2)}
+        fbw = np.zeros((64 * 48, 7), np.float32)
+        rw = orc.oracle_wpt_render_pass(C.byref(d2), 1, 50, 5, 1, 1, oracle.ptr(fbw), mode(d2), 4)
+        out["c2_wpt_direct1_64x48" + name] = {"fb": digest(fbw), "rays": int(rw)}
     return out
 
 

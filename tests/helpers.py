@@ -42,8 +42,8 @@ def camera_rays(desc, w, h, seed=0):
     return r
 
 
-def oracle_intersect(orc, desc, rays, any_hit=False, tie=None, threads=0):
-    tie = tie_rule(desc) if tie is None else tie
+def oracle_intersect(orc, desc, rays, any_hit=False, tie=None, threads=0, trees=None):
+    tie = tie_rule(desc, orc, trees) if tie is None else tie
     n = rays.shape[0]
     hits = np.zeros((n, 4), np.int32)
     orc.oracle_intersect(C.byref(desc), n, oracle.ptr(rays), oracle.ptr(hits), 1 if any_hit else 0, tie, threads)
@@ -63,11 +63,61 @@ def oracle_trace(orc, desc, rays, mode=0, tie=0, threads=0):
     return t, u, v, tri, node, st
 
 
-def tie_rule(desc):
-    """Oracle tie rule matching the device traversal the scene selects: the
-    reference's first-found order for CTL_SCENE_BINARY_BVH, else the wide
-    BVH's lowest-(triangle, node) rule (oracle TIE_MIN_INDEX = 1)."""
-    return 0 if desc.flags & 2 else 1
+_WIDE_KEY = [None]
+
+
+def _addr(p):
+    return C.cast(p, C.c_void_p).value or 0
+
+
+def _sample_digest(desc):
+    """Digest of the first and last binary nodes and of the mesh records (a freed
+    scene's addresses can be reused by the next one)."""
+    import hashlib
+    h = hashlib.sha1()
+    n = int(desc.n_bvh_nodes)
+    for first in (0, max(0, n - 64)):
+        k = min(64, n - first)
+        if k > 0:
+            h.update(C.string_at(_addr(desc.bvh_nodes) + 64 * first, 64 * k))
+    if desc.n_meshes:
+        h.update(C.string_at(_addr(desc.meshes), 20 * desc.n_meshes))
+    if desc.n_scene_bvh_nodes:
+        h.update(C.string_at(_addr(desc.scene_bvh_nodes), 64 * min(64, desc.n_scene_bvh_nodes)))
+    return h.hexdigest()
+
+
+def device_wide_trees(tracer, uploaded):
+    """The 4-wide trees as the device holds them (after a refit by animate /
+    set_transform, whose topology is the uploaded desc's), for tie_rule(trees=)."""
+    return tracer.wide_trees(uploaded)
+
+
+def register_wide(orc, desc, trees=None):
+    """Hand the scene's 4-wide trees to the oracle (oracle_set_wide): the given
+    (device read-back) trees, else the library's host collapse of desc, which is
+    what the upload builds (tests/test_reference_order.py checks the two agree)."""
+    import cudatracerlib_amd as ctl
+    mesh, wbase, sc = trees if trees is not None else ctl.host_wide_trees(desc)
+    orc.oracle_set_wide(C.byref(desc), oracle.ptr(mesh), mesh.shape[0], oracle.ptr(wbase), wbase.size,
+                        oracle.ptr(sc), sc.shape[0])
+
+
+def tie_rule(desc, orc=None, trees=None):
+    """Oracle traversal mode matching the device traversal the scene selects:
+    the reference's own binary order for CTL_SCENE_BINARY_BVH (0), else the
+    product's 4-wide per-ray order (oracle.TRAVERSE_WIDE = 2) over the same
+    4-wide trees, registered here."""
+    if desc.flags & 2:
+        return 0
+    orc = orc or oracle.load()
+    key = (_addr(desc.bvh_nodes), desc.n_bvh_nodes, _addr(desc.scene_bvh_nodes), desc.n_scene_bvh_nodes,
+           _addr(desc.tri_indices), desc.n_tri_indices, _addr(desc.meshes), desc.flags & 4, desc.scene_start_node,
+           _sample_digest(desc))
+    if trees is not None or _WIDE_KEY[0] != key:
+        register_wide(orc, desc, trees)
+        _WIDE_KEY[0] = None if trees is not None else key
+    return 2
 
 
 def binary_bvh(desc):
@@ -89,12 +139,13 @@ def select_bvh(desc, bvh):
             "binary": binary_bvh(desc) if bvh == "binary" else desc}[bvh]
 
 
-def oracle_render(orc, desc, params, passes, w, h, threads=0, fb=None, first_pass=0):
+def oracle_render(orc, desc, params, passes, w, h, threads=0, fb=None, first_pass=0, trees=None):
     if fb is None:
         fb = np.zeros((w * h, 7), np.float32)
     rays = 0
     for p in range(first_pass, first_pass + passes):
-        rays += orc.oracle_render_pass(C.byref(desc), C.byref(params), p, oracle.ptr(fb), tie_rule(desc), threads, 1,
+        rays += orc.oracle_render_pass(C.byref(desc), C.byref(params), p, oracle.ptr(fb), tie_rule(desc, orc, trees),
+                                       threads, 1,
                                        None)
     return fb, rays
 
@@ -125,3 +176,77 @@ def cross_rank_strays(orc, pass_index, w, h, ranks, tile=64):
     inside = (lx < w) & (ly < h)
     land = ((ly // tile) * tx + lx // tile) % ranks
     return int(((own != land) & inside).sum())
+
+
+def grid_room(ctl, offset, n=24, size=4.0, w=64, h=64):
+    """Axis-aligned box room translated to `offset`: six walls and three inner
+    slabs, each an n x n grid of quads (two triangles), one diffuse material.
+    Flat walls made of many triangles whose boxes touch, far from the origin
+    when offset is large: the worst case for the slab arithmetic
+    (lo * idir - o * idir) and for the Woop t of grazing rays.  Returns
+    (host scene, desc); the host scene owns the desc's arrays."""
+    verts, idx = [], []
+    o = np.array(offset, np.float64)
+
+    def wall(origin, u, v):
+        b = len(verts)
+        for j in range(n + 1):
+            for i in range(n + 1):
+                verts.append(origin + u * (i / n) + v * (j / n))
+        for j in range(n):
+            for i in range(n):
+                a = b + j * (n + 1) + i
+                idx.append((a, a + 1, a + n + 2))
+                idx.append((a, a + n + 2, a + n + 1))
+
+    ex, ey, ez = np.eye(3) * size
+    wall(o, ex, ey); wall(o + ez, ey, ex); wall(o, ey, ez)
+    wall(o + ex, ez, ey); wall(o, ez, ex); wall(o + ey, ex, ez)
+    for k in range(1, 4):
+        wall(o + ex * (k / 4) + ey * 0.1 + ez * 0.1, ey * 0.5, ez * 0.5)
+    s = ctl.HostScene()
+    m = s.add_mesh(np.array(verts, np.float32), np.array(idx, np.uint32), [ctl.diffuse_material(0.5, 0.5, 0.5)])
+    s.add_node(m)
+    c = o + size / 2
+    s.set_camera(tuple(c - [0, 0, size * 0.4]), tuple(c), (0, 1, 0), 60.0, w, h)
+    return s, s.compile()
+
+
+def grazing_rays(desc, offset, n, seed, size=4.0):
+    """Rays starting on (or 1e-4 off) the room's walls, nearly parallel to the
+    wall they start on (that axis' direction component scaled by 1e-7..1e-2)."""
+    rng = np.random.default_rng(seed)
+    o = np.array(offset, np.float64)
+    orig = o + rng.random((n, 3)) * size
+    ax = rng.integers(0, 3, n)
+    orig[np.arange(n), ax] = (o[ax] + np.where(rng.random(n) < 0.5, 0.0, size)
+                              + rng.normal(0, 1e-4, n) * (rng.random(n) < 0.5))
+    d = rng.normal(size=(n, 3))
+    d[np.arange(n), ax] *= 10.0 ** rng.uniform(-7, -2, n)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r = np.zeros((n, 8), np.float32)
+    r[:, 0:3] = orig
+    r[:, 3] = np.float32(desc.ray_eps)
+    r[:, 4:7] = d
+    r[:, 7] = 3.0e38
+    return r
+
+
+def classify_orders(ref, other):
+    """Per-ray comparison of two batch results (ctl_hit rows): the reference's
+    binary order vs another traversal order over the same scene.  ties: same t,
+    another triangle (both exact-t candidates; first found differs);
+    ref_culled: the other order found a strictly closer hit (a box whose rounded
+    slab entry lies past a hit inside it was culled on the reference's path);
+    other_culled: the reference found a strictly closer hit; hit_miss: one
+    side hit, the other missed."""
+    rt, ot = ref[:, 0].view(np.float32), other[:, 0].view(np.float32)
+    rh, oh = ref[:, 2] >= 0, other[:, 2] >= 0
+    diff = (ref != other).any(axis=1)
+    both = rh & oh
+    return {"rays": int(ref.shape[0]), "differ": int(diff.sum()),
+            "ties": int((diff & both & (rt == ot) & (ref[:, 2] != other[:, 2])).sum()),
+            "ref_culled": int((diff & both & (ot < rt)).sum()),
+            "other_culled": int((diff & both & (rt < ot)).sum()),
+            "hit_miss": int((diff & (rh != oh)).sum()),
+            "same_hit_other_fields": int((diff & both & (rt == ot) & (ref[:, 2] == other[:, 2])).sum())}

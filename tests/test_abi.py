@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert abi.load().ctl_abi_version() == 1
+    assert abi.load().ctl_abi_version() == 2   # round 4: ctl_env_light 112 B, ctl_fb_reduce d_out, wide-tree reads
 
 
 def test_reference_layout_sizes():

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import oracle
-from helpers import binary_bvh, oracle_intersect, oracle_render, random_rays, tie_rule
+from helpers import binary_bvh, device_wide_trees, oracle_intersect, oracle_render, random_rays
 
 
 def skinned_tube(nseg=24, nring=16, radius=0.5, length=4.0):
@@ -235,7 +235,8 @@ def test_animated_traversal_and_render_bit_exact(ctl, orc, dev, bvh):
     pt.animate(0, f0, f1, 0.6)
     d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.6)
     rays = random_rays(d2, 20000, seed=3, tmin=d2.ray_eps)   # batch tmin = traceRay's eps (brute force below)
-    want = oracle_intersect(orc, d2, rays, tie=tie_rule(d2))
+    trees = None if bvh == "binary" else device_wide_trees(pt, d)   # refit boxes, the upload's topology
+    want = oracle_intersect(orc, d2, rays, trees=trees)
     r = torch.from_numpy(rays).to(dev)
     hits = torch.zeros((rays.shape[0], 4), dtype=torch.int32, device=dev)
     pt.intersect_buffers(rays.shape[0], r.data_ptr(), hits.data_ptr(), False)
@@ -249,7 +250,7 @@ def test_animated_traversal_and_render_bit_exact(ctl, orc, dev, bvh):
     orc.oracle_brute_force(C.byref(d2), rays.shape[0], oracle.ptr(rays), oracle.ptr(bt), oracle.ptr(btri), 0)
     assert np.array_equal(got[:, 0].view(np.float32)[hit], bt[hit])
     p = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
-    want_fb, wrays = oracle_render(orc, d2, p, 2, w, h)
+    want_fb, wrays = oracle_render(orc, d2, p, 2, w, h, trees=trees)
     fb = torch.zeros((w * h, 7), dtype=torch.float32, device=dev)
     pt.params = p
     pt.reset_rays()

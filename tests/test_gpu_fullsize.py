@@ -10,7 +10,7 @@ import time
 import numpy as np
 import pytest
 
-from helpers import binary_bvh, oracle_render
+from helpers import binary_bvh, oracle_render, tie_rule
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 
@@ -138,17 +138,16 @@ def test_full_size_c3_reference_dopass_loop(ctl, dev, c3):
     assert max(up[1:]) < 1e-3, up
 
 
-def test_full_size_c4_eight_rank_shards(ctl, orc, dev, c3):
-    """BASELINE configs[3] (C4) on one GPU: the 10M-triangle C3 scene at 1080p
-    sharded over 8 ranks (tile % 8 == rank, IBlockSampler.h:100-108), each
-    rank's 8 passes in one ctl_render_passes launch (the bench's N = 8 step).
-    The 8 rank framebuffers sum bit for bit to the 1-rank framebuffer of the same
-    passes (every pixel has one owner, Image.cu:22-44 adds in the 1-GPU order);
-    rank 0's framebuffer equals the oracle's rank-0 render on every 97th pixel;
-    the ranks' rays add up to the 1-rank count plus the few apron paths a rank
-    traces for its neighbours; no stack overflow (ctl_sync)."""
-    _, d = c3
-    N, first = 8, 64
+def eight_rank_shards(ctl, orc, d, dev, first):
+    """The scene at 1080p sharded over 8 ranks (tile % 8 == rank,
+    IBlockSampler.h:100-108), each rank's 8 passes in one ctl_render_passes
+    launch (the bench's N = 8 step): the 8 rank framebuffers sum bit for bit to
+    the 1-rank framebuffer of the same passes (every pixel has one owner,
+    Image.cu:22-44 adds in the 1-GPU order); rank 0's framebuffer equals the
+    oracle's rank-0 render on every 97th pixel; the ranks' rays add up to the
+    1-rank count plus the few apron paths a rank traces for its neighbours; no
+    stack overflow (ctl_sync)."""
+    N = 8
     pt = ctl.PathTracer(0)
     try:
         pt.upload_scene(d)
@@ -185,7 +184,7 @@ def test_full_size_c4_eight_rank_shards(ctl, orc, dev, c3):
     want = np.zeros((W * H, 7), np.float32)
     p0 = ctl.PTParams(1, 50, 5, 1, 64, N, 0, 0)
     for p in range(first, first + N):
-        orc.oracle_render_pass(C.byref(d), C.byref(p0), p, oracle.ptr(want), 1, ORACLE_THREADS, 97, None)
+        orc.oracle_render_pass(C.byref(d), C.byref(p0), p, oracle.ptr(want), tie_rule(d), ORACLE_THREADS, 97, None)
     lin = np.arange(W * H)
     ok = lin % 97 == 0
     for p in range(first, first + N):
@@ -205,13 +204,30 @@ def test_full_size_c4_eight_rank_shards(ctl, orc, dev, c3):
     assert np.array_equal(rank0[ok].view(np.uint32), want[ok].view(np.uint32))
 
 
-def test_full_size_c5_pass_bit_exact(ctl, orc, dev, c3):
+def test_full_size_c4_eight_rank_shards(ctl, orc, dev, c3):
+    """BASELINE configs[3] (C4) on one GPU: the 10M-triangle C3 scene, 8 ranks."""
+    eight_rank_shards(ctl, orc, c3[1], dev, 64)
+
+
+@pytest.fixture(scope="module")
+def c5(ctl, c3):
     c3[0].close()                      # free the C3 host arrays first
     hs = ctl.HostScene().generate(5, 1.0, W, H)
-    try:
-        d = hs.compile()
-        assert d.n_tri_data > 9_900_000 and d.n_textures >= 2
-        p = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
-        check(*full_pass(ctl, orc, d, dev, p)[:4])
-    finally:
-        hs.close()
+    d = hs.compile()
+    assert d.n_tri_data > 9_900_000 and d.n_textures >= 2
+    yield hs, d
+    hs.close()
+
+
+def test_full_size_c5_pass_bit_exact(ctl, orc, dev, c5):
+    p = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
+    check(*full_pass(ctl, orc, c5[1], dev, p)[:4])
+
+
+def test_full_size_c5_eight_rank_shards(ctl, orc, dev, c5):
+    """BASELINE configs[4] (C5: roughdielectric + MIP-mapped textures, 10 M
+    triangles, 1080p, 8 GPUs) in its multi-GPU form on one GPU: the full-shading
+    path kernel (path_kernel_persistent FULL) renders each rank's 8 passes in one
+    launch; the rank images sum bit for bit to the 1-rank image, rank 0 equals the
+    oracle's rank render, ray counts add up."""
+    eight_rank_shards(ctl, orc, c5[1], dev, 72)

@@ -9,7 +9,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from helpers import binary_bvh, oracle_intersect, oracle_render, random_rays
+from helpers import binary_bvh, device_wide_trees, oracle_intersect, oracle_render, random_rays
 
 pytestmark = pytest.mark.gpu
 
@@ -190,6 +190,7 @@ def test_set_transform_on_device_matches_recompiled_scene(ctl, orc, dev, bvh):
         lights = pt.read_array(A.CTL_ARRAY_LIGHTS, 0, d2.n_lights, np.uint32, 12)
         eps = pt.read_array(A.CTL_ARRAY_RAY_EPS, 0, 1, np.float32, 1)
         box = pt.read_array(A.CTL_ARRAY_SCENE_BOX, 0, 1, np.float32, 6)
+        trees = None if bvh == "binary" else device_wide_trees(pt, d)   # instance tree refit on the device
         fb = torch.zeros((w * h, 7), dtype=torch.float32, device=dev)
         pt.reset_rays()
         for k in range(3):
@@ -209,7 +210,7 @@ def test_set_transform_on_device_matches_recompiled_scene(ctl, orc, dev, bvh):
     assert np.array_equal(lights, arr(d2.lights, d2.n_lights, np.uint32, 12))
     assert eps.view(np.uint32)[0, 0] == np.float32(d2.ray_eps).view(np.uint32)
     assert np.array_equal(box.view(np.uint32)[0], np.array(list(d2.box_min) + list(d2.box_max), np.float32).view(np.uint32))
-    want, wrays = oracle_render(orc, d2, p, 3, w, h)
+    want, wrays = oracle_render(orc, d2, p, 3, w, h, trees=trees)
     old, _ = oracle_render(orc, d, p, 3, w, h)
     assert not np.array_equal(old.view(np.uint32), want.view(np.uint32))   # the move is visible
     assert grays == wrays

@@ -17,4 +17,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   echo "pmc group $i: $grp"
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc/g$i -o run -- python3 bench.py $ARGS > gpurun_out/pmc/g$i.json 2> gpurun_out/pmc/g$i.err || { echo "PMC group $i failed"; tail -5 gpurun_out/pmc/g$i.err; exit 1; }
 done
-python3 tools_pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.txt && cat gpurun_out/pmc/summary.txt
+python3 tools/tools_pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.txt && cat gpurun_out/pmc/summary.txt

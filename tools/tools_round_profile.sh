@@ -5,8 +5,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-./tools_profile.sh > gpurun_out/profile.log 2>&1 || { echo "PROFILE FAILED"; tail -20 gpurun_out/profile.log; exit 1; }
-./tools_pmc.sh > gpurun_out/pmc.log 2>&1 || { echo "PMC FAILED"; tail -20 gpurun_out/pmc.log; exit 1; }
+bash tools/tools_profile.sh > gpurun_out/profile.log 2>&1 || { echo "PROFILE FAILED"; tail -20 gpurun_out/profile.log; exit 1; }
+bash tools/tools_pmc.sh > gpurun_out/pmc.log 2>&1 || { echo "PMC FAILED"; tail -20 gpurun_out/pmc.log; exit 1; }
 cp gpurun_out/pmc/pmc.json profiles/r99_pmc.json   # box-local: the bench below reads the newest profile
 timeout -k 10 900 python bench.py "$@" > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { echo "BENCH FAILED"; tail -20 gpurun_out/bench_full.err; exit 1; }
 cat gpurun_out/bench_full.json

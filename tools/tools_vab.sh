@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of variant libraries (cudatracerlib_amd/_var<name>, "base" = _lib) at the driver's
-# bench shape, C3 headline + C5 leg: VARS="base p1 base p1" ./tools_vab.sh [extra bench args]
+# bench shape, C3 headline + C5 leg: VARS="base p1 base p1" bash tools/tools_vab.sh [extra bench args]
 set -o pipefail
 mkdir -p gpurun_out/vab
 export TMPDIR=/tmp
