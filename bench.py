@@ -84,8 +84,9 @@ def parse(argv=None):
                          "launch per pass, the reference's DoPass granularity)")
     ap.add_argument("--one-pass-leg", type=int, default=8,
                     help="passes of the one-launch-per-pass comparison leg (0: skip)")
-    ap.add_argument("--bvh", default="wide", choices=["wide", "wideq", "binary"],
-                    help="device traversal: 4-wide collapsed BVH, or the reference's binary order")
+    ap.add_argument("--bvh", default="wide", choices=["wide", "wideq", "w8", "binary"],
+                    help="device traversal: 4-wide collapsed BVH (wideq: 64-B quantized nodes; w8: the 8-wide "
+                         "compressed tree), or the reference's binary order")
     ap.add_argument("--dopass-leg", type=int, default=8,
                     help="passes of the reference DoPass leg (ctl_scene_update + sampler tables + one "
                          "ctl_render_pass per pass; 0: skip)")
@@ -499,6 +500,7 @@ def c5_leg(ctl, dev, torch, stream, sptr, a, threads):
     hs = ctl.HostScene().generate(5, 1.0, a.width, a.height)
     hs.set_bvh_builder(a.builder, a.sbvh_alpha)
     d = hs.compile(threads=threads)
+    apply_bvh(ctl, d, a.bvh)
     t_build = time.perf_counter() - t0
     pt = ctl.PathTracer(dev.index or 0, max_path_length=a.max_path_length, rr_start_depth=a.rr_start,
                         shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, schedule="persistent")
@@ -531,6 +533,12 @@ def c5_leg(ctl, dev, torch, stream, sptr, a, threads):
             "passes": a.c5_passes, "launches": len(ev), "ms_per_pass": round(ms / a.c5_passes, 3),
             "rays_per_pass": int(rays / a.c5_passes), "mrays_s": round(rays / (ms * 1e-3) / 1e6, 2),
             "scene_build_s": round(t_build, 1)}
+
+
+def apply_bvh(ctl, desc, bvh):
+    """The device tree format --bvh selects (a scene flag of the desc)."""
+    desc.flags |= {"wide": 0, "binary": ctl.CTL_SCENE_BINARY_BVH, "wideq": ctl._abi.CTL_SCENE_WIDE_QUANT,
+                   "w8": ctl._abi.CTL_SCENE_WIDE8}[bvh]
 
 
 def launch_check(a, world, rank):
@@ -610,10 +618,7 @@ def main(argv=None):
         hs.set_bvh_params(a.split_alpha, a.split_depth, a.bins, a.max_leaf)
     hs.set_bvh_builder(a.builder, a.sbvh_alpha)
     desc = hs.compile(threads=threads)
-    if a.bvh == "binary":
-        desc.flags |= ctl.CTL_SCENE_BINARY_BVH
-    elif a.bvh == "wideq":
-        desc.flags |= ctl._abi.CTL_SCENE_WIDE_QUANT
+    apply_bvh(ctl, desc, a.bvh)
     t_build = time.perf_counter() - t0
     log(f"[rank {rank}] scene config {a.config}: {desc.n_tri_data} tris, {desc.n_bvh_nodes} BVH nodes, "
         f"built in {t_build:.1f}s with {threads} threads")

@@ -30,6 +30,7 @@
 #include "../ctl_shade.h"
 #include "../host/bvh_wide.h"
 #include "../ctl_qnode.h"
+#include "../host/bvh_w8.h"
 
 namespace ctl {
 
@@ -639,6 +640,16 @@ CTL_API ctl_status ctl_scene_read(ctl_ctx* c, uint32_t array, uint64_t first, ui
         case CTL_ARRAY_ENV:
             if (!S.env) { c->err = "scene_read: no environment light"; return CTL_ERR_STATE; }
             src = S.env; elem = sizeof(ctl_env_light); n = 1; break;
+        case CTL_ARRAY_W8_NODES:
+        case CTL_ARRAY_W8_WOOP:
+        case CTL_ARRAY_W8_INDICES: {
+            if (!S.w8_on) { c->err = "scene_read: no 8-wide tree in use (" + c->w8_why + ")"; return CTL_ERR_STATE; }
+            const int a = array == CTL_ARRAY_W8_NODES ? SA_W8 : array == CTL_ARRAY_W8_WOOP ? SA_W8WOOP : SA_W8IDX;
+            elem = array == CTL_ARRAY_W8_NODES ? sizeof(W8Node) : array == CTL_ARRAY_W8_WOOP ? sizeof(ctl_woop_tri) : 4;
+            src = c->sarr[a].p;
+            n = c->sarr[a].bytes / elem;
+            break;
+        }
         case CTL_ARRAY_WIDE_BVH:
         case CTL_ARRAY_SCENE_WIDE_BVH:
         case CTL_ARRAY_MESH_WIDE_BASE:

@@ -542,7 +542,8 @@ struct AnimState;
 // KernelDynamicScene stream, reused by ctl_scene_update while it fits.
 enum SceneArr : int {
     SA_BVH, SA_WOOP, SA_IDX, SA_TRI, SA_MATS, SA_MESHES, SA_NODES, SA_SBVH, SA_XF, SA_IXF, SA_LIGHTS, SA_LTRIS,
-    SA_LCDF, SA_LUT, SA_TEX, SA_TEXDATA, SA_ENV, SA_ENVDATA, SA_WBVH, SA_SWBVH, SA_WBASE, SA_COUNT
+    SA_LCDF, SA_LUT, SA_TEX, SA_TEXDATA, SA_ENV, SA_ENVDATA, SA_WBVH, SA_SWBVH, SA_WBASE, SA_W8, SA_W8WOOP, SA_W8IDX,
+    SA_COUNT
 };
 struct SceneArray {
     void* p = nullptr;
@@ -592,6 +593,7 @@ struct ctl_ctx {
     hipEvent_t pass_ev[2] = {nullptr, nullptr}; // bracket the last render pass (ctl_last_pass_ms)
     bool pass_timed = false;
     size_t wide_nodes = 0;
+    std::string w8_why;                         // why the last upload kept the 4-wide traversal (CTL_SCENE_WIDE8)
     int stack_bound = 0;                        // worst-case traversal stack of the uploaded scene
     uint8_t* d_tile_flags = nullptr;            // PixelVarianceBuffer block flags
     size_t tile_flags_cap = 0;

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S_arg, PathParams
 //    pending ray are loop-carried, keeping the register peak low.
 // Work items are independent (own sampler index, own sample slot), so the
 // framebuffer is bit-identical to path_kernel's.
-template <bool STATS, bool SINGLE, bool WIDE, int FULL>
+template <bool STATS, bool SINGLE, int WIDE, int FULL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ? (FULL ? CTL_PERSIST_WAVES_FULL : CTL_PERSIST_WAVES) : 2))) void path_kernel_persistent(DevScene S_arg, PathParams P_arg, const float* s1,
                                                                  const float2* s2, uint64_t items,
                                                                  unsigned long long* cursor, unsigned long long* counters,
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
 // grid; lanes whose ray finished take the next ray from a wave-aggregated
 // atomic cursor between traversal rounds (the reference fetches per warp per
 // batch of 32 rays, :379-399), so waves stay full on incoherent rays.
-template <bool ANY, bool STATS, bool SINGLE, bool WIDE>
+template <bool ANY, bool STATS, bool SINGLE, int WIDE>
 // Two segments (rays, hits)[0, n) then (rays2, hits2)[0, n2) in one launch: the
 // wavefront tracer's payload and secondary batches share one resident grid and
 // one tail.
@@ -709,11 +709,13 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
     } while (0)
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;
+    const bool w8 = wide && single && c->scene.w8_on;
 #define IK2(AN, ST)                                                       \
     do {                                                                  \
-        if (ST) { if (single) IK(AN, true, true, false); else IK(AN, true, false, false); } \
-        else if (wide) { if (single) IK(AN, false, true, true); else IK(AN, false, false, true); } \
-        else { if (single) IK(AN, false, true, false); else IK(AN, false, false, false); } \
+        if (ST) { if (single) IK(AN, true, true, 0); else IK(AN, true, false, 0); } \
+        else if (w8) IK(AN, false, true, 2);                              \
+        else if (wide) { if (single) IK(AN, false, true, 1); else IK(AN, false, false, 1); } \
+        else { if (single) IK(AN, false, true, 0); else IK(AN, false, false, 0); } \
     } while (0)
     if (stats) { if (any_hit) IK2(true, true); else IK2(false, true); }
     else { if (any_hit) IK2(true, false); else IK2(false, false); }
@@ -827,9 +829,10 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
         } while (0)
 #define PK2(ST, SG, WD) do { if (full == kShadeEnv) PK(ST, SG, WD, kShadeEnv); else if (full == kShadeAlpha) PK(ST, SG, WD, kShadeAlpha); \
                               else if (full) PK(ST, SG, WD, kShadeFull); else PK(ST, SG, WD, kShadeLean); } while (0)
-        if (stats) { if (single) PK2(true, true, false); else PK2(true, false, false); }
-        else if (wide) { if (single) PK2(false, true, true); else PK2(false, false, true); }
-        else { if (single) PK2(false, true, false); else PK2(false, false, false); }
+        if (stats) { if (single) PK2(true, true, 0); else PK2(true, false, 0); }
+        else if (wide && single && c->scene.w8_on) PK2(false, true, 2);
+        else if (wide) { if (single) PK2(false, true, 1); else PK2(false, false, 1); }
+        else { if (single) PK2(false, true, 0); else PK2(false, false, 0); }
 #undef PK2
 #undef PK
     } else {

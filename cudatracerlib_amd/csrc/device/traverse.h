@@ -27,6 +27,8 @@
 //  * no FMA contraction (-ffp-contract=off) => bit-identical to the CPU oracle.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
+
 #include "../ctl_bsdf.h"
 
 namespace ctl {
@@ -109,6 +111,11 @@ struct DevScene {
     uint32_t alpha;              // KernelDynamicScene::doAlphaMapping (some material has an alpha map)
     uint32_t s_wnode_base;
     uint32_t quant;              // wide trees in the 64-B quantized format (ctl_qnode.h)
+    // 8-wide compressed tree of a one-mesh scene (host/bvh_w8.h), traversed when WIDE == 2
+    const float4* w8;            // 80-B nodes, five float4 each, root at node 0
+    const float4* w8_woop;       // its leaf entries' TriIntersectorData, relaid in node order
+    const uint32_t* w8_idx;      // their TriIntersectorData2 words
+    uint32_t w8_on;              // the W8 tree is present (and selected)
     // InfiniteLight (ctl_env.h): light env_index of lights[], 0xFFFFFFFF without one
     uint32_t env_index;
     const ctl_env_light* env;
@@ -228,7 +235,7 @@ __device__ __forceinline__ void xform_rows(const float4* M, f3 p, f3 d, f3& po, 
 // (__traceRay_internal__<true>, TraceHelper.cu:136-154), active when the scene
 // has alpha maps; the batch intersectKernel never alpha-tests.
 template <int ANY, bool STATS, bool SINGLE, bool WIDE = false, bool ALPHA = false>
-struct Traverser {
+struct Traverser4 {
     RayLocal cur;
     RayLocal world;   // unused when SINGLE
     HitRec h;
@@ -785,8 +792,229 @@ struct Traverser {
     }
 };
 
+// ---------------------------------------------------------------------------
+// 8-wide compressed traversal (WIDE == 2, one-mesh scenes; host/bvh_w8.h).
+//
+// Per ray: the current node group G (24-bit child base, the hit inner slots as
+// an 8-bit mask in key order, key = slot ^ octant) in registers, one group per
+// pushed level on the lane stack, the node to visit next, and up to two leaf
+// groups (a node's hit leaf entries: base + 24-bit mask over the relaid
+// entries).  Of a node's hit inner children the nearest (entry distance, its
+// low 3 bits replaced by the slot) is visited next, the others after its
+// subtree in key order.  A node visit is five
+// 16-B loads: the grid header, child / leaf bases with the leaf metadata, and
+// the 48 child planes as bytes; each slab plane is fma(q, s idir, p idir - ood)
+// on the exact grid value p + q s (q s exact, the decode folded into the slab).
+// Culling and spans as the 4-wide loop (kepler_math on the bits, against
+// tcull); children visited near-to-far by octant slot order, no sort.
+// Speculation as the 4-wide mesh level: after its first leaf group a lane
+// walks on (same tcull) to its second, then tests both and takes the new
+// distance; cut short by the wave it keeps tcull and a phantom first group.
+// The oracle restates this order (oracle/oracle.cpp trace_w8).
+// ---------------------------------------------------------------------------
+template <int ANY, bool STATS, bool ALPHA = false>
+struct Traverser8 {
+    RayLocal cur;
+    HitRec h;
+    float span_tmin, tri_tmin, tcull;
+    uint32_t grp;             // nodes left after `next`: hits8 (key order) << 24 | child base
+    int32_t next;             // the node to visit next, -1: the first slot of grp
+    uint32_t t1b, t1m, t2b, t2m;   // leaf groups: entry base, entry mask
+    uint32_t oct;             // sign bits of idir (x: 1, y: 2, z: 4)
+    uint32_t instIdx, triOffset;
+    bool held;                // a first leaf group is pending (or was tested early: phantom)
+    bool exhausted;           // no node group left
+    bool done;
+    bool anyhit;              // ANY == 2 only
+
+    __device__ __forceinline__ void init(const DevScene& S, f3 o, f3 d, float smin, float tmn, float tmaxv,
+                                         LaneStack& st, TraceStats* stats) {
+        h.t = tmaxv; h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
+        tcull = tmaxv;
+        span_tmin = smin; tri_tmin = tmn;
+        st.sp = 0;
+        st.overflow = false;
+        st.push(0);   // the empty group at the bottom
+        done = (S.n_nodes == 0);
+        exhausted = false;
+        held = false;
+        t1b = t1m = t2b = t2m = 0;
+        if (STATS) stats->inst++;
+        instIdx = ~(uint32_t)S.start_node;   // the scene's one instance (TracerayTemplate's startNode < 0)
+        f3 o2, d2;
+        xform_rows(S.inv_xf + 4 * instIdx, o, d, o2, d2);
+        cur.set(o2.x, o2.y, o2.z, d2.x, d2.y, d2.z);
+        triOffset = S.s_tri_offset;
+        oct = ((uint32_t)__float_as_int(cur.idx) >> 31) | (((uint32_t)__float_as_int(cur.idy) >> 31) << 1) |
+              (((uint32_t)__float_as_int(cur.idz) >> 31) << 2);
+        grp = 0;
+        next = 0;                   // the root
+    }
+
+    __device__ __forceinline__ bool alpha_survives(const DevScene& S, uint32_t gtri, float u, float v) const {
+        const ctl_triangle_data td = S.tri_data[gtri];
+        const ctl_material& m = S.mats[((td.w[1] >> 16) & 0xffu) + S.nodes[instIdx].material_offset];
+        if (!m.alpha_state) return true;
+        const bool q = (S.flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
+        const f2 a = mk2(half_to_float(td.w[5] & 0xffffu, q), half_to_float(td.w[5] >> 16, q));
+        const f2 b = mk2(half_to_float(td.w[6] & 0xffffu, q), half_to_float(td.w[6] >> 16, q));
+        const f2 c = mk2(half_to_float(td.w[7] & 0xffffu, q), half_to_float(td.w[7] >> 16, q));
+        const f2 uv = u * a + v * b + (1 - u - v) * c;
+        return material_alpha_test(m, TexView{S.textures, S.tex_data}, uv);
+    }
+
+    // the entries of one leaf group, ascending; true = any-hit termination
+    __device__ __forceinline__ bool leaves(const DevScene& S, uint32_t base, uint32_t mask, TraceStats* stats) {
+        while (mask) {
+            const uint32_t e = base + (uint32_t)(__ffs(mask) - 1);
+            mask &= mask - 1u;
+            const float4* tv = S.w8_woop + 3u * e;
+            const float4 v00 = tv[0], v11 = tv[1], v22 = tv[2];
+            CTL_PROF_COUNT(stats, leaf_lanes, leaf_waves);
+            if (STATS) stats->tris++;
+            float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
+            float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
+            float t = Oz * invDz;
+            if (t > tri_tmin && t < h.t) {   // TraceHelper.cu:121
+                float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
+                float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
+                float u = Ox + t * Dx;
+                if (u >= 0.0f) {
+                    float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
+                    float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
+                    float v = Oy + t * Dy;
+                    if (v >= 0.0f && u + v <= 1.0f) {
+                        const uint32_t gtri = (S.w8_idx[e] >> 1) + triOffset;
+                        if (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v)) {
+                            h.node = instIdx; h.tri = gtri; h.u = u; h.v = v; h.t = t;
+                            if (ANY == 1 || (ANY == 2 && anyhit)) { done = true; return true; }
+                        }
+                    }
+                }
+            }
+        }
+        return false;
+    }
+
+    __device__ __forceinline__ void round(const DevScene& S, LaneStack& st, TraceStats* stats) {
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        const int tminBits = __float_as_int(span_tmin);
+        const int tBits = __float_as_int(tcull);
+        const bool nx = oct & 1u, ny = oct & 2u, nz = oct & 4u;
+        while (t2m == 0 && !exhausted) {
+            if (next < 0) {
+                if ((grp >> 24) == 0) {
+                    grp = (uint32_t)st.pop();
+                    if ((grp >> 24) == 0) { exhausted = true; break; }
+                }
+                const uint32_t hits = grp >> 24;
+                next = (int32_t)((grp & 0xffffffu) + ((uint32_t)(__ffs(hits) - 1) ^ oct));
+                grp = ((hits & (hits - 1u)) << 24) | (grp & 0xffffffu);
+            }
+            CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
+            if (STATS) stats->nodes++;
+            const uint32_t node = (uint32_t)next;
+            const float4* n = S.w8 + 5u * node;
+            const float4 A = n[0];
+            uint4 B = reinterpret_cast<const uint4*>(n)[1];
+            uint4 Cx = reinterpret_cast<const uint4*>(n)[2];
+            uint4 Cy = reinterpret_cast<const uint4*>(n)[3];
+            uint4 Cz = reinterpret_cast<const uint4*>(n)[4];
+            asm volatile("" : "+v"(B.x), "+v"(B.y), "+v"(B.z), "+v"(B.w));
+            const uint32_t hw = __float_as_uint(A.w);
+            // grid steps 2^(e - 127): the exponent byte into the fp32 exponent field
+            const float sx = __uint_as_float((hw & 0xffu) << 23), sy = __uint_as_float(((hw >> 8) & 0xffu) << 23);
+            const float sz = __uint_as_float(((hw >> 16) & 0xffu) << 23);
+            const uint32_t imask = hw >> 24;
+            const float ax = sx * cur.idx, ay = sy * cur.idy, az = sz * cur.idz;
+            const float bx = __builtin_fmaf(A.x, cur.idx, -cur.oodx), by = __builtin_fmaf(A.y, cur.idy, -cur.oody);
+            const float bz = __builtin_fmaf(A.z, cur.idz, -cur.oodz);
+            // near / far plane words by the ray's direction signs
+            const uint32_t nx0 = nx ? Cx.z : Cx.x, nx1 = nx ? Cx.w : Cx.y, fx0 = nx ? Cx.x : Cx.z, fx1 = nx ? Cx.y : Cx.w;
+            const uint32_t ny0 = ny ? Cy.z : Cy.x, ny1 = ny ? Cy.w : Cy.y, fy0 = ny ? Cy.x : Cy.z, fy1 = ny ? Cy.y : Cy.w;
+            const uint32_t nz0 = nz ? Cz.z : Cz.x, nz1 = nz ? Cz.w : Cz.y, fz0 = nz ? Cz.x : Cz.z, fz1 = nz ? Cz.y : Cz.w;
+#define CTL_QB8(W, K) ((float)(((W) >> (8 * (K))) & 0xffu))
+#define CTL_SLAB2(W, K0, K1, A_, B_) \
+    __builtin_elementwise_fma(v2f{CTL_QB8(W, K0), CTL_QB8(W, K1)}, v2f{(A_), (A_)}, v2f{(B_), (B_)})
+            uint32_t hit8 = 0, nearest = 0xffffffffu;
+            // nearest hit inner child: its entry bits with the slot in the low 3 bits
+#define CTL_W8_NEAR(MN, MX, SL) \
+            nearest = min(nearest, (MX >= MN && ((imask >> (SL)) & 1u)) ? ((__float_as_uint(MN) & ~7u) | (SL)) : 0xffffffffu);
+#define CTL_W8_PAIR(WNX, WFX, WNY, WFY, WNZ, WFZ, K0, K1, S0)                                               \
+            {                                                                                               \
+                const v2f vnx = CTL_SLAB2(WNX, K0, K1, ax, bx), vfx = CTL_SLAB2(WFX, K0, K1, ax, bx);        \
+                const v2f vny = CTL_SLAB2(WNY, K0, K1, ay, by), vfy = CTL_SLAB2(WFY, K0, K1, ay, by);        \
+                const v2f vnz = CTL_SLAB2(WNZ, K0, K1, az, bz), vfz = CTL_SLAB2(WFZ, K0, K1, az, bz);        \
+                const float mn0 = __int_as_float(imax3(__float_as_int(vnx.x), __float_as_int(vny.x),        \
+                                                       max(__float_as_int(vnz.x), tminBits)));              \
+                const float mx0 = __int_as_float(imin3(__float_as_int(vfx.x), __float_as_int(vfy.x),        \
+                                                       min(__float_as_int(vfz.x), tBits)));                 \
+                const float mn1 = __int_as_float(imax3(__float_as_int(vnx.y), __float_as_int(vny.y),        \
+                                                       max(__float_as_int(vnz.y), tminBits)));              \
+                const float mx1 = __int_as_float(imin3(__float_as_int(vfx.y), __float_as_int(vfy.y),        \
+                                                       min(__float_as_int(vfz.y), tBits)));                 \
+                hit8 |= (mx0 >= mn0 ? 1u << (S0) : 0u) | (mx1 >= mn1 ? 2u << (S0) : 0u);                   \
+                CTL_W8_NEAR(mn0, mx0, (S0))                                                                 \
+                CTL_W8_NEAR(mn1, mx1, (S0) + 1)                                                             \
+            }
+            CTL_W8_PAIR(nx0, fx0, ny0, fy0, nz0, fz0, 0, 1, 0)
+            CTL_W8_PAIR(nx0, fx0, ny0, fy0, nz0, fz0, 2, 3, 2)
+            CTL_W8_PAIR(nx1, fx1, ny1, fy1, nz1, fz1, 0, 1, 4)
+            CTL_W8_PAIR(nx1, fx1, ny1, fy1, nz1, fz1, 2, 3, 6)
+#undef CTL_W8_PAIR
+#undef CTL_W8_NEAR
+#undef CTL_SLAB2
+#undef CTL_QB8
+            // hit leaf slots -> their entries' bits over leaf_base (meta: bits << 5 | offset)
+            const uint32_t lhit = hit8 & ~imask;
+            uint32_t tm = 0;
+            if (lhit) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const uint32_t m = ((i < 4 ? B.z : B.w) >> (8 * (i & 3))) & 0xffu;
+                    tm |= ((lhit >> i) & 1u) ? (m >> 5) << (m & 31u) : 0u;
+                }
+            }
+            // hit inner slots in key order (bit slot ^ oct)
+            uint32_t ih = hit8 & imask;
+            ih = (oct & 1u) ? (((ih & 0x55u) << 1) | ((ih >> 1) & 0x55u)) : ih;
+            ih = (oct & 2u) ? (((ih & 0x33u) << 2) | ((ih >> 2) & 0x33u)) : ih;
+            ih = (oct & 4u) ? (((ih & 0x0fu) << 4) | ((ih >> 4) & 0x0fu)) : ih;
+            if (ih) {
+                // the nearest inner child next; the node's other hit inner children (key order) as
+                // the group after it; the group `node` came from waits on the stack
+                const uint32_t ns = nearest & 7u;
+                if (grp >> 24) st.push((int)grp);
+                grp = ((ih & ~(1u << (ns ^ oct))) << 24) | B.x;
+                next = (int32_t)(B.x + ns);
+            } else {
+                next = -1;
+            }
+            if (tm) {
+                if (!held) { t1b = B.y; t1m = tm; held = true; }
+                else { t2b = B.y; t2m = tm; }
+            }
+            if (__popcll(__ballot(!held)) < CTL_LEAF_BREAK) break;
+        }
+        // a lane still walking towards its second leaf group when the wave stopped
+        const bool cut = held && t2m == 0 && !exhausted;
+        if (held) {
+            if (leaves(S, t1b, t1m, stats)) return;
+            if (leaves(S, t2b, t2m, stats)) return;
+        }
+        t1m = t2m = 0;
+        held = cut;   // phantom: walk on to the next leaf group with the old tcull
+        if (!cut) tcull = h.t;
+        if (exhausted) done = true;
+    }
+};
+
+template <int ANY, bool STATS, bool SINGLE, int WIDE = 0, bool ALPHA = false>
+using Traverser = typename std::conditional<WIDE == 2, Traverser8<ANY, STATS, ALPHA>,
+                                            Traverser4<ANY, STATS, SINGLE, WIDE != 0, ALPHA>>::type;
+
 // Whole traversal of one ray (megakernel, batch kernel).
-template <int ANY, bool STATS, bool SINGLE, bool WIDE = false, bool ALPHA = false>
+template <int ANY, bool STATS, bool SINGLE, int WIDE = 0, bool ALPHA = false>
 __device__ __forceinline__ bool trace_one(const DevScene& S, f3 ori, f3 dir, float span_tmin, float tri_tmin,
                                           HitRec& h, LaneStack& st, TraceStats* stats) {
     Traverser<ANY, STATS, SINGLE, WIDE, ALPHA> T;

@@ -15,6 +15,7 @@ _lib = None
 TIE_FIRST_FOUND = 0   # the reference's binary visit order (the reference semantics)
 TIE_MIN_INDEX = 1     # round-3 device rule, kept for comparison
 TRAVERSE_WIDE = 2     # the product's 4-wide per-ray order over trees registered with oracle_set_wide
+TRAVERSE_W8 = 3       # the product's 8-wide compressed order over the tree registered with oracle_set_w8
 
 
 def build():
@@ -32,6 +33,7 @@ def load():
     vp = C.c_void_p
     sig = {
         "oracle_set_wide": (None, [C.POINTER(SceneDesc), vp, C.c_uint64, vp, C.c_uint32, vp, C.c_uint64]),
+        "oracle_set_w8": (None, [C.POINTER(SceneDesc), vp, C.c_uint64, vp, vp, C.c_uint64]),
         "oracle_woop_set": (None, [vp, vp, vp, vp]),
         "oracle_woop_get": (None, [vp, vp, vp, vp]),
         "oracle_xorwow_uniforms": (None, [C.c_uint64, C.c_uint64, C.c_uint64, vp]),

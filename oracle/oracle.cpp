@@ -179,8 +179,9 @@ struct SceneView {
 // with the round-3 device rule (exact-t ties to the lowest (triangle, node),
 // boxes culled 2^14 ulps late), kept for the regression digests of round 3;
 // TRAVERSE_WIDE = the product's 4-wide per-ray order (trace_two_level_wide)
-// over the 4-wide trees registered with oracle_set_wide.
-enum TieMode { TIE_FIRST_FOUND = 0, TIE_MIN_INDEX = 1, TRAVERSE_WIDE = 2 };
+// over the 4-wide trees registered with oracle_set_wide; TRAVERSE_W8 = its
+// 8-wide compressed order (trace_w8) over the tree registered with oracle_set_w8.
+enum TieMode { TIE_FIRST_FOUND = 0, TIE_MIN_INDEX = 1, TRAVERSE_WIDE = 2, TRAVERSE_W8 = 3 };
 
 struct Hit {
     float t; float u, v; uint32_t tri; uint32_t node;
@@ -200,10 +201,19 @@ bool scene_has_alpha(const ctl_scene_desc* d) {   // DynamicScene.cpp:586 doAlph
 
 bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
                           Stats* st, bool alpha);
+bool trace_w8(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit, Stats* st,
+              bool alpha);
+bool trace_w8_sorted(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
+                     Stats* st);
 
 bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
                      int tie, Stats* st, bool alpha = false) {
     if (tie == TRAVERSE_WIDE) return trace_two_level_wide(S, ori, dir, spanTmin, triTmin, h, anyHit, st, alpha);
+    if (tie == TRAVERSE_W8) {
+        static const bool sorted = std::getenv("ORACLE_W8_SORTED") != nullptr;
+        if (sorted) return trace_w8_sorted(S, ori, dir, spanTmin, triTmin, h, anyHit, st);
+        return trace_w8(S, ori, dir, spanTmin, triTmin, h, anyHit, st, alpha);
+    }
     const ctl_scene_desc* d = S.d;
     if (d->n_nodes == 0) return false;
     const float* sceneNodes = reinterpret_cast<const float*>(d->scene_bvh_nodes);
@@ -468,6 +478,259 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
                 break;
             }
         }
+    }
+    return found;
+}
+
+// ---------------------------------------------------------------------------
+// The product's 8-wide compressed order (NOT a reference function), a
+// sequential statement of device/traverse.h Traverser8 over the tree
+// registered with oracle_set_w8 (host/bvh_w8.h layout, read back from the
+// device or built by ctl_host_w8_tree).  One-mesh scenes.
+//
+// Per node: grid steps s = 2^(e - 127), per axis a = s * idir and
+// b = fma(p, idir, -ood); each plane is fma(q, a, b) (q the byte, near / far by
+// the sign of idir); spans, culling against tcull and the hit test as the
+// 4-wide order.  Of a node's hit inner children the nearest (smallest entry,
+// its low 3 bits replaced by the slot) is visited next, the others after it
+// in increasing slot ^ octant (as a group that waits on the stack while the
+// nearest child's subtree is visited); a node's hit leaf slots form one leaf
+// group (entry mask over leaf_base).  After its first leaf group the ray walks on with the same tcull
+// until its second, tests both (entries ascending) and takes tcull = the
+// closest hit.
+// ---------------------------------------------------------------------------
+struct W8Trees {
+    const void* key_nodes = nullptr;
+    uint64_t key_n = 0;
+    std::vector<uint32_t> nodes;   // 20 words (80 B) per node
+    std::vector<float> woop;       // 12 floats per entry
+    std::vector<uint32_t> idx;
+    bool set = false;
+};
+W8Trees g_w8;
+
+bool trace_w8(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit, Stats* st,
+              bool alpha) {
+    const ctl_scene_desc* d = S.d;
+    if (d->n_nodes == 0) return false;
+    if (!g_w8.set || g_w8.key_nodes != (const void*)d->bvh_nodes || g_w8.key_n != d->n_bvh_nodes ||
+        d->scene_start_node >= 0) {
+        std::fprintf(stderr, "oracle: TRAVERSE_W8 without an 8-wide tree registered for this one-mesh scene\n");
+        std::abort();
+    }
+    const W8Trees& W = g_w8;
+    const uint32_t inst = ~(uint32_t)d->scene_start_node;
+    const ctl_kernel_mesh& mesh = d->meshes[d->nodes[inst].mesh_index];
+    if (st) st->inst++;
+    M44 modl = S.inv(inst);
+    WRay cur;
+    cur.set(transformPoint(modl, ori), transformDirection(modl, dir));
+    const uint32_t oct = ((uint32_t)as_int(cur.idx) >> 31) | (((uint32_t)as_int(cur.idy) >> 31) << 1) |
+                         (((uint32_t)as_int(cur.idz) >> 31) << 2);
+    const int tminBits = as_int(spanTmin);
+    std::vector<uint32_t> stack;
+    stack.push_back(0u);
+    uint32_t grp = 0;   // the group of nodes left to visit after `next`: hits (slot ^ oct order) << 24 | child base
+    uint32_t t1b = 0, t1m = 0, t2b = 0, t2m = 0;
+    bool held = false, exhausted = false, found = false;
+    float tcull = h.t;
+    auto leaves = [&](uint32_t base, uint32_t mask) -> bool {   // true = any-hit termination
+        for (; mask; mask &= mask - 1u) {
+            const uint32_t e = base + (uint32_t)__builtin_ctz(mask);
+            const float* v = W.woop.data() + 12 * (size_t)e;
+            if (st) st->tris++;
+            float Oz = v[3] - cur.ox * v[0] - cur.oy * v[1] - cur.oz * v[2];
+            float invDz = 1.0f / (cur.dx * v[0] + cur.dy * v[1] + cur.dz * v[2]);
+            float t = Oz * invDz;
+            if (t > triTmin && t < h.t) {
+                float Ox = v[7] + cur.ox * v[4] + cur.oy * v[5] + cur.oz * v[6];
+                float Dx = cur.dx * v[4] + cur.dy * v[5] + cur.dz * v[6];
+                float u = Ox + t * Dx;
+                if (u >= 0.0f) {
+                    float Oy = v[11] + cur.ox * v[8] + cur.oy * v[9] + cur.oz * v[10];
+                    float Dy = cur.dx * v[8] + cur.dy * v[9] + cur.dz * v[10];
+                    float vv = Oy + t * Dy;
+                    if (vv >= 0.0f && u + vv <= 1.0f) {
+                        const uint32_t gtri = (W.idx[e] >> 1) + mesh.triangle_offset;
+                        if (!alpha || alpha_survives(d, gtri, inst, u, vv)) {
+                            h.node = inst; h.tri = gtri; h.u = u; h.v = vv; h.t = t;
+                            found = true;
+                            if (anyHit) return true;
+                        }
+                    }
+                }
+            }
+        }
+        return false;
+    };
+    int64_t next = 0;   // the node to visit next (the root first), -1: take the group's first slot
+    for (;;) {
+        const int tBits = as_int(tcull);
+        while (t2m == 0 && !exhausted) {
+            if (next < 0) {
+                if ((grp >> 24) == 0) {
+                    grp = stack.back();
+                    stack.pop_back();
+                    if ((grp >> 24) == 0) { exhausted = true; break; }
+                }
+                const uint32_t hits = grp >> 24;
+                next = (int64_t)((grp & 0xffffffu) + ((uint32_t)__builtin_ctz(hits) ^ oct));
+                grp = ((hits & (hits - 1u)) << 24) | (grp & 0xffffffu);
+            }
+            if (st) st->nodes++;
+            const uint32_t* n = W.nodes.data() + 20 * (size_t)next;
+            float px, py, pz;
+            std::memcpy(&px, n + 0, 4); std::memcpy(&py, n + 1, 4); std::memcpy(&pz, n + 2, 4);
+            const uint32_t hw = n[3], childBase = n[4], leafBase = n[5], meta0 = n[6], meta1 = n[7];
+            const float sx = as_float((int32_t)((hw & 0xffu) << 23)), sy = as_float((int32_t)(((hw >> 8) & 0xffu) << 23));
+            const float sz = as_float((int32_t)(((hw >> 16) & 0xffu) << 23));
+            const uint32_t imask = hw >> 24;
+            const float ax = sx * cur.idx, ay = sy * cur.idy, az = sz * cur.idz;
+            const float bx = std::fma(px, cur.idx, -cur.oodx), by = std::fma(py, cur.idy, -cur.oody);
+            const float bz = std::fma(pz, cur.idz, -cur.oodz);
+            const bool nx = oct & 1u, ny = oct & 2u, nz = oct & 4u;
+            // words: x lo 8..9, x hi 10..11, y lo 12..13, y hi 14..15, z lo 16..17, z hi 18..19
+            uint32_t hit8 = 0, nearest = 0xffffffffu;
+            for (int i = 0; i < 8; i++) {
+                auto q = [&](int w) { return (float)((n[w + (i >> 2)] >> (8 * (i & 3))) & 0xffu); };
+                const float vnx = std::fma(q(nx ? 10 : 8), ax, bx), vfx = std::fma(q(nx ? 8 : 10), ax, bx);
+                const float vny = std::fma(q(ny ? 14 : 12), ay, by), vfy = std::fma(q(ny ? 12 : 14), ay, by);
+                const float vnz = std::fma(q(nz ? 18 : 16), az, bz), vfz = std::fma(q(nz ? 16 : 18), az, bz);
+                const float mn = as_float(imax3(as_int(vnx), as_int(vny), omax(as_int(vnz), tminBits)));
+                const float mx = as_float(imin3(as_int(vfx), as_int(vfy), omin(as_int(vfz), tBits)));
+                if (mx >= mn) {
+                    hit8 |= 1u << i;
+                    // nearest inner child: entry bits with the slot in the low 3 bits
+                    if ((imask >> i) & 1u) nearest = omin(nearest, ((uint32_t)as_int(mn) & ~7u) | (uint32_t)i);
+                }
+            }
+            const uint32_t lhit = hit8 & ~imask;
+            uint32_t tm = 0;
+            for (int i = 0; i < 8; i++) {
+                const uint32_t m = ((i < 4 ? meta0 : meta1) >> (8 * (i & 3))) & 0xffu;
+                if ((lhit >> i) & 1u) tm |= (m >> 5) << (m & 31u);
+            }
+            uint32_t ih = 0;
+            for (int i = 0; i < 8; i++)
+                if (((hit8 & imask) >> i) & 1u) ih |= 1u << (i ^ (int)oct);
+            if (ih) {
+                // the nearest inner child next, the node's other hit inner children (octant order) as
+                // a group; the group the node came from waits on the stack
+                const uint32_t ns = nearest & 7u;
+                if (grp >> 24) stack.push_back(grp);
+                grp = ((ih & ~(1u << (ns ^ oct))) << 24) | childBase;
+                next = (int64_t)(childBase + ns);
+            } else {
+                next = -1;
+            }
+            if (tm) {
+                if (!held) { t1b = leafBase; t1m = tm; held = true; }
+                else { t2b = leafBase; t2m = tm; }
+            }
+        }
+        if (held) {
+            if (leaves(t1b, t1m)) return true;
+            if (leaves(t2b, t2m)) return true;
+        }
+        t1m = t2m = 0;
+        held = false;
+        tcull = h.t;
+        if (exhausted) break;
+    }
+    return found;
+}
+
+// Measurement only (ORACLE_W8_SORTED=1 in the environment): the same 8-wide
+// tree visited near-first by each child's entry distance (a full sort, as the
+// 4-wide order does) instead of by octant slot, to size what the octant order
+// costs in node visits.  Not a device order.
+bool trace_w8_sorted(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
+                     Stats* st) {
+    const ctl_scene_desc* d = S.d;
+    const W8Trees& W = g_w8;
+    const uint32_t inst = ~(uint32_t)d->scene_start_node;
+    const ctl_kernel_mesh& mesh = d->meshes[d->nodes[inst].mesh_index];
+    M44 modl = S.inv(inst);
+    WRay cur;
+    cur.set(transformPoint(modl, ori), transformDirection(modl, dir));
+    const uint32_t oct = ((uint32_t)as_int(cur.idx) >> 31) | (((uint32_t)as_int(cur.idy) >> 31) << 1) |
+                         (((uint32_t)as_int(cur.idz) >> 31) << 2);
+    const int tminBits = as_int(spanTmin);
+    std::vector<int64_t> stack;   // node index, or -1 - (leaf group index into lg)
+    std::vector<std::pair<uint32_t, uint32_t>> lg;
+    stack.push_back(0);
+    bool found = false;
+    while (!stack.empty()) {
+        const int64_t top = stack.back();
+        stack.pop_back();
+        if (top < 0) {
+            auto [base, mask] = lg[(size_t)(-1 - top)];
+            for (; mask; mask &= mask - 1u) {
+                const uint32_t e = base + (uint32_t)__builtin_ctz(mask);
+                const float* v = W.woop.data() + 12 * (size_t)e;
+                if (st) st->tris++;
+                float Oz = v[3] - cur.ox * v[0] - cur.oy * v[1] - cur.oz * v[2];
+                float invDz = 1.0f / (cur.dx * v[0] + cur.dy * v[1] + cur.dz * v[2]);
+                float t = Oz * invDz;
+                if (t > triTmin && t < h.t) {
+                    float u = (v[7] + cur.ox * v[4] + cur.oy * v[5] + cur.oz * v[6]) + t * (cur.dx * v[4] + cur.dy * v[5] + cur.dz * v[6]);
+                    if (u >= 0.0f) {
+                        float vv = (v[11] + cur.ox * v[8] + cur.oy * v[9] + cur.oz * v[10]) + t * (cur.dx * v[8] + cur.dy * v[9] + cur.dz * v[10]);
+                        if (vv >= 0.0f && u + vv <= 1.0f) {
+                            h.node = inst; h.tri = (W.idx[e] >> 1) + mesh.triangle_offset; h.u = u; h.v = vv; h.t = t;
+                            found = true;
+                            if (anyHit) return true;
+                        }
+                    }
+                }
+            }
+            continue;
+        }
+        if (st) st->nodes++;
+        const uint32_t* n = W.nodes.data() + 20 * (size_t)top;
+        float px, py, pz;
+        std::memcpy(&px, n + 0, 4); std::memcpy(&py, n + 1, 4); std::memcpy(&pz, n + 2, 4);
+        const uint32_t hw = n[3], childBase = n[4], leafBase = n[5], meta0 = n[6], meta1 = n[7];
+        const float sx = as_float((int32_t)((hw & 0xffu) << 23)), sy = as_float((int32_t)(((hw >> 8) & 0xffu) << 23));
+        const float sz = as_float((int32_t)(((hw >> 16) & 0xffu) << 23));
+        const uint32_t imask = hw >> 24;
+        const float ax = sx * cur.idx, ay = sy * cur.idy, az = sz * cur.idz;
+        const float bx = std::fma(px, cur.idx, -cur.oodx), by = std::fma(py, cur.idy, -cur.oody);
+        const float bz = std::fma(pz, cur.idz, -cur.oodz);
+        const bool nx = oct & 1u, ny = oct & 2u, nz = oct & 4u;
+        const int tBits = as_int(h.t);
+        // items: inner children and leaf children, with (entry bits, octant key)
+        struct It { int dist; int key; int64_t v; };
+        std::vector<It> kids;
+        static const int policy = std::getenv("ORACLE_W8_POLICY") ? std::atoi(std::getenv("ORACLE_W8_POLICY")) : 0;
+        for (int i = 0; i < 8; i++) {
+            auto q = [&](int w) { return (float)((n[w + (i >> 2)] >> (8 * (i & 3))) & 0xffu); };
+            const float vnx = std::fma(q(nx ? 10 : 8), ax, bx), vfx = std::fma(q(nx ? 8 : 10), ax, bx);
+            const float vny = std::fma(q(ny ? 14 : 12), ay, by), vfy = std::fma(q(ny ? 12 : 14), ay, by);
+            const float vnz = std::fma(q(nz ? 18 : 16), az, bz), vfz = std::fma(q(nz ? 16 : 18), az, bz);
+            const float mn = as_float(imax3(as_int(vnx), as_int(vny), omax(as_int(vnz), tminBits)));
+            const float mx = as_float(imin3(as_int(vfx), as_int(vfy), omin(as_int(vfz), tBits)));
+            if (!(mx >= mn)) continue;
+            const int key = i ^ (int)oct;
+            if ((imask >> i) & 1u) {
+                kids.push_back({as_int(mn), key, (int64_t)(childBase + (uint32_t)i)});
+            } else {
+                const uint32_t m = ((i < 4 ? meta0 : meta1) >> (8 * (i & 3))) & 0xffu;
+                lg.push_back({leafBase, (m >> 5) << (m & 31u)});
+                kids.push_back({policy == 2 ? -1 : as_int(mn), policy == 2 ? -1 : key, -(int64_t)lg.size()});
+            }
+        }
+        // policy 0: entry distance; 1: octant key; 2: leaves first then octant; 3: nearest first, rest octant
+        if (policy == 0) std::stable_sort(kids.begin(), kids.end(), [](auto& a, auto& b) { return a.dist > b.dist; });
+        else std::stable_sort(kids.begin(), kids.end(), [](auto& a, auto& b) { return a.key > b.key; });
+        if (policy == 3 && !kids.empty()) {
+            size_t best = 0;
+            for (size_t k = 1; k < kids.size(); k++) if (kids[k].dist < kids[best].dist) best = k;
+            It b = kids[best];
+            kids.erase(kids.begin() + (long)best);
+            kids.push_back(b);
+        }
+        for (auto& k : kids) stack.push_back(k.v);
     }
     return found;
 }
@@ -1529,6 +1792,21 @@ void oracle_set_wide(const ctl_scene_desc* d, const void* mesh_nodes, uint64_t n
     g_wide.wbase.assign(wbase, wbase + n_wbase);
     g_wide.scene.assign(sc, sc + 32 * n_scene_nodes);
     g_wide.set = true;
+}
+
+// Registers the 8-wide tree of one-mesh scene d for TRAVERSE_W8 (host/bvh_w8.h:
+// 80-B nodes, relaid TriIntersectorData entries and their index words).
+void oracle_set_w8(const ctl_scene_desc* d, const void* nodes, uint64_t n_nodes, const void* woop,
+                   const uint32_t* idx, uint64_t n_entries) {
+    std::lock_guard<std::mutex> g(g_wide_mtx);
+    g_w8.key_nodes = d->bvh_nodes;
+    g_w8.key_n = d->n_bvh_nodes;
+    const uint32_t* nw = static_cast<const uint32_t*>(nodes);
+    const float* wf = static_cast<const float*>(woop);
+    g_w8.nodes.assign(nw, nw + 20 * n_nodes);
+    g_w8.woop.assign(wf, wf + 12 * n_entries);
+    g_w8.idx.assign(idx, idx + n_entries);
+    g_w8.set = true;
 }
 
 void oracle_woop_set(const float* v0, const float* v1, const float* v2, float* out12) {

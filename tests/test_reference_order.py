@@ -23,7 +23,7 @@ import pytest
 
 import oracle
 from helpers import (binary_bvh, camera_rays, classify_orders, grazing_rays, grid_room, oracle_intersect,
-                     random_rays, tie_rule)
+                     random_rays, select_bvh, tie_rule, w8_bvh)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -123,6 +123,38 @@ def gpu_hits(pt, rays, dev, any_hit=False):
     return h.cpu().numpy()
 
 
+@pytest.mark.parametrize("config,scale", [(2, 0.25), (3, 0.004), (5, 0.003)])
+def test_w8_order_vs_reference_order_small(ctl, orc, config, scale):
+    """The 8-wide compressed order (oracle mode 3) against the reference order
+    and the 4-wide order, on the same rays."""
+    d = scene(ctl, config, scale)
+    d8 = w8_bvh(d)
+    rays = np.concatenate([random_rays(d, 40000, seed=config), camera_rays(d, 96, 64, seed=config)])
+    ref = oracle_intersect(orc, d, rays, tie=0)
+    assert tie_rule(d8) == oracle.TRAVERSE_W8
+    w8 = oracle_intersect(orc, d8, rays)
+    c = classify_orders(ref, w8)
+    assert c["differ"] <= MAX_DIFFER_FRAC * c["rays"], c
+    assert c["hit_miss"] == 0 and c["same_hit_other_fields"] == 0, c
+    t = ctl.host_w8_tree(d8)
+    assert t is not None and t[1].shape[0] == d.n_tri_indices   # every leaf entry relaid once
+
+
+@pytest.mark.gpu
+def test_device_w8_tree_equals_host(ctl, dev):
+    d = w8_bvh(scene(ctl, 3, 0.004))
+    pt = ctl.PathTracer(0)
+    try:
+        pt.upload_scene(d)
+        got = pt.w8_tree(d)
+    finally:
+        pt.close()
+    want = ctl.host_w8_tree(d)
+    assert got is not None
+    for g, w in zip(got, want):
+        assert g.shape == w.shape and np.array_equal(g.view(np.uint32), w.view(np.uint32))
+
+
 @pytest.mark.gpu
 def test_device_wide_trees_equal_host(ctl, dev):
     """The trees ctl_scene_upload builds (read back, CTL_ARRAY_WIDE_BVH ...) are
@@ -142,7 +174,7 @@ def test_device_wide_trees_equal_host(ctl, dev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["c3_random", "c3_camera", "room_origin", "room_1e4", "room_far"])
-@pytest.mark.parametrize("bvh", ["wide", "binary"])
+@pytest.mark.parametrize("bvh", ["wide", "w8", "binary"])
 def test_hits_independent_of_ray_order(ctl, orc, dev, case, bvh):
     """ctl_intersect on the same rays in their original order and under three
     random permutations: identical per-ray hits (a ray's result does not depend
@@ -157,11 +189,12 @@ def test_hits_independent_of_ray_order(ctl, orc, dev, case, bvh):
                "room_far": (-3.0e4, 2.0e3, 5.0e4)}[case]
         d = room(ctl, off)
         rays = grazing_rays(d, off, 200000, seed=11)
-    if bvh == "binary":
-        d = binary_bvh(d)
+    d = select_bvh(d, bvh)
     pt = ctl.PathTracer(0)
     try:
         pt.upload_scene(d)
+        if bvh == "w8":
+            assert pt.w8_tree(d) is not None      # the upload did build the 8-wide tree
         base = gpu_hits(pt, rays, dev)
         base_any = gpu_hits(pt, rays, dev, any_hit=True)
         rng = np.random.default_rng(5)
