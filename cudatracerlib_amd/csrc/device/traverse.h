@@ -863,35 +863,49 @@ struct Traverser8 {
         return material_alpha_test(m, TexView{S.textures, S.tex_data}, uv);
     }
 
-    // the entries of one leaf group, ascending; true = any-hit termination
-    __device__ __forceinline__ bool leaves(const DevScene& S, uint32_t base, uint32_t mask, TraceStats* stats) {
-        while (mask) {
-            const uint32_t e = base + (uint32_t)(__ffs(mask) - 1);
-            mask &= mask - 1u;
-            const float4* tv = S.w8_woop + 3u * e;
-            const float4 v00 = tv[0], v11 = tv[1], v22 = tv[2];
-            CTL_PROF_COUNT(stats, leaf_lanes, leaf_waves);
-            if (STATS) stats->tris++;
-            float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
-            float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
-            float t = Oz * invDz;
-            if (t > tri_tmin && t < h.t) {   // TraceHelper.cu:121
-                float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
-                float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
-                float u = Ox + t * Dx;
-                if (u >= 0.0f) {
-                    float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
-                    float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
-                    float v = Oy + t * Dy;
-                    if (v >= 0.0f && u + v <= 1.0f) {
-                        const uint32_t gtri = (S.w8_idx[e] >> 1) + triOffset;
-                        if (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v)) {
-                            h.node = instIdx; h.tri = gtri; h.u = u; h.v = v; h.t = t;
-                            if (ANY == 1 || (ANY == 2 && anyhit)) { done = true; return true; }
-                        }
+    // one Woop test (TraceHelper.cu:118-161); true = any-hit termination
+    __device__ __forceinline__ bool test8(const DevScene& S, uint32_t e, float4 v00, float4 v11, float4 v22,
+                                          TraceStats* stats) {
+        CTL_PROF_COUNT(stats, leaf_lanes, leaf_waves);
+        if (STATS) stats->tris++;
+        float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
+        float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
+        float t = Oz * invDz;
+        if (t > tri_tmin && t < h.t) {   // TraceHelper.cu:121
+            float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
+            float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
+            float u = Ox + t * Dx;
+            if (u >= 0.0f) {
+                float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
+                float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
+                float v = Oy + t * Dy;
+                if (v >= 0.0f && u + v <= 1.0f) {
+                    const uint32_t gtri = (S.w8_idx[e] >> 1) + triOffset;
+                    if (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v)) {
+                        h.node = instIdx; h.tri = gtri; h.u = u; h.v = v; h.t = t;
+                        if (ANY == 1 || (ANY == 2 && anyhit)) { done = true; return true; }
                     }
                 }
             }
+        }
+        return false;
+    }
+
+    // the entries of one leaf group, ascending, loaded two at a time (one
+    // dependent load latency per pair); true = any-hit termination
+    __device__ __forceinline__ bool leaves(const DevScene& S, uint32_t base, uint32_t mask, TraceStats* stats) {
+        while (mask) {
+            const uint32_t e0 = base + (uint32_t)(__ffs(mask) - 1);
+            mask &= mask - 1u;
+            const bool two = mask != 0;
+            const uint32_t e1 = two ? base + (uint32_t)(__ffs(mask) - 1) : e0;
+            mask &= two ? mask - 1u : mask;
+            const float4* t0 = S.w8_woop + 3u * e0;
+            const float4* t1 = S.w8_woop + 3u * e1;
+            const float4 a0 = t0[0], a1 = t0[1], a2 = t0[2];
+            const float4 b0 = t1[0], b1 = t1[1], b2 = t1[2];
+            if (test8(S, e0, a0, a1, a2, stats)) return true;
+            if (two && test8(S, e1, b0, b1, b2, stats)) return true;
         }
         return false;
     }

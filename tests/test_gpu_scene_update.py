@@ -165,3 +165,72 @@ def test_update_switches_tree_format(ctl, orc, dev):
         assert grays == wrays and same(got, want)
     finally:
         pt.close()
+
+
+@pytest.mark.parametrize("bvh", ["wide", "w8"])
+def test_update_tri_indices_alone_rebuilds_trees(ctl, orc, dev, bvh):
+    """CTL_DIRTY_TRI_INDICES alone, same size: the 4-wide (and 8-wide) trees
+    carry per-leaf entry counts and relaid entries derived from the
+    TriIntersectorData2 flags, so they are rebuilt.  The update merges leaves
+    (a cleared last-in-leaf flag) and renames triangles; the image equals the
+    oracle's over the new arrays in the device order and in the reference's."""
+    from helpers import select_bvh, tie_rule
+    hs, d = scene(ctl)
+    d = select_bvh(d, bvh)
+    idx = np.ctypeslib.as_array(C.cast(d.tri_indices, C.POINTER(C.c_uint32)), shape=(d.n_tri_indices,)).copy()
+    ends = np.nonzero(idx[:-1] & 1)[0]
+    merge = ends[::5]
+    idx2 = idx.copy()
+    idx2[merge] &= ~np.uint32(1)                        # the leaf runs on into the next one's entries
+    ntri = int(d.n_tri_data)
+    idx2 = ((((idx2 >> 1) + 7) % ntri) << 1) | (idx2 & 1)   # and names other triangles
+    d2 = copy_desc(d)
+    d2.tri_indices = idx2.ctypes.data_as(C.POINTER(C.c_uint32))
+    pt = ctl.PathTracer(0)
+    try:
+        pt.upload_scene(d)
+        render(ctl, pt, dev, 1)
+        pt.update_scene(d2, ctl._abi.CTL_DIRTY_TRI_INDICES)
+        got, grays = render(ctl, pt, dev, 2, first=3)
+    finally:
+        pt.close()
+    want, wrays = oracle_render(orc, d2, params(ctl), 2, W, H, first_pass=3)
+    assert grays == wrays and same(got, want)
+    ref = np.zeros_like(want)
+    import oracle
+    for p in (3, 4):
+        orc.oracle_render_pass(C.byref(d2), C.byref(params(ctl)), p, oracle.ptr(ref), 0, 0, 1, None)
+    assert same(got, ref)                               # and the reference order agrees
+    old, _ = oracle_render(orc, d, params(ctl), 2, W, H, first_pass=3)
+    assert not same(old, want)                          # the update is visible
+    del idx2
+
+
+def test_set_transform_then_tree_update_returns_to_desc(ctl, orc, dev):
+    """After ctl_scene_set_transform, an update that re-uploads a tree group
+    (CTL_DIRTY_MESHES) returns the transforms, the instance tree, the moved
+    light's ShapeSet and the epsilon to the desc together: the image and the
+    light records equal those of the unmoved scene."""
+    from test_gpu_instances import MOVES, instanced_scene
+    d = instanced_scene(ctl, W, H)
+    A = ctl._abi
+    pt = ctl.PathTracer(0)
+    try:
+        pt.upload_scene(d)
+        lt0 = pt.read_array(A.CTL_ARRAY_LIGHT_TRIS, 0, d.n_light_tris, np.uint32, 16)
+        for node, xf in MOVES.items():
+            pt.set_transform(node, xf)
+        moved = pt.read_array(A.CTL_ARRAY_LIGHT_TRIS, 0, d.n_light_tris, np.uint32, 16)
+        assert not np.array_equal(moved, lt0)
+        pt.update_scene(d, A.CTL_DIRTY_MESHES)
+        lt = pt.read_array(A.CTL_ARRAY_LIGHT_TRIS, 0, d.n_light_tris, np.uint32, 16)
+        xf = pt.read_array(A.CTL_ARRAY_NODE_XF, 0, d.n_nodes, np.float32, 16)
+        pt.params = params(ctl)
+        got, grays = render(ctl, pt, dev, 2)
+    finally:
+        pt.close()
+    assert np.array_equal(lt, lt0)
+    want_xf = np.ctypeslib.as_array(C.cast(d.node_xf, C.POINTER(C.c_float)), shape=(d.n_nodes * 16,))
+    assert np.array_equal(xf.ravel().view(np.uint32), want_xf.view(np.uint32))
+    want, wrays = oracle_render(orc, d, params(ctl), 2, W, H)
+    assert grays == wrays and same(got, want)
