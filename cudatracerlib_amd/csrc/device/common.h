@@ -416,13 +416,22 @@ __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, c
 // this memory slot instead of PathVars, so they hold no VGPRs across the traces;
 // they are read back only for a textured material, the one consumer of the
 // partials.  has_partials is then `depth > 1` (the first hit always computes them).
-template <int FULL, bool SINGLE = false>
+// pk: when non-null (persistent kernel, PK = its LDS park), the path variables
+// other than the ray, depth / specular and the sampler state are still parked
+// in LDS on entry and are read where they are used: pX for the first-hit
+// partials, brdf_pdf and last_nor for an emitter's MIS weight, wo and brdf_pdf
+// just before the BSDF sample, cl and cf at the end.  So they hold no VGPRs
+// across the out-of-line texture and microfacet calls.  The arithmetic is the
+// same either way.
+struct NoPark {};
+template <int FULL, bool SINGLE = false, class PK = NoPark>
 __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P, SamplerDev& rng, PathVars& v,
-                                          const HitRec& r, ShadowReq& sh, float4* part = nullptr) {
+                                          const HitRec& r, ShadowReq& sh, float4* part = nullptr,
+                                          const PK* pk = nullptr) {
+    constexpr bool kLazy = !std::is_same<PK, NoPark>::value;
     const uint32_t node = SINGLE ? ~(uint32_t)S.start_node : r.node;
     sh.valid = false;
     bsdf_rec b;
-    b.wo = v.wo;
     b.sampled_type = 0;
     b.type_mask = kEAll;
     dgeom dg;
@@ -441,6 +450,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
     }
     if (FULL) {
         if (v.depth == 1) {   // bRec.dg.computePartials(r, rX, rY) (PathTracer.cu:60-61)
+            if constexpr (kLazy) pk->load_px(v);
             f3 co, dX, dY;
             sensor_diff(S, v.pX, co, dX, dY);
             compute_partials(dg, co, dX, co, dY);
@@ -466,6 +476,7 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
         const ctl_light L = S.lights[li];
         float misWeight = 1.0f;
         if (!(!P.direct || v.depth == 1 || v.specular)) {   // PathTracer.cu:66-67
+            if constexpr (kLazy) pk->load_mis(v);
             direct_rec dRec;
             dRec.ref = v.rori; dRec.refN = v.last_nor; dRec.p = dg.P; dRec.n = dg.n;
             dRec.d = v.rdir; dRec.dist = r.t; dRec.measure = kESolidAngle;
@@ -474,7 +485,9 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
         }
         f3 w = -v.rdir;
         spec Le = (dot(dg.sys.n, w) <= 0) ? mk3s(0.0f) : mk3(L.radiance[0], L.radiance[1], L.radiance[2]);
+        if constexpr (kLazy) pk->load_cl_cf(v);
         v.cl = v.cl + (v.cf * misWeight) * Le;
+        if constexpr (kLazy) pk->store_cl(v);
     }
     // a textured diffuse hit: one texture lookup for the BSDF sample and the NEE evaluation
     // The diffuse reflectance is evaluated here for every diffuse hit (refl(mat)
@@ -485,13 +498,16 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
     spec Rtex = refl(mat);
     if (texd) Rtex = diffuse_reflectance(mat, dg, &tex);
     const spec* Rp = FULL ? &Rtex : nullptr;
+    if constexpr (kLazy) pk->load_sample_state(v);
+    b.wo = v.wo;
     spec f = FULL ? bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex, Rp)
                   : diffuse_sample(mat, b, v.brdf_pdf, rng.next2());
     v.last_nor = dg.sys.n;
     if (P.direct && (mat.combined_type & kESmooth) != 0 && S.n_lights) {   // PathTracer.cu:82-83
         nee_sample<FULL>(S, rng, mat, b, dg, tex, sh, Rp);
-        if (sh.valid) sh.add = v.cf * sh.add;
     }
+    if constexpr (kLazy) pk->load_cl_cf(v);
+    if (sh.valid) sh.add = v.cf * sh.add;
     v.specular = (b.sampled_type & kEDelta) != 0;
     v.cf = v.cf * f;
     v.rori = dg.P;

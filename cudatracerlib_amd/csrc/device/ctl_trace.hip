@@ -110,7 +110,34 @@ struct Park {
         sh.add = get3(16);
         rng.a = geti(19); rng.b = geti(20); rng.d1 = geti(21); rng.d2 = geti(22);
     }
+    // Partial loads and stores (CTL_LAZY_PARK): after a trace the lane loads only
+    // depth / specular and the sampler state; shade_hit reads the rest where it
+    // is used (common.h shade_hit, `pk`), and only what changed goes back.
+    __device__ __forceinline__ void load_core(PathVars& v, SamplerDev& rng) const {
+        const uint32_t ds = geti(15);
+        v.depth = (int)(ds >> 1); v.specular = (ds & 1u) != 0;
+        rng.a = geti(19); rng.b = geti(20); rng.d1 = geti(21); rng.d2 = geti(22);
+    }
+    __device__ __forceinline__ void load_px(PathVars& v) const { v.pX.x = get(12); v.pX.y = get(13); }
+    __device__ __forceinline__ void load_mis(PathVars& v) const { v.brdf_pdf = get(14); v.last_nor = get3(6); }
+    __device__ __forceinline__ void load_sample_state(PathVars& v) const { v.wo = get3(9); v.brdf_pdf = get(14); }
+    __device__ __forceinline__ void load_cl_cf(PathVars& v) const { v.cl = get3(0); v.cf = get3(3); }
+    __device__ __forceinline__ void store_cl(const PathVars& v) const { put3(0, v.cl); }
+    __device__ __forceinline__ void store_depth(const PathVars& v) const {
+        puti(15, ((uint32_t)v.depth << 1) | (v.specular ? 1u : 0u));
+    }
+    // after shade_hit: everything it can change (not the pixel position)
+    __device__ __forceinline__ void store_shaded(const PathVars& v, const ShadowReq& sh, const SamplerDev& rng) const {
+        put3(0, v.cl); put3(3, v.cf); put3(6, v.last_nor); put3(9, v.wo);
+        put(14, v.brdf_pdf);
+        store_depth(v);
+        put3(16, sh.add);
+        puti(21, rng.d1); puti(22, rng.d2);
+    }
 };
+#ifndef CTL_LAZY_PARK
+#define CTL_LAZY_PARK 1
+#endif
 
 // dynamic LDS of path_kernel_persistent: lane stacks + the work item word per
 // lane + the parked path state
@@ -120,7 +147,7 @@ constexpr size_t persistent_lds_bytes() {
 
 // Megakernel schedule: PathTrace<true> (PathTracer.cu:10-113) with the
 // traversals inline in the bounce, as the reference's pathKernel2 runs it.
-template <bool STATS, bool SINGLE, bool WIDE, int FULL>
+template <bool STATS, bool SINGLE, int WIDE, int FULL>
 struct PathCtx {
     const DevScene& S;
     const PathParams& P;
@@ -219,7 +246,7 @@ __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict
 }
 
 // One path per thread (the reference's pathKernel2 launch shape).
-template <bool STATS, bool SINGLE, bool WIDE, int FULL>
+template <bool STATS, bool SINGLE, int WIDE, int FULL>
 __global__ __launch_bounds__(kBlock) void path_kernel(DevScene S_arg, PathParams P_arg, const float* s1, const float2* s2,
                                                       ctl_pixel* fb, unsigned long long* counters, SampleSlots PS) {
     const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
@@ -370,27 +397,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
 #ifdef CTL_PROFILE_TRACE
             prof_trace += wall_clock64() - pc0;
 #endif
-            if (CTL_PARK) park.load(v, sh, rng);
+            constexpr bool lazy = CTL_PARK && CTL_LAZY_PARK && FULL != kShadeLean;
+            if (lazy) park.load_core(v, rng);
+            else if (CTL_PARK) park.load(v, sh, rng);
             bool cont;
             if (shadowPhase) {
+                if (lazy) { v.cl = park.get3(0); sh.add = park.get3(16); }
                 if (!shadow_occluded(S, shadowAny, h, sh.dist)) v.cl = v.cl + sh.add;
                 shadowPhase = false;
                 cont = !ending && v.depth++ < P.max_path_length;
+                if (lazy && cont) { park.store_cl(v); park.store_depth(v); }
             } else if (h.tri == 0xffffffffu) {
+                if (lazy) park.load(v, sh, rng);
                 v.cl = v.cl + env_miss<FULL>(S, P, v);   // PathTracer.cu:98-111
                 cont = false;
             } else {
-                ending = !shade_hit<FULL, SINGLE>(S, P, rng, v, h, sh, CTL_PART_SLOT ? PS.s + *pkw : nullptr);
+                float4* part = CTL_PART_SLOT ? PS.s + *pkw : nullptr;
+                ending = lazy ? !shade_hit<FULL, SINGLE, Park>(S, P, rng, v, h, sh, part, &park)
+                              : !shade_hit<FULL, SINGLE>(S, P, rng, v, h, sh, part);
                 shadowPhase = sh.valid;
                 cont = sh.valid || (!ending && v.depth++ < P.max_path_length);
+                if (lazy && cont) park.store_shaded(v, sh, rng);
             }
             if (!cont) {
                 uint32_t px, py, ps, kk;
                 split((uint32_t)*pkw, ps, kk);
                 work_pixel(P, kk, px, py);
+                if (lazy) park.load_px(v);
                 store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
                 active = false;
-            } else if (CTL_PARK) {
+            } else if (CTL_PARK && !lazy) {
                 park.store(v, sh, rng);
             }
         }
@@ -840,9 +876,10 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
                                               P, s1, s2, fb, c->d_counters, PS)
 #define MK2(ST, SG, WD) do { if (full == kShadeEnv) MK(ST, SG, WD, kShadeEnv); else if (full == kShadeAlpha) MK(ST, SG, WD, kShadeAlpha); \
                               else if (full) MK(ST, SG, WD, kShadeFull); else MK(ST, SG, WD, kShadeLean); } while (0)
-        if (stats) { if (single) MK2(true, true, false); else MK2(true, false, false); }
-        else if (wide) { if (single) MK2(false, true, true); else MK2(false, false, true); }
-        else { if (single) MK2(false, true, false); else MK2(false, false, false); }
+        if (stats) { if (single) MK2(true, true, 0); else MK2(true, false, 0); }
+        else if (wide && single && c->scene.w8_on) MK2(false, true, 2);
+        else if (wide) { if (single) MK2(false, true, 1); else MK2(false, false, 1); }
+        else { if (single) MK2(false, true, 0); else MK2(false, false, 0); }
 #undef MK2
 #undef MK
     }

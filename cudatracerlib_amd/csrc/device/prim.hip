@@ -37,7 +37,7 @@ __device__ __forceinline__ float depth_d3d(float d, float n, float f) {
 #ifndef CTL_PRIM_WAVES
 #define CTL_PRIM_WAVES 0   // waves/SIMD hint for prim_kernel (0: the compiler's choice)
 #endif
-template <bool SINGLE, bool WIDE, int FULL>
+template <bool SINGLE, int WIDE, int FULL>
 __global__ __launch_bounds__(kBlock)
 #if CTL_PRIM_WAVES
 __attribute__((amdgpu_waves_per_eu(CTL_PRIM_WAVES)))
@@ -219,8 +219,9 @@ CTL_API ctl_status ctl_prim_pass(ctl_ctx* c, const ctl_prim_params* p, ctl_pixel
     } while (0)
 #define PRK2(SG, WD) do { if (full == kShadeEnv) PRK(SG, WD, kShadeEnv); else if (full == kShadeAlpha) PRK(SG, WD, kShadeAlpha); \
                            else if (full) PRK(SG, WD, kShadeFull); else PRK(SG, WD, kShadeLean); } while (0)
-    if (wide) { if (single) PRK2(true, true); else PRK2(false, true); }
-    else { if (single) PRK2(true, false); else PRK2(false, false); }
+    if (wide && single && c->scene.w8_on) PRK2(true, 2);
+    else if (wide) { if (single) PRK2(true, 1); else PRK2(false, 1); }
+    else { if (single) PRK2(true, 0); else PRK2(false, 0); }
 #undef PRK2
 #undef PRK
     CTL_HIP(c, hipGetLastError());

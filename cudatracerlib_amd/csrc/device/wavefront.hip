@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kBlock) void wf_gen_kernel(DevScene S_arg, PathPara
 #define CTL_WF_REFILL_MIN 40   // refill once this many lanes of the wave wait (as the batch traversal)
 #endif
 constexpr int kWfRefillMin = CTL_WF_REFILL_MIN;
-template <int MODE, bool STATS, bool SINGLE, bool WIDE, bool ALPHA>
+template <int MODE, bool STATS, bool SINGLE, int WIDE, bool ALPHA>
 __global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S_arg, WfState W, const uint32_t* queue,
                                                           const uint32_t* countp, uint32_t* cursor,
                                                           unsigned long long* counters) {
@@ -176,9 +176,10 @@ void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32
 #define LT2(SG, WD) do { if (alpha) LT(false, SG, WD, true); else LT(false, SG, WD, false); } while (0)
     const bool wide = c->scene.wide != 0 && !stats;   // stats: the reference's binary traversal
     const bool alpha = c->scene.alpha != 0;
-    if (stats) { if (single) LT(true, true, false, false); else LT(true, false, false, false); }
-    else if (wide) { if (single) LT2(true, true); else LT2(false, true); }
-    else { if (single) LT2(true, false); else LT2(false, false); }
+    if (stats) { if (single) LT(true, true, 0, false); else LT(true, false, 0, false); }
+    else if (wide && single && c->scene.w8_on) LT2(true, 2);
+    else if (wide) { if (single) LT2(true, 1); else LT2(false, 1); }
+    else { if (single) LT2(true, 0); else LT2(false, 0); }
 #undef LT2
 #undef LT
 }

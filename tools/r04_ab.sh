@@ -10,7 +10,7 @@ tail -2 gpurun_out/ab4/w8_tests.log
 fi
 LEGS="--steps 20 --warmup 5 --no-cpu-baseline --wpt-passes 0 --dopass-leg 0 --one-pass-leg 0 --closest-shadow-passes 0 --prim-passes 0 --c5-passes 16"
 i=0
-for spec in ${RUNS:-"base:wide" "base:w8" "r3:wide" "lazy:wide" "lazygm:wide" "gm:wide" "qf:wideq" "spec0:wide" "base:w8" "base:wide"}; do
+for spec in ${RUNS:-"base:wide" "base:w8" "r3:wide" "nolazy:wide" "lazygm:wide" "base:w8" "base:wide"}; do
   v=${spec%%:*}; b=${spec##*:}
   case $v in
     base) L=cudatracerlib_amd/_lib/libctl_trace.so; D=. ; X="--binary-passes 0";;
