@@ -609,36 +609,40 @@ CTL_HD spec diffuse_reflectance(const ctl_material& m, const dgeom& dg, const Te
 // diffuse reflectance at dg when the caller already evaluated it (a textured
 // diffuse hit samples and evaluates the same texture at the same dg for the
 // BSDF sample and for next-event estimation: one lookup serves both).
+// gm: the same material in global memory (the scene's array element), handed
+// to the out-of-line rough-dielectric calls so the caller's register copy of
+// the 80-B record need not be written to scratch for them.
 CTL_HD spec bsdf_sample(const ctl_material& m, bsdf_rec& b, float& pdf, f2 sample, const dgeom& dg, const TexView* tex,
-                        const spec* R = nullptr) {
+                        const spec* R = nullptr, const ctl_material* gm = nullptr) {
     if (m.bsdf_type == CTL_BSDF_DIFFUSE) {
         if (!diffuse_sample_dir(m, b, pdf, sample)) return mk3s(0.0f);
         return (R ? *R : diffuse_reflectance(m, dg, tex)) * 1.0f;
     }
     const bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
-    spec res = rough_sample(m, b, pdf, sample);
+    spec res = rough_sample(gm ? *gm : m, b, pdf, sample);
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
     return res;
 }
 
-CTL_HD spec bsdf_f(const ctl_material& m, bsdf_rec& b, const dgeom& dg, const TexView* tex, const spec* R = nullptr) {
+CTL_HD spec bsdf_f(const ctl_material& m, bsdf_rec& b, const dgeom& dg, const TexView* tex, const spec* R = nullptr,
+                   const ctl_material* gm = nullptr) {
     if (m.bsdf_type == CTL_BSDF_DIFFUSE) {
         if (!(b.type_mask & m.combined_type)) return mk3s(0.0f);
         return diffuse_f_refl(m, b, R ? *R : diffuse_reflectance(m, dg, tex));
     }
     const bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
-    spec res = rough_f(m, b);
+    spec res = rough_f(gm ? *gm : m, b);
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
     return res;
 }
 
-CTL_HD float bsdf_pdf(const ctl_material& m, bsdf_rec& b) {
+CTL_HD float bsdf_pdf(const ctl_material& m, bsdf_rec& b, const ctl_material* gm = nullptr) {
     if (m.bsdf_type == CTL_BSDF_DIFFUSE) return diffuse_pdf(m, b);
     const bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
-    float res = rough_pdf(m, b);
+    float res = rough_pdf(gm ? *gm : m, b);
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
     return res;
 }

@@ -359,7 +359,7 @@ __device__ __forceinline__ spec env_miss(const DevScene& S, const PathParams& P,
 template <int FULL>
 __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, const ctl_material& mat,
                                            const bsdf_rec& b, const dgeom& dg, const TexView& tex, ShadowReq& sh,
-                                           const spec* R = nullptr) {
+                                           const spec* R = nullptr, const ctl_material* gm = nullptr) {
     f2 sample = rng.next2();
     const uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
     uint32_t first = 0, cnt = nl;   // STL_upper_bound
@@ -384,11 +384,11 @@ __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, c
         bsdf_rec b2 = b;
         b2.wo = to_local(dg.sys, dRec.d);
         b2.type_mask = kEAll & ~kEDelta;
-        spec bsdfVal = FULL ? bsdf_f(mat, b2, dg, &tex, R) : diffuse_f(mat, b2);
+        spec bsdfVal = FULL ? bsdf_f(mat, b2, dg, &tex, R, gm) : diffuse_f(mat, b2);
         if (!spec_zero(bsdfVal)) {
             float weight = 1.0f;
             if (dRec.measure != kEDiscrete)
-                weight = power_heuristic(dRec.pdf * lpdf, FULL ? bsdf_pdf(mat, b2) : diffuse_pdf(mat, b2));
+                weight = power_heuristic(dRec.pdf * lpdf, FULL ? bsdf_pdf(mat, b2, gm) : diffuse_pdf(mat, b2));
             spec ret = value * bsdfVal * weight;
             ret = ret * mk3s(1.0f);
             sh.valid = true;
@@ -442,7 +442,8 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
     const ctl_node* N = S.nodes + node;
     fill_dg(td, load_m44(S.xf + 4 * node), mk2(r.u, r.v), P.half_quirk, LutDecode{S.normal_lut}, dg);
     b.wi = to_local(dg.sys, -v.rdir);
-    const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N->material_offset];
+    const ctl_material* gmat = S.mats + (((td.w[1] >> 16) & 0xffu) + N->material_offset);
+    const ctl_material mat = *gmat;
     if (mat.two_sided && b.wi.z < 0) {
         dg.n = -dg.n;
         dg.sys.n = -dg.sys.n;
@@ -500,11 +501,11 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
     const spec* Rp = FULL ? &Rtex : nullptr;
     if constexpr (kLazy) pk->load_sample_state(v);
     b.wo = v.wo;
-    spec f = FULL ? bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex, Rp)
+    spec f = FULL ? bsdf_sample(mat, b, v.brdf_pdf, rng.next2(), dg, &tex, Rp, gmat)
                   : diffuse_sample(mat, b, v.brdf_pdf, rng.next2());
     v.last_nor = dg.sys.n;
     if (P.direct && (mat.combined_type & kESmooth) != 0 && S.n_lights) {   // PathTracer.cu:82-83
-        nee_sample<FULL>(S, rng, mat, b, dg, tex, sh, Rp);
+        nee_sample<FULL>(S, rng, mat, b, dg, tex, sh, Rp, gmat);
     }
     if constexpr (kLazy) pk->load_cl_cf(v);
     if (sh.valid) sh.add = v.cf * sh.add;

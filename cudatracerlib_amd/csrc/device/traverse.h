@@ -55,6 +55,12 @@ constexpr int kStackMax = 128;
 #ifndef CTL_LEAF_SPECULATE
 #define CTL_LEAF_SPECULATE 1
 #endif
+// CTL_SPEC_STEPS K > 0: the walk after a postponed leaf visits at most K inner
+// nodes (0: until the next leaf).
+#ifndef CTL_SPEC_STEPS
+#define CTL_SPEC_STEPS 0
+#endif
+constexpr int kSpecSteps = CTL_SPEC_STEPS;
 
 // Per-ray visit order (round 4).  Every traversal is a function of its ray
 // alone, never of the other rays of its wave:
@@ -242,6 +248,7 @@ struct Traverser4 {
     float span_tmin, tri_tmin;
     float tcull;   // cull distance of the 4-wide node loops (h.t, or its value before a phantom leaf)
     int nodeAddr, leafAddr, level, meshSent;
+    int specLeft;     // CTL_SPEC_STEPS: inner nodes the walk past a postponed leaf may still visit
     uint32_t nodeBase, triBase, idxBase, triOffset, instIdx;
     bool done, resumeLeaves;
     bool anyhit;   // ANY == 2 only
@@ -264,6 +271,7 @@ struct Traverser4 {
         done = (S.n_nodes == 0);
         resumeLeaves = false;
         meshSent = 0;
+        specLeft = 0;
         if (SINGLE) {
             // start_node < 0: TracerayTemplate calls the instance callback directly (BVHTraversal.h:130-131)
             if (STATS) stats->inst++;
@@ -509,7 +517,8 @@ struct Traverser4 {
         // speculation only inside a mesh (the instance level stops at its first leaf)
         const bool spec = CTL_LEAF_SPECULATE && (SINGLE || level == 1);
         const int tBits = __float_as_int(tcull);
-        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (spec || leafAddr >= 0)) {
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL &&
+               ((spec && (kSpecSteps == 0 || specLeft > 0)) || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
@@ -574,7 +583,9 @@ struct Traverser4 {
             CTL_WIDE_CHILD(k3, ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y)
 #endif
 #undef CTL_WIDE_CHILD
+            const bool held = leafAddr < 0;
             wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
+            if (kSpecSteps > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpecSteps : specLeft);
             if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
@@ -596,7 +607,8 @@ struct Traverser4 {
         // speculation only inside a mesh (the instance level stops at its first leaf)
         const bool spec = CTL_LEAF_SPECULATE && (SINGLE || level == 1);
         const int tBits = __float_as_int(tcull);
-        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (spec || leafAddr >= 0)) {
+        while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL &&
+               ((spec && (kSpecSteps == 0 || specLeft > 0)) || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
@@ -657,7 +669,9 @@ struct Traverser4 {
             CTL_WIDE_CHILD(k2, c2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x)
             CTL_WIDE_CHILD(k3, c3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y)
 #undef CTL_WIDE_CHILD
+            const bool held = leafAddr < 0;
             wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
+            if (kSpecSteps > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpecSteps : specLeft);
             if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
@@ -728,7 +742,7 @@ struct Traverser4 {
         resumeLeaves = false;
         // a speculating lane the wave stopped before it reached its next leaf
         const bool cut = WIDE && CTL_LEAF_SPECULATE && (SINGLE || level == 1) && leafAddr < 0 &&
-                         (unsigned)nodeAddr < (unsigned)CTL_SENTINEL;
+                         (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (kSpecSteps == 0 || specLeft > 0);
 #ifdef CTL_PROFILE_TRACE
         {
             const uint32_t nl = (uint32_t)__popcll(__ballot(leafAddr < 0));

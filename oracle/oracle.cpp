@@ -408,12 +408,18 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
         enter(~(uint32_t)d->scene_start_node);
         level = 1;
     }
+    // measurement only: ORACLE_WIDE_NOSPEC=1 stops at the first leaf in the mesh level too
+    static const bool nospec = std::getenv("ORACLE_WIDE_NOSPEC") != nullptr;
+    static const int kSpec = std::getenv("ORACLE_SPEC_STEPS") ? std::atoi(std::getenv("ORACLE_SPEC_STEPS")) : 0;
+    int specLeft = 0;
     for (;;) {
-        const bool spec = level == 1;
+        const bool spec = level == 1 && !nospec;
         const float* tree = level ? W.mesh.data() + 32 * (size_t)wnodeBase : W.scene.data();
         const int tBits = as_int(tcull);
         const bool nx = as_int(cur.idx) < 0, ny = as_int(cur.idy) < 0, nz = as_int(cur.idz) < 0;
-        while ((unsigned)nodeAddr < (unsigned)EntrypointSentinel && (spec || leafAddr >= 0)) {
+        while ((unsigned)nodeAddr < (unsigned)EntrypointSentinel &&
+               ((spec && (kSpec == 0 || specLeft > 0)) || leafAddr >= 0)) {
+            const bool held = leafAddr < 0;
             if (st) st->nodes++;
             const float* n = tree + 32 * (size_t)nodeAddr;
             int k[4], c[4];
@@ -440,6 +446,7 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
                 next = pop();
             }
             nodeAddr = next;
+            if (kSpec > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpec : specLeft);
         }
         bool entered = false;
         while (leafAddr < 0) {
