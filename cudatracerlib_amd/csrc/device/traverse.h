@@ -785,8 +785,15 @@ struct Traverser4 {
                 if (nodeAddr < 0) nodeAddr = st.pop();
             }
         }
+#ifndef CTL_CUT_UPDATE
         if (cut) leafAddr = kPhantomLeaf;   // walk on to the next leaf with the old tcull
         else tcull = h.t;
+#else
+        // measurement only: a cut lane resumes with the new distance (round 3's
+        // wave-dependent behaviour; not the per-ray order the oracle restates)
+        (void)cut;
+        tcull = h.t;
+#endif
         if (nodeAddr == CTL_SENTINEL) {
             if (!SINGLE && level == 1) {
                 // mesh traversal finished (bottom sentinel or a sentinel child)
