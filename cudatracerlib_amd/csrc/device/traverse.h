@@ -61,6 +61,14 @@ constexpr int kStackMax = 128;
 #define CTL_SPEC_STEPS 0
 #endif
 constexpr int kSpecSteps = CTL_SPEC_STEPS;
+// CTL_IFIF 1: one-mesh scenes on the 4-wide float tree run the unified-fetch
+// loop (Traverser4::round_ifif): every iteration each lane either steps one
+// node or tests one leaf (two entries), both through the same seven 16-B loads,
+// and a leaf is tested as soon as it is reached (no postponement, no
+// speculation: the order of ORACLE_WIDE_NOSPEC).
+#ifndef CTL_IFIF
+#define CTL_IFIF 0
+#endif
 
 // Per-ray visit order (round 4).  Every traversal is a function of its ray
 // alone, never of the other rays of its wave:
@@ -727,9 +735,134 @@ struct Traverser4 {
         }
     }
 
+    // Woop test of one entry; the TriIntersectorData2 word is loaded only for
+    // an accepted hit.  true = any-hit termination.
+    __device__ __forceinline__ bool test_entry_lazy(const DevScene& S, float4 v00, float4 v11, float4 v22,
+                                                    uint32_t entry, TraceStats* stats) {
+        CTL_PROF_COUNT(stats, leaf_lanes, leaf_waves);
+        if (STATS) stats->tris++;
+        float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
+        float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
+        float t = Oz * invDz;
+        if (t > tri_tmin && t < h.t) {
+            float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
+            float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
+            float u = Ox + t * Dx;
+            if (u >= 0.0f) {
+                float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
+                float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
+                float v = Oy + t * Dy;
+                if (v >= 0.0f && u + v <= 1.0f) {
+                    const uint32_t gtri = (S.tri_idx[idxBase + entry] >> 1) + triOffset;
+                    if (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v)) {
+                        h.node = instIdx; h.tri = gtri; h.u = u; h.v = v; h.t = t;
+                        if (ANY == 1 || (ANY == 2 && anyhit)) { done = true; return true; }
+                    }
+                }
+            }
+        }
+        return false;
+    }
+
+    // Unified-fetch traversal of a one-mesh 4-wide float tree (CTL_IFIF): per
+    // iteration a lane on an inner node loads its near/far planes and child
+    // word, a lane on a leaf loads two Woop entries, with the same seven 16-B
+    // load instructions (per-lane addresses), so node steps and leaf tests of
+    // one wave share one memory round trip.  A leaf is tested when reached
+    // and the cull distance is the current hit: the order is the no-speculation
+    // order (oracle TRAVERSE_WIDE with ORACLE_WIDE_NOSPEC), a function of the
+    // ray alone.  Runs the whole traversal in one call.
+    __device__ __forceinline__ void round_ifif(const DevScene& S, LaneStack& st, TraceStats* stats) {
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const char* nbytes = reinterpret_cast<const char*>(S.wbvh);
+        const char* tbytes = reinterpret_cast<const char*>(S.woop + triBase);
+        const v2f ix = {cur.idx, cur.idx}, iy = {cur.idy, cur.idy}, iz = {cur.idz, cur.idz};
+        const v2f ox = {cur.oodx, cur.oodx}, oy = {cur.oody, cur.oody}, oz = {cur.oodz, cur.oodz};
+        const int tminBits = __float_as_int(span_tmin);
+        const uint32_t sx = (uint32_t)(__float_as_int(cur.idx) >> 31) & 16u;
+        const uint32_t sy = (uint32_t)(__float_as_int(cur.idy) >> 31) & 16u;
+        const uint32_t sz = (uint32_t)(__float_as_int(cur.idz) >> 31) & 16u;
+        uint32_t onx = sx, ofx = 16u - sx, ony = 32u + sy, ofy = 48u - sy, onz = 64u + sz, ofz = 80u - sz;
+        asm volatile("" : "+v"(onx), "+v"(ofx), "+v"(ony), "+v"(ofy), "+v"(onz), "+v"(ofz));
+        leafAddr = -1;   // wide_advance never postpones
+        // batch traversals hand the wave back for a refill once fewer than 24 lanes
+        // still traverse (the CTL_REFILL_MIN rule); the path kernel never needs to
+        constexpr int kKeep = ANY == 2 ? 0 : 24;
+        while (true) {
+            if ((unsigned)nodeAddr == (unsigned)CTL_SENTINEL) { done = true; return; }
+            const bool isLeaf = nodeAddr < 0;
+            const uint32_t code = (uint32_t)(~nodeAddr);
+            const uint32_t first = code >> 3, cnt = code & 7u;
+            // per-lane byte addresses of the seven loads: node planes + child word,
+            // or entries first and first + 1 (the first again for a one-entry leaf)
+            const char* nb = nbytes + ((size_t)(nodeBase + (uint32_t)nodeAddr) << 7);
+            const char* t0 = tbytes + (size_t)first * 48u;
+            const char* t1 = cnt >= 2 ? t0 + 48 : t0;
+            const v4f L0 = *reinterpret_cast<const v4f*>(isLeaf ? t0 : nb + onx);
+            const v4f L1 = *reinterpret_cast<const v4f*>(isLeaf ? t0 + 16 : nb + ofx);
+            const v4f L2 = *reinterpret_cast<const v4f*>(isLeaf ? t0 + 32 : nb + ony);
+            const v4f L3 = *reinterpret_cast<const v4f*>(isLeaf ? t1 : nb + ofy);
+            const v4f L4 = *reinterpret_cast<const v4f*>(isLeaf ? t1 + 16 : nb + onz);
+            const v4f L5 = *reinterpret_cast<const v4f*>(isLeaf ? t1 + 32 : nb + ofz);
+            int4 ch = *reinterpret_cast<const int4*>(isLeaf ? t0 : nb + 96);
+            asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
+            if (isLeaf) {
+                if (first == 214783647u) {
+                    // the reference's skipped leaf value (BVHTraversal.h:109,221)
+                } else if (cnt == 0) {
+                    leafAddr = nodeAddr;   // a long leaf: walk its last-in-leaf flags
+                    leaf_tris(S, stats);
+                    leafAddr = -1;
+                    if (done) return;
+                } else {
+                    auto f4 = [](v4f a) { return make_float4(a.x, a.y, a.z, a.w); };
+                    if (test_entry_lazy(S, f4(L0), f4(L1), f4(L2), first, stats)) return;
+                    if (cnt >= 2 && test_entry_lazy(S, f4(L3), f4(L4), f4(L5), first + 1, stats)) return;
+                    if (cnt > 2) { nodeAddr = ~(int)(((first + 2u) << 3) | (cnt - 2u)); continue; }
+                }
+                tcull = h.t;
+                nodeAddr = st.pop();
+            } else {
+                CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
+                if (STATS) stats->nodes++;
+                const int sp = st.sp;
+                const bool fast = sp + 3 <= kLdsStack;
+                const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
+                const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
+                const int tBits = __float_as_int(tcull);
+                const v2f nx01 = L0.xy * ix - ox, nx23 = L0.zw * ix - ox;
+                const v2f fx01 = L1.xy * ix - ox, fx23 = L1.zw * ix - ox;
+                const v2f ny01 = L2.xy * iy - oy, ny23 = L2.zw * iy - oy;
+                const v2f fy01 = L3.xy * iy - oy, fy23 = L3.zw * iy - oy;
+                const v2f nz01 = L4.xy * iz - oz, nz23 = L4.zw * iz - oz;
+                const v2f fz01 = L5.xy * iz - oz, fz23 = L5.zw * iz - oz;
+                int k0, k1, k2, k3;
+#define CTL_WIDE_CHILD(K, NX, FX, NY, FY, NZ, FZ)                                                       \
+                {                                                                                       \
+                    const float cmin = __int_as_float(imax3(__float_as_int(NX), __float_as_int(NY),      \
+                                                            max(__float_as_int(NZ), tminBits)));         \
+                    const float cmax = __int_as_float(imin3(__float_as_int(FX), __float_as_int(FY),      \
+                                                            min(__float_as_int(FZ), tBits)));            \
+                    K = (cmax >= cmin) ? __float_as_int(cmin) : 0x7fffffff;                             \
+                }
+                CTL_WIDE_CHILD(k0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x)
+                CTL_WIDE_CHILD(k1, nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y)
+                CTL_WIDE_CHILD(k2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x)
+                CTL_WIDE_CHILD(k3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y)
+#undef CTL_WIDE_CHILD
+                wide_advance(k0, k1, k2, k3, ch.x, ch.y, ch.z, ch.w, fast, sp, top1, top2, st);
+            }
+            if (kKeep > 0 && __popcll(__ballot(true)) < kKeep) return;
+        }
+    }
+
     // One round: inner nodes until every active lane holds a postponed leaf,
     // then the postponed leaves (and the level transitions).
     __device__ __forceinline__ void round(const DevScene& S, LaneStack& st, TraceStats* stats) {
+        if (CTL_IFIF && SINGLE && WIDE && !STATS) {
+            if (!S.quant) { round_ifif(S, st, stats); return; }
+        }
 #ifdef CTL_PROFILE_TRACE
         stats->round_r = (uint32_t)__popcll(__ballot(1));
         if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) stats->rounds++;

@@ -413,7 +413,7 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
     static const int kSpec = std::getenv("ORACLE_SPEC_STEPS") ? std::atoi(std::getenv("ORACLE_SPEC_STEPS")) : 0;
     int specLeft = 0;
     for (;;) {
-        const bool spec = level == 1 && !nospec;
+        const bool spec = level == 1 && !(nospec && single);
         const float* tree = level ? W.mesh.data() + 32 * (size_t)wnodeBase : W.scene.data();
         const int tBits = as_int(tcull);
         const bool nx = as_int(cur.idx) < 0, ny = as_int(cur.idy) < 0, nz = as_int(cur.idz) < 0;
