@@ -69,6 +69,11 @@ constexpr int kSpecSteps = CTL_SPEC_STEPS;
 #ifndef CTL_IFIF
 #define CTL_IFIF 0
 #endif
+// CTL_SPEC_NOPOP 1: the walk past a postponed leaf also stops at a node with
+// no hit child (where it would pop the stack): it only descends.
+#ifndef CTL_SPEC_NOPOP
+#define CTL_SPEC_NOPOP 0
+#endif
 
 // Per-ray visit order (round 4).  Every traversal is a function of its ray
 // alone, never of the other rays of its wave:
@@ -259,6 +264,7 @@ struct Traverser4 {
     int specLeft;     // CTL_SPEC_STEPS: inner nodes the walk past a postponed leaf may still visit
     uint32_t nodeBase, triBase, idxBase, triOffset, instIdx;
     bool done, resumeLeaves;
+    bool specStop;   // CTL_SPEC_NOPOP: this round's walk past the postponed leaf ended at a pop
     bool anyhit;   // ANY == 2 only
 
     __device__ __forceinline__ void enter_instance(const DevScene& S, uint32_t inst, f3 o, f3 d) {
@@ -280,6 +286,7 @@ struct Traverser4 {
         resumeLeaves = false;
         meshSent = 0;
         specLeft = 0;
+        specStop = false;
         if (SINGLE) {
             // start_node < 0: TracerayTemplate calls the instance callback directly (BVHTraversal.h:130-131)
             if (STATS) stats->inst++;
@@ -435,8 +442,8 @@ struct Traverser4 {
     // distances; misses carry 0x7fffffff and sort last), take the nearest,
     // push the others far-to-near, postpone a leaf.  Shared by the float and
     // quantized 4-wide loops.
-    __device__ __forceinline__ void wide_advance(int k0, int k1, int k2, int k3, int c0, int c1, int c2, int c3,
-                                                 bool fast, int sp, int top1, int top2, LaneStack& st) {
+    __device__ __forceinline__ int wide_advance(int k0, int k1, int k2, int k3, int c0, int c1, int c2, int c3,
+                                                bool fast, int sp, int top1, int top2, LaneStack& st) {
 #define CTL_CX(KA, CA, KB, CB)                      \
         {                                       \
             const bool sw = KB < KA;            \
@@ -467,6 +474,7 @@ struct Traverser4 {
             }
             nodeAddr = next;
             st.sp = nsp;
+            return m;
         } else {
             if (k3 != 0x7fffffff) st.push(c3);
             if (k2 != 0x7fffffff) st.push(c2);
@@ -476,6 +484,7 @@ struct Traverser4 {
                 leafAddr = nodeAddr;
                 nodeAddr = st.pop();
             }
+            return k0 != 0x7fffffff;
         }
     }
 
@@ -526,7 +535,7 @@ struct Traverser4 {
         const bool spec = CTL_LEAF_SPECULATE && (SINGLE || level == 1);
         const int tBits = __float_as_int(tcull);
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL &&
-               ((spec && (kSpecSteps == 0 || specLeft > 0)) || leafAddr >= 0)) {
+               ((spec && (kSpecSteps == 0 || specLeft > 0) && !specStop) || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
@@ -592,7 +601,8 @@ struct Traverser4 {
 #endif
 #undef CTL_WIDE_CHILD
             const bool held = leafAddr < 0;
-            wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
+            const int m = wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
+            if (CTL_SPEC_NOPOP && held && m == 0) specStop = true;
             if (kSpecSteps > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpecSteps : specLeft);
             if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
@@ -616,7 +626,7 @@ struct Traverser4 {
         const bool spec = CTL_LEAF_SPECULATE && (SINGLE || level == 1);
         const int tBits = __float_as_int(tcull);
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL &&
-               ((spec && (kSpecSteps == 0 || specLeft > 0)) || leafAddr >= 0)) {
+               ((spec && (kSpecSteps == 0 || specLeft > 0) && !specStop) || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
@@ -678,7 +688,8 @@ struct Traverser4 {
             CTL_WIDE_CHILD(k3, c3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y)
 #undef CTL_WIDE_CHILD
             const bool held = leafAddr < 0;
-            wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
+            const int m = wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
+            if (CTL_SPEC_NOPOP && held && m == 0) specStop = true;
             if (kSpecSteps > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpecSteps : specLeft);
             if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
@@ -873,9 +884,11 @@ struct Traverser4 {
         }
         else inner_binary(S, st, stats);
         resumeLeaves = false;
+        const bool stopped = specStop;
+        specStop = false;
         // a speculating lane the wave stopped before it reached its next leaf
         const bool cut = WIDE && CTL_LEAF_SPECULATE && (SINGLE || level == 1) && leafAddr < 0 &&
-                         (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (kSpecSteps == 0 || specLeft > 0);
+                         (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (kSpecSteps == 0 || specLeft > 0) && !stopped;
 #ifdef CTL_PROFILE_TRACE
         {
             const uint32_t nl = (uint32_t)__popcll(__ballot(leafAddr < 0));

@@ -412,6 +412,7 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
     static const bool nospec = std::getenv("ORACLE_WIDE_NOSPEC") != nullptr;
     static const int kSpec = std::getenv("ORACLE_SPEC_STEPS") ? std::atoi(std::getenv("ORACLE_SPEC_STEPS")) : 0;
     int specLeft = 0;
+    static const bool nopop = std::getenv("ORACLE_SPEC_NOPOP") != nullptr;
     for (;;) {
         const bool spec = level == 1 && !(nospec && single);
         const float* tree = level ? W.mesh.data() + 32 * (size_t)wnodeBase : W.scene.data();
@@ -441,12 +442,14 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
             for (int i = 0; i < 4; i++) m += k[i] != 0x7fffffff;
             for (int i = m - 1; i >= 1; i--) stack.push_back(c[i]);
             int next = m > 0 ? c[0] : pop();
+            const bool stopWalk = nopop && held && m == 0;
             if (next < 0 && leafAddr >= 0) {   // postpone one leaf
                 leafAddr = next;
                 next = pop();
             }
             nodeAddr = next;
             if (kSpec > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpec : specLeft);
+            if (stopWalk) break;
         }
         bool entered = false;
         while (leafAddr < 0) {
