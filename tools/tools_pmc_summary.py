@@ -29,9 +29,9 @@ import sys
 root = sys.argv[1]
 PASSES = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 FAMILIES = {
-    "path_kernel": "path_kernel_persistent<false, true, true, 0>",
-    "path_kernel_full": "path_kernel_persistent<false, true, true, 1>",
-    "primary_intersect": "intersect_kernel<false, false, true, true>",
+    "path_kernel": "path_kernel_persistent<false, true, 1, 0>",
+    "path_kernel_full": "path_kernel_persistent<false, true, 1, 1>",
+    "primary_intersect": "intersect_kernel<false, false, true, 1>",
     "prim_kernel": "prim_kernel<",
     "fold_samples": "fold_samples_kernel",
     "sampler": "sampler_kernel",
@@ -48,7 +48,7 @@ for f in sorted(glob.glob(os.path.join(root, "g*", "**", "*counter_collection.cs
         agg[fam][c] += float(row.get("Counter_Value", 0))
         disp[fam][c].add((f, row.get("Dispatch_Id")))
 
-here = os.path.dirname(os.path.abspath(__file__))
+here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # the repo root
 sys.path.insert(0, here)
 from buildid import source_fingerprint  # noqa: E402
 libp = os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_trace.so")
