@@ -74,6 +74,12 @@ constexpr int kSpecSteps = CTL_SPEC_STEPS;
 #ifndef CTL_SPEC_NOPOP
 #define CTL_SPEC_NOPOP 0
 #endif
+// CTL_BREAK_ALL 1: the 4-wide node loop counts every lane still in it (looking
+// for a leaf or walking past one) against CTL_LEAF_BREAK, not only the lanes
+// that look for their first leaf, so fewer walking lanes are cut.
+#ifndef CTL_BREAK_ALL
+#define CTL_BREAK_ALL 0
+#endif
 
 // Per-ray visit order (round 4).  Every traversal is a function of its ray
 // alone, never of the other rays of its wave:
@@ -604,7 +610,7 @@ struct Traverser4 {
             const int m = wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
             if (CTL_SPEC_NOPOP && held && m == 0) specStop = true;
             if (kSpecSteps > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpecSteps : specLeft);
-            if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
+            if (__popcll(__ballot(CTL_BREAK_ALL || leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
@@ -691,7 +697,7 @@ struct Traverser4 {
             const int m = wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
             if (CTL_SPEC_NOPOP && held && m == 0) specStop = true;
             if (kSpecSteps > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpecSteps : specLeft);
-            if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
+            if (__popcll(__ballot(CTL_BREAK_ALL || leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
