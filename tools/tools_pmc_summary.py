@@ -32,6 +32,8 @@ FAMILIES = {
     "path_kernel": "path_kernel_persistent<false, true, 1, 0>",
     "path_kernel_full": "path_kernel_persistent<false, true, 1, 1>",
     "primary_intersect": "intersect_kernel<false, false, true, 1>",
+    "path_kernel_w8": "path_kernel_persistent<false, true, 2, 0>",
+    "primary_intersect_w8": "intersect_kernel<false, false, true, 2>",
     "prim_kernel": "prim_kernel<",
     "fold_samples": "fold_samples_kernel",
     "sampler": "sampler_kernel",
