@@ -52,7 +52,7 @@ CTL_HD spec env_texel(const EnvView& E, int x, int y) {
     x = clampi_ref(x, 0, w - 1);
     y = clampi_ref(y, 0, h - 1);
     const uint32_t c = E.texels[t.offsets[0] + (uint32_t)y * (uint32_t)w + (uint32_t)x];
-    return mk3(float(c & 0xffu) / 255.0f, float((c >> 8) & 0xffu) / 255.0f, float((c >> 16) & 0xffu) / 255.0f);
+    return mk3(unorm8(c & 0xffu), unorm8((c >> 8) & 0xffu), unorm8((c >> 16) & 0xffu));
 }
 
 CTL_HD float interval_to_tent(float sample) {   // Warp::intervalToTent (Math/Warp.h:13-27)
