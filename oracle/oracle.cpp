@@ -408,7 +408,11 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
         enter(~(uint32_t)d->scene_start_node);
         level = 1;
     }
-    // measurement only: ORACLE_WIDE_NOSPEC=1 stops at the first leaf in the mesh level too
+    // Measurement only (profiles/r04_ab_spec.txt), never set by the tests of the
+    // shipped order: ORACLE_WIDE_NOSPEC=1 stops at the first leaf in the mesh level of a
+    // one-mesh scene (the order of the device's CTL_LEAF_SPECULATE=0 / CTL_IFIF=1 builds);
+    // ORACLE_SPEC_STEPS=K bounds the walk past a postponed leaf to K inner nodes
+    // (CTL_SPEC_STEPS=K); ORACLE_SPEC_NOPOP=1 ends it where it would pop (CTL_SPEC_NOPOP=1).
     static const bool nospec = std::getenv("ORACLE_WIDE_NOSPEC") != nullptr;
     static const int kSpec = std::getenv("ORACLE_SPEC_STEPS") ? std::atoi(std::getenv("ORACLE_SPEC_STEPS")) : 0;
     int specLeft = 0;
