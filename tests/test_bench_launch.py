@@ -51,3 +51,12 @@ def test_launch_groups_near_equal():
     for steps in range(1, 70):
         g = bench.launch_groups(steps, 8)
         assert sum(g) == steps and max(g) - min(g) <= 1 and max(g) <= 8
+
+
+@pytest.mark.parametrize("rank", [-1, 8])
+def test_emulate_rank_outside_the_job_is_refused(rank):
+    """--emulate-ranks N --emulate-rank r times rank r's share of an N-GPU job
+    (DESIGN §8); a rank outside 0..N-1 is refused before anything touches a GPU."""
+    r = _run(["--emulate-ranks", "8", "--emulate-rank", str(rank), "--no-cpu-baseline"], timeout=120)
+    assert r.returncode == 2
+    assert "outside 0..7" in r.stderr
