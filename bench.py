@@ -84,9 +84,9 @@ def parse(argv=None):
                          "launch per pass, the reference's DoPass granularity)")
     ap.add_argument("--one-pass-leg", type=int, default=8,
                     help="passes of the one-launch-per-pass comparison leg (0: skip)")
-    ap.add_argument("--bvh", default="wide", choices=["wide", "wideq", "w8", "binary"],
-                    help="device traversal: 4-wide collapsed BVH (wideq: 64-B quantized nodes; w8: the 8-wide "
-                         "compressed tree), or the reference's binary order")
+    ap.add_argument("--bvh", default="wide", choices=["wide", "wideq", "binary"],
+                    help="device traversal: 4-wide collapsed BVH (wideq: 64-B quantized nodes), or the reference's "
+                         "binary order")
     ap.add_argument("--dopass-leg", type=int, default=8,
                     help="passes of the reference DoPass leg (ctl_scene_update + sampler tables + one "
                          "ctl_render_pass per pass; 0: skip)")
@@ -152,20 +152,12 @@ def pmc_profile():
     tools_pmc.sh + tools_pmc_summary.py) and whether it was measured on the
     libctl_trace.so this run loads."""
     import glob
-    import hashlib
     here = os.path.dirname(os.path.abspath(__file__))
     files = sorted(glob.glob(os.path.join(here, "profiles", "r[0-9][0-9]*_pmc.json")))
     if not files:
         return None, None, False
     j = json.load(open(files[-1]))
-    lib = os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_trace.so")
-    match = hashlib.sha256(open(lib, "rb").read()).hexdigest() == j.get("lib_sha256")
-    if not match and j.get("src_sha256"):
-        # hipcc builds are not byte-reproducible: a rebuild of the profiled sources
-        # matches through the source fingerprint (buildid.py)
-        from buildid import source_fingerprint
-        match = "sources" if source_fingerprint(here) == j["src_sha256"] else False
-    return j, os.path.relpath(files[-1], here), match
+    return j, os.path.relpath(files[-1], here), build_match(j, here)
 
 
 def roofline(prof, fam, ms, alg_bytes, kernel, units=None):
@@ -185,6 +177,10 @@ def roofline(prof, fam, ms, alg_bytes, kernel, units=None):
     scale = 1.0
     if units is not None and k.get("units_per_launch"):
         scale = units / k["units_per_launch"]
+    elif units is not None and k:
+        # counters of another launch shape without its unit count cannot be scaled to this one
+        k = {}
+        match = "profile has no units_per_launch for " + fam
     hbm = k.get("hbm_bytes")
     hbm = hbm * scale if hbm else hbm
     r = {"bound": "hbm", "achieved": None, "peak": PEAK_HBM, "unit": "GB/s", "frac": None, "traffic": hbm,
@@ -303,7 +299,7 @@ def primary_ray_leg(pt, dev, stream, sptr, torch, pass_index, prof, launches=10)
     torch.cuda.synchronize(dev)
     ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / launches
     kname = "intersect_kernel<closest,single,wide> (ctl_intersect over ctl_camera_rays)"
-    rl = roofline(prof, "primary_intersect", ms, alg, kname)
+    rl = roofline(prof, "primary_intersect", ms, alg, kname, units=n)   # counters per ray, scaled to n rays
     rl["alg_model"].update({"inner_nodes": int(st[1]), "tri_tests": int(st[2]), "instances": int(st[3])})
     return {
         "kernel": kname,
@@ -423,10 +419,28 @@ def binary_leg(ctl, pt, desc, fb, stream, sptr, torch, pass_index, passes):
             "passes": passes, "ms_per_pass": round(ms / passes, 3), "mrays_s": round(rays / (ms * 1e-3) / 1e6, 2)}
 
 
+def build_match(j, here):
+    """Whether a committed record was measured on the libctl_trace.so this run
+    loads: True (library hash), "sources" (a rebuild of the same sources,
+    buildid.py: hipcc builds are not byte-reproducible) or False."""
+    import hashlib
+    lib = os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_trace.so")
+    if hashlib.sha256(open(lib, "rb").read()).hexdigest() == j.get("lib_sha256"):
+        return True
+    if j.get("src_sha256"):
+        from buildid import source_fingerprint
+        return "sources" if source_fingerprint(here) == j["src_sha256"] else False
+    return False
+
+
 def reference_order_record():
-    """The newest committed distance of the default 4-wide order from the
-    reference's binary order (profiles/rNN_reference_order.json, written by
-    tests/test_reference_order.py::test_full_size_c3_reference_order_distance)."""
+    """The newest committed distance of the shipped default from the reference's
+    CPU path (profiles/rNN_reference_order.json, written by
+    tests/test_reference_order.py::test_full_size_c3_reference_order_distance):
+    per-ray order classes, NEE visibility flips of the any-hit shadow query
+    against the reference's closest-hit Occluded, and one full pass against the
+    oracle's render of the reference's CPU path; `record_matches_binary` ties it
+    to this run's library."""
     import glob
     here = os.path.dirname(os.path.abspath(__file__))
     files = sorted(glob.glob(os.path.join(here, "profiles", "r[0-9][0-9]*_reference_order.json")))
@@ -434,10 +448,20 @@ def reference_order_record():
         return None
     j = json.load(open(files[-1]))
     t = j.get("total", {})
-    return {"rays": t.get("rays"), "differing_rays": t.get("differ"), "ties": t.get("ties"),
-            "reference_culled": t.get("ref_culled"), "wide_culled": t.get("other_culled"),
-            "pixels_over_1e-4_rel": (j.get("pass") or {}).get("pixels_over_1e-4_rel"),
-            "pixels": (j.get("pass") or {}).get("pixels"), "source": os.path.relpath(files[-1], here)}
+    ps = j.get("pass") or {}
+    ref = ps.get("reference_cpu_path", ps)   # round 4 records: one comparison, any-hit on both sides
+    out = {"rays": t.get("rays"), "differing_rays": t.get("differ"), "ties": t.get("ties"),
+           "reference_culled": t.get("ref_culled"), "wide_culled": t.get("other_culled"),
+           "pixels": ref.get("pixels"), "pixels_over_1e-4_rel": ref.get("pixels_over_1e-4_rel"),
+           "pixels_differing": ref.get("pixels_differing"),
+           "vs": ("the reference CPU path (binary order, closest-hit Occluded)" if "reference_cpu_path" in ps
+                  else "binary order with any-hit shadows"),
+           "source": os.path.relpath(files[-1], here),
+           "record_matches_binary": build_match(j.get("build", {}), here) if j.get("build") else False}
+    if j.get("nee_visibility"):
+        out["nee_visibility_flips"] = j["nee_visibility"].get("visibility_flips")
+        out["nee_rays"] = j["nee_visibility"].get("rays")
+    return out
 
 
 def wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_index, passes):
@@ -537,24 +561,63 @@ def c5_leg(ctl, dev, torch, stream, sptr, a, threads):
 
 def apply_bvh(ctl, desc, bvh):
     """The device tree format --bvh selects (a scene flag of the desc)."""
-    desc.flags |= {"wide": 0, "binary": ctl.CTL_SCENE_BINARY_BVH, "wideq": ctl._abi.CTL_SCENE_WIDE_QUANT,
-                   "w8": ctl._abi.CTL_SCENE_WIDE8}[bvh]
+    desc.flags |= {"wide": 0, "binary": ctl.CTL_SCENE_BINARY_BVH, "wideq": ctl._abi.CTL_SCENE_WIDE_QUANT}[bvh]
+
+
+def rank_report(dist, world, elapsed_s, steps, reduce_ms, dev):
+    """Every rank's wall time per step of the timed region (its own bracket,
+    the framebuffer reduce included) and the time of its reduce alone, plus the
+    world size and backend the process group runs: the N-GPU line's `ranks`
+    record, so a scaling run explains itself (slowest rank, reduce share).
+    Collective: every rank calls it."""
+    import torch
+    mine = torch.tensor([elapsed_s * 1e3 / max(1, steps), -1.0 if reduce_ms is None else float(reduce_ms)],
+                        dtype=torch.float64, device=dev)
+    if world > 1:
+        allv = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+    else:
+        allv = [mine]
+    ms = [round(float(v[0]), 4) for v in allv]
+    return {"world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else None,
+            "ms_per_step": ms, "ms_per_step_min": min(ms), "ms_per_step_max": max(ms),
+            "reduce_ms": [round(float(v[1]), 4) for v in allv] if world > 1 else None,
+            "note": "per rank: its timed-region wall time / steps (the reduce included) and the framebuffer "
+                    "reduce alone (HIP events around shard.reduce_framebuffer); value uses the max over ranks"}
 
 
 def launch_check(a, world, rank):
     """--launch-check: every rank joins the process group (gloo) and the ranks
-    count themselves; rank 0 prints the line shape the bench prints, with
-    n_gpus = the ranks that reported."""
+    count themselves, reduce a 1920 x 64 PixelData framebuffer through
+    shard.reduce_framebuffer and report their times like the bench's N-GPU
+    line (`ranks`); rank 0 prints the line shape, with n_gpus = the ranks that
+    reported.  No GPU, no scene."""
     import torch
     import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from cudatracerlib_amd import shard
     if world > 1:
         dist.init_process_group("gloo")
     t = torch.ones(1, dtype=torch.int64)
     if world > 1:
         dist.all_reduce(t)
+    fb = torch.zeros((1920 * 64, 7), dtype=torch.float32)
+    fb[rank::max(1, world), :] = 1.0   # disjoint pixels per rank, as the tile shards
+    t0 = time.perf_counter()
+    red_ms = None
+    if world > 1:
+        dist.barrier()
+        r0 = time.perf_counter()
+        img = shard.reduce_framebuffer(fb, dist, out=torch.empty_like(fb))
+        red_ms = (time.perf_counter() - r0) * 1e3
+        if rank == 0 and not bool((img == 1.0).all()):
+            raise RuntimeError("launch-check: the reduced framebuffer is not the union of the shards")
+    elapsed = time.perf_counter() - t0
+    ranks = rank_report(dist, world, elapsed, 1, red_ms, torch.device("cpu"))
     if rank == 0:
         print(json.dumps({"metric": "launch-check", "n_gpus": int(t.item()), "world_size": world,
-                          "gpus_requested": a.gpus}), flush=True)
+                          "gpus_requested": a.gpus, "ranks": ranks}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -697,8 +760,13 @@ def main(argv=None):
         step(s, timed=True, nsteps=g)
         s += g
     ev1.record(stream)
+    red0 = red1 = None
     if world > 1:
+        red0 = torch.cuda.Event(enable_timing=True)
+        red1 = torch.cuda.Event(enable_timing=True)
+        red0.record(stream)
         shard.reduce_framebuffer(fb, dist, out=image)   # RCCL over xGMI, into rank 0's image
+        red1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -747,6 +815,7 @@ def main(argv=None):
         except Exception as e:
             c5 = {"error": f"{type(e).__name__}: {e}"}
     red = dev if a.backend == "nccl" else torch.device("cpu")
+    ranks = rank_report(dist, world, elapsed, a.steps, red0.elapsed_time(red1) if red0 is not None else None, red)
     tt = torch.tensor([elapsed], dtype=torch.float64, device=red)
     rr = torch.tensor([rays, 1], dtype=torch.int64, device=red)   # rays, ranks that rendered
     if world > 1:
@@ -810,6 +879,7 @@ def main(argv=None):
                 **({"emulated_ranks": shards, "emulated_rank": tile_rank} if shards != world else {}),
             },
             "roofline": rl,
+            "ranks": ranks,
             "primary_rays": prim,
             "one_pass_launches": single,
             "reference_dopass": dopass,
@@ -829,9 +899,13 @@ def main(argv=None):
             ref_hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
             ref_hs.set_bvh_builder("sbvh", 1.0e-5).set_bvh_params(0.0, 8, 0, 8)
             ref_desc = ref_hs.compile(threads=threads)
-            out["cpu_baseline"] = cpu_baseline(ref_desc, pt.params, a.cpu_seconds, cc["threads"])
+            # and its own shadow test: a closest-hit traceRay + distance test (Occluded)
+            ref_params = ctl.PTParams.from_buffer_copy(pt.params)
+            ref_params.shadow_any_hit = 0
+            out["cpu_baseline"] = cpu_baseline(ref_desc, ref_params, a.cpu_seconds, cc["threads"])
             out["cpu_baseline"].update({k: v for k, v in cc.items() if k != "threads"})
-            out["cpu_baseline"]["bvh"] = "SBVH, leaves <= 8 (the reference's SplitBVHBuilder configuration)"
+            out["cpu_baseline"]["bvh"] = ("SBVH, leaves <= 8 (the reference's SplitBVHBuilder configuration), binary "
+                                          "visit order, closest-hit Occluded shadow rays: the reference's CPU path")
             out["cpu_baseline"]["note"] = (
                 "threads = min(affinity set, cgroup quota, the job's CPU share OMP_NUM_THREADS); the oracle's "
                 "rays are independent, so the rate scales about linearly with threads (per_thread_mrays_s)")

@@ -291,23 +291,6 @@ def host_wide_trees(desc):
     return mesh, wbase, scene
 
 
-def host_w8_tree(desc):
-    """The 8-wide tree ctl_scene_upload builds under CTL_SCENE_WIDE8
-    (ctl_host_w8_tree): (nodes (n, 20) uint32 = 80-B records, relaid Woop
-    entries (m, 12) float32, their index words (m,) uint32), or None when the
-    scene cannot use it (then the upload keeps the 4-wide traversal)."""
-    L = lib()
-    nn, ne = C.c_uint64(0), C.c_uint64(0)
-    if L.ctl_host_w8_tree(C.byref(desc), None, 0, C.byref(nn), None, None, 0, C.byref(ne)) != 0:
-        return None
-    nodes = np.zeros((nn.value, 20), np.uint32)
-    woop = np.zeros((ne.value, 12), np.float32)
-    idx = np.zeros(ne.value, np.uint32)
-    _check(L.ctl_host_w8_tree(C.byref(desc), nodes.ctypes.data, nn.value, C.byref(nn), woop.ctypes.data,
-                              idx.ctypes.data, ne.value, C.byref(ne)), None, "ctl_host_w8_tree")
-    return nodes, woop, idx
-
-
 class Tracer:
     """Per-GPU traversal context (InitializeKernel/UpdateKernel/IntersectBuffers)."""
 
@@ -352,6 +335,12 @@ class Tracer:
         _check(self._L.ctl_intersect(self._ctx, int(n), rays_ptr, hits_ptr, 1 if any_hit else 0, stream),
                self._ctx, "ctl_intersect")
 
+    def occluded(self, n, rays_ptr, out_ptr, any_hit=False, stream=0):
+        """KernelDynamicScene::Occluded(ray, 0, ray.tmax) per ray into uint32 out
+        (ctl_occluded): the reference's closest-hit form or the any-hit query."""
+        _check(self._L.ctl_occluded(self._ctx, int(n), rays_ptr, out_ptr, 1 if any_hit else 0, stream),
+               self._ctx, "ctl_occluded")
+
     def intersect_stats(self, n, rays_ptr, hits_ptr, any_hit=False, stream=0):
         out = (C.c_uint64 * 4)()
         _check(self._L.ctl_intersect_stats(self._ctx, int(n), rays_ptr, hits_ptr, 1 if any_hit else 0, out, stream),
@@ -385,18 +374,6 @@ class Tracer:
         wbase = self.read_array(_abi.CTL_ARRAY_MESH_WIDE_BASE, 0, wbase0.size, np.uint32, 1).reshape(-1)
         scene = self.read_array(_abi.CTL_ARRAY_SCENE_WIDE_BVH, 0, scene0.shape[0], np.float32, 32)
         return mesh, wbase, scene
-
-    def w8_tree(self, desc):
-        """The 8-wide tree the device traverses (CTL_ARRAY_W8_*; the upload's pad
-        entry dropped), in host_w8_tree's layout; None when the scene uses the
-        4-wide traversal."""
-        h = host_w8_tree(desc)
-        if h is None:
-            return None
-        nodes = self.read_array(_abi.CTL_ARRAY_W8_NODES, 0, h[0].shape[0], np.uint32, 20)
-        woop = self.read_array(_abi.CTL_ARRAY_W8_WOOP, 0, h[1].shape[0], np.float32, 12)
-        idx = self.read_array(_abi.CTL_ARRAY_W8_INDICES, 0, h[2].size, np.uint32, 1).reshape(-1)
-        return nodes, woop, idx
 
     def rays_traced(self):
         return int(self._L.ctl_rays_traced(self._ctx))

@@ -10,11 +10,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # CTL_LIB overrides the library path (variant builds for measurements).
 LIB_PATH = os.environ.get("CTL_LIB") or os.path.join(_HERE, "_lib", "libctl_trace.so")
 
+# CTL_ABI_VERSION of the include/ctl_trace.h these bindings mirror; load()
+# refuses a library that reports another (mismatched struct layouts).
+ABI_VERSION = 3
 CTL_OK = 0
 CTL_SCENE_HALF_HOST_QUIRK = 1
 CTL_SCENE_BINARY_BVH = 2
 CTL_SCENE_WIDE_QUANT = 4
-CTL_SCENE_WIDE8 = 8
 CTL_DEFAULT_SPLIT_ALPHA = 0.1875   # include/ctl_trace.h
 CTL_XMSH_MATERIAL_RECORD_SIZE = 148
 CTL_COMM_ID_BYTES = 128
@@ -41,8 +43,7 @@ CTL_DIRTY_TEXTURES, CTL_DIRTY_ENV, CTL_DIRTY_ALL = 256, 512, 1023
 (CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS,
  CTL_ARRAY_SAMPLES_1D, CTL_ARRAY_SAMPLES_2D, CTL_ARRAY_NODE_XF, CTL_ARRAY_NODE_INV_XF, CTL_ARRAY_LIGHTS,
  CTL_ARRAY_LIGHT_TRIS, CTL_ARRAY_LIGHT_CDF, CTL_ARRAY_SCENE_BOX, CTL_ARRAY_ENV, CTL_ARRAY_WIDE_BVH,
- CTL_ARRAY_SCENE_WIDE_BVH, CTL_ARRAY_MESH_WIDE_BASE, CTL_ARRAY_W8_NODES, CTL_ARRAY_W8_WOOP,
- CTL_ARRAY_W8_INDICES) = range(21)
+ CTL_ARRAY_SCENE_WIDE_BVH, CTL_ARRAY_MESH_WIDE_BASE) = range(18)
 
 
 class BVHNode(C.Structure):          # BVHNodeData, 64 B
@@ -209,6 +210,7 @@ SYMBOLS = [
     ("ctl_sampler_generate", C.c_int32, [_vp, C.c_uint64, _vp]),
     ("ctl_sampler_upload", C.c_int32, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
     ("ctl_intersect", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, _vp]),
+    ("ctl_occluded", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, _vp]),
     ("ctl_render_pass", C.c_int32, [_vp, C.POINTER(PTParams), _vp, _vp]),
     ("ctl_render_passes", C.c_int32, [_vp, C.POINTER(PTParams), C.c_uint64, C.c_uint32, _vp, _vp]),
     ("ctl_wpt_render_pass", C.c_int32, [_vp, C.POINTER(WptParams), _vp, _vp]),
@@ -218,8 +220,6 @@ SYMBOLS = [
     ("ctl_sync", C.c_int32, [_vp, _vp]),
     ("ctl_scene_stack_bound", C.c_int32, [_vp]),
     ("ctl_host_bvh_stack_bound", C.c_int32, [_vp, C.c_uint64, C.c_int32, _vp]),
-    ("ctl_host_w8_tree", C.c_int32, [C.POINTER(SceneDesc), _vp, C.c_uint64, C.POINTER(C.c_uint64), _vp, _vp,
-                                     C.c_uint64, C.POINTER(C.c_uint64)]),
     ("ctl_host_wide_trees", C.c_int32, [C.POINTER(SceneDesc), _vp, C.c_uint64, C.POINTER(C.c_uint64), _vp, _vp,
                                         C.c_uint64, C.POINTER(C.c_uint64)]),
     ("ctl_intersect_stats", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, C.POINTER(C.c_uint64), _vp]),
@@ -278,6 +278,9 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    v = lib.ctl_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"{path} reports CTL_ABI_VERSION {v}, these bindings are for {ABI_VERSION}: rebuild it")
     if path == LIB_PATH:
         _lib = lib
     return lib

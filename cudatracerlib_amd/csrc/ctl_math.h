@@ -39,8 +39,8 @@ CTL_HD float fracf_ref(float f) { return f - floorf(f); }                 // Mat
 // On the device the fp64 library bodies are large (range reduction, ~30-60
 // fp64 ops and their register pairs); each one stays out of line so a caller's
 // register peak does not include them (rough_sample: 148 -> 69 VGPRs, which is
-// what lets the C5 path kernel run at 4 waves/SIMD).  -DCTL_CR_INLINE inlines them.
-#if defined(__HIP__) && !defined(CTL_CR_INLINE)
+// what lets the C5 path kernel run at 4 waves/SIMD).
+#if defined(__HIP__)
 #define CTL_CR static __host__ __device__ __noinline__
 #else
 #define CTL_CR CTL_HD

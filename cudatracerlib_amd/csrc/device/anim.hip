@@ -30,7 +30,6 @@
 #include "../ctl_shade.h"
 #include "../host/bvh_wide.h"
 #include "../ctl_qnode.h"
-#include "../host/bvh_w8.h"
 
 namespace ctl {
 
@@ -68,7 +67,7 @@ struct AnimState {
     const uint32_t* d_tris = nullptr;
     float* d_mesh_boxes = nullptr;      // 6 per mesh
     float* d_inst_boxes = nullptr;      // 6 per node
-    float* d_eps = nullptr;             // scene box (6) + eps
+    float* d_eps = nullptr;             // scene box (6) + eps + cull_m (3)
     float* h_eps = nullptr;             // pinned
     float4* d_P = nullptr;
     float4* d_N = nullptr;
@@ -263,13 +262,15 @@ __global__ __launch_bounds__(kAB) void inst_box_kernel(const ctl_node* __restric
 // scene box = union of the instance boxes; eps = 1e-4 * |size| (DynamicScene.cpp:587);
 // the environment light's scene sphere follows the box (UpdateScene re-runs
 // InfiniteLight::Update, DynamicScene.cpp:540-542, Light.h:316-323)
-__global__ void scene_eps_kernel(const float* inst, uint32_t n, float* out, ctl_env_light* env) {
+__global__ void scene_eps_kernel(const float* inst, uint32_t n, float* out, ctl_env_light* env, const float* mesh_boxes,
+                                 uint32_t n_meshes) {
     float lo[3], hi[3];
     box_empty(lo, hi);
     for (uint32_t i = 0; i < n; i++) box_extend(lo, hi, inst + 6 * i, inst + 6 * i + 3);
     for (int k = 0; k < 3; k++) { out[k] = lo[k]; out[3 + k] = hi[k]; }
     const f3 size = mk3(hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]);
     out[6] = 1e-4f * length(size);
+    cull_bound(lo, hi, mesh_boxes, n_meshes, out + 7);   // DevScene::cull_m of the moved scene
     if (env) {
         const f3 l = mk3(lo[0], lo[1], lo[2]), h = mk3(hi[0], hi[1], hi[2]);
         const f3 c = (l + h) * 0.5f;   // AABB::Center
@@ -424,8 +425,8 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
     A->n_meshes = d->n_meshes;
     A->n_nodes = d->n_nodes;
     if (!anim_upload(A, &A->d_mesh_boxes, d->mesh_boxes, 6ull * d->n_meshes) ||
-        !anim_alloc(A, &A->d_inst_boxes, 6ull * std::max(1u, d->n_nodes)) || !anim_alloc(A, &A->d_eps, 8) ||
-        hipHostMalloc((void**)&A->h_eps, 8 * sizeof(float), hipHostMallocDefault) != hipSuccess)
+        !anim_alloc(A, &A->d_inst_boxes, 6ull * std::max(1u, d->n_nodes)) || !anim_alloc(A, &A->d_eps, 10) ||
+        hipHostMalloc((void**)&A->h_eps, 10 * sizeof(float), hipHostMallocDefault) != hipSuccess)
         return fail("animation state allocation failed");
     const bool wide = !wn.empty() || !sw.empty();
     // the instance tree's refit plan: animated meshes and moved nodes (ctl_scene_set_transform)
@@ -537,13 +538,14 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
         launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);
         hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps,
-                           const_cast<ctl_env_light*>(S.env));
-        if (hipMemcpyAsync(A->h_eps, A->d_eps, 7 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                           const_cast<ctl_env_light*>(S.env), A->d_mesh_boxes, A->n_meshes);
+        if (hipMemcpyAsync(A->h_eps, A->d_eps, 10 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {
             c->err = "scene_animate: epsilon readback failed";
             return CTL_ERR_HIP;
         }
         S.ray_eps = A->h_eps[6];
+        for (int k = 0; k < 3; k++) S.cull_m[k] = A->h_eps[7 + k];
         c->device_eps = true;
     }
     c->device_edited = true;
@@ -587,14 +589,15 @@ CTL_API ctl_status ctl_scene_set_transform(ctl_ctx* c, uint32_t node, const ctl_
     if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
     if (S.wide) launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);
     hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps,
-                       const_cast<ctl_env_light*>(S.env));
+                       const_cast<ctl_env_light*>(S.env), A->d_mesh_boxes, A->n_meshes);
     if (hipGetLastError() != hipSuccess) { c->err = "scene_set_transform: launch failed"; return CTL_ERR_HIP; }
-    if (hipMemcpyAsync(A->h_eps, A->d_eps, 7 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(A->h_eps, A->d_eps, 10 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
         c->err = "scene_set_transform: epsilon readback failed";
         return CTL_ERR_HIP;
     }
     S.ray_eps = A->h_eps[6];
+    for (int k = 0; k < 3; k++) S.cull_m[k] = A->h_eps[7 + k];
     c->device_eps = true;
     c->device_edited = true;
     return CTL_OK;
@@ -640,16 +643,6 @@ CTL_API ctl_status ctl_scene_read(ctl_ctx* c, uint32_t array, uint64_t first, ui
         case CTL_ARRAY_ENV:
             if (!S.env) { c->err = "scene_read: no environment light"; return CTL_ERR_STATE; }
             src = S.env; elem = sizeof(ctl_env_light); n = 1; break;
-        case CTL_ARRAY_W8_NODES:
-        case CTL_ARRAY_W8_WOOP:
-        case CTL_ARRAY_W8_INDICES: {
-            if (!S.w8_on) { c->err = "scene_read: no 8-wide tree in use (" + c->w8_why + ")"; return CTL_ERR_STATE; }
-            const int a = array == CTL_ARRAY_W8_NODES ? SA_W8 : array == CTL_ARRAY_W8_WOOP ? SA_W8WOOP : SA_W8IDX;
-            elem = array == CTL_ARRAY_W8_NODES ? sizeof(W8Node) : array == CTL_ARRAY_W8_WOOP ? sizeof(ctl_woop_tri) : 4;
-            src = c->sarr[a].p;
-            n = c->sarr[a].bytes / elem;
-            break;
-        }
         case CTL_ARRAY_WIDE_BVH:
         case CTL_ARRAY_SCENE_WIDE_BVH:
         case CTL_ARRAY_MESH_WIDE_BASE:

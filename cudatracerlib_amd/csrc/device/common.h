@@ -166,11 +166,10 @@ __device__ __forceinline__ void add_sample(ctl_pixel* fb, const PathParams& P, f
 // A kernel's by-value record argument read in place from the kernel-argument
 // segment (device pass; `arg` itself on the host pass, which never runs it).
 // off = the argument's byte offset among the explicit arguments, laid out in
-// order at their natural alignment (kernarg_next).  -DCTL_KERNARG_BYVALUE
-// keeps the by-value copies for A/B runs.
+// order at their natural alignment (kernarg_next).
 template <class T>
 __device__ __forceinline__ const T& kernarg_ref(const T& arg, size_t off) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(CTL_KERNARG_BYVALUE)
+#if defined(__HIP_DEVICE_COMPILE__)
     (void)arg;
     return *reinterpret_cast<const T*>((const char*)__builtin_amdgcn_kernarg_segment_ptr() + off);
 #else
@@ -523,12 +522,20 @@ __device__ __forceinline__ bool shade_hit(const DevScene& S, const PathParams& P
 
 // KernelDynamicScene::Occluded(ray, 0, dist) decided from a finished shadow
 // traversal (KernelDynamicScene.cu:70-80): any-hit over (eps, dist - eps), or
-// the reference's closest hit tested against (eps, dist - eps).
+// the reference's closest hit tested against (eps, dist - eps), where a miss
+// with an infinite dist is not occluded (:77-78).
 __device__ __forceinline__ bool shadow_occluded(const DevScene& S, bool any_hit, const HitRec& h, float dist) {
     if (any_hit) return h.tri != 0xffffffffu;
     bool end = h.t < dist - S.ray_eps;
+    if (isinf(dist) && h.tri == 0xffffffffu) end = false;
     return h.t > 0 + S.ray_eps && end;
 }
+// The any-hit shadow query over (eps, dist - eps) culls boxes at
+// dist + slab_slack(ray) (traverse.h), not at its acceptance bound: a box whose
+// rounded slab entry lands past dist - eps, or past dist (the slab cancels two
+// products of size |o| |idir|), can hold a hit below dist - eps, which the
+// reference's closest-hit query finds (it culls nothing before its first hit).
+// tests/test_shadow_query.py measures the rules against the reference's form.
 
 // Wavefront path state, structure of arrays (capacity = paths per pass).
 struct WfState {
@@ -559,7 +566,7 @@ struct AnimState;
 // KernelDynamicScene stream, reused by ctl_scene_update while it fits.
 enum SceneArr : int {
     SA_BVH, SA_WOOP, SA_IDX, SA_TRI, SA_MATS, SA_MESHES, SA_NODES, SA_SBVH, SA_XF, SA_IXF, SA_LIGHTS, SA_LTRIS,
-    SA_LCDF, SA_LUT, SA_TEX, SA_TEXDATA, SA_ENV, SA_ENVDATA, SA_WBVH, SA_SWBVH, SA_WBASE, SA_W8, SA_W8WOOP, SA_W8IDX,
+    SA_LCDF, SA_LUT, SA_TEX, SA_TEXDATA, SA_ENV, SA_ENVDATA, SA_WBVH, SA_SWBVH, SA_WBASE,
     SA_COUNT
 };
 struct SceneArray {
@@ -610,7 +617,6 @@ struct ctl_ctx {
     hipEvent_t pass_ev[2] = {nullptr, nullptr}; // bracket the last render pass (ctl_last_pass_ms)
     bool pass_timed = false;
     size_t wide_nodes = 0;
-    std::string w8_why;                         // why the last upload kept the 4-wide traversal (CTL_SCENE_WIDE8)
     int stack_bound = 0;                        // worst-case traversal stack of the uploaded scene
     uint8_t* d_tile_flags = nullptr;            // PixelVarianceBuffer block flags
     size_t tile_flags_cap = 0;

@@ -68,17 +68,8 @@ namespace {
 // traversal's register peak no longer stacks on top of the shading state.
 // 16 KB stacks + 1 KB work words + 23 KB parked state = 40 KB per 256-thread
 // block: 4 blocks per CU, i.e. the 4 waves/SIMD the VGPR budget targets.
-// Lean kernel VGPR spills 36 -> 11; C3 2983 -> 3219 Mrays/s (same box, -DCTL_PARK=0 A/B).
-#ifndef CTL_PARK
-#define CTL_PARK 1
-#endif
-constexpr int kParkWords = CTL_PARK ? 23 : 0;
-// The FULL kernel keeps a path's first-hit texture partials in its own sample
-// slot (written only when the path ends) rather than in four VGPRs carried
-// through every trace (shade_hit's `part`).
-#ifndef CTL_PART_SLOT
-#define CTL_PART_SLOT 1
-#endif
+// Lean kernel VGPR spills 36 -> 11; C3 2983 -> 3219 Mrays/s (profiles/r03_park_slack_ab.txt).
+constexpr int kParkWords = 23;
 struct Park {
     int tid;
     __device__ __forceinline__ void put(int w, float x) const {
@@ -110,7 +101,7 @@ struct Park {
         sh.add = get3(16);
         rng.a = geti(19); rng.b = geti(20); rng.d1 = geti(21); rng.d2 = geti(22);
     }
-    // Partial loads and stores (CTL_LAZY_PARK): after a trace the lane loads only
+    // Partial loads and stores (the FULL kernels): after a trace the lane loads only
     // depth / specular and the sampler state; shade_hit reads the rest where it
     // is used (common.h shade_hit, `pk`), and only what changed goes back.
     __device__ __forceinline__ void load_core(PathVars& v, SamplerDev& rng) const {
@@ -135,9 +126,6 @@ struct Park {
         puti(21, rng.d1); puti(22, rng.d2);
     }
 };
-#ifndef CTL_LAZY_PARK
-#define CTL_LAZY_PARK 1
-#endif
 
 // dynamic LDS of path_kernel_persistent: lane stacks + the work item word per
 // lane + the parked path state
@@ -176,7 +164,8 @@ struct PathCtx {
             HitRec h;
             h.t = any ? sh.dist - S.ray_eps : FLT_MAX; h.tri = 0xffffffffu; h.node = 0xffffffffu; h.u = h.v = 0.0f;
             rays++;
-            if (any) ok &= trace_one<1, STATS, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
+            if (any) ok &= trace_one<1, STATS, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts,
+                                                                                sh.dist);
             else ok &= trace_one<0, STATS, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, v.rori, sh.d, 0.0f, S.ray_eps, h, st, &ts);
             if (!shadow_occluded(S, any, h, sh.dist)) v.cl = v.cl + sh.add;
         }
@@ -367,7 +356,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                         if (!apron_keep(P, kk, pX)) PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                         else if (v.depth++ < P.max_path_length) active = true;
                         else store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
-                        if (CTL_PARK && active) park.store(v, sh, rng);
+                        if (active) park.store(v, sh, rng);
                     } else {
                         PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // work item outside the image: no sample
                     }
@@ -389,7 +378,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             if (S.n_nodes != 0) {
                 Traverser<2, STATS, SINGLE, WIDE, CTL_ALPHA_OF(FULL)> T;
                 T.anyhit = shadowPhase && shadowAny;
-                T.init(S, v.rori, shadowPhase ? sh.d : v.rdir, 0.0f, S.ray_eps, h.t, st, &ts);
+                T.init(S, v.rori, shadowPhase ? sh.d : v.rdir, 0.0f, S.ray_eps, h.t, st, &ts,
+                       T.anyhit ? sh.dist : -1.0f);
                 while (!T.done) T.round(S, st, &ts);
                 h = T.h;
                 ok &= !st.overflow;
@@ -397,9 +387,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
 #ifdef CTL_PROFILE_TRACE
             prof_trace += wall_clock64() - pc0;
 #endif
-            constexpr bool lazy = CTL_PARK && CTL_LAZY_PARK && FULL != kShadeLean;
+            // the FULL kernels read parked state where the shading uses it (Park's
+            // partial loads), the lean kernel all of it after the trace
+            constexpr bool lazy = FULL != kShadeLean;
             if (lazy) park.load_core(v, rng);
-            else if (CTL_PARK) park.load(v, sh, rng);
+            else park.load(v, sh, rng);
             bool cont;
             if (shadowPhase) {
                 if (lazy) { v.cl = park.get3(0); sh.add = park.get3(16); }
@@ -412,7 +404,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                 v.cl = v.cl + env_miss<FULL>(S, P, v);   // PathTracer.cu:98-111
                 cont = false;
             } else {
-                float4* part = CTL_PART_SLOT ? PS.s + *pkw : nullptr;
+                // the FULL kernel keeps the path's first-hit texture partials in its own
+                // sample slot (written only when the path ends), not in four VGPRs
+                // carried through every trace
+                float4* part = PS.s + *pkw;
                 ending = lazy ? !shade_hit<FULL, SINGLE, Park>(S, P, rng, v, h, sh, part, &park)
                               : !shade_hit<FULL, SINGLE>(S, P, rng, v, h, sh, part);
                 shadowPhase = sh.valid;
@@ -426,7 +421,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                 if (lazy) park.load_px(v);
                 store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
                 active = false;
-            } else if (CTL_PARK && !lazy) {
+            } else if (!lazy) {
                 park.store(v, sh, rng);
             }
         }
@@ -467,14 +462,7 @@ template <bool ANY, bool STATS, bool SINGLE, int WIDE>
 #define CTL_REFILL_MIN 40   // batch traversal: refill once at least this many lanes of the wave wait for a ray
                            // (C3 WPT sweep 1/8/24/32/40/48/56: 1093/1222/1505/1563/1564/1569/1545 Mrays/s)
 #endif
-#ifndef CTL_INTERSECT_WAVES
-#define CTL_INTERSECT_WAVES 0   // waves/SIMD hint for the batch traversal (0: compiler's choice)
-#endif
-__global__ __launch_bounds__(kBlock)
-#if CTL_INTERSECT_WAVES
-__attribute__((amdgpu_waves_per_eu(CTL_INTERSECT_WAVES)))
-#endif
-void intersect_kernel(DevScene S_arg, int64_t n, const ctl_ray* rays, ctl_hit* hits,
+__global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            int64_t n2, const ctl_ray* rays2, ctl_hit* hits2,
                                                            unsigned long long* cursor, unsigned long long* counters,
                                                            const uint32_t* dcount, uint32_t band_w) {
@@ -571,6 +559,34 @@ __global__ __launch_bounds__(kBlock) void camera_ray_kernel(DevScene S_arg, Path
     float4* r4 = reinterpret_cast<float4*>(rays + g);
     r4[0] = o4;
     r4[1] = d4;
+}
+
+// Batch KernelDynamicScene::Occluded(Ray(o, d), 0, tmax) (KernelDynamicScene.cu:70-80),
+// tmax = the ray's d.w (o.w ignored), with the path kernels' semantics: the
+// reference's closest-hit form (ANYQ false) or the any-hit query of
+// shadow_any_hit = 1 (boxes culled at tmax + slab_slack, traverse.h).  traceRay flavour: span tmin
+// 0, triangles t > eps, the alpha test when the scene has alpha maps.  One ray
+// per lane: a checker and a drop-in for callers of Occluded, not a hot path.
+template <bool ANYQ, bool SINGLE, int WIDE>
+__global__ __launch_bounds__(kBlock) void occluded_kernel(DevScene S_arg, int64_t n, const ctl_ray* rays, uint32_t* out,
+                                                          unsigned long long* counters) {
+    const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
+    CTL_LANE_STACK(st);
+    TraceStats ts{0, 0, 0};
+    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= n) return;
+    const float4* r4 = reinterpret_cast<const float4*>(rays + g);
+    const float4 o = r4[0], d = r4[1];
+    const float dist = d.w;
+    HitRec h;
+    h.t = ANYQ ? dist - S.ray_eps : FLT_MAX;
+    h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
+    bool ok = true;
+    if (S.n_nodes != 0)
+        ok = trace_one<ANYQ ? 1 : 0, false, SINGLE, WIDE, true>(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), 0.0f,
+                                                               S.ray_eps, h, st, &ts, ANYQ ? dist : -1.0f);
+    out[g] = shadow_occluded(S, ANYQ, h, dist) ? 1u : 0u;
+    if (!ok) atomicAdd(&counters[1], 1ull);
 }
 
 }  // namespace
@@ -745,11 +761,9 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
     } while (0)
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;
-    const bool w8 = wide && single && c->scene.w8_on;
 #define IK2(AN, ST)                                                       \
     do {                                                                  \
         if (ST) { if (single) IK(AN, true, true, 0); else IK(AN, true, false, 0); } \
-        else if (w8) IK(AN, false, true, 2);                              \
         else if (wide) { if (single) IK(AN, false, true, 1); else IK(AN, false, false, 1); } \
         else { if (single) IK(AN, false, true, 0); else IK(AN, false, false, 0); } \
     } while (0)
@@ -769,6 +783,31 @@ CTL_API ctl_status ctl_intersect(ctl_ctx* c, int64_t n, const ctl_ray* d_rays, c
     if (r != CTL_OK) return r;
     // the batch call counts N rays (g_RayTracedCounterHost += N, TraceHelper.cu:745)
     return add_rays(c, (uint64_t)n, reinterpret_cast<hipStream_t>(stream));
+}
+
+CTL_API ctl_status ctl_occluded(ctl_ctx* c, int64_t n, const ctl_ray* d_rays, uint32_t* d_out, int32_t any_hit,
+                                void* stream) {
+    if (!c || n < 0 || (n > 0 && (!d_rays || !d_out))) return CTL_ERR_INVALID;
+    if (!c->has_scene) { c->err = "occluded: no scene uploaded"; return CTL_ERR_STATE; }
+    if (c->overflow_seen) return CTL_ERR_STATE;   // c->err names the overflow (ctl_sync)
+    CTL_HIP(c, hipSetDevice(c->device));
+    if (n == 0) return CTL_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+    if (grid.x == 0 || (uint64_t)(n + kBlock - 1) / kBlock > 0x7fffffffull) {
+        c->err = "occluded: batch too large for one launch";
+        return CTL_ERR_INVALID;
+    }
+    const bool single = c->scene.single != 0, wide = c->scene.wide != 0;
+#define OK_(AQ, SG, WD) hipLaunchKernelGGL((occluded_kernel<AQ, SG, WD>), grid, dim3(kBlock), kStackLdsBytes, s, \
+                                           c->scene, n, d_rays, d_out, c->d_counters)
+#define OK2(AQ) do { if (wide) { if (single) OK_(AQ, true, 1); else OK_(AQ, false, 1); } \
+                     else { if (single) OK_(AQ, true, 0); else OK_(AQ, false, 0); } } while (0)
+    if (any_hit) OK2(true); else OK2(false);
+#undef OK2
+#undef OK_
+    CTL_HIP(c, hipGetLastError());
+    return add_rays(c, (uint64_t)n, s);   // each Occluded is one traceRay (TraceHelper.cu:176)
 }
 
 static ctl_status prepare_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb, PathParams& P,
@@ -866,7 +905,6 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
 #define PK2(ST, SG, WD) do { if (full == kShadeEnv) PK(ST, SG, WD, kShadeEnv); else if (full == kShadeAlpha) PK(ST, SG, WD, kShadeAlpha); \
                               else if (full) PK(ST, SG, WD, kShadeFull); else PK(ST, SG, WD, kShadeLean); } while (0)
         if (stats) { if (single) PK2(true, true, 0); else PK2(true, false, 0); }
-        else if (wide && single && c->scene.w8_on) PK2(false, true, 2);
         else if (wide) { if (single) PK2(false, true, 1); else PK2(false, false, 1); }
         else { if (single) PK2(false, true, 0); else PK2(false, false, 0); }
 #undef PK2
@@ -877,7 +915,6 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
 #define MK2(ST, SG, WD) do { if (full == kShadeEnv) MK(ST, SG, WD, kShadeEnv); else if (full == kShadeAlpha) MK(ST, SG, WD, kShadeAlpha); \
                               else if (full) MK(ST, SG, WD, kShadeFull); else MK(ST, SG, WD, kShadeLean); } while (0)
         if (stats) { if (single) MK2(true, true, 0); else MK2(true, false, 0); }
-        else if (wide && single && c->scene.w8_on) MK2(false, true, 2);
         else if (wide) { if (single) MK2(false, true, 1); else MK2(false, false, 1); }
         else { if (single) MK2(false, true, 0); else MK2(false, false, 0); }
 #undef MK2

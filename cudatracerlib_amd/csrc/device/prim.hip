@@ -141,7 +141,8 @@ void prim_kernel(DevScene S_arg, PathParams P_arg, PrimParams Q, const float* s1
                                 hs.t = sh.dist - S.ray_eps; hs.u = hs.v = 0.0f;
                                 hs.tri = 0xffffffffu; hs.node = 0xffffffffu;
                                 rays++;
-                                ok &= trace_one<1, false, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, dg.P, sh.d, 0.0f, S.ray_eps, hs, st, &ts);
+                                ok &= trace_one<1, false, SINGLE, WIDE, CTL_ALPHA_OF(FULL)>(S, dg.P, sh.d, 0.0f, S.ray_eps, hs, st, &ts,
+                                                                                             sh.dist);
                                 if (!shadow_occluded(S, true, hs, sh.dist)) direct = sh.add;
                             }
                         }
@@ -219,8 +220,7 @@ CTL_API ctl_status ctl_prim_pass(ctl_ctx* c, const ctl_prim_params* p, ctl_pixel
     } while (0)
 #define PRK2(SG, WD) do { if (full == kShadeEnv) PRK(SG, WD, kShadeEnv); else if (full == kShadeAlpha) PRK(SG, WD, kShadeAlpha); \
                            else if (full) PRK(SG, WD, kShadeFull); else PRK(SG, WD, kShadeLean); } while (0)
-    if (wide && single && c->scene.w8_on) PRK2(true, 2);
-    else if (wide) { if (single) PRK2(true, 1); else PRK2(false, 1); }
+    if (wide) { if (single) PRK2(true, 1); else PRK2(false, 1); }
     else { if (single) PRK2(true, 0); else PRK2(false, 0); }
 #undef PRK2
 #undef PRK

@@ -27,7 +27,6 @@
 
 #include "../../../include/ctl_trace.h"
 #include "../host/bvh_wide.h"
-#include "../host/bvh_w8.h"
 #include "../ctl_qnode.h"
 #include "common.h"
 
@@ -207,6 +206,7 @@ void set_constants(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty) {
     // and its epsilon wins over the desc's until the instances are uploaded again.
     if (!c->device_eps || (dirty & CTL_DIRTY_NODES)) {
         S.ray_eps = d->ray_eps;
+        cull_bound(d->box_min, d->box_max, d->mesh_boxes, d->n_meshes, S.cull_m);
         c->device_eps = false;
     }
     for (int i = 0; i < CTL_MAX_NUM_LIGHTS; i++) S.light_cdf[i] = d->light_cdf[i];
@@ -216,7 +216,7 @@ void set_constants(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty) {
 
 ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream_t s) {
     // a change of the device tree format rebuilds the trees
-    const uint32_t tree_bits = CTL_SCENE_BINARY_BVH | CTL_SCENE_WIDE_QUANT | CTL_SCENE_WIDE8;
+    const uint32_t tree_bits = CTL_SCENE_BINARY_BVH | CTL_SCENE_WIDE_QUANT;
     if ((d->flags & tree_bits) != c->tree_flags) dirty |= kDirtyTrees;
     // quantized trees are encoded together
     if ((d->flags & CTL_SCENE_WIDE_QUANT) && (dirty & kDirtyTrees)) dirty |= kDirtyTrees;
@@ -367,46 +367,6 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
         }
         S.quant = q ? 1 : 0;
         SD_HIP(c, hipStreamSynchronize(s));   // wn / sw / qn / qs are locals
-    }
-    // the 8-wide tree of a one-mesh scene (host/bvh_w8.h); leaf entries relaid per node
-    if (mesh_trees || (dirty & (CTL_DIRTY_WOOP | CTL_DIRTY_NODES))) {
-        S.w8_on = 0;
-        c->w8_why.clear();
-        const bool want8 = wide && (d->flags & CTL_SCENE_WIDE8) && d->n_anim_meshes == 0 && d->n_nodes > 0 &&
-                           d->scene_start_node < 0;
-        if (want8) {
-            const uint32_t node = ~(uint32_t)d->scene_start_node;
-            const uint32_t mi = node < d->n_nodes ? d->nodes[node].mesh_index : 0xffffffffu;
-            W8Tree t;
-            if (mi < d->n_meshes && d->meshes[mi].bvh_node_offset / 4 < d->n_bvh_nodes &&
-                d->meshes[mi].bvh_indices_offset <= d->n_tri_indices &&
-                (uint64_t)d->meshes[mi].bvh_triangle_offset / 3 <= d->n_woop_tris) {
-                const ctl_kernel_mesh& M = d->meshes[mi];
-                const size_t first = M.bvh_node_offset / 4;
-                const uint64_t e0 = M.bvh_indices_offset;
-                // Woop records of the mesh: bvh_triangle_offset is in float4 units (3 per entry)
-                if (build_w8(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, d->woop_tris + M.bvh_triangle_offset / 3,
-                             d->tri_indices + e0, (size_t)std::min<uint64_t>(d->n_tri_indices - e0,
-                                                                             d->n_woop_tris - M.bvh_triangle_offset / 3),
-                             t, &c->w8_why) &&
-                    t.stack_bound <= kStackMax) {
-                    t.woop.push_back(ctl_woop_tri{});   // one zeroed entry past the end
-                    t.idx.push_back(0u);
-                    if ((r = put(c, SA_W8, t.nodes.data(), t.nodes.size() * sizeof(W8Node), 0, s)) != CTL_OK) return r;
-                    if ((r = put(c, SA_W8WOOP, t.woop.data(), t.woop.size() * sizeof(ctl_woop_tri), 0, s)) != CTL_OK) return r;
-                    if ((r = put(c, SA_W8IDX, t.idx.data(), t.idx.size() * sizeof(uint32_t), 0, s)) != CTL_OK) return r;
-                    SD_HIP(c, hipStreamSynchronize(s));   // t is a local
-                    S.w8_on = 1;
-                } else if (c->w8_why.empty()) {
-                    c->w8_why = "W8: stack deeper than the device stack";
-                }
-            } else {
-                c->w8_why = "W8: mesh offsets out of range";
-            }
-        }
-        S.w8 = S.w8_on ? dptr<float4>(c, SA_W8) : nullptr;
-        S.w8_woop = S.w8_on ? dptr<float4>(c, SA_W8WOOP) : nullptr;
-        S.w8_idx = S.w8_on ? dptr<uint32_t>(c, SA_W8IDX) : nullptr;
     }
     if (mesh_trees || top_tree) {
         S.wide = wide ? 1 : 0;

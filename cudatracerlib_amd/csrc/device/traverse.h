@@ -49,37 +49,6 @@ constexpr int kStackMax = 128;
 #ifndef CTL_LEAF_BREAK
 #define CTL_LEAF_BREAK 4
 #endif
-// CTL_LEAF_SPECULATE 1 (default): in the 4-wide mesh trees a lane that holds a
-// postponed leaf keeps visiting nodes (with the cull distance it had when it
-// postponed) until it reaches its next leaf; 0: it waits for the leaf phase.
-#ifndef CTL_LEAF_SPECULATE
-#define CTL_LEAF_SPECULATE 1
-#endif
-// CTL_SPEC_STEPS K > 0: the walk after a postponed leaf visits at most K inner
-// nodes (0: until the next leaf).
-#ifndef CTL_SPEC_STEPS
-#define CTL_SPEC_STEPS 0
-#endif
-constexpr int kSpecSteps = CTL_SPEC_STEPS;
-// CTL_IFIF 1: one-mesh scenes on the 4-wide float tree run the unified-fetch
-// loop (Traverser4::round_ifif): every iteration each lane either steps one
-// node or tests one leaf (two entries), both through the same seven 16-B loads,
-// and a leaf is tested as soon as it is reached (no postponement, no
-// speculation: the order of ORACLE_WIDE_NOSPEC).
-#ifndef CTL_IFIF
-#define CTL_IFIF 0
-#endif
-// CTL_SPEC_NOPOP 1: the walk past a postponed leaf also stops at a node with
-// no hit child (where it would pop the stack): it only descends.
-#ifndef CTL_SPEC_NOPOP
-#define CTL_SPEC_NOPOP 0
-#endif
-// CTL_BREAK_ALL 1: the 4-wide node loop counts every lane still in it (looking
-// for a leaf or walking past one) against CTL_LEAF_BREAK, not only the lanes
-// that look for their first leaf, so fewer walking lanes are cut.
-#ifndef CTL_BREAK_ALL
-#define CTL_BREAK_ALL 0
-#endif
 
 // Per-ray visit order (round 4).  Every traversal is a function of its ray
 // alone, never of the other rays of its wave:
@@ -122,6 +91,9 @@ struct DevScene {
     uint32_t n_lights;
     uint32_t flags;
     float ray_eps;
+    // per axis, max |coordinate| of the scene box and of every mesh's local box:
+    // bounds |lo| of every BVH box for the any-hit shadow cull (slab_slack)
+    float cull_m[3];
     float light_cdf[CTL_MAX_NUM_LIGHTS];
     ctl_camera camera;
     // single-instance fast path (start_node < 0): mesh of node ~start_node
@@ -136,11 +108,6 @@ struct DevScene {
     uint32_t alpha;              // KernelDynamicScene::doAlphaMapping (some material has an alpha map)
     uint32_t s_wnode_base;
     uint32_t quant;              // wide trees in the 64-B quantized format (ctl_qnode.h)
-    // 8-wide compressed tree of a one-mesh scene (host/bvh_w8.h), traversed when WIDE == 2
-    const float4* w8;            // 80-B nodes, five float4 each, root at node 0
-    const float4* w8_woop;       // its leaf entries' TriIntersectorData, relaid in node order
-    const uint32_t* w8_idx;      // their TriIntersectorData2 words
-    uint32_t w8_on;              // the W8 tree is present (and selected)
     // InfiniteLight (ctl_env.h): light env_index of lights[], 0xFFFFFFFF without one
     uint32_t env_index;
     const ctl_env_light* env;
@@ -242,6 +209,39 @@ struct RayLocal {
     }
 };
 
+// Bound on the rounding error of a slab distance of ray r (the Aila-Laine
+// `lo * idir - o * idir`: each product and the difference rounded, idir itself
+// rounded: at most 3 * 2^-24 (|lo| + |o|) |idir| per axis), with m[a] >= |lo|
+// of every box (DevScene::cull_m): 2^-20 max_a (|o_a| + m_a) |idir_a|.  A box
+// whose computed entry exceeds dist + slack has its exact entry past dist, so
+// the any-hit shadow query culls at dist + slack (oracle occluded_query).
+// Evaluated in this order on both sides, so the cull distance is bit-identical.
+__host__ __device__ inline float slab_slack(float ox, float oy, float oz, float idx, float idy, float idz,
+                                            const float* m) {
+    const float ex = (fabsf(ox) + m[0]) * fabsf(idx);
+    const float ey = (fabsf(oy) + m[1]) * fabsf(idy);
+    const float ez = (fabsf(oz) + m[2]) * fabsf(idz);
+    const float e = ex > ey ? ex : ey;
+    return (e > ez ? e : ez) * 0x1p-20f;
+}
+// DevScene::cull_m: per axis, max |coordinate| of the scene box (lo, hi) and of
+// the local boxes of the meshes (6 floats each, lo xyz then hi xyz).
+__host__ __device__ inline void cull_bound(const float* lo, const float* hi, const float* mesh_boxes, uint32_t n_meshes,
+                                           float m[3]) {
+    for (int a = 0; a < 3; a++) {
+        float v = fabsf(lo[a]) > fabsf(hi[a]) ? fabsf(lo[a]) : fabsf(hi[a]);
+        for (uint32_t i = 0; mesh_boxes && i < n_meshes; i++) {
+            const float l = fabsf(mesh_boxes[6 * i + a]), h = fabsf(mesh_boxes[6 * i + 3 + a]);
+            v = l > v ? l : v;
+            v = h > v ? h : v;
+        }
+        m[a] = v;
+    }
+}
+__device__ __forceinline__ float slab_slack(const RayLocal& r, const float* m) {
+    return slab_slack(r.ox, r.oy, r.oz, r.idx, r.idy, r.idz, m);
+}
+
 // Transform by a row-major float4x4 given as 4 float4 rows (float4x4.h:398-408).
 __device__ __forceinline__ void xform_rows(const float4* M, f3 p, f3 d, f3& po, f3& doo) {
     float4 r0 = M[0], r1 = M[1], r2 = M[2], r3 = M[3];
@@ -265,12 +265,14 @@ struct Traverser4 {
     RayLocal world;   // unused when SINGLE
     HitRec h;
     float span_tmin, tri_tmin;
-    float tcull;   // cull distance of the 4-wide node loops (h.t, or its value before a phantom leaf)
+    // cull distance of the node loops: h.t, or its value before a phantom leaf;
+    // the any-hit shadow query's: dist + slab_slack of the current level's ray
+    // (init's anyDist = dist; its acceptance bound is h.t = dist - eps)
+    float tcull;
+    float cullDist;   // that query's dist (instance entry / exit recompute tcull)
     int nodeAddr, leafAddr, level, meshSent;
-    int specLeft;     // CTL_SPEC_STEPS: inner nodes the walk past a postponed leaf may still visit
     uint32_t nodeBase, triBase, idxBase, triOffset, instIdx;
     bool done, resumeLeaves;
-    bool specStop;   // CTL_SPEC_NOPOP: this round's walk past the postponed leaf ended at a pop
     bool anyhit;   // ANY == 2 only
 
     __device__ __forceinline__ void enter_instance(const DevScene& S, uint32_t inst, f3 o, f3 d) {
@@ -280,10 +282,16 @@ struct Traverser4 {
         cur.set(o2.x, o2.y, o2.z, d2.x, d2.y, d2.z);
     }
 
+    // any-hit: h.t only changes when the query ends, so tcull keeps its start value
+    __device__ __forceinline__ bool any_query() const { return ANY == 1 || (ANY == 2 && anyhit); }
+
+    // anyDist >= 0: an any-hit shadow query to a light at anyDist (boxes culled
+    // at anyDist + slab_slack); ignored by closest-hit queries
     __device__ __forceinline__ void init(const DevScene& S, f3 o, f3 d, float smin, float tmn, float tmaxv,
-                                         LaneStack& st, TraceStats* stats) {
+                                         LaneStack& st, TraceStats* stats, float anyDist = -1.0f) {
         h.t = tmaxv; h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
         tcull = tmaxv;
+        cullDist = anyDist;
         span_tmin = smin; tri_tmin = tmn;
         st.sp = 0;
         st.overflow = false;
@@ -291,8 +299,6 @@ struct Traverser4 {
         done = (S.n_nodes == 0);
         resumeLeaves = false;
         meshSent = 0;
-        specLeft = 0;
-        specStop = false;
         if (SINGLE) {
             // start_node < 0: TracerayTemplate calls the instance callback directly (BVHTraversal.h:130-131)
             if (STATS) stats->inst++;
@@ -310,6 +316,7 @@ struct Traverser4 {
             if (S.start_node < 0) { leafAddr = S.start_node; nodeAddr = CTL_SENTINEL; }
             else { leafAddr = 0; nodeAddr = WIDE ? 0 : S.start_node; }
         }
+        if (any_query() && anyDist >= 0.0f) tcull = anyDist + slab_slack(cur, S.cull_m);
     }
 
     // TriangleData UV set 0 at (u, v) -> Material::AlphaTest (TraceHelper.cu:140-152)
@@ -387,12 +394,8 @@ struct Traverser4 {
                 float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
                 float v = Oy + t * Dy;
                 if (v >= 0.0f && u + v <= 1.0f) {
-#ifdef CTL_LEAF_IDX_LAZY
-                    const uint32_t gtri = (S.tri_idx[idxBase + entry] >> 1) + triOffset;
-#else
                     (void)entry;
                     const uint32_t gtri = (index >> 1) + triOffset;
-#endif
                     if (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v)) {
                         h.node = instIdx;
                         h.tri = gtri;
@@ -426,18 +429,12 @@ struct Traverser4 {
         const uint32_t* ti = S.tri_idx + idxBase + first;
         for (uint32_t i = 0; i < cnt; i += 2) {
             const float4 a0 = tv[3 * i], a1 = tv[3 * i + 1], a2 = tv[3 * i + 2];
-#ifdef CTL_LEAF_IDX_LAZY
-            const uint32_t ia = 0, ib = 0;
-#else
             const uint32_t ia = ti[i];
             uint32_t ib = ia;
-#endif
             float4 b0 = a0, b1 = a1, b2 = a2;
             if (i + 1 < cnt) {
                 b0 = tv[3 * i + 3]; b1 = tv[3 * i + 4]; b2 = tv[3 * i + 5];
-#ifndef CTL_LEAF_IDX_LAZY
                 ib = ti[i + 1];
-#endif
             }
             if (test_entry(S, a0, a1, a2, first + i, ia, stats)) return;
             if (i + 1 < cnt && test_entry(S, b0, b1, b2, first + i + 1, ib, stats)) return;
@@ -503,7 +500,6 @@ struct Traverser4 {
     //    on a {-0, +0} pair (and NaN); under the int-ordered span, clamped
     //    below by tmin >= +0, that can only add visits to boxes that end behind
     //    the ray origin, which hold no hit with t > eps, so hits are unchanged.
-    //    CTL_WIDE_MINMAX builds the previous min/max form for A/B runs;
     //  * empty child slots carry NaN boxes: their span compare is false, so no
     //    sentinel test per child;
     //  * hit children sorted near-first by a 5-comparator network on the entry
@@ -522,7 +518,6 @@ struct Traverser4 {
         const v2f ix = {cur.idx, cur.idx}, iy = {cur.idy, cur.idy}, iz = {cur.idz, cur.idz};
         const v2f ox = {cur.oodx, cur.oodx}, oy = {cur.oody, cur.oody}, oz = {cur.oodz, cur.oodz};
         const int tminBits = __float_as_int(span_tmin);
-#ifndef CTL_WIDE_MINMAX
         // Near/far planes chosen per ray by the sign of its inverse direction:
         // for idir >= 0, lo*idir - ood <= hi*idir - ood (rounding is monotone),
         // so the near plane IS the reference's min of the pair and the far
@@ -536,12 +531,11 @@ struct Traverser4 {
         uint32_t onx = sx, ofx = 16u - sx, ony = 32u + sy, ofy = 48u - sy, onz = 64u + sz, ofz = 80u - sz;
         // opaque to the optimiser: otherwise it splits off + (16 - s) into two ops per load
         asm volatile("" : "+v"(onx), "+v"(ofx), "+v"(ony), "+v"(ofy), "+v"(onz), "+v"(ofz));
-#endif
         // speculation only inside a mesh (the instance level stops at its first leaf)
-        const bool spec = CTL_LEAF_SPECULATE && (SINGLE || level == 1);
+        const bool spec = SINGLE || level == 1;
         const int tBits = __float_as_int(tcull);
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL &&
-               ((spec && (kSpecSteps == 0 || specLeft > 0) && !specStop) || leafAddr >= 0)) {
+               (spec || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
@@ -549,7 +543,6 @@ struct Traverser4 {
             CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
             if (STATS) stats->nodes++;
             int k0, k1, k2, k3;
-#ifndef CTL_WIDE_MINMAX
             const uint32_t off = (nodeBase + (uint32_t)nodeAddr) << 7;
             const v4f nx = *reinterpret_cast<const v4f*>(nbytes + (off + onx));
             const v4f fx = *reinterpret_cast<const v4f*>(nbytes + (off + ofx));
@@ -578,39 +571,9 @@ struct Traverser4 {
             CTL_WIDE_CHILD(k1, nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y)
             CTL_WIDE_CHILD(k2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x)
             CTL_WIDE_CHILD(k3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y)
-#else
-            const v4f* n = nodes + (size_t)(nodeBase + (uint32_t)nodeAddr) * 8u;
-            const v4f lox = n[0], hix = n[1], loy = n[2], hiy = n[3], loz = n[4], hiz = n[5];
-            int4 ch = reinterpret_cast<const int4*>(n)[6];
-            asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
-            const v2f ax01 = lox.xy * ix - ox, ax23 = lox.zw * ix - ox;
-            const v2f bx01 = hix.xy * ix - ox, bx23 = hix.zw * ix - ox;
-            const v2f ay01 = loy.xy * iy - oy, ay23 = loy.zw * iy - oy;
-            const v2f by01 = hiy.xy * iy - oy, by23 = hiy.zw * iy - oy;
-            const v2f az01 = loz.xy * iz - oz, az23 = loz.zw * iz - oz;
-            const v2f bz01 = hiz.xy * iz - oz, bz23 = hiz.zw * iz - oz;
-            int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-#define CTL_WIDE_CHILD(K, AX, BX, AY, BY, AZ, BZ)                                                        \
-            {                                                                                            \
-                const int zlo = min(__float_as_int(AZ), __float_as_int(BZ));                             \
-                const int zhi = max(__float_as_int(AZ), __float_as_int(BZ));                             \
-                const float cmin = __int_as_float(imax3(__float_as_int(fminf(AX, BX)),                    \
-                                                        __float_as_int(fminf(AY, BY)), max(zlo, tminBits))); \
-                const float cmax = __int_as_float(imin3(__float_as_int(fmaxf(AX, BX)),                    \
-                                                        __float_as_int(fmaxf(AY, BY)), min(zhi, tBits)));  \
-                K = (cmax >= cmin) ? __float_as_int(cmin) : 0x7fffffff;                                  \
-            }
-            CTL_WIDE_CHILD(k0, ax01.x, bx01.x, ay01.x, by01.x, az01.x, bz01.x)
-            CTL_WIDE_CHILD(k1, ax01.y, bx01.y, ay01.y, by01.y, az01.y, bz01.y)
-            CTL_WIDE_CHILD(k2, ax23.x, bx23.x, ay23.x, by23.x, az23.x, bz23.x)
-            CTL_WIDE_CHILD(k3, ax23.y, bx23.y, ay23.y, by23.y, az23.y, bz23.y)
-#endif
 #undef CTL_WIDE_CHILD
-            const bool held = leafAddr < 0;
-            const int m = wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
-            if (CTL_SPEC_NOPOP && held && m == 0) specStop = true;
-            if (kSpecSteps > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpecSteps : specLeft);
-            if (__popcll(__ballot(CTL_BREAK_ALL || leafAddr >= 0)) < CTL_LEAF_BREAK) break;
+            wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
+            if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
@@ -629,10 +592,10 @@ struct Traverser4 {
         const bool negx = __float_as_int(cur.idx) < 0, negy = __float_as_int(cur.idy) < 0;
         const bool negz = __float_as_int(cur.idz) < 0;
         // speculation only inside a mesh (the instance level stops at its first leaf)
-        const bool spec = CTL_LEAF_SPECULATE && (SINGLE || level == 1);
+        const bool spec = SINGLE || level == 1;
         const int tBits = __float_as_int(tcull);
         while (!resumeLeaves && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL &&
-               ((spec && (kSpecSteps == 0 || specLeft > 0) && !specStop) || leafAddr >= 0)) {
+               (spec || leafAddr >= 0)) {
             const int sp = st.sp;
             const bool fast = sp + 3 <= kLdsStack;
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
@@ -652,20 +615,6 @@ struct Traverser4 {
             const uint32_t nyw = negy ? why : wly, fyw = negy ? wly : why;
             const uint32_t nzw = negz ? whz : wlz, fzw = negz ? wlz : whz;
 #define CTL_QB(W, K) ((float)(((W) >> (8 * (K))) & 0xffu))
-#ifdef CTL_QUANT_FUSED
-            // experiment: the decode folded into the slab, (p + q s) idir - ood =
-            // fma(q, s idir, p idir - ood): one cvt + half a packed fma per bound
-            const float axs = qa.w * cur.idx, ays = qb.x * cur.idy, azs = qb.y * cur.idz;
-            const float bxs = qa.x * cur.idx - cur.oodx, bys = qa.y * cur.idy - cur.oody, bzs = qa.z * cur.idz - cur.oodz;
-#define CTL_QPAIR(W, A, B, K0, K1) \
-    __builtin_elementwise_fma(v2f{CTL_QB(W, K0), CTL_QB(W, K1)}, v2f{(A), (A)}, v2f{(B), (B)})
-            const v2f nx01 = CTL_QPAIR(nxw, axs, bxs, 0, 1), nx23 = CTL_QPAIR(nxw, axs, bxs, 2, 3);
-            const v2f fx01 = CTL_QPAIR(fxw, axs, bxs, 0, 1), fx23 = CTL_QPAIR(fxw, axs, bxs, 2, 3);
-            const v2f ny01 = CTL_QPAIR(nyw, ays, bys, 0, 1), ny23 = CTL_QPAIR(nyw, ays, bys, 2, 3);
-            const v2f fy01 = CTL_QPAIR(fyw, ays, bys, 0, 1), fy23 = CTL_QPAIR(fyw, ays, bys, 2, 3);
-            const v2f nz01 = CTL_QPAIR(nzw, azs, bzs, 0, 1), nz23 = CTL_QPAIR(nzw, azs, bzs, 2, 3);
-            const v2f fz01 = CTL_QPAIR(fzw, azs, bzs, 0, 1), fz23 = CTL_QPAIR(fzw, azs, bzs, 2, 3);
-#else
             // p + q * s in one fused op: q * s is exact (q < 256, s a power of two), so the
             // fused result is the encoder's p + q * s (mul, then add) bit for bit
 #define CTL_QPAIR(W, P, SC, K0, K1) \
@@ -676,7 +625,6 @@ struct Traverser4 {
             const v2f fy01 = CTL_QPAIR(fyw, qa.y, qb.x, 0, 1) * iy - oy, fy23 = CTL_QPAIR(fyw, qa.y, qb.x, 2, 3) * iy - oy;
             const v2f nz01 = CTL_QPAIR(nzw, qa.z, qb.y, 0, 1) * iz - oz, nz23 = CTL_QPAIR(nzw, qa.z, qb.y, 2, 3) * iz - oz;
             const v2f fz01 = CTL_QPAIR(fzw, qa.z, qb.y, 0, 1) * iz - oz, fz23 = CTL_QPAIR(fzw, qa.z, qb.y, 2, 3) * iz - oz;
-#endif
 #undef CTL_QPAIR
 #undef CTL_QB
             int k0, k1, k2, k3, c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
@@ -693,11 +641,8 @@ struct Traverser4 {
             CTL_WIDE_CHILD(k2, c2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x)
             CTL_WIDE_CHILD(k3, c3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y)
 #undef CTL_WIDE_CHILD
-            const bool held = leafAddr < 0;
-            const int m = wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
-            if (CTL_SPEC_NOPOP && held && m == 0) specStop = true;
-            if (kSpecSteps > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpecSteps : specLeft);
-            if (__popcll(__ballot(CTL_BREAK_ALL || leafAddr >= 0)) < CTL_LEAF_BREAK) break;
+            wide_advance(k0, k1, k2, k3, c0, c1, c2, c3, fast, sp, top1, top2, st);
+            if (__popcll(__ballot(leafAddr >= 0)) < CTL_LEAF_BREAK) break;
         }
     }
 
@@ -725,13 +670,13 @@ struct Traverser4 {
             const float c1loz = nz.z * cur.idz - cur.oodz;
             const float c1hiz = nz.w * cur.idz - cur.oodz;
             const float c0min = span_begin(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, span_tmin);
-            const float c0max = span_end(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, h.t);
+            const float c0max = span_end(c0lox, c0hix, c0loy, c0hiy, c0loz, c0hiz, tcull);
             const float c1lox = n1xy.x * cur.idx - cur.oodx;
             const float c1hix = n1xy.y * cur.idx - cur.oodx;
             const float c1loy = n1xy.z * cur.idy - cur.oody;
             const float c1hiy = n1xy.w * cur.idy - cur.oody;
             const float c1min = span_begin(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, span_tmin);
-            const float c1max = span_end(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, h.t);
+            const float c1max = span_end(c1lox, c1hix, c1loy, c1hiy, c1loz, c1hiz, tcull);
             bool swp = (c1min < c0min);
             bool tc0 = (c0max >= c0min);
             bool tc1 = (c1max >= c1min);
@@ -752,134 +697,9 @@ struct Traverser4 {
         }
     }
 
-    // Woop test of one entry; the TriIntersectorData2 word is loaded only for
-    // an accepted hit.  true = any-hit termination.
-    __device__ __forceinline__ bool test_entry_lazy(const DevScene& S, float4 v00, float4 v11, float4 v22,
-                                                    uint32_t entry, TraceStats* stats) {
-        CTL_PROF_COUNT(stats, leaf_lanes, leaf_waves);
-        if (STATS) stats->tris++;
-        float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
-        float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
-        float t = Oz * invDz;
-        if (t > tri_tmin && t < h.t) {
-            float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
-            float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
-            float u = Ox + t * Dx;
-            if (u >= 0.0f) {
-                float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
-                float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
-                float v = Oy + t * Dy;
-                if (v >= 0.0f && u + v <= 1.0f) {
-                    const uint32_t gtri = (S.tri_idx[idxBase + entry] >> 1) + triOffset;
-                    if (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v)) {
-                        h.node = instIdx; h.tri = gtri; h.u = u; h.v = v; h.t = t;
-                        if (ANY == 1 || (ANY == 2 && anyhit)) { done = true; return true; }
-                    }
-                }
-            }
-        }
-        return false;
-    }
-
-    // Unified-fetch traversal of a one-mesh 4-wide float tree (CTL_IFIF): per
-    // iteration a lane on an inner node loads its near/far planes and child
-    // word, a lane on a leaf loads two Woop entries, with the same seven 16-B
-    // load instructions (per-lane addresses), so node steps and leaf tests of
-    // one wave share one memory round trip.  A leaf is tested when reached
-    // and the cull distance is the current hit: the order is the no-speculation
-    // order (oracle TRAVERSE_WIDE with ORACLE_WIDE_NOSPEC), a function of the
-    // ray alone.  Runs the whole traversal in one call.
-    __device__ __forceinline__ void round_ifif(const DevScene& S, LaneStack& st, TraceStats* stats) {
-        typedef float v2f __attribute__((ext_vector_type(2)));
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        const char* nbytes = reinterpret_cast<const char*>(S.wbvh);
-        const char* tbytes = reinterpret_cast<const char*>(S.woop + triBase);
-        const v2f ix = {cur.idx, cur.idx}, iy = {cur.idy, cur.idy}, iz = {cur.idz, cur.idz};
-        const v2f ox = {cur.oodx, cur.oodx}, oy = {cur.oody, cur.oody}, oz = {cur.oodz, cur.oodz};
-        const int tminBits = __float_as_int(span_tmin);
-        const uint32_t sx = (uint32_t)(__float_as_int(cur.idx) >> 31) & 16u;
-        const uint32_t sy = (uint32_t)(__float_as_int(cur.idy) >> 31) & 16u;
-        const uint32_t sz = (uint32_t)(__float_as_int(cur.idz) >> 31) & 16u;
-        uint32_t onx = sx, ofx = 16u - sx, ony = 32u + sy, ofy = 48u - sy, onz = 64u + sz, ofz = 80u - sz;
-        asm volatile("" : "+v"(onx), "+v"(ofx), "+v"(ony), "+v"(ofy), "+v"(onz), "+v"(ofz));
-        leafAddr = -1;   // wide_advance never postpones
-        // batch traversals hand the wave back for a refill once fewer than 24 lanes
-        // still traverse (the CTL_REFILL_MIN rule); the path kernel never needs to
-        constexpr int kKeep = ANY == 2 ? 0 : 24;
-        while (true) {
-            if ((unsigned)nodeAddr == (unsigned)CTL_SENTINEL) { done = true; return; }
-            const bool isLeaf = nodeAddr < 0;
-            const uint32_t code = (uint32_t)(~nodeAddr);
-            const uint32_t first = code >> 3, cnt = code & 7u;
-            // per-lane byte addresses of the seven loads: node planes + child word,
-            // or entries first and first + 1 (the first again for a one-entry leaf)
-            const char* nb = nbytes + ((size_t)(nodeBase + (uint32_t)nodeAddr) << 7);
-            const char* t0 = tbytes + (size_t)first * 48u;
-            const char* t1 = cnt >= 2 ? t0 + 48 : t0;
-            const v4f L0 = *reinterpret_cast<const v4f*>(isLeaf ? t0 : nb + onx);
-            const v4f L1 = *reinterpret_cast<const v4f*>(isLeaf ? t0 + 16 : nb + ofx);
-            const v4f L2 = *reinterpret_cast<const v4f*>(isLeaf ? t0 + 32 : nb + ony);
-            const v4f L3 = *reinterpret_cast<const v4f*>(isLeaf ? t1 : nb + ofy);
-            const v4f L4 = *reinterpret_cast<const v4f*>(isLeaf ? t1 + 16 : nb + onz);
-            const v4f L5 = *reinterpret_cast<const v4f*>(isLeaf ? t1 + 32 : nb + ofz);
-            int4 ch = *reinterpret_cast<const int4*>(isLeaf ? t0 : nb + 96);
-            asm volatile("" : "+v"(ch.x), "+v"(ch.y), "+v"(ch.z), "+v"(ch.w));
-            if (isLeaf) {
-                if (first == 214783647u) {
-                    // the reference's skipped leaf value (BVHTraversal.h:109,221)
-                } else if (cnt == 0) {
-                    leafAddr = nodeAddr;   // a long leaf: walk its last-in-leaf flags
-                    leaf_tris(S, stats);
-                    leafAddr = -1;
-                    if (done) return;
-                } else {
-                    auto f4 = [](v4f a) { return make_float4(a.x, a.y, a.z, a.w); };
-                    if (test_entry_lazy(S, f4(L0), f4(L1), f4(L2), first, stats)) return;
-                    if (cnt >= 2 && test_entry_lazy(S, f4(L3), f4(L4), f4(L5), first + 1, stats)) return;
-                    if (cnt > 2) { nodeAddr = ~(int)(((first + 2u) << 3) | (cnt - 2u)); continue; }
-                }
-                tcull = h.t;
-                nodeAddr = st.pop();
-            } else {
-                CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
-                if (STATS) stats->nodes++;
-                const int sp = st.sp;
-                const bool fast = sp + 3 <= kLdsStack;
-                const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
-                const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
-                const int tBits = __float_as_int(tcull);
-                const v2f nx01 = L0.xy * ix - ox, nx23 = L0.zw * ix - ox;
-                const v2f fx01 = L1.xy * ix - ox, fx23 = L1.zw * ix - ox;
-                const v2f ny01 = L2.xy * iy - oy, ny23 = L2.zw * iy - oy;
-                const v2f fy01 = L3.xy * iy - oy, fy23 = L3.zw * iy - oy;
-                const v2f nz01 = L4.xy * iz - oz, nz23 = L4.zw * iz - oz;
-                const v2f fz01 = L5.xy * iz - oz, fz23 = L5.zw * iz - oz;
-                int k0, k1, k2, k3;
-#define CTL_WIDE_CHILD(K, NX, FX, NY, FY, NZ, FZ)                                                       \
-                {                                                                                       \
-                    const float cmin = __int_as_float(imax3(__float_as_int(NX), __float_as_int(NY),      \
-                                                            max(__float_as_int(NZ), tminBits)));         \
-                    const float cmax = __int_as_float(imin3(__float_as_int(FX), __float_as_int(FY),      \
-                                                            min(__float_as_int(FZ), tBits)));            \
-                    K = (cmax >= cmin) ? __float_as_int(cmin) : 0x7fffffff;                             \
-                }
-                CTL_WIDE_CHILD(k0, nx01.x, fx01.x, ny01.x, fy01.x, nz01.x, fz01.x)
-                CTL_WIDE_CHILD(k1, nx01.y, fx01.y, ny01.y, fy01.y, nz01.y, fz01.y)
-                CTL_WIDE_CHILD(k2, nx23.x, fx23.x, ny23.x, fy23.x, nz23.x, fz23.x)
-                CTL_WIDE_CHILD(k3, nx23.y, fx23.y, ny23.y, fy23.y, nz23.y, fz23.y)
-#undef CTL_WIDE_CHILD
-                wide_advance(k0, k1, k2, k3, ch.x, ch.y, ch.z, ch.w, fast, sp, top1, top2, st);
-            }
-            if (kKeep > 0 && __popcll(__ballot(true)) < kKeep) return;
-        }
-    }
-
     // One round: inner nodes until every active lane holds a postponed leaf,
     // then the postponed leaves (and the level transitions).
     __device__ __forceinline__ void round(const DevScene& S, LaneStack& st, TraceStats* stats) {
-        if (CTL_IFIF && SINGLE && WIDE && !STATS) {
-            if (!S.quant) { round_ifif(S, st, stats); return; }
-        }
 #ifdef CTL_PROFILE_TRACE
         stats->round_r = (uint32_t)__popcll(__ballot(1));
         if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) stats->rounds++;
@@ -890,11 +710,8 @@ struct Traverser4 {
         }
         else inner_binary(S, st, stats);
         resumeLeaves = false;
-        const bool stopped = specStop;
-        specStop = false;
         // a speculating lane the wave stopped before it reached its next leaf
-        const bool cut = WIDE && CTL_LEAF_SPECULATE && (SINGLE || level == 1) && leafAddr < 0 &&
-                         (unsigned)nodeAddr < (unsigned)CTL_SENTINEL && (kSpecSteps == 0 || specLeft > 0) && !stopped;
+        const bool cut = WIDE && (SINGLE || level == 1) && leafAddr < 0 && (unsigned)nodeAddr < (unsigned)CTL_SENTINEL;
 #ifdef CTL_PROFILE_TRACE
         {
             const uint32_t nl = (uint32_t)__popcll(__ballot(leafAddr < 0));
@@ -930,22 +747,16 @@ struct Traverser4 {
                     level = 1;
                     nodeAddr = 0;             // mesh root (TraceHelper.cu:170)
                     leafAddr = 0;
-                    tcull = h.t;
+                    if (!any_query()) tcull = h.t;
+                    else if (cullDist >= 0.0f) tcull = cullDist + slab_slack(cur, S.cull_m);   // the mesh's ray
                     return;
                 }
                 leafAddr = nodeAddr;
                 if (nodeAddr < 0) nodeAddr = st.pop();
             }
         }
-#ifndef CTL_CUT_UPDATE
         if (cut) leafAddr = kPhantomLeaf;   // walk on to the next leaf with the old tcull
-        else tcull = h.t;
-#else
-        // measurement only: a cut lane resumes with the new distance (round 3's
-        // wave-dependent behaviour; not the per-ray order the oracle restates)
-        (void)cut;
-        tcull = h.t;
-#endif
+        else if (!any_query()) tcull = h.t;
         if (nodeAddr == CTL_SENTINEL) {
             if (!SINGLE && level == 1) {
                 // mesh traversal finished (bottom sentinel or a sentinel child)
@@ -954,6 +765,7 @@ struct Traverser4 {
                 level = 0;
                 nodeBase = 0;
                 cur = world;
+                if (any_query() && cullDist >= 0.0f) tcull = cullDist + slab_slack(cur, S.cull_m);
                 leafAddr = saved;
                 nodeAddr = saved;
                 if (saved < 0) nodeAddr = st.pop();
@@ -965,247 +777,15 @@ struct Traverser4 {
     }
 };
 
-// ---------------------------------------------------------------------------
-// 8-wide compressed traversal (WIDE == 2, one-mesh scenes; host/bvh_w8.h).
-//
-// Per ray: the current node group G (24-bit child base, the hit inner slots as
-// an 8-bit mask in key order, key = slot ^ octant) in registers, one group per
-// pushed level on the lane stack, the node to visit next, and up to two leaf
-// groups (a node's hit leaf entries: base + 24-bit mask over the relaid
-// entries).  Of a node's hit inner children the nearest (entry distance, its
-// low 3 bits replaced by the slot) is visited next, the others after its
-// subtree in key order.  A node visit is five
-// 16-B loads: the grid header, child / leaf bases with the leaf metadata, and
-// the 48 child planes as bytes; each slab plane is fma(q, s idir, p idir - ood)
-// on the exact grid value p + q s (q s exact, the decode folded into the slab).
-// Culling and spans as the 4-wide loop (kepler_math on the bits, against
-// tcull); children visited near-to-far by octant slot order, no sort.
-// Speculation as the 4-wide mesh level: after its first leaf group a lane
-// walks on (same tcull) to its second, then tests both and takes the new
-// distance; cut short by the wave it keeps tcull and a phantom first group.
-// The oracle restates this order (oracle/oracle.cpp trace_w8).
-// ---------------------------------------------------------------------------
-template <int ANY, bool STATS, bool ALPHA = false>
-struct Traverser8 {
-    RayLocal cur;
-    HitRec h;
-    float span_tmin, tri_tmin, tcull;
-    uint32_t grp;             // nodes left after `next`: hits8 (key order) << 24 | child base
-    int32_t next;             // the node to visit next, -1: the first slot of grp
-    uint32_t t1b, t1m, t2b, t2m;   // leaf groups: entry base, entry mask
-    uint32_t oct;             // sign bits of idir (x: 1, y: 2, z: 4)
-    uint32_t instIdx, triOffset;
-    bool held;                // a first leaf group is pending (or was tested early: phantom)
-    bool exhausted;           // no node group left
-    bool done;
-    bool anyhit;              // ANY == 2 only
-
-    __device__ __forceinline__ void init(const DevScene& S, f3 o, f3 d, float smin, float tmn, float tmaxv,
-                                         LaneStack& st, TraceStats* stats) {
-        h.t = tmaxv; h.u = h.v = 0.0f; h.tri = 0xffffffffu; h.node = 0xffffffffu;
-        tcull = tmaxv;
-        span_tmin = smin; tri_tmin = tmn;
-        st.sp = 0;
-        st.overflow = false;
-        st.push(0);   // the empty group at the bottom
-        done = (S.n_nodes == 0);
-        exhausted = false;
-        held = false;
-        t1b = t1m = t2b = t2m = 0;
-        if (STATS) stats->inst++;
-        instIdx = ~(uint32_t)S.start_node;   // the scene's one instance (TracerayTemplate's startNode < 0)
-        f3 o2, d2;
-        xform_rows(S.inv_xf + 4 * instIdx, o, d, o2, d2);
-        cur.set(o2.x, o2.y, o2.z, d2.x, d2.y, d2.z);
-        triOffset = S.s_tri_offset;
-        oct = ((uint32_t)__float_as_int(cur.idx) >> 31) | (((uint32_t)__float_as_int(cur.idy) >> 31) << 1) |
-              (((uint32_t)__float_as_int(cur.idz) >> 31) << 2);
-        grp = 0;
-        next = 0;                   // the root
-    }
-
-    __device__ __forceinline__ bool alpha_survives(const DevScene& S, uint32_t gtri, float u, float v) const {
-        const ctl_triangle_data td = S.tri_data[gtri];
-        const ctl_material& m = S.mats[((td.w[1] >> 16) & 0xffu) + S.nodes[instIdx].material_offset];
-        if (!m.alpha_state) return true;
-        const bool q = (S.flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
-        const f2 a = mk2(half_to_float(td.w[5] & 0xffffu, q), half_to_float(td.w[5] >> 16, q));
-        const f2 b = mk2(half_to_float(td.w[6] & 0xffffu, q), half_to_float(td.w[6] >> 16, q));
-        const f2 c = mk2(half_to_float(td.w[7] & 0xffffu, q), half_to_float(td.w[7] >> 16, q));
-        const f2 uv = u * a + v * b + (1 - u - v) * c;
-        return material_alpha_test(m, TexView{S.textures, S.tex_data}, uv);
-    }
-
-    // one Woop test (TraceHelper.cu:118-161); true = any-hit termination
-    __device__ __forceinline__ bool test8(const DevScene& S, uint32_t e, float4 v00, float4 v11, float4 v22,
-                                          TraceStats* stats) {
-        CTL_PROF_COUNT(stats, leaf_lanes, leaf_waves);
-        if (STATS) stats->tris++;
-        float Oz = v00.w - cur.ox * v00.x - cur.oy * v00.y - cur.oz * v00.z;
-        float invDz = 1.0f / (cur.dx * v00.x + cur.dy * v00.y + cur.dz * v00.z);
-        float t = Oz * invDz;
-        if (t > tri_tmin && t < h.t) {   // TraceHelper.cu:121
-            float Ox = v11.w + cur.ox * v11.x + cur.oy * v11.y + cur.oz * v11.z;
-            float Dx = cur.dx * v11.x + cur.dy * v11.y + cur.dz * v11.z;
-            float u = Ox + t * Dx;
-            if (u >= 0.0f) {
-                float Oy = v22.w + cur.ox * v22.x + cur.oy * v22.y + cur.oz * v22.z;
-                float Dy = cur.dx * v22.x + cur.dy * v22.y + cur.dz * v22.z;
-                float v = Oy + t * Dy;
-                if (v >= 0.0f && u + v <= 1.0f) {
-                    const uint32_t gtri = (S.w8_idx[e] >> 1) + triOffset;
-                    if (!ALPHA || !S.alpha || alpha_survives(S, gtri, u, v)) {
-                        h.node = instIdx; h.tri = gtri; h.u = u; h.v = v; h.t = t;
-                        if (ANY == 1 || (ANY == 2 && anyhit)) { done = true; return true; }
-                    }
-                }
-            }
-        }
-        return false;
-    }
-
-    // the entries of one leaf group, ascending, loaded two at a time (one
-    // dependent load latency per pair); true = any-hit termination
-    __device__ __forceinline__ bool leaves(const DevScene& S, uint32_t base, uint32_t mask, TraceStats* stats) {
-        while (mask) {
-            const uint32_t e0 = base + (uint32_t)(__ffs(mask) - 1);
-            mask &= mask - 1u;
-            const bool two = mask != 0;
-            const uint32_t e1 = two ? base + (uint32_t)(__ffs(mask) - 1) : e0;
-            mask &= two ? mask - 1u : mask;
-            const float4* t0 = S.w8_woop + 3u * e0;
-            const float4* t1 = S.w8_woop + 3u * e1;
-            const float4 a0 = t0[0], a1 = t0[1], a2 = t0[2];
-            const float4 b0 = t1[0], b1 = t1[1], b2 = t1[2];
-            if (test8(S, e0, a0, a1, a2, stats)) return true;
-            if (two && test8(S, e1, b0, b1, b2, stats)) return true;
-        }
-        return false;
-    }
-
-    __device__ __forceinline__ void round(const DevScene& S, LaneStack& st, TraceStats* stats) {
-        typedef float v2f __attribute__((ext_vector_type(2)));
-        const int tminBits = __float_as_int(span_tmin);
-        const int tBits = __float_as_int(tcull);
-        const bool nx = oct & 1u, ny = oct & 2u, nz = oct & 4u;
-        while (t2m == 0 && !exhausted) {
-            if (next < 0) {
-                if ((grp >> 24) == 0) {
-                    grp = (uint32_t)st.pop();
-                    if ((grp >> 24) == 0) { exhausted = true; break; }
-                }
-                const uint32_t hits = grp >> 24;
-                next = (int32_t)((grp & 0xffffffu) + ((uint32_t)(__ffs(hits) - 1) ^ oct));
-                grp = ((hits & (hits - 1u)) << 24) | (grp & 0xffffffu);
-            }
-            CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
-            if (STATS) stats->nodes++;
-            const uint32_t node = (uint32_t)next;
-            const float4* n = S.w8 + 5u * node;
-            const float4 A = n[0];
-            uint4 B = reinterpret_cast<const uint4*>(n)[1];
-            uint4 Cx = reinterpret_cast<const uint4*>(n)[2];
-            uint4 Cy = reinterpret_cast<const uint4*>(n)[3];
-            uint4 Cz = reinterpret_cast<const uint4*>(n)[4];
-            asm volatile("" : "+v"(B.x), "+v"(B.y), "+v"(B.z), "+v"(B.w));
-            const uint32_t hw = __float_as_uint(A.w);
-            // grid steps 2^(e - 127): the exponent byte into the fp32 exponent field
-            const float sx = __uint_as_float((hw & 0xffu) << 23), sy = __uint_as_float(((hw >> 8) & 0xffu) << 23);
-            const float sz = __uint_as_float(((hw >> 16) & 0xffu) << 23);
-            const uint32_t imask = hw >> 24;
-            const float ax = sx * cur.idx, ay = sy * cur.idy, az = sz * cur.idz;
-            const float bx = __builtin_fmaf(A.x, cur.idx, -cur.oodx), by = __builtin_fmaf(A.y, cur.idy, -cur.oody);
-            const float bz = __builtin_fmaf(A.z, cur.idz, -cur.oodz);
-            // near / far plane words by the ray's direction signs
-            const uint32_t nx0 = nx ? Cx.z : Cx.x, nx1 = nx ? Cx.w : Cx.y, fx0 = nx ? Cx.x : Cx.z, fx1 = nx ? Cx.y : Cx.w;
-            const uint32_t ny0 = ny ? Cy.z : Cy.x, ny1 = ny ? Cy.w : Cy.y, fy0 = ny ? Cy.x : Cy.z, fy1 = ny ? Cy.y : Cy.w;
-            const uint32_t nz0 = nz ? Cz.z : Cz.x, nz1 = nz ? Cz.w : Cz.y, fz0 = nz ? Cz.x : Cz.z, fz1 = nz ? Cz.y : Cz.w;
-#define CTL_QB8(W, K) ((float)(((W) >> (8 * (K))) & 0xffu))
-#define CTL_SLAB2(W, K0, K1, A_, B_) \
-    __builtin_elementwise_fma(v2f{CTL_QB8(W, K0), CTL_QB8(W, K1)}, v2f{(A_), (A_)}, v2f{(B_), (B_)})
-            uint32_t hit8 = 0, nearest = 0xffffffffu;
-            // nearest hit inner child: its entry bits with the slot in the low 3 bits
-#define CTL_W8_NEAR(MN, MX, SL) \
-            nearest = min(nearest, (MX >= MN && ((imask >> (SL)) & 1u)) ? ((__float_as_uint(MN) & ~7u) | (SL)) : 0xffffffffu);
-#define CTL_W8_PAIR(WNX, WFX, WNY, WFY, WNZ, WFZ, K0, K1, S0)                                               \
-            {                                                                                               \
-                const v2f vnx = CTL_SLAB2(WNX, K0, K1, ax, bx), vfx = CTL_SLAB2(WFX, K0, K1, ax, bx);        \
-                const v2f vny = CTL_SLAB2(WNY, K0, K1, ay, by), vfy = CTL_SLAB2(WFY, K0, K1, ay, by);        \
-                const v2f vnz = CTL_SLAB2(WNZ, K0, K1, az, bz), vfz = CTL_SLAB2(WFZ, K0, K1, az, bz);        \
-                const float mn0 = __int_as_float(imax3(__float_as_int(vnx.x), __float_as_int(vny.x),        \
-                                                       max(__float_as_int(vnz.x), tminBits)));              \
-                const float mx0 = __int_as_float(imin3(__float_as_int(vfx.x), __float_as_int(vfy.x),        \
-                                                       min(__float_as_int(vfz.x), tBits)));                 \
-                const float mn1 = __int_as_float(imax3(__float_as_int(vnx.y), __float_as_int(vny.y),        \
-                                                       max(__float_as_int(vnz.y), tminBits)));              \
-                const float mx1 = __int_as_float(imin3(__float_as_int(vfx.y), __float_as_int(vfy.y),        \
-                                                       min(__float_as_int(vfz.y), tBits)));                 \
-                hit8 |= (mx0 >= mn0 ? 1u << (S0) : 0u) | (mx1 >= mn1 ? 2u << (S0) : 0u);                   \
-                CTL_W8_NEAR(mn0, mx0, (S0))                                                                 \
-                CTL_W8_NEAR(mn1, mx1, (S0) + 1)                                                             \
-            }
-            CTL_W8_PAIR(nx0, fx0, ny0, fy0, nz0, fz0, 0, 1, 0)
-            CTL_W8_PAIR(nx0, fx0, ny0, fy0, nz0, fz0, 2, 3, 2)
-            CTL_W8_PAIR(nx1, fx1, ny1, fy1, nz1, fz1, 0, 1, 4)
-            CTL_W8_PAIR(nx1, fx1, ny1, fy1, nz1, fz1, 2, 3, 6)
-#undef CTL_W8_PAIR
-#undef CTL_W8_NEAR
-#undef CTL_SLAB2
-#undef CTL_QB8
-            // hit leaf slots -> their entries' bits over leaf_base (meta: bits << 5 | offset)
-            const uint32_t lhit = hit8 & ~imask;
-            uint32_t tm = 0;
-            if (lhit) {
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const uint32_t m = ((i < 4 ? B.z : B.w) >> (8 * (i & 3))) & 0xffu;
-                    tm |= ((lhit >> i) & 1u) ? (m >> 5) << (m & 31u) : 0u;
-                }
-            }
-            // hit inner slots in key order (bit slot ^ oct)
-            uint32_t ih = hit8 & imask;
-            ih = (oct & 1u) ? (((ih & 0x55u) << 1) | ((ih >> 1) & 0x55u)) : ih;
-            ih = (oct & 2u) ? (((ih & 0x33u) << 2) | ((ih >> 2) & 0x33u)) : ih;
-            ih = (oct & 4u) ? (((ih & 0x0fu) << 4) | ((ih >> 4) & 0x0fu)) : ih;
-            if (ih) {
-                // the nearest inner child next; the node's other hit inner children (key order) as
-                // the group after it; the group `node` came from waits on the stack
-                const uint32_t ns = nearest & 7u;
-                if (grp >> 24) st.push((int)grp);
-                grp = ((ih & ~(1u << (ns ^ oct))) << 24) | B.x;
-                next = (int32_t)(B.x + ns);
-            } else {
-                next = -1;
-            }
-            if (tm) {
-                if (!held) { t1b = B.y; t1m = tm; held = true; }
-                else { t2b = B.y; t2m = tm; }
-            }
-            if (__popcll(__ballot(!held)) < CTL_LEAF_BREAK) break;
-        }
-        // a lane still walking towards its second leaf group when the wave stopped
-        const bool cut = held && t2m == 0 && !exhausted;
-        if (held) {
-            if (leaves(S, t1b, t1m, stats)) return;
-            if (leaves(S, t2b, t2m, stats)) return;
-        }
-        t1m = t2m = 0;
-        held = cut;   // phantom: walk on to the next leaf group with the old tcull
-        if (!cut) tcull = h.t;
-        if (exhausted) done = true;
-    }
-};
-
 template <int ANY, bool STATS, bool SINGLE, int WIDE = 0, bool ALPHA = false>
-using Traverser = typename std::conditional<WIDE == 2, Traverser8<ANY, STATS, ALPHA>,
-                                            Traverser4<ANY, STATS, SINGLE, WIDE != 0, ALPHA>>::type;
+using Traverser = Traverser4<ANY, STATS, SINGLE, WIDE != 0, ALPHA>;
 
 // Whole traversal of one ray (megakernel, batch kernel).
 template <int ANY, bool STATS, bool SINGLE, int WIDE = 0, bool ALPHA = false>
 __device__ __forceinline__ bool trace_one(const DevScene& S, f3 ori, f3 dir, float span_tmin, float tri_tmin,
-                                          HitRec& h, LaneStack& st, TraceStats* stats) {
+                                          HitRec& h, LaneStack& st, TraceStats* stats, float anyDist = -1.0f) {
     Traverser<ANY, STATS, SINGLE, WIDE, ALPHA> T;
-    T.init(S, ori, dir, span_tmin, tri_tmin, h.t, st, stats);
+    T.init(S, ori, dir, span_tmin, tri_tmin, h.t, st, stats, anyDist);
     while (!T.done) T.round(S, st, stats);
     h = T.h;
     return !st.overflow;

@@ -120,9 +120,7 @@ __global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S_arg, WfStat
             } else if (MODE == 1) {
                 W.sh_occ[ray] = T.h.tri != 0xffffffffu ? 1u : 0u;
             } else {
-                const float dist = W.sh_d[ray].w;
-                bool end = T.h.t < dist - S.ray_eps;
-                W.sh_occ[ray] = (T.h.t > 0 + S.ray_eps && end) ? 1u : 0u;
+                W.sh_occ[ray] = shadow_occluded(S, false, T.h, W.sh_d[ray].w) ? 1u : 0u;
             }
             ovf |= st.overflow;
             haveRay = false;
@@ -145,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S_arg, WfStat
                     } else {
                         const float4 o = W.sh_o[ray], d = W.sh_d[ray];
                         T.init(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), 0.0f, S.ray_eps,
-                               MODE == 1 ? o.w : FLT_MAX, st, &ts);
+                               MODE == 1 ? o.w : FLT_MAX, st, &ts, MODE == 1 ? d.w : -1.0f);
                     }
                 } else {
                     exhausted = true;
@@ -177,7 +175,6 @@ void launch_trace(ctl_ctx* c, hipStream_t s, const uint32_t* queue, const uint32
     const bool wide = c->scene.wide != 0 && !stats;   // stats: the reference's binary traversal
     const bool alpha = c->scene.alpha != 0;
     if (stats) { if (single) LT(true, true, 0, false); else LT(true, false, 0, false); }
-    else if (wide && single && c->scene.w8_on) LT2(true, 2);
     else if (wide) { if (single) LT2(true, 1); else LT2(false, 1); }
     else { if (single) LT2(true, 0); else LT2(false, 0); }
 #undef LT2

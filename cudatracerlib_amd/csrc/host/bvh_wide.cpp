@@ -76,9 +76,6 @@ struct Collapser {
     std::vector<uint8_t> fsplit;        // per node: the j of f(x)
 
     void plan(int32_t root) {
-#ifdef CTL_COLLAPSE_GREEDY
-        (void)root;
-#else
         g.assign(n_nodes * 4, 0.0f);
         choice.assign(n_nodes * 4, 0);
         fsplit.assign(n_nodes, 1);
@@ -129,7 +126,6 @@ struct Collapser {
                 choice[4 * x + k - 1] = (uint8_t)ck;
             }
         }
-#endif
     }
 
     // the slots subtree x fills with a budget of k (x's box taken from its parent)
@@ -147,20 +143,6 @@ struct Collapser {
         Kid k[4];
         int nk = 2;
         binary_kids(node_of(v), (uint32_t)v >> 2, k[0], k[1]);
-#ifdef CTL_COLLAPSE_GREEDY
-        // greedy collapse: open the inner child of largest surface area until four children
-        while (nk < 4) {
-            int best = -1;
-            float bestArea = -1.0f;
-            for (int i = 0; i < nk; i++)
-                if (is_inner(k[i].v) && kid_area(k[i]) > bestArea) { bestArea = kid_area(k[i]); best = i; }
-            if (best < 0) break;
-            Kid a, b;
-            binary_kids(node_of(k[best].v), (uint32_t)k[best].v >> 2, a, b);
-            k[best] = a;
-            k[nk++] = b;
-        }
-#else
         {
             const Kid a = k[0], b = k[1];
             const int j = fsplit[(size_t)v / 4];
@@ -168,7 +150,6 @@ struct Collapser {
             expand(a, j, k, nk);
             expand(b, 4 - j, k, nk);
         }
-#endif
         const size_t me = out.size();
         out.push_back(WideNode{});
         if (src) {

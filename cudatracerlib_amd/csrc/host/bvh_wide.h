@@ -15,9 +15,9 @@
 //
 // Which binary nodes become wide nodes is chosen by the SAH-optimal dynamic
 // program over the fixed leaves (minimum summed surface area of the wide
-// nodes; bvh_wide.cpp); -DCTL_COLLAPSE_GREEDY restores the greedy collapse
-// (open the inner child of largest surface area until four children).  C3:
-// 2606 -> 2647 Mrays/s.  Leaves, leaf entries and Woop data are shared with
+// nodes; bvh_wide.cpp).  Against the greedy collapse (open the inner child of
+// largest surface area until four children) C3 2606 -> 2647 Mrays/s
+// (profiles/r02_collapse_dp_vs_greedy.txt).  Leaves, leaf entries and Woop data are shared with
 // the binary tree.
 #pragma once
 #include <cstdint>

@@ -41,7 +41,9 @@
 extern "C" {
 #endif
 
-#define CTL_ABI_VERSION 2   /* 2: round 4 (ctl_env_light 112 B, ctl_fb_reduce d_out, wide-tree reads) */
+#define CTL_ABI_VERSION 3   /* 2: round 4 (ctl_env_light 112 B, ctl_fb_reduce d_out, wide-tree reads);
+                               3: round 5 (ctl_occluded; CTL_SCENE_WIDE8 / CTL_ARRAY_W8_* / ctl_host_w8_tree
+                               removed) */
 
 #if defined(_WIN32)
 #define CTL_API __declspec(dllexport)
@@ -266,15 +268,10 @@ enum {
      * node bytes; changes which nodes are visited, never which triangle is hit.
      * Off (default): 128-B float nodes, measured faster on MI355X.
      * Ignored for scenes with animated meshes (the refit writes float nodes). */
-    CTL_SCENE_WIDE_QUANT = 1u << 2,
-    /* one-mesh scenes (scene_start_node < 0) without animated meshes: also
-     * build the 8-wide compressed tree (80-B nodes, octant-ordered children,
-     * leaf entries relaid per node; csrc/host/bvh_w8.h) and traverse it in the
-     * persistent path kernel and the batch traversal (the other schedules keep
-     * the 4-wide trees).  A tree it cannot represent (a leaf of more than 3
-     * entries, 2^24 nodes) keeps the 4-wide traversal (CTL_ARRAY_W8_NODES
-     * then reads CTL_ERR_STATE).                                             */
-    CTL_SCENE_WIDE8 = 1u << 3
+    CTL_SCENE_WIDE_QUANT = 1u << 2
+    /* 1u << 3 is reserved: ABI v2's 8-wide compressed tree (CTL_SCENE_WIDE8),
+     * measured 18 % slower on C3 and kept as probes/round4_variants.patch; v3 ignores
+     * the bit. */
 };
 
 /* AnimatedVertex (Engine/AnimatedMesh.h:10-22), 40 B: rest position and
@@ -447,6 +444,21 @@ CTL_API ctl_status ctl_sampler_upload(ctl_ctx* ctx, const float* seq1d, const fl
 CTL_API ctl_status ctl_intersect(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays, ctl_hit* d_hits,
                                  int32_t any_hit, void* stream);
 
+/* Batched KernelDynamicScene::Occluded(Ray(o, d), 0, tmax)
+ * (Engine/KernelDynamicScene.cu:70-80), the shadow test EstimateDirect makes
+ * (Kernel/TraceAlgorithms.cu:55), over device buffers; asynchronous on `stream`.
+ * Per ray: tmax = d_rays[i].tmax (the light distance), tmin (o.w) ignored;
+ * d_out[i] = 1 when occluded.  any_hit = 0: the reference's form, a closest-hit
+ * traceRay and eps < t < tmax - eps (a miss with tmax = inf is not occluded);
+ * any_hit = 1: the query ctl_pt_params.shadow_any_hit = 1 runs in the path
+ * kernels, any hit with eps < t < tmax - eps, boxes culled at tmax.  traceRay's
+ * traversal (span tmin 0, the alpha test in scenes with alpha maps) in the
+ * scene's tree order (CTL_SCENE_BINARY_BVH: the reference's).  Counts n rays
+ * (each Occluded is one traceRay).  How often the two forms disagree is
+ * measured in tests/test_shadow_query.py and DESIGN.md §5. */
+CTL_API ctl_status ctl_occluded(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays, uint32_t* d_out, int32_t any_hit,
+                                void* stream);
+
 /* One progressive PathTracer pass (one sample per owned pixel) accumulated
  * into the caller's device framebuffer d_fb[width*height] (PixelData,
  * Engine/Image.cu:22-44).  Uses the tables from the last ctl_sampler_generate /
@@ -559,13 +571,7 @@ enum {
      * more); instance tree: ~node), 0x76543210 an empty slot.                */
     CTL_ARRAY_WIDE_BVH = 15,       /* all mesh trees                          */
     CTL_ARRAY_SCENE_WIDE_BVH = 16, /* the instance tree (root at node 0)      */
-    CTL_ARRAY_MESH_WIDE_BASE = 17, /* uint32 per mesh: its tree's first node  */
-    /* the 8-wide tree (CTL_SCENE_WIDE8; CTL_ERR_STATE when not in use):
-     * 80-B nodes (host/bvh_w8.h), its relaid TriIntersectorData (48 B) and
-     * TriIntersectorData2 (uint32) entries                                     */
-    CTL_ARRAY_W8_NODES = 18,
-    CTL_ARRAY_W8_WOOP = 19,
-    CTL_ARRAY_W8_INDICES = 20
+    CTL_ARRAY_MESH_WIDE_BASE = 17  /* uint32 per mesh: its tree's first node  */
 };
 CTL_API ctl_status ctl_scene_read(ctl_ctx* ctx, uint32_t array, uint64_t first, uint64_t count, void* host_dst);
 
@@ -709,14 +715,6 @@ CTL_API ctl_status ctl_render_pass_stats(ctl_ctx* ctx, const ctl_pt_params* para
 CTL_API ctl_status ctl_host_wide_trees(const ctl_scene_desc* desc, void* mesh_out, uint64_t mesh_capacity,
                                        uint64_t* n_mesh_nodes, uint32_t* wbase_out, void* scene_out,
                                        uint64_t scene_capacity, uint64_t* n_scene_nodes);
-
-/* The 8-wide tree ctl_scene_upload builds under CTL_SCENE_WIDE8 for a one-mesh
- * scene (CTL_ARRAY_W8_* layouts, without the upload's zeroed pad entry); sizes
- * with NULL outputs.  CTL_ERR_INVALID (ctl_host_last_error) for a scene the
- * tree cannot represent. */
-CTL_API ctl_status ctl_host_w8_tree(const ctl_scene_desc* desc, void* nodes_out, uint64_t nodes_capacity,
-                                    uint64_t* n_nodes, void* woop_out, uint32_t* indices_out,
-                                    uint64_t entries_capacity, uint64_t* n_entries);
 
 CTL_API ctl_status ctl_host_bvh_stack_bound(const ctl_bvh_node* nodes, uint64_t n_nodes, int32_t root_value,
                                             int32_t out[2]);

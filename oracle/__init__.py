@@ -13,9 +13,9 @@ LIB = os.path.join(_HERE, "_build", "liboracle.so")
 _lib = None
 
 TIE_FIRST_FOUND = 0   # the reference's binary visit order (the reference semantics)
-TIE_MIN_INDEX = 1     # round-3 device rule, kept for comparison
 TRAVERSE_WIDE = 2     # the product's 4-wide per-ray order over trees registered with oracle_set_wide
-TRAVERSE_W8 = 3       # the product's 8-wide compressed order over the tree registered with oracle_set_w8
+# any-hit shadow query culling: tmax - eps (round 4) / tmax / none / tmax + slab slack (the product's)
+CULL_AT_ACCEPT, CULL_AT_TMAX, CULL_AT_INF, CULL_SLAB = 0, 1, 2, 3
 
 
 def build():
@@ -33,7 +33,6 @@ def load():
     vp = C.c_void_p
     sig = {
         "oracle_set_wide": (None, [C.POINTER(SceneDesc), vp, C.c_uint64, vp, C.c_uint32, vp, C.c_uint64]),
-        "oracle_set_w8": (None, [C.POINTER(SceneDesc), vp, C.c_uint64, vp, vp, C.c_uint64]),
         "oracle_woop_set": (None, [vp, vp, vp, vp]),
         "oracle_woop_get": (None, [vp, vp, vp, vp]),
         "oracle_xorwow_uniforms": (None, [C.c_uint64, C.c_uint64, C.c_uint64, vp]),
@@ -45,6 +44,8 @@ def load():
         "oracle_trace": (None, [C.POINTER(SceneDesc), C.c_int64, vp, C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp,
                                 C.c_int32]),
         "oracle_intersect": (None, [C.POINTER(SceneDesc), C.c_int64, vp, vp, C.c_int32, C.c_int32, C.c_int32]),
+        "oracle_occluded": (None, [C.POINTER(SceneDesc), C.c_int64, vp, vp, C.c_int32, C.c_int32, C.c_int32,
+                                   C.c_int32]),
         "oracle_brute_force": (None, [C.POINTER(SceneDesc), C.c_int64, vp, vp, vp, C.c_int32]),
         "oracle_render_pass": (C.c_uint64, [C.POINTER(SceneDesc), C.POINTER(PTParams), C.c_uint64, vp, C.c_int32,
                                             C.c_int32, C.c_uint32, vp]),

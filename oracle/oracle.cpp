@@ -85,17 +85,12 @@ struct Stats { uint64_t nodes = 0, tris = 0, inst = 0; };
 
 // TracerayTemplate, pointer overload (BVHTraversal.h:122-232).  spanTmin is 0
 // for traceRay and the ray's tmin for the batch kernel (TraceHelper.cu:469).
-// cullSlack > 0 (TIE_MIN_INDEX, the wide-BVH device rule): boxes are culled
-// against rayT plus that many ulps, so the closest hit is tested in any visit
-// order (device/traverse.h cull_bits); 0 keeps the reference's culling.
-constexpr int kCullSlack = 1 << 14;
-inline float cull_t(float t, int slack) {
-    const int b = as_int(t);
-    return b >= 0 ? as_float(std::min(b + slack, 0x7f800000)) : t;
-}
+// Boxes are culled against rayT, the current hit (the reference), or against
+// cullFloor when that is larger: the any-hit shadow query's cull distance,
+// which lies past its acceptance bound rayT (occluded(), kShadowCull).
 template <class CLB>
 bool traceray_template(V3 ori, V3 dir, float& rayT, float spanTmin, const CLB& clb, const float* nodes4,
-                       int bvhNodesOffset, int startNode, Stats* st, int cullSlack = 0) {
+                       int bvhNodesOffset, int startNode, Stats* st, float cullFloor = 0.0f) {
     if (startNode < 0) return clb(~startNode);
     bool found = false;
     // index 1 holds the sentinel; index 0 only absorbs the pop of an already
@@ -116,7 +111,7 @@ bool traceray_template(V3 ori, V3 dir, float& rayT, float spanTmin, const CLB& c
         while ((unsigned int)nodeAddr < (unsigned int)EntrypointSentinel) {
             const float* n = nodes4 + 4 * (size_t)(bvhNodesOffset + nodeAddr);
             if (st) st->nodes++;
-            const float tc = cull_t(rayT, cullSlack);
+            const float tc = cullFloor > rayT ? cullFloor : rayT;
             int c0i, c1i;
             std::memcpy(&c0i, n + 12, 4);
             std::memcpy(&c1i, n + 13, 4);
@@ -175,13 +170,11 @@ struct SceneView {
 };
 
 // Traversal modes: TIE_FIRST_FOUND = the reference's binary visit order
-// (BVHTraversal.h host branch, TraceHelper.cu:121); TIE_MIN_INDEX = that order
-// with the round-3 device rule (exact-t ties to the lowest (triangle, node),
-// boxes culled 2^14 ulps late), kept for the regression digests of round 3;
-// TRAVERSE_WIDE = the product's 4-wide per-ray order (trace_two_level_wide)
-// over the 4-wide trees registered with oracle_set_wide; TRAVERSE_W8 = its
-// 8-wide compressed order (trace_w8) over the tree registered with oracle_set_w8.
-enum TieMode { TIE_FIRST_FOUND = 0, TIE_MIN_INDEX = 1, TRAVERSE_WIDE = 2, TRAVERSE_W8 = 3 };
+// (BVHTraversal.h host branch, TraceHelper.cu:121); TRAVERSE_WIDE = the
+// product's 4-wide per-ray order (trace_two_level_wide) over the 4-wide trees
+// registered with oracle_set_wide.  (Mode 1, round 3's tie rule, and mode 3,
+// round 4's 8-wide order, are retired: probes/round4_variants.patch.)
+enum TieMode { TIE_FIRST_FOUND = 0, TRAVERSE_WIDE = 2 };
 
 struct Hit {
     float t; float u, v; uint32_t tri; uint32_t node;
@@ -199,28 +192,69 @@ bool scene_has_alpha(const ctl_scene_desc* d) {   // DynamicScene.cpp:586 doAlph
     return false;
 }
 
-bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
-                          Stats* st, bool alpha);
-bool trace_w8(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit, Stats* st,
-              bool alpha);
-bool trace_w8_sorted(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
-                     Stats* st);
+// Box culling of the any-hit shadow query (occluded_query): CULL_SLAB is the
+// product's rule, dist + slab_slack of each level's ray; the others are
+// measured alternatives (tests/test_shadow_query.py).
+enum ShadowCull { CULL_AT_ACCEPT = 0, CULL_AT_TMAX = 1, CULL_AT_INF = 2, CULL_SLAB = 3 };
 
-bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
-                     int tie, Stats* st, bool alpha = false) {
-    if (tie == TRAVERSE_WIDE) return trace_two_level_wide(S, ori, dir, spanTmin, triTmin, h, anyHit, st, alpha);
-    if (tie == TRAVERSE_W8) {
-        static const bool sorted = std::getenv("ORACLE_W8_SORTED") != nullptr;
-        if (sorted) return trace_w8_sorted(S, ori, dir, spanTmin, triTmin, h, anyHit, st);
-        return trace_w8(S, ori, dir, spanTmin, triTmin, h, anyHit, st, alpha);
+// DevScene::cull_m (device/traverse.h cull_bound): per axis, max |coordinate| of
+// the scene box and of every mesh's local box.
+void cull_bound(const ctl_scene_desc* d, float m[3]) {
+    for (int a = 0; a < 3; a++) {
+        float v = fabsf(d->box_min[a]) > fabsf(d->box_max[a]) ? fabsf(d->box_min[a]) : fabsf(d->box_max[a]);
+        for (uint32_t i = 0; d->mesh_boxes && i < d->n_meshes; i++) {
+            const float l = fabsf(d->mesh_boxes[6 * i + a]), hh = fabsf(d->mesh_boxes[6 * i + 3 + a]);
+            v = l > v ? l : v;
+            v = hh > v ? hh : v;
+        }
+        m[a] = v;
     }
+}
+
+// device/traverse.h slab_slack: 2^-20 max_a (|o_a| + m_a) |idir_a|, a bound (with
+// margin) on the rounding of the slab distances lo * idir - o * idir of this ray.
+float slab_slack(V3 o, V3 d, const float m[3]) {
+    const float ooeps = powf(2.0f, -80.0f);
+    const float idx = 1.0f / (fabsf(d.x) > ooeps ? d.x : o_copysign(ooeps, d.x));
+    const float idy = 1.0f / (fabsf(d.y) > ooeps ? d.y : o_copysign(ooeps, d.y));
+    const float idz = 1.0f / (fabsf(d.z) > ooeps ? d.z : o_copysign(ooeps, d.z));
+    const float ex = (fabsf(o.x) + m[0]) * fabsf(idx);
+    const float ey = (fabsf(o.y) + m[1]) * fabsf(idy);
+    const float ez = (fabsf(o.z) + m[2]) * fabsf(idz);
+    const float e = ex > ey ? ex : ey;
+    return (e > ez ? e : ez) * powf(2.0f, -20.0f);
+}
+
+// The cull distance of an any-hit query's BVH level whose ray is (o, d); mode < 0:
+// none beyond the acceptance bound (a plain any-hit query).
+struct AnyCull {
+    int mode = -1;
+    float dist = 0.0f;
+    float m[3] = {0.0f, 0.0f, 0.0f};
+    float at(V3 o, V3 d, float accept) const {
+        switch (mode) {
+            case CULL_AT_TMAX: return dist;
+            case CULL_AT_INF: return INFINITY;
+            case CULL_SLAB: return dist + slab_slack(o, d, m);
+            default: return accept;
+        }
+    }
+};
+
+bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
+                          Stats* st, bool alpha, const AnyCull& ac);
+
+// ac (any-hit only): the shadow query's per-level cull distance (AnyCull).
+bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
+                     int tie, Stats* st, bool alpha = false, const AnyCull& ac0 = AnyCull()) {
+    const AnyCull ac = anyHit ? ac0 : AnyCull();
+    if (tie == TRAVERSE_WIDE) return trace_two_level_wide(S, ori, dir, spanTmin, triTmin, h, anyHit, st, alpha, ac);
     const ctl_scene_desc* d = S.d;
     if (d->n_nodes == 0) return false;
     const float* sceneNodes = reinterpret_cast<const float*>(d->scene_bvh_nodes);
     const float* meshNodes = reinterpret_cast<const float*>(d->bvh_nodes);
     const float* tris = reinterpret_cast<const float*>(d->woop_tris);
     bool done = false;   // any-hit termination
-    const int slack = tie == TIE_MIN_INDEX ? kCullSlack : 0;
     auto instClb = [&](int nodeIdx) -> bool {
         if (done) return false;
         if (st) st->inst++;
@@ -239,12 +273,7 @@ bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float t
                 float invDz = 1.0f / (dl.x * v[0] + dl.y * v[1] + dl.z * v[2]);
                 float t = Oz * invDz;
                 unsigned int gtri = (index >> 1) + mesh.triangle_offset;
-                // TIE_MIN_INDEX: an exact-t tie goes to the lower (triangle, node)
-                // whatever the visit order (the rule of the wide-BVH device path);
-                // a hit at exactly the initial tmax is still rejected.
-                bool closer = t < h.t || (tie == TIE_MIN_INDEX && t == h.t && h.tri != UINT_MAX &&
-                                          (gtri < h.tri || (gtri == h.tri && (uint32_t)nodeIdx < h.node)));
-                if (t > triTmin && closer) {
+                if (t > triTmin && t < h.t) {
                     float Ox = v[7] + ol.x * v[4] + ol.y * v[5] + ol.z * v[6];
                     float Dx = dl.x * v[4] + dl.y * v[5] + dl.z * v[6];
                     float u = Ox + t * Dx;
@@ -266,9 +295,11 @@ bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float t
             }
             return found;
         };
-        return traceray_template(ol, dl, h.t, spanTmin, triClb, meshNodes, (int)mesh.bvh_node_offset, 0, st, slack);
+        return traceray_template(ol, dl, h.t, spanTmin, triClb, meshNodes, (int)mesh.bvh_node_offset, 0, st,
+                                 ac.at(ol, dl, h.t));
     };
-    return traceray_template(ori, dir, h.t, spanTmin, instClb, sceneNodes, 0, d->scene_start_node, st, slack);
+    return traceray_template(ori, dir, h.t, spanTmin, instClb, sceneNodes, 0, d->scene_start_node, st,
+                             ac.at(ori, dir, h.t));
 }
 
 // ---------------------------------------------------------------------------
@@ -327,7 +358,7 @@ struct WRay {
 };
 
 bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
-                          Stats* st, bool alpha) {
+                          Stats* st, bool alpha, const AnyCull& ac) {
     const ctl_scene_desc* d = S.d;
     if (d->n_nodes == 0) return false;
     const WideTrees& W = wide_trees_for(d);
@@ -348,7 +379,11 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
     int level = 0, nodeAddr = 0, leafAddr = 0;
     size_t meshSent = 0;
     uint32_t wnodeBase = 0, triBase = 0, idxBase = 0, triOffset = 0, inst = 0;
-    float tcull = h.t;
+    // any-hit: h.t only changes when the query ends; the cull distance is the
+    // level's (ac.at of the world ray, then of each instance's ray)
+    const float accept = h.t;
+    float cullAny = ac.at(v3(world.ox, world.oy, world.oz), v3(world.dx, world.dy, world.dz), accept);
+    float tcull = cullAny;
     const int tminBits = as_int(spanTmin);
     bool found = false;
     auto enter = [&](uint32_t node) {   // TraceHelper.cu:91-100
@@ -361,6 +396,7 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
         M44 modl = S.inv(node);
         cur.set(transformPoint(modl, v3(world.ox, world.oy, world.oz)),
                 transformDirection(modl, v3(world.dx, world.dy, world.dz)));
+        cullAny = ac.at(v3(cur.ox, cur.oy, cur.oz), v3(cur.dx, cur.dy, cur.dz), accept);   // the mesh's ray
     };
     // one Woop test (TraceHelper.cu:118-161); true = any-hit termination
     auto test = [&](uint32_t e) -> bool {
@@ -407,24 +443,14 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
     if (single) {
         enter(~(uint32_t)d->scene_start_node);
         level = 1;
+        tcull = cullAny;
     }
-    // Measurement only (profiles/r04_ab_spec.txt), never set by the tests of the
-    // shipped order: ORACLE_WIDE_NOSPEC=1 stops at the first leaf in the mesh level of a
-    // one-mesh scene (the order of the device's CTL_LEAF_SPECULATE=0 / CTL_IFIF=1 builds);
-    // ORACLE_SPEC_STEPS=K bounds the walk past a postponed leaf to K inner nodes
-    // (CTL_SPEC_STEPS=K); ORACLE_SPEC_NOPOP=1 ends it where it would pop (CTL_SPEC_NOPOP=1).
-    static const bool nospec = std::getenv("ORACLE_WIDE_NOSPEC") != nullptr;
-    static const int kSpec = std::getenv("ORACLE_SPEC_STEPS") ? std::atoi(std::getenv("ORACLE_SPEC_STEPS")) : 0;
-    int specLeft = 0;
-    static const bool nopop = std::getenv("ORACLE_SPEC_NOPOP") != nullptr;
     for (;;) {
-        const bool spec = level == 1 && !(nospec && single);
+        const bool spec = level == 1;
         const float* tree = level ? W.mesh.data() + 32 * (size_t)wnodeBase : W.scene.data();
         const int tBits = as_int(tcull);
         const bool nx = as_int(cur.idx) < 0, ny = as_int(cur.idy) < 0, nz = as_int(cur.idz) < 0;
-        while ((unsigned)nodeAddr < (unsigned)EntrypointSentinel &&
-               ((spec && (kSpec == 0 || specLeft > 0)) || leafAddr >= 0)) {
-            const bool held = leafAddr < 0;
+        while ((unsigned)nodeAddr < (unsigned)EntrypointSentinel && (spec || leafAddr >= 0)) {
             if (st) st->nodes++;
             const float* n = tree + 32 * (size_t)nodeAddr;
             int k[4], c[4];
@@ -446,14 +472,11 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
             for (int i = 0; i < 4; i++) m += k[i] != 0x7fffffff;
             for (int i = m - 1; i >= 1; i--) stack.push_back(c[i]);
             int next = m > 0 ? c[0] : pop();
-            const bool stopWalk = nopop && held && m == 0;
             if (next < 0 && leafAddr >= 0) {   // postpone one leaf
                 leafAddr = next;
                 next = pop();
             }
             nodeAddr = next;
-            if (kSpec > 0) specLeft = held ? specLeft - 1 : (leafAddr < 0 ? kSpec : specLeft);
-            if (stopWalk) break;
         }
         bool entered = false;
         while (leafAddr < 0) {
@@ -477,7 +500,7 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
                 if (nodeAddr < 0) nodeAddr = pop();
             }
         }
-        tcull = h.t;
+        tcull = anyHit ? cullAny : h.t;
         if (entered) continue;
         if (nodeAddr == EntrypointSentinel) {
             if (level == 1 && !single) {
@@ -485,6 +508,8 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
                 const int saved = pop();
                 level = 0;
                 cur = world;
+                cullAny = ac.at(v3(world.ox, world.oy, world.oz), v3(world.dx, world.dy, world.dz), accept);
+                if (anyHit) tcull = cullAny;
                 leafAddr = saved;
                 nodeAddr = saved;
                 if (saved < 0) nodeAddr = pop();
@@ -492,259 +517,6 @@ bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, fl
                 break;
             }
         }
-    }
-    return found;
-}
-
-// ---------------------------------------------------------------------------
-// The product's 8-wide compressed order (NOT a reference function), a
-// sequential statement of device/traverse.h Traverser8 over the tree
-// registered with oracle_set_w8 (host/bvh_w8.h layout, read back from the
-// device or built by ctl_host_w8_tree).  One-mesh scenes.
-//
-// Per node: grid steps s = 2^(e - 127), per axis a = s * idir and
-// b = fma(p, idir, -ood); each plane is fma(q, a, b) (q the byte, near / far by
-// the sign of idir); spans, culling against tcull and the hit test as the
-// 4-wide order.  Of a node's hit inner children the nearest (smallest entry,
-// its low 3 bits replaced by the slot) is visited next, the others after it
-// in increasing slot ^ octant (as a group that waits on the stack while the
-// nearest child's subtree is visited); a node's hit leaf slots form one leaf
-// group (entry mask over leaf_base).  After its first leaf group the ray walks on with the same tcull
-// until its second, tests both (entries ascending) and takes tcull = the
-// closest hit.
-// ---------------------------------------------------------------------------
-struct W8Trees {
-    const void* key_nodes = nullptr;
-    uint64_t key_n = 0;
-    std::vector<uint32_t> nodes;   // 20 words (80 B) per node
-    std::vector<float> woop;       // 12 floats per entry
-    std::vector<uint32_t> idx;
-    bool set = false;
-};
-W8Trees g_w8;
-
-bool trace_w8(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit, Stats* st,
-              bool alpha) {
-    const ctl_scene_desc* d = S.d;
-    if (d->n_nodes == 0) return false;
-    if (!g_w8.set || g_w8.key_nodes != (const void*)d->bvh_nodes || g_w8.key_n != d->n_bvh_nodes ||
-        d->scene_start_node >= 0) {
-        std::fprintf(stderr, "oracle: TRAVERSE_W8 without an 8-wide tree registered for this one-mesh scene\n");
-        std::abort();
-    }
-    const W8Trees& W = g_w8;
-    const uint32_t inst = ~(uint32_t)d->scene_start_node;
-    const ctl_kernel_mesh& mesh = d->meshes[d->nodes[inst].mesh_index];
-    if (st) st->inst++;
-    M44 modl = S.inv(inst);
-    WRay cur;
-    cur.set(transformPoint(modl, ori), transformDirection(modl, dir));
-    const uint32_t oct = ((uint32_t)as_int(cur.idx) >> 31) | (((uint32_t)as_int(cur.idy) >> 31) << 1) |
-                         (((uint32_t)as_int(cur.idz) >> 31) << 2);
-    const int tminBits = as_int(spanTmin);
-    std::vector<uint32_t> stack;
-    stack.push_back(0u);
-    uint32_t grp = 0;   // the group of nodes left to visit after `next`: hits (slot ^ oct order) << 24 | child base
-    uint32_t t1b = 0, t1m = 0, t2b = 0, t2m = 0;
-    bool held = false, exhausted = false, found = false;
-    float tcull = h.t;
-    auto leaves = [&](uint32_t base, uint32_t mask) -> bool {   // true = any-hit termination
-        for (; mask; mask &= mask - 1u) {
-            const uint32_t e = base + (uint32_t)__builtin_ctz(mask);
-            const float* v = W.woop.data() + 12 * (size_t)e;
-            if (st) st->tris++;
-            float Oz = v[3] - cur.ox * v[0] - cur.oy * v[1] - cur.oz * v[2];
-            float invDz = 1.0f / (cur.dx * v[0] + cur.dy * v[1] + cur.dz * v[2]);
-            float t = Oz * invDz;
-            if (t > triTmin && t < h.t) {
-                float Ox = v[7] + cur.ox * v[4] + cur.oy * v[5] + cur.oz * v[6];
-                float Dx = cur.dx * v[4] + cur.dy * v[5] + cur.dz * v[6];
-                float u = Ox + t * Dx;
-                if (u >= 0.0f) {
-                    float Oy = v[11] + cur.ox * v[8] + cur.oy * v[9] + cur.oz * v[10];
-                    float Dy = cur.dx * v[8] + cur.dy * v[9] + cur.dz * v[10];
-                    float vv = Oy + t * Dy;
-                    if (vv >= 0.0f && u + vv <= 1.0f) {
-                        const uint32_t gtri = (W.idx[e] >> 1) + mesh.triangle_offset;
-                        if (!alpha || alpha_survives(d, gtri, inst, u, vv)) {
-                            h.node = inst; h.tri = gtri; h.u = u; h.v = vv; h.t = t;
-                            found = true;
-                            if (anyHit) return true;
-                        }
-                    }
-                }
-            }
-        }
-        return false;
-    };
-    int64_t next = 0;   // the node to visit next (the root first), -1: take the group's first slot
-    for (;;) {
-        const int tBits = as_int(tcull);
-        while (t2m == 0 && !exhausted) {
-            if (next < 0) {
-                if ((grp >> 24) == 0) {
-                    grp = stack.back();
-                    stack.pop_back();
-                    if ((grp >> 24) == 0) { exhausted = true; break; }
-                }
-                const uint32_t hits = grp >> 24;
-                next = (int64_t)((grp & 0xffffffu) + ((uint32_t)__builtin_ctz(hits) ^ oct));
-                grp = ((hits & (hits - 1u)) << 24) | (grp & 0xffffffu);
-            }
-            if (st) st->nodes++;
-            const uint32_t* n = W.nodes.data() + 20 * (size_t)next;
-            float px, py, pz;
-            std::memcpy(&px, n + 0, 4); std::memcpy(&py, n + 1, 4); std::memcpy(&pz, n + 2, 4);
-            const uint32_t hw = n[3], childBase = n[4], leafBase = n[5], meta0 = n[6], meta1 = n[7];
-            const float sx = as_float((int32_t)((hw & 0xffu) << 23)), sy = as_float((int32_t)(((hw >> 8) & 0xffu) << 23));
-            const float sz = as_float((int32_t)(((hw >> 16) & 0xffu) << 23));
-            const uint32_t imask = hw >> 24;
-            const float ax = sx * cur.idx, ay = sy * cur.idy, az = sz * cur.idz;
-            const float bx = std::fma(px, cur.idx, -cur.oodx), by = std::fma(py, cur.idy, -cur.oody);
-            const float bz = std::fma(pz, cur.idz, -cur.oodz);
-            const bool nx = oct & 1u, ny = oct & 2u, nz = oct & 4u;
-            // words: x lo 8..9, x hi 10..11, y lo 12..13, y hi 14..15, z lo 16..17, z hi 18..19
-            uint32_t hit8 = 0, nearest = 0xffffffffu;
-            for (int i = 0; i < 8; i++) {
-                auto q = [&](int w) { return (float)((n[w + (i >> 2)] >> (8 * (i & 3))) & 0xffu); };
-                const float vnx = std::fma(q(nx ? 10 : 8), ax, bx), vfx = std::fma(q(nx ? 8 : 10), ax, bx);
-                const float vny = std::fma(q(ny ? 14 : 12), ay, by), vfy = std::fma(q(ny ? 12 : 14), ay, by);
-                const float vnz = std::fma(q(nz ? 18 : 16), az, bz), vfz = std::fma(q(nz ? 16 : 18), az, bz);
-                const float mn = as_float(imax3(as_int(vnx), as_int(vny), omax(as_int(vnz), tminBits)));
-                const float mx = as_float(imin3(as_int(vfx), as_int(vfy), omin(as_int(vfz), tBits)));
-                if (mx >= mn) {
-                    hit8 |= 1u << i;
-                    // nearest inner child: entry bits with the slot in the low 3 bits
-                    if ((imask >> i) & 1u) nearest = omin(nearest, ((uint32_t)as_int(mn) & ~7u) | (uint32_t)i);
-                }
-            }
-            const uint32_t lhit = hit8 & ~imask;
-            uint32_t tm = 0;
-            for (int i = 0; i < 8; i++) {
-                const uint32_t m = ((i < 4 ? meta0 : meta1) >> (8 * (i & 3))) & 0xffu;
-                if ((lhit >> i) & 1u) tm |= (m >> 5) << (m & 31u);
-            }
-            uint32_t ih = 0;
-            for (int i = 0; i < 8; i++)
-                if (((hit8 & imask) >> i) & 1u) ih |= 1u << (i ^ (int)oct);
-            if (ih) {
-                // the nearest inner child next, the node's other hit inner children (octant order) as
-                // a group; the group the node came from waits on the stack
-                const uint32_t ns = nearest & 7u;
-                if (grp >> 24) stack.push_back(grp);
-                grp = ((ih & ~(1u << (ns ^ oct))) << 24) | childBase;
-                next = (int64_t)(childBase + ns);
-            } else {
-                next = -1;
-            }
-            if (tm) {
-                if (!held) { t1b = leafBase; t1m = tm; held = true; }
-                else { t2b = leafBase; t2m = tm; }
-            }
-        }
-        if (held) {
-            if (leaves(t1b, t1m)) return true;
-            if (leaves(t2b, t2m)) return true;
-        }
-        t1m = t2m = 0;
-        held = false;
-        tcull = h.t;
-        if (exhausted) break;
-    }
-    return found;
-}
-
-// Measurement only (ORACLE_W8_SORTED=1 in the environment): the same 8-wide
-// tree visited near-first by each child's entry distance (a full sort, as the
-// 4-wide order does) instead of by octant slot, to size what the octant order
-// costs in node visits.  Not a device order.
-bool trace_w8_sorted(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
-                     Stats* st) {
-    const ctl_scene_desc* d = S.d;
-    const W8Trees& W = g_w8;
-    const uint32_t inst = ~(uint32_t)d->scene_start_node;
-    const ctl_kernel_mesh& mesh = d->meshes[d->nodes[inst].mesh_index];
-    M44 modl = S.inv(inst);
-    WRay cur;
-    cur.set(transformPoint(modl, ori), transformDirection(modl, dir));
-    const uint32_t oct = ((uint32_t)as_int(cur.idx) >> 31) | (((uint32_t)as_int(cur.idy) >> 31) << 1) |
-                         (((uint32_t)as_int(cur.idz) >> 31) << 2);
-    const int tminBits = as_int(spanTmin);
-    std::vector<int64_t> stack;   // node index, or -1 - (leaf group index into lg)
-    std::vector<std::pair<uint32_t, uint32_t>> lg;
-    stack.push_back(0);
-    bool found = false;
-    while (!stack.empty()) {
-        const int64_t top = stack.back();
-        stack.pop_back();
-        if (top < 0) {
-            auto [base, mask] = lg[(size_t)(-1 - top)];
-            for (; mask; mask &= mask - 1u) {
-                const uint32_t e = base + (uint32_t)__builtin_ctz(mask);
-                const float* v = W.woop.data() + 12 * (size_t)e;
-                if (st) st->tris++;
-                float Oz = v[3] - cur.ox * v[0] - cur.oy * v[1] - cur.oz * v[2];
-                float invDz = 1.0f / (cur.dx * v[0] + cur.dy * v[1] + cur.dz * v[2]);
-                float t = Oz * invDz;
-                if (t > triTmin && t < h.t) {
-                    float u = (v[7] + cur.ox * v[4] + cur.oy * v[5] + cur.oz * v[6]) + t * (cur.dx * v[4] + cur.dy * v[5] + cur.dz * v[6]);
-                    if (u >= 0.0f) {
-                        float vv = (v[11] + cur.ox * v[8] + cur.oy * v[9] + cur.oz * v[10]) + t * (cur.dx * v[8] + cur.dy * v[9] + cur.dz * v[10]);
-                        if (vv >= 0.0f && u + vv <= 1.0f) {
-                            h.node = inst; h.tri = (W.idx[e] >> 1) + mesh.triangle_offset; h.u = u; h.v = vv; h.t = t;
-                            found = true;
-                            if (anyHit) return true;
-                        }
-                    }
-                }
-            }
-            continue;
-        }
-        if (st) st->nodes++;
-        const uint32_t* n = W.nodes.data() + 20 * (size_t)top;
-        float px, py, pz;
-        std::memcpy(&px, n + 0, 4); std::memcpy(&py, n + 1, 4); std::memcpy(&pz, n + 2, 4);
-        const uint32_t hw = n[3], childBase = n[4], leafBase = n[5], meta0 = n[6], meta1 = n[7];
-        const float sx = as_float((int32_t)((hw & 0xffu) << 23)), sy = as_float((int32_t)(((hw >> 8) & 0xffu) << 23));
-        const float sz = as_float((int32_t)(((hw >> 16) & 0xffu) << 23));
-        const uint32_t imask = hw >> 24;
-        const float ax = sx * cur.idx, ay = sy * cur.idy, az = sz * cur.idz;
-        const float bx = std::fma(px, cur.idx, -cur.oodx), by = std::fma(py, cur.idy, -cur.oody);
-        const float bz = std::fma(pz, cur.idz, -cur.oodz);
-        const bool nx = oct & 1u, ny = oct & 2u, nz = oct & 4u;
-        const int tBits = as_int(h.t);
-        // items: inner children and leaf children, with (entry bits, octant key)
-        struct It { int dist; int key; int64_t v; };
-        std::vector<It> kids;
-        static const int policy = std::getenv("ORACLE_W8_POLICY") ? std::atoi(std::getenv("ORACLE_W8_POLICY")) : 0;
-        for (int i = 0; i < 8; i++) {
-            auto q = [&](int w) { return (float)((n[w + (i >> 2)] >> (8 * (i & 3))) & 0xffu); };
-            const float vnx = std::fma(q(nx ? 10 : 8), ax, bx), vfx = std::fma(q(nx ? 8 : 10), ax, bx);
-            const float vny = std::fma(q(ny ? 14 : 12), ay, by), vfy = std::fma(q(ny ? 12 : 14), ay, by);
-            const float vnz = std::fma(q(nz ? 18 : 16), az, bz), vfz = std::fma(q(nz ? 16 : 18), az, bz);
-            const float mn = as_float(imax3(as_int(vnx), as_int(vny), omax(as_int(vnz), tminBits)));
-            const float mx = as_float(imin3(as_int(vfx), as_int(vfy), omin(as_int(vfz), tBits)));
-            if (!(mx >= mn)) continue;
-            const int key = i ^ (int)oct;
-            if ((imask >> i) & 1u) {
-                kids.push_back({as_int(mn), key, (int64_t)(childBase + (uint32_t)i)});
-            } else {
-                const uint32_t m = ((i < 4 ? meta0 : meta1) >> (8 * (i & 3))) & 0xffu;
-                lg.push_back({leafBase, (m >> 5) << (m & 31u)});
-                kids.push_back({policy == 2 ? -1 : as_int(mn), policy == 2 ? -1 : key, -(int64_t)lg.size()});
-            }
-        }
-        // policy 0: entry distance; 1: octant key; 2: leaves first then octant; 3: nearest first, rest octant
-        if (policy == 0) std::stable_sort(kids.begin(), kids.end(), [](auto& a, auto& b) { return a.dist > b.dist; });
-        else std::stable_sort(kids.begin(), kids.end(), [](auto& a, auto& b) { return a.key > b.key; });
-        if (policy == 3 && !kids.empty()) {
-            size_t best = 0;
-            for (size_t k = 1; k < kids.size(); k++) if (kids[k].dist < kids[best].dist) best = k;
-            It b = kids[best];
-            kids.erase(kids.begin() + (long)best);
-            kids.push_back(b);
-        }
-        for (auto& k : kids) stack.push_back(k.v);
     }
     return found;
 }
@@ -1232,6 +1004,9 @@ inline float power_heuristic(float fPdf, float gPdf) {   // MonteCarlo.h:29-33 w
     return (f * f) / (f * f + g * g);
 }
 
+// The product's any-hit shadow cull rule (device/traverse.h slab_slack).
+constexpr int kShadowCull = CULL_SLAB;
+
 struct RenderCtx {
     SceneView S;
     Sampler* rng;
@@ -1242,19 +1017,36 @@ struct RenderCtx {
     Stats st;
 };
 
-bool occluded(RenderCtx& C, V3 ori, V3 dir, float tmax) {   // KernelDynamicScene.cu:70-80 with tmin=0
-    C.rays++;
-    float eps = C.S.d->ray_eps;
+// KernelDynamicScene::Occluded(Ray(ori, dir), 0, tmax) (KernelDynamicScene.cu:70-80).
+// Closest-hit form (the reference): traceRay, then eps < t < tmax - eps; a miss
+// with an infinite tmax is not occluded (:77-78).  Any-hit form (the product's
+// shadow_any_hit = 1): is there a hit with eps < t < tmax - eps.  Its boxes are
+// culled past the acceptance bound (kShadowCull = CULL_SLAB: tmax + slab_slack):
+// a box whose rounded slab entry lands past tmax - eps, or past tmax, can still
+// hold a hit below tmax - eps, which the closest-hit form finds (it culls at its
+// current hit, or not at all before the first one).
+bool occluded_query(const SceneView& S, V3 ori, V3 dir, float tmax, bool anyHit, int tie, int cull, Stats* st) {
+    const float eps = S.d->ray_eps;
     Hit h;
-    if (C.anyHitShadow) {
-        h.t = tmax - eps; h.tri = UINT_MAX; h.node = UINT_MAX;
-        if (C.S.d->n_nodes == 0) return false;
-        trace_two_level(C.S, ori, dir, 0.0f, eps, h, true, C.tie, &C.st, scene_has_alpha(C.S.d));
+    if (anyHit) {
+        h.t = tmax - eps; h.tri = UINT_MAX; h.node = UINT_MAX; h.u = h.v = 0.0f;
+        if (S.d->n_nodes == 0) return false;
+        AnyCull ac;
+        ac.mode = cull;
+        ac.dist = tmax;
+        cull_bound(S.d, ac.m);
+        trace_two_level(S, ori, dir, 0.0f, eps, h, true, tie, st, scene_has_alpha(S.d), ac);
         return h.tri != UINT_MAX;
     }
-    trace_ray(C.S, ori, dir, h, C.tie, &C.st);
+    trace_ray(S, ori, dir, h, tie, st);
     bool end = h.t < tmax - eps;
+    if (std::isinf(tmax) && h.tri == UINT_MAX) end = false;
     return h.t > 0 + eps && end;
+}
+
+bool occluded(RenderCtx& C, V3 ori, V3 dir, float tmax) {   // with tmin = 0, as EstimateDirect calls it
+    C.rays++;
+    return occluded_query(C.S, ori, dir, tmax, C.anyHitShadow, C.tie, kShadowCull, &C.st);
 }
 
 Spec estimate_direct(RenderCtx& C, BRec bRec, const ctl_material& mat, const ctl_light& light, float light_pdf) {
@@ -1808,21 +1600,6 @@ void oracle_set_wide(const ctl_scene_desc* d, const void* mesh_nodes, uint64_t n
     g_wide.set = true;
 }
 
-// Registers the 8-wide tree of one-mesh scene d for TRAVERSE_W8 (host/bvh_w8.h:
-// 80-B nodes, relaid TriIntersectorData entries and their index words).
-void oracle_set_w8(const ctl_scene_desc* d, const void* nodes, uint64_t n_nodes, const void* woop,
-                   const uint32_t* idx, uint64_t n_entries) {
-    std::lock_guard<std::mutex> g(g_wide_mtx);
-    g_w8.key_nodes = d->bvh_nodes;
-    g_w8.key_n = d->n_bvh_nodes;
-    const uint32_t* nw = static_cast<const uint32_t*>(nodes);
-    const float* wf = static_cast<const float*>(woop);
-    g_w8.nodes.assign(nw, nw + 20 * n_nodes);
-    g_w8.woop.assign(wf, wf + 12 * n_entries);
-    g_w8.idx.assign(idx, idx + n_entries);
-    g_w8.set = true;
-}
-
 void oracle_woop_set(const float* v0, const float* v1, const float* v2, float* out12) {
     woop_set(v3(v0[0], v0[1], v0[2]), v3(v1[0], v1[1], v1[2]), v3(v2[0], v2[1], v2[2]), out12);
 }
@@ -1924,6 +1701,32 @@ void oracle_trace(const ctl_scene_desc* desc, int64_t n, const ctl_ray* rays, in
     for (int i = 0; i < threads; i++) ts.emplace_back(worker);
     for (auto& t : ts) t.join();
     if (stats) for (int i = 0; i < 4; i++) stats[i] = acc[i];
+}
+
+// Occluded(Ray(o, d), 0, tmax) per ray (rays[i].tmax = tmax, tmin ignored): the
+// reference's closest-hit form (any_hit 0) or the any-hit query (any_hit 1)
+// with boxes culled at tmax - eps (cull 0, round 4's rule), at tmax (1), not
+// past the ray origin (2) or at tmax + slab_slack (3, the product's).
+void oracle_occluded(const ctl_scene_desc* desc, int64_t n, const ctl_ray* rays, uint8_t* out, int32_t any_hit,
+                     int32_t tie, int32_t cull, int32_t threads) {
+    SceneView S{desc};
+    if (threads <= 0) threads = (int)std::thread::hardware_concurrency();
+    std::atomic<int64_t> next{0};
+    auto worker = [&]() {
+        for (;;) {
+            const int64_t base = next.fetch_add(256);
+            if (base >= n) break;
+            const int64_t end = std::min<int64_t>(n, base + 256);
+            for (int64_t i = base; i < end; i++) {
+                const ctl_ray& r = rays[i];
+                out[i] = occluded_query(S, v3(r.o[0], r.o[1], r.o[2]), v3(r.d[0], r.d[1], r.d[2]), r.tmax, any_hit != 0,
+                                        tie, cull, nullptr) ? 1 : 0;
+            }
+        }
+    };
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; i++) ts.emplace_back(worker);
+    for (auto& t : ts) t.join();
 }
 
 // Batch kernel output layout (ctl_hit), TraceHelper.cu:722-731.

@@ -105,25 +105,12 @@ def register_wide(orc, desc, trees=None):
 
 def tie_rule(desc, orc=None, trees=None):
     """Oracle traversal mode matching the device traversal the scene selects:
-    the reference's own binary order for CTL_SCENE_BINARY_BVH (0); under
-    CTL_SCENE_WIDE8 on a scene the 8-wide tree represents, the product's 8-wide
-    order (oracle.TRAVERSE_W8 = 3); else the product's 4-wide per-ray order
-    (oracle.TRAVERSE_WIDE = 2) over the same trees, registered here."""
+    the reference's own binary order for CTL_SCENE_BINARY_BVH (0); else the
+    product's 4-wide per-ray order (oracle.TRAVERSE_WIDE = 2) over the same
+    trees, registered here."""
     if desc.flags & 2:
         return 0
     orc = orc or oracle.load()
-    if desc.flags & 8:
-        import cudatracerlib_amd as ctl
-        key = ("w8", _addr(desc.bvh_nodes), desc.n_bvh_nodes, _addr(desc.woop_tris), _sample_digest(desc))
-        if _WIDE_KEY[0] != key:
-            t = ctl.host_w8_tree(desc) if desc.scene_start_node < 0 and desc.n_anim_meshes == 0 else None
-            if t is not None:
-                nodes, woop, idx = t
-                orc.oracle_set_w8(C.byref(desc), oracle.ptr(nodes), nodes.shape[0], oracle.ptr(woop),
-                                  oracle.ptr(idx), idx.size)
-                _WIDE_KEY[0] = key
-        if _WIDE_KEY[0] == key:
-            return 3
     key = (_addr(desc.bvh_nodes), desc.n_bvh_nodes, _addr(desc.scene_bvh_nodes), desc.n_scene_bvh_nodes,
            _addr(desc.tri_indices), desc.n_tri_indices, _addr(desc.meshes), desc.flags & 4, desc.scene_start_node,
            _sample_digest(desc))
@@ -131,13 +118,6 @@ def tie_rule(desc, orc=None, trees=None):
         register_wide(orc, desc, trees)
         _WIDE_KEY[0] = None if trees is not None else key
     return 2
-
-
-def w8_bvh(desc):
-    """Copy of a compiled scene desc that selects the 8-wide compressed tree."""
-    d = type(desc).from_buffer_copy(desc)
-    d.flags |= 8
-    return d
 
 
 def binary_bvh(desc):
@@ -156,7 +136,6 @@ def wide_quant(desc):
 
 def select_bvh(desc, bvh):
     return {"wide": desc, "wideq": wide_quant(desc) if bvh == "wideq" else desc,
-            "w8": w8_bvh(desc) if bvh == "w8" else desc,
             "binary": binary_bvh(desc) if bvh == "binary" else desc}[bvh]
 
 

@@ -26,7 +26,20 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert abi.load().ctl_abi_version() == 2   # round 4: ctl_env_light 112 B, ctl_fb_reduce d_out, wide-tree reads
+    # round 5: ctl_occluded; the 8-wide tree's flag, arrays and ctl_host_w8_tree gone
+    assert abi.load().ctl_abi_version() == 3 == abi.ABI_VERSION
+
+
+def test_load_refuses_another_abi_version(tmp_path, monkeypatch):
+    """A library reporting another CTL_ABI_VERSION (stale build, CTL_LIB variant)
+    is refused before anything binds to its struct layouts."""
+    import shutil
+    copy = tmp_path / "libctl_trace.so"   # another path: load() does not return its cached handle
+    shutil.copy(abi.LIB_PATH, copy)
+    monkeypatch.setattr(abi, "ABI_VERSION", abi.ABI_VERSION + 1)
+    with pytest.raises(RuntimeError, match="CTL_ABI_VERSION"):
+        abi.load(str(copy))
+
 
 
 def test_reference_layout_sizes():

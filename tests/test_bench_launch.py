@@ -30,12 +30,34 @@ def test_gpus_n_without_launcher_spawns_n_ranks(n):
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout   # one line, from rank 0
     assert lines[0]["n_gpus"] == n and lines[0]["world_size"] == n
+    # the N-rank line explains itself: every rank's step time, its reduce time, the group
+    rk = lines[0]["ranks"]
+    assert rk["world_size"] == n and rk["backend"] == "gloo"
+    assert len(rk["ms_per_step"]) == n and len(rk["reduce_ms"]) == n
+    assert rk["ms_per_step_min"] == min(rk["ms_per_step"]) and rk["ms_per_step_max"] == max(rk["ms_per_step"])
+    assert all(0.0 <= x <= y for x, y in zip(rk["reduce_ms"], rk["ms_per_step"]))
 
 
 def test_single_gpu_runs_in_process():
     r = _run(["--gpus", "1", "--launch-check"])
     assert r.returncode == 0, r.stderr[-2000:]
-    assert json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["ranks"]["world_size"] == 1 and line["ranks"]["reduce_ms"] is None
+
+
+def test_roofline_scales_per_unit_counters():
+    """Profile counters recorded per unit (render passes, or rays for the primary
+    leg) scale to the timed launch; counters without a unit count are not
+    applied to another launch shape (a sharded run's 1/N launch)."""
+    prof = {"kernels": {"primary_intersect": {"units_per_launch": 2_000_000, "hbm_bytes": 100e6,
+                                              "l2_read_bytes": 1e9, "ta_busy": 0.7},
+                        "nounits": {"hbm_bytes": 100e6}}}
+    full = bench.roofline((prof, "p", True), "primary_intersect", 0.5, 1e9, "k", units=2_000_000)
+    eighth = bench.roofline((prof, "p", True), "primary_intersect", 0.5 / 8, 1e9 / 8, "k", units=250_000)
+    assert full["traffic"] == 100e6 and eighth["traffic"] == 100e6 / 8
+    assert eighth["frac_hbm"] == full["frac_hbm"] and eighth["frac_l2"] == full["frac_l2"]
+    none = bench.roofline((prof, "p", True), "nounits", 0.5, 1e9, "k", units=250_000)
+    assert none["traffic"] is None and none["frac"] is None and "no units_per_launch" in str(none["profile_matches_binary"])
 
 
 def test_mismatched_launcher_world_size_fails():

@@ -49,7 +49,7 @@ def gpu_intersect(tracer, desc, rays, any_hit, dev):
 
 @pytest.mark.parametrize("config,scale", [(1, 1.0), (2, 0.25), (3, 0.004)])
 @pytest.mark.parametrize("kind", ["random", "camera"])
-@pytest.mark.parametrize("bvh", ["wide", "wideq", "w8", "binary"])
+@pytest.mark.parametrize("bvh", ["wide", "wideq", "binary"])
 def test_intersect_closest_bit_exact(ctl, orc, tracer, dev, config, scale, kind, bvh):
     d = select_bvh(scene(ctl, config, scale, 96, 64), bvh)
     rays = random_rays(d, 50000, seed=config) if kind == "random" else camera_rays(d, 96, 64, seed=config)
@@ -64,7 +64,7 @@ def test_intersect_closest_bit_exact(ctl, orc, tracer, dev, config, scale, kind,
 
 
 @pytest.mark.parametrize("config,scale", [(1, 1.0), (2, 0.25)])
-@pytest.mark.parametrize("bvh", ["wide", "w8", "binary"])
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
 def test_intersect_any_hit(ctl, orc, tracer, dev, config, scale, bvh):
     """Any-hit returns *a* hit (order dependent, TraceHelper.cu:675-679): the
     hit/miss decision must equal the oracle's, and the reported triangle must
@@ -96,7 +96,7 @@ def render_gpu(ctl, tracer, desc, params, passes, w, h, dev, first_pass=0):
 @pytest.mark.parametrize("config,scale,w,h,passes", [(1, 1.0, 64, 64, 4), (2, 0.25, 96, 64, 2), (3, 0.003, 64, 48, 2)])
 @pytest.mark.parametrize("any_hit", [1, 0])
 @pytest.mark.parametrize("mode", ["persistent", "wavefront", "megakernel"])
-@pytest.mark.parametrize("bvh", ["wide", "wideq", "w8", "binary"])
+@pytest.mark.parametrize("bvh", ["wide", "wideq", "binary"])
 def test_render_pass_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, passes, any_hit, mode, bvh):
     d = select_bvh(scene(ctl, config, scale, w, h), bvh)
     p = ctl.PTParams(1, 50, 5, any_hit, 64, 1, 0, {"persistent": 0, "megakernel": ctl.CTL_PT_MEGAKERNEL,
@@ -303,7 +303,7 @@ def test_last_pass_ms(ctl, dev):
 
 @pytest.mark.parametrize("mode", ["persistent", "wavefront", "megakernel"])
 @pytest.mark.parametrize("any_hit", [1, 0])
-@pytest.mark.parametrize("bvh", ["wide", "w8"])
+@pytest.mark.parametrize("bvh", ["wide"])
 def test_render_c5_bit_exact(ctl, orc, tracer, dev, mode, any_hit, bvh):
     """C5 shading: roughdielectric (Beckmann + GGX, visible-normal
     sampling), image textures with trilinear and EWA MIP filtering driven by the
@@ -399,7 +399,7 @@ def test_image_resolve_and_variance_buffer(ctl, orc, dev):
 
 
 @pytest.mark.parametrize("mode", ["persistent", "wavefront", "megakernel"])
-@pytest.mark.parametrize("bvh", ["wide", "w8", "binary"])
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
 def test_render_alpha_tested_traversal(ctl, orc, tracer, dev, mode, bvh):
     """Alpha-tested traceRay (TraceHelper.cu:136-154, Material::AlphaTest):
     a checker alpha map (alpha channel), a luminance-thresholded texture and a

@@ -23,7 +23,7 @@ import pytest
 
 import oracle
 from helpers import (binary_bvh, camera_rays, classify_orders, grazing_rays, grid_room, oracle_intersect,
-                     random_rays, select_bvh, tie_rule, w8_bvh)
+                     random_rays, select_bvh, tie_rule)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -123,38 +123,6 @@ def gpu_hits(pt, rays, dev, any_hit=False):
     return h.cpu().numpy()
 
 
-@pytest.mark.parametrize("config,scale", [(2, 0.25), (3, 0.004), (5, 0.003)])
-def test_w8_order_vs_reference_order_small(ctl, orc, config, scale):
-    """The 8-wide compressed order (oracle mode 3) against the reference order
-    and the 4-wide order, on the same rays."""
-    d = scene(ctl, config, scale)
-    d8 = w8_bvh(d)
-    rays = np.concatenate([random_rays(d, 40000, seed=config), camera_rays(d, 96, 64, seed=config)])
-    ref = oracle_intersect(orc, d, rays, tie=0)
-    assert tie_rule(d8) == oracle.TRAVERSE_W8
-    w8 = oracle_intersect(orc, d8, rays)
-    c = classify_orders(ref, w8)
-    assert c["differ"] <= MAX_DIFFER_FRAC * c["rays"], c
-    assert c["hit_miss"] == 0 and c["same_hit_other_fields"] == 0, c
-    t = ctl.host_w8_tree(d8)
-    assert t is not None and t[1].shape[0] == d.n_tri_indices   # every leaf entry relaid once
-
-
-@pytest.mark.gpu
-def test_device_w8_tree_equals_host(ctl, dev):
-    d = w8_bvh(scene(ctl, 3, 0.004))
-    pt = ctl.PathTracer(0)
-    try:
-        pt.upload_scene(d)
-        got = pt.w8_tree(d)
-    finally:
-        pt.close()
-    want = ctl.host_w8_tree(d)
-    assert got is not None
-    for g, w in zip(got, want):
-        assert g.shape == w.shape and np.array_equal(g.view(np.uint32), w.view(np.uint32))
-
-
 @pytest.mark.gpu
 def test_device_wide_trees_equal_host(ctl, dev):
     """The trees ctl_scene_upload builds (read back, CTL_ARRAY_WIDE_BVH ...) are
@@ -174,7 +142,7 @@ def test_device_wide_trees_equal_host(ctl, dev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["c3_random", "c3_camera", "room_origin", "room_1e4", "room_far"])
-@pytest.mark.parametrize("bvh", ["wide", "w8", "binary"])
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
 def test_hits_independent_of_ray_order(ctl, orc, dev, case, bvh):
     """ctl_intersect on the same rays in their original order and under three
     random permutations: identical per-ray hits (a ray's result does not depend
@@ -193,8 +161,6 @@ def test_hits_independent_of_ray_order(ctl, orc, dev, case, bvh):
     pt = ctl.PathTracer(0)
     try:
         pt.upload_scene(d)
-        if bvh == "w8":
-            assert pt.w8_tree(d) is not None      # the upload did build the 8-wide tree
         base = gpu_hits(pt, rays, dev)
         base_any = gpu_hits(pt, rays, dev, any_hit=True)
         rng = np.random.default_rng(5)
@@ -240,17 +206,69 @@ def secondary_rays(desc, prim, hits, rng, n):
     return b, s
 
 
+def nee_shadow_rays(desc, prim, hits, rng, n):
+    """NEE-like shadow rays (ctl_ray: o, d, tmax = dist) from camera-ray hit
+    points to points drawn uniformly by area on the scene's light triangles
+    (ShapeSet::SamplePosition's distribution, fp64 inputs), as EstimateDirect
+    hands them to Occluded(Ray(p, d), 0, dist)."""
+    hit = np.nonzero(hits[:, 2] >= 0)[0]
+    sel = rng.choice(hit, size=min(n, hit.size), replace=False)
+    t = hits[sel, 0].view(np.float32)[:, None]
+    p = (prim[sel, 0:3] + t * prim[sel, 4:7]).astype(np.float32)
+    lt = [desc.light_tris[i] for i in range(desc.n_light_tris)]
+    P = np.array([[list(x.p[k]) for k in range(3)] for x in lt], np.float64)        # (L, 3, 3)
+    area = np.array([x.area for x in lt], np.float64)
+    k = rng.choice(len(lt), size=sel.size, p=area / area.sum())
+    u, v = rng.random(sel.size), rng.random(sel.size)
+    flip = u + v > 1
+    u[flip], v[flip] = 1 - u[flip], 1 - v[flip]
+    q = P[k, 0] + u[:, None] * (P[k, 1] - P[k, 0]) + v[:, None] * (P[k, 2] - P[k, 0])
+    w = q - p
+    dist = np.linalg.norm(w, axis=1)
+    s = np.zeros((sel.size, 8), np.float32)
+    s[:, 0:3] = p
+    s[:, 4:7] = w / dist[:, None]
+    s[:, 7] = dist
+    return s[dist > 1e-3]
+
+
+def pixel_distance(img, want):
+    a, b = img[:, :3].astype(np.float64), want[:, :3].astype(np.float64)
+    rel = np.abs(a - b) / np.maximum(np.abs(b), 1e-30)
+    rel[(a == b)] = 0.0
+    over = (rel > 1e-4).any(axis=1) | (img[:, 6] != want[:, 6])
+    return {"pixels": int(img.shape[0]), "pixels_over_1e-4_rel": int(over.sum()),
+            "pixels_differing": int((img.view(np.uint32) != want.view(np.uint32)).any(axis=1).sum()),
+            "max_rel": float(rel.max())}
+
+
+def build_stamp():
+    """Hashes of the library and of its sources (buildid.py), so a record can be
+    matched to the binary that produced it (bench.py reference_order_record)."""
+    import hashlib
+    import sys
+    sys.path.insert(0, ROOT)
+    from buildid import source_fingerprint
+    lib = os.path.join(ROOT, "cudatracerlib_amd", "_lib", "libctl_trace.so")
+    return {"lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(), "src_sha256": source_fingerprint(ROOT)}
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(1200)
 def test_full_size_c3_reference_order_distance(ctl, orc, dev):
-    """C3 at full size (10 M triangles, 1080p): one pass's camera rays plus a
-    million bounce-like and a million shadow-like rays from their hits, through
-    ctl_intersect (default 4-wide order): bit-exact to the oracle's statement of
-    that order, and classified against the reference's binary order.  Then one
-    full PathTracer pass (default kernel, any-hit shadow rays, whose boolean is
-    the reference's Occluded) against the oracle's reference-order render, per
-    pixel at 1e-4 relative.  The counts go to gpurun_out/reference_order.json
-    (bench.py reports the committed copy under profiles/)."""
+    """C3 at full size (10 M triangles, 1080p) against the reference's own CPU
+    path.  (1) One pass's camera rays plus a million bounce-like and a million
+    shadow-like rays from their hits, through ctl_intersect (default 4-wide
+    order): bit-exact to the oracle's statement of that order, classified
+    against the reference's binary order.  (2) A million NEE shadow rays to
+    points on the lights: the shipped any-hit query (ctl_occluded) against the
+    reference's closest-hit Occluded in its binary order (visibility flips).
+    (3) One full PathTracer pass of the shipped default (4-wide order, any-hit
+    shadow rays) against the oracle's render of the reference's CPU path
+    (binary order, closest-hit Occluded) and against the same order with
+    any-hit shadows, per pixel at 1e-4 relative.  The counts and the build's
+    hashes go to gpurun_out/reference_order.json (bench.py reports the
+    committed copy under profiles/)."""
     W, H = 1920, 1080
     hs = ctl.HostScene().generate(3, 1.0, W, H)
     d = hs.compile()
@@ -269,7 +287,13 @@ def test_full_size_c3_reference_order_distance(ctl, orc, dev):
         bounce, shadow = secondary_rays(d, prim, ph, rng, 1_000_000)
         bh = gpu_hits(pt, bounce, dev)
         sh = gpu_hits(pt, shadow, dev)
-        # one full pass, default schedule and order
+        nee = nee_shadow_rays(d, prim, ph, rng, 1_000_000)
+        nr = torch.from_numpy(nee).to(dev)
+        occ = torch.zeros(nee.shape[0], dtype=torch.int32, device=dev)
+        pt.occluded(nee.shape[0], nr.data_ptr(), occ.data_ptr(), True)
+        torch.cuda.synchronize()
+        nee_any = occ.cpu().numpy().astype(np.uint8)
+        # one full pass, default schedule, order and shadow query
         pt.params = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
         fb = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
         pt.reset_rays()
@@ -278,7 +302,7 @@ def test_full_size_c3_reference_order_distance(ctl, orc, dev):
         img, grays = fb.cpu().numpy(), pt.rays_traced()
     finally:
         pt.close()
-    out = {"scene": f"C3 {d.n_tri_data} tris, {W}x{H}", "classes": {}}
+    out = {"scene": f"C3 {d.n_tri_data} tris, {W}x{H}", "build": build_stamp(), "classes": {}}
     for name, r, g in (("camera", prim, ph), ("bounce", bounce, bh), ("shadow_closest", shadow, sh)):
         wide = oracle_intersect(orc, d, r, threads=16)
         bad = np.nonzero((wide != g).any(axis=1))[0]
@@ -287,21 +311,34 @@ def test_full_size_c3_reference_order_distance(ctl, orc, dev):
         out["classes"][name] = classify_orders(ref, g)
     tot = {k: sum(c[k] for c in out["classes"].values()) for k in next(iter(out["classes"].values()))}
     out["total"] = tot
-    # the pass, against the reference order's render of the same pass
-    want = np.zeros((W * H, 7), np.float32)
-    wrays = orc.oracle_render_pass(C.byref(d), C.byref(ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)), 0, oracle.ptr(want),
-                                   0, 16, 1, None)
-    a, b = img[:, :3].astype(np.float64), want[:, :3].astype(np.float64)
-    rel = np.abs(a - b) / np.maximum(np.abs(b), 1e-30)
-    rel[(a == b)] = 0.0
-    over = (rel > 1e-4).any(axis=1) | (img[:, 6] != want[:, 6])
-    out["pass"] = {"pixels": W * H, "pixels_over_1e-4_rel": int(over.sum()),
-                   "pixels_differing": int((img.view(np.uint32) != want.view(np.uint32)).any(axis=1).sum()),
-                   "rays_gpu": int(grays), "rays_reference_order": int(wrays)}
+    # NEE visibility: the shipped query against the reference's Occluded
+    tie = tie_rule(d, orc)
+
+    def occ_oracle(any_hit, order, cull=oracle.CULL_SLAB):
+        o = np.zeros(nee.shape[0], np.uint8)
+        orc.oracle_occluded(C.byref(d), nee.shape[0], oracle.ptr(nee), oracle.ptr(o), int(any_hit), order, cull, 16)
+        return o
+    assert np.array_equal(nee_any, occ_oracle(True, tie))           # ctl_occluded states the product's query
+    ref_occ = occ_oracle(False, 0)
+    out["nee_visibility"] = {"rays": int(nee.shape[0]), "reference_occluded": int(ref_occ.sum()),
+                             "visibility_flips": int((nee_any != ref_occ).sum()),
+                             "flips_round4_rule": int((occ_oracle(True, tie, oracle.CULL_AT_ACCEPT) != ref_occ).sum())}
+    # the pass, against the reference's CPU path and against the binary order with any-hit shadows
+    renders = {}
+    for key, any_hit in (("reference_cpu_path", 0), ("binary_order_any_hit", 1)):
+        want = np.zeros((W * H, 7), np.float32)
+        wr = orc.oracle_render_pass(C.byref(d), C.byref(ctl.PTParams(1, 50, 5, any_hit, 64, 1, 0, 0)), 0,
+                                    oracle.ptr(want), 0, 16, 1, None)
+        renders[key] = pixel_distance(img, want)
+        renders[key]["rays_reference"] = int(wr)
+    renders["rays_gpu"] = int(grays)
+    out["pass"] = renders
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "reference_order.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
     assert tot["hit_miss"] == 0 and tot["same_hit_other_fields"] == 0, out
     assert tot["differ"] <= MAX_DIFFER_FRAC * tot["rays"], out
-    assert out["pass"]["pixels_over_1e-4_rel"] <= MAX_PIXEL_OVER_FRAC * W * H, out
+    assert out["nee_visibility"]["visibility_flips"] <= MAX_DIFFER_FRAC * nee.shape[0], out
+    for key in ("reference_cpu_path", "binary_order_any_hit"):
+        assert renders[key]["pixels_over_1e-4_rel"] <= MAX_PIXEL_OVER_FRAC * W * H, out

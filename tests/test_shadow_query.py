@@ -1,25 +1,159 @@
-"""The NEE shadow query as any-hit gives the image of the reference's
-closest-hit `Occluded` (KernelDynamicScene.cu:70-80, PathTracer.cu:40-47).
+"""The NEE shadow test: the reference's closest-hit `Occluded` against the
+any-hit query the path kernels run (ctl_pt_params.shadow_any_hit = 1).
 
-Closest-hit: occluded iff the nearest hit t satisfies eps < t < dist - eps.
-Every triangle test accepts only t > eps (TraceHelper.cu:121 with tmin = eps),
-so the nearest hit exists below dist - eps exactly when some hit does, which is
-what the any-hit query with t_max = dist - eps answers.  The traversal culls a
-box only beyond the current t_max, so neither query can miss an accepted hit.
-Checked here on the oracle (the GPU suite checks each mode against it bit for
-bit): framebuffers of both modes are identical, so a drop-in user sets
-shadow_any_hit = 1 and gets the headline rate."""
+Reference (KernelDynamicScene.cu:70-80, called by EstimateDirect,
+TraceAlgorithms.cu:55): trace the closest hit (boxes culled at the current
+hit, nothing culled before the first), occluded iff eps < t < dist - eps.
+Product: any hit with eps < t < dist - eps, boxes culled at
+dist + slab_slack(ray) (device/traverse.h), slab_slack = 2^-20 max_a
+(|o_a| + M_a) |idir_a| with M_a bounding every box coordinate.  The two agree
+whenever the traversals test the same triangles below dist - eps.  The
+Aila-Laine slab `lo * idir - o * idir` cancels two products of size
+|o| |idir|: for rays nearly parallel to an axis far from the origin its error
+reaches tenths of a world unit while the Woop t stays accurate, so a box can
+round its entry past dist although a triangle inside it lies below dist - eps.
+The reference, which culls nothing before its first hit, tests such a box and
+reports the occluder; a query culled at dist - eps (round 4) or at dist skips
+it; slab_slack bounds that rounding (3 * 2^-24 (|lo| + |o|) |idir| per axis),
+so the product's query visits every box the reference can reach a hit in.
+Measured here, not argued: adversarial rooms of touching grid walls at the
+origin, 1e4 and 5e4 away, shadow rays from wall points to wall points (half of
+them to the wall they start on: grazing), and the same rays with dist moved so
+that dist - eps straddles the reference's hit within +-3 ulps.  Counts for the
+product's rule and the alternatives (round 4's cull at dist - eps, cull at
+dist, no cull) go to gpurun_out/shadow_query.json.  On the GPU, ctl_occluded is held to the oracle's
+statement of both forms bit for bit, and the full-size C3 test
+(test_reference_order.py) counts flips on realistic NEE rays."""
 import ctypes as C
+import json
+import os
 
 import numpy as np
 import pytest
 
 import oracle
-from helpers import oracle_render
+from helpers import grid_room, oracle_intersect, oracle_render, select_bvh, tie_rule
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OFFSETS = {"origin": (0.0, 0.0, 0.0), "1e4": (1.0e4, 1.0e4, 1.0e4), "far": (-3.0e4, 2.0e3, 5.0e4)}
+# Bound on the product's flips (rays whose any-hit answer differs from the
+# reference's closest-hit Occluded), fraction of the rays.  Measured: 0 on every
+# natural set, 0 / 3 / 3 of ~45 k boundary rays, the same as no culling at all
+# (those 3 are boxes the reference itself culls at its current hit); culled at
+# dist instead: 4-734-2599 natural, 8-3085-4730 boundary.
+MAX_FLIP_FRAC = 1e-4
+ROOMS = {}
+
+
+def room(ctl, key):
+    if key not in ROOMS:
+        ROOMS[key] = grid_room(ctl, OFFSETS[key])
+    return ROOMS[key][1]
+
+
+def occluded(orc, d, rays, any_hit, tie, cull=oracle.CULL_SLAB, threads=8):
+    out = np.zeros(rays.shape[0], np.uint8)
+    orc.oracle_occluded(C.byref(d), rays.shape[0], oracle.ptr(rays), oracle.ptr(out), 1 if any_hit else 0, tie, cull,
+                        threads)
+    return out
+
+
+def wall_shadow_rays(orc, d, off, n, seed, size=4.0):
+    """Shadow rays (ctl_ray: o, d, tmax = dist) from the hit points of rays
+    leaving the room's inside towards points on its walls; half of the targets
+    lie on the wall the ray starts from."""
+    rng = np.random.default_rng(seed)
+    o = np.array(off, np.float64)
+    r = np.zeros((n, 8), np.float32)
+    r[:, 0:3] = o + size * (0.2 + 0.6 * rng.random((n, 3)))
+    dd = rng.normal(size=(n, 3))
+    r[:, 4:7] = dd / np.linalg.norm(dd, axis=1, keepdims=True)
+    r[:, 3] = d.ray_eps
+    r[:, 7] = 3.0e38
+    h = oracle_intersect(orc, d, r, tie=0, threads=8)
+    ok = h[:, 2] >= 0
+    r, h = r[ok], h[ok]
+    P = (r[:, 0:3] + h[:, 0].view(np.float32)[:, None] * r[:, 4:7]).astype(np.float32)   # fp32 o + t d
+    m = P.shape[0]
+    rel = (P.astype(np.float64) - o) / size
+    pax = np.argmin(np.minimum(np.abs(rel), np.abs(1 - rel)), axis=1)        # the wall P lies on
+    pside = np.where(np.abs(rel[np.arange(m), pax]) < 0.5, 0.0, size)
+    same = rng.random(m) < 0.5
+    ax = np.where(same, pax, rng.integers(0, 3, m))
+    side = np.where(same, pside, np.where(rng.random(m) < 0.5, 0.0, size))
+    Q = o + size * rng.random((m, 3))
+    Q[np.arange(m), ax] = o[ax] + side
+    v = Q - P
+    dist = np.linalg.norm(v, axis=1)
+    s = np.zeros((m, 8), np.float32)
+    s[:, 0:3] = P
+    s[:, 4:7] = v / dist[:, None]
+    s[:, 7] = dist
+    return s[dist > 1e-3]
+
+
+def boundary_rays(orc, d, s, seed):
+    """The same rays with dist set so that dist - eps lies within +-3 ulps of
+    the reference's closest hit: the occluder sits right at the window's end."""
+    rng = np.random.default_rng(seed)
+    r = s.copy()
+    r[:, 3] = d.ray_eps
+    r[:, 7] = 3.0e38
+    h = oracle_intersect(orc, d, r, tie=0, threads=8)
+    ok = h[:, 2] >= 0
+    b = s[ok].copy()
+    dist = (h[ok, 0].view(np.float32) + np.float32(d.ray_eps)).astype(np.float32)
+    bits = dist.view(np.int32) + rng.integers(-3, 4, dist.size).astype(np.int32)   # positive floats: +-k ulps
+    b[:, 7] = bits.view(np.float32)
+    return b
+
+
+@pytest.mark.parametrize("key", list(OFFSETS))
+def test_any_hit_vs_closest_hit_occluded_rooms(ctl, key):
+    orc = oracle.load()
+    d = room(ctl, key)
+    tie_rule(d, orc)   # registers the 4-wide trees for the product's order
+    s = wall_shadow_rays(orc, d, OFFSETS[key], 60000, seed=1)
+    rec = {}
+    for kind, rays in (("natural", s), ("boundary", boundary_rays(orc, d, s, seed=2))):
+        ref = occluded(orc, d, rays, False, oracle.TIE_FIRST_FOUND)   # the reference CPU path
+        n = rays.shape[0]
+        prod = occluded(orc, d, rays, True, oracle.TRAVERSE_WIDE)   # shipped: 4-wide order, dist + slab_slack
+        r4 = occluded(orc, d, rays, True, oracle.TRAVERSE_WIDE, oracle.CULL_AT_ACCEPT)
+        at_dist = occluded(orc, d, rays, True, oracle.TRAVERSE_WIDE, oracle.CULL_AT_TMAX)
+        inf = occluded(orc, d, rays, True, oracle.TRAVERSE_WIDE, oracle.CULL_AT_INF)
+        binary = occluded(orc, d, rays, True, oracle.TIE_FIRST_FOUND)
+        closest_wide = occluded(orc, d, rays, False, oracle.TRAVERSE_WIDE)
+        c = {"rays": n, "reference_occluded": int(ref.sum()),
+             "flips": int((prod != ref).sum()),
+             "flips_query_misses_occluder": int(((ref == 1) & (prod == 0)).sum()),
+             "flips_binary_order": int((binary != ref).sum()),
+             "flips_round4_rule_cull_at_dist_minus_eps": int((r4 != ref).sum()),
+             "flips_cull_at_dist": int((at_dist != ref).sum()),
+             "flips_no_cull": int((inf != ref).sum()),
+             "flips_closest_hit_4wide_order": int((closest_wide != ref).sum())}
+        rec[kind] = c
+        # the slack only adds visits: never more flips than the tighter culls
+        assert c["flips"] <= c["flips_cull_at_dist"] <= c["flips_round4_rule_cull_at_dist_minus_eps"], c
+        assert c["flips"] <= MAX_FLIP_FRAC * n, (key, kind, c)
+        # no occluder the reference reports is culled away: what remains are boxes the
+        # reference's own closest-hit culling skipped (no culling at all gives the same)
+        assert c["flips_query_misses_occluder"] == 0, c
+        assert c["flips"] == c["flips_no_cull"], c
+        # the closest-hit form in the product's order differs only where culling does
+        assert c["flips_closest_hit_4wide_order"] <= max(2, 1e-4 * n), c
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    path = os.path.join(ROOT, "gpurun_out", "shadow_query.json")
+    allrec = json.load(open(path)) if os.path.exists(path) else {}
+    allrec[key] = rec
+    json.dump(allrec, open(path, "w"), indent=1)
 
 
 @pytest.mark.parametrize("config,scale,w,h", [(1, 1.0, 96, 64), (2, 0.02, 96, 64), (5, 0.002, 96, 64)])
-def test_any_hit_shadow_query_equals_closest_hit(ctl, config, scale, w, h):
+def test_any_hit_shadow_query_renders_like_closest_hit(ctl, config, scale, w, h):
+    """On the generated scenes (near the origin, no grazing walls far out) both
+    shadow forms give the same framebuffer bit for bit: an empirical check, the
+    rooms above show where they part."""
     orc = oracle.load()
     hs = ctl.HostScene().generate(config, scale, w, h)
     d = hs.compile(threads=4)
@@ -30,3 +164,58 @@ def test_any_hit_shadow_query_equals_closest_hit(ctl, config, scale, w, h):
         fbs.append(fb)
     assert fbs[0][:, 6].sum() > 0
     assert np.array_equal(fbs[0].view(np.uint32), fbs[1].view(np.uint32))
+
+
+def test_occluded_infinite_tmax(ctl):
+    """Occluded with tmax = inf (KernelDynamicScene.cu:77-78): a miss is not
+    occluded in either form; a hit is."""
+    orc = oracle.load()
+    d = room(ctl, "origin")
+    r = np.zeros((2, 8), np.float32)
+    r[:, 0:3] = np.array(OFFSETS["origin"]) + 2.0
+    r[0, 4:7] = (0.0, 0.0, 1.0)       # hits the far wall
+    r[1, 0:3] = (-50.0, -50.0, -50.0)
+    r[1, 4:7] = (0.0, 0.0, -1.0)      # leaves the scene
+    r[:, 7] = np.inf
+    for any_hit in (False, True):
+        for tie in (oracle.TIE_FIRST_FOUND, tie_rule(d, orc)):
+            assert list(occluded(orc, d, r, any_hit, tie)) == [1, 0]
+
+
+# ---------------------------------------------------------------------------
+# GPU: ctl_occluded is the oracle's statement of both forms, bit for bit
+# ---------------------------------------------------------------------------
+torch = pytest.importorskip("torch")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", list(OFFSETS))
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_gpu_occluded_equals_oracle(ctl, key, bvh):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    orc = oracle.load()
+    d = select_bvh(room(ctl, key), bvh)
+    tie = tie_rule(d, orc)
+    s = wall_shadow_rays(orc, d, OFFSETS[key], 60000, seed=3)
+    rays = np.concatenate([s, boundary_rays(orc, d, s, seed=4)])
+    rays[:100, 7] = np.inf
+    pt = ctl.PathTracer(0)
+    try:
+        pt.upload_scene(d)
+        r = torch.from_numpy(rays).cuda()
+        got = {}
+        for any_hit in (False, True):
+            out = torch.zeros(rays.shape[0], dtype=torch.int32, device="cuda")
+            pt.reset_rays()
+            pt.occluded(rays.shape[0], r.data_ptr(), out.data_ptr(), any_hit)
+            pt.sync()
+            assert pt.rays_traced() == rays.shape[0]
+            got[any_hit] = out.cpu().numpy().astype(np.uint8)
+    finally:
+        pt.close()
+    for any_hit in (False, True):
+        want = occluded(orc, d, rays, any_hit, tie)
+        bad = np.nonzero(want != got[any_hit])[0]
+        assert bad.size == 0, (any_hit, bad[:10], rays[bad[:3]])
+    assert 0.05 < got[False].mean() < 0.95

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Every rank's share of an N-GPU job (default 8), emulated on one GPU at the
-# driver's bench shape: profiles/r04_emulated_rank{r}_of_N.json.
+# driver's bench shape: profiles/rNN_emulated_rank{r}_of_N.json.
 set -o pipefail
 mkdir -p gpurun_out/emul
 export TMPDIR=/tmp

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 GPU check: the whole -m gpu suite (one process), smoke, then the
+# Round GPU check: the whole -m gpu suite (one process), smoke, then the
 # driver-shaped bench.  Every GPU step has its own time limit; the first
 # failure ends the call.
 set -o pipefail

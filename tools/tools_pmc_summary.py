@@ -13,8 +13,10 @@ profiles/rNN_pmc.json) for the roofline fractions of the same binary:
   cycles         GRBM_GUI_ACTIVE / 8 per launch (kernel cycles of one XCD)
 
 The path-kernel families also carry units_per_launch (render passes per
-profiled launch; tools_pmc.sh profiles one 8-pass ctl_render_passes launch), so
-bench.py scales the counters to whatever launch shape it times.
+profiled launch; tools_pmc.sh profiles one 8-pass ctl_render_passes launch),
+and primary_intersect its rays per launch (the profiled runs' bench lines,
+primary_rays.rays_per_launch), so bench.py scales the counters to whatever
+launch shape it times (a rank's 1/N image included).
 Usage: tools_pmc_summary.py <dir> [passes per profiled path-kernel launch]
 """
 import collections
@@ -32,8 +34,6 @@ FAMILIES = {
     "path_kernel": "path_kernel_persistent<false, true, 1, 0>",
     "path_kernel_full": "path_kernel_persistent<false, true, 1, 1>",
     "primary_intersect": "intersect_kernel<false, false, true, 1>",
-    "path_kernel_w8": "path_kernel_persistent<false, true, 2, 0>",
-    "primary_intersect_w8": "intersect_kernel<false, false, true, 2>",
     "prim_kernel": "prim_kernel<",
     "fold_samples": "fold_samples_kernel",
     "sampler": "sampler_kernel",
@@ -62,12 +62,24 @@ try:
                                               stderr=subprocess.DEVNULL).decode().strip()
 except Exception:
     out["git_head"] = None
+# rays per primary_intersect launch, from the bench lines of the profiled runs
+prim_rays = set()
+for f in glob.glob(os.path.join(root, "g*.json")):
+    for line in open(f):
+        if line.startswith("{"):
+            pr = (json.loads(line).get("primary_rays") or {}).get("rays_per_launch")
+            if pr:
+                prim_rays.add(int(pr))
+if len(prim_rays) > 1:
+    raise SystemExit(f"profiled runs disagree on primary rays per launch: {sorted(prim_rays)}")
 for fam, a in sorted(agg.items()):
     n = {c: max(1, len(d)) for c, d in disp[fam].items()}
     per = {c: v / n[c] for c, v in a.items()}
     k = {"launches": max(n.values()), "counters_per_launch": {c: round(v, 1) for c, v in sorted(per.items())}}
     if fam.startswith("path_kernel"):
         k["units_per_launch"] = PASSES
+    if fam == "primary_intersect" and prim_rays:
+        k["units_per_launch"] = prim_rays.pop()   # rays
     if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
         k["hbm_bytes"] = (2.0 * per["FETCH_SIZE"] + per["WRITE_SIZE"]) * 1024.0
     if "TCP_TCC_READ_REQ_sum" in per:
