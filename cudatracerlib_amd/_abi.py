@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CTL_LIB overrides the library path (variant builds for measurements).
+# CTL_LIB overrides the library path (the sanitizer build, tools/san_tests.sh).
 LIB_PATH = os.environ.get("CTL_LIB") or os.path.join(_HERE, "_lib", "libctl_trace.so")
 
 # CTL_ABI_VERSION of the include/ctl_trace.h these bindings mirror; load()

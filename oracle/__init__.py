@@ -9,7 +9,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(_HERE, "_build", "liboracle.so")
+# ORACLE_LIB: another build of the same sources (the sanitizer build, tools/san_tests.sh)
+LIB = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "_build", "liboracle.so")
 _lib = None
 
 TIE_FIRST_FOUND = 0   # the reference's binary visit order (the reference semantics)

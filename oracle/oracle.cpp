@@ -225,20 +225,25 @@ float slab_slack(V3 o, V3 d, const float m[3]) {
     return (e > ez ? e : ez) * powf(2.0f, -20.0f);
 }
 
-// The cull distance of an any-hit query's BVH level whose ray is (o, d); mode < 0:
-// none beyond the acceptance bound (a plain any-hit query).
+// The cull distance of an any-hit query's BVH level whose ray is (o, d), at
+// least its acceptance bound; mode < 0 (every closest-hit query, a plain
+// any-hit query): the acceptance bound itself, i.e. the current hit.
 struct AnyCull {
     int mode = -1;
     float dist = 0.0f;
     float m[3] = {0.0f, 0.0f, 0.0f};
     float at(V3 o, V3 d, float accept) const {
+        float c = accept;
         switch (mode) {
-            case CULL_AT_TMAX: return dist;
-            case CULL_AT_INF: return INFINITY;
-            case CULL_SLAB: return dist + slab_slack(o, d, m);
-            default: return accept;
+            case CULL_AT_TMAX: c = dist; break;
+            case CULL_AT_INF: c = INFINITY; break;
+            case CULL_SLAB: c = dist + slab_slack(o, d, m); break;
+            default: break;
         }
+        return c > accept ? c : accept;
     }
+    // traceray_template's cullFloor: 0 (none) unless this is a shadow query
+    float floor(V3 o, V3 d, float accept) const { return mode < 0 ? 0.0f : at(o, d, accept); }
 };
 
 bool trace_two_level_wide(const SceneView& S, V3 ori, V3 dir, float spanTmin, float triTmin, Hit& h, bool anyHit,
@@ -296,10 +301,10 @@ bool trace_two_level(const SceneView& S, V3 ori, V3 dir, float spanTmin, float t
             return found;
         };
         return traceray_template(ol, dl, h.t, spanTmin, triClb, meshNodes, (int)mesh.bvh_node_offset, 0, st,
-                                 ac.at(ol, dl, h.t));
+                                 ac.floor(ol, dl, h.t));
     };
     return traceray_template(ori, dir, h.t, spanTmin, instClb, sceneNodes, 0, d->scene_start_node, st,
-                             ac.at(ori, dir, h.t));
+                             ac.floor(ori, dir, h.t));
 }
 
 // ---------------------------------------------------------------------------

@@ -1,7 +1,10 @@
 """Regression fixtures of the oracle itself: SHA-256 digests of small oracle
 renders (C1 PrimTracer first_f, C2 PathTracer Direct 1 / 0, WavefrontPathTracer),
 each in the reference's binary visit order (mode 0) and in the product's 4-wide
-per-ray order (mode 2, tests/helpers.py tie_rule).  These are NOT reference outputs (the reference
+per-ray order (mode 2, tests/helpers.py tie_rule); the node / triangle visits
+of a closest-hit and an any-hit batch in each order (culling changes them even
+where the hits stay the same); and the occlusion answers of a shadow-ray set
+for each shadow form and cull rule (oracle_occluded).  These are NOT reference outputs (the reference
 ships none and cannot be built here): they pin the restatement
 against unintended changes, and the GPU parity tests pin the HIP path to it.
 
@@ -47,6 +50,30 @@ def compute():
             r2 = sum(orc.oracle_render_pass(C.byref(d2), C.byref(pp), k, oracle.ptr(fb2), mode(d2), 4, 1, None)
                      for k in range(2))
             out[f"c2_path_direct{direct}_64x48x2" + name] = {"fb": digest(fb2), "rays": int(r2)}
+        rays = np.zeros((4096, 8), np.float32)
+        rng = np.random.default_rng(7)
+        lo, hi = np.array(d2.box_min[:]), np.array(d2.box_max[:])
+        rays[:, 0:3] = lo + (hi - lo) * rng.random((4096, 3))
+        dd = rng.normal(size=(4096, 3))
+        rays[:, 4:7] = dd / np.linalg.norm(dd, axis=1, keepdims=True)
+        rays[:, 3] = d2.ray_eps
+        rays[:, 7] = np.linalg.norm(hi - lo) * rng.random(4096)
+        vis = {}
+        for bmode, label in ((1, "closest"), (2, "any")):
+            t = np.zeros(4096, np.float32)
+            u = np.zeros(4096, np.uint32)
+            st = np.zeros(4, np.uint64)
+            orc.oracle_trace(C.byref(d2), 4096, oracle.ptr(rays), bmode, mode(d2), oracle.ptr(t), oracle.ptr(t),
+                             oracle.ptr(t), oracle.ptr(u), oracle.ptr(u), oracle.ptr(st), 4)
+            vis[label] = [int(x) for x in st]
+        out["c2_batch_visits" + name] = vis
+        occ = {}
+        for any_hit, cull, label in ((0, 0, "closest"), (1, oracle.CULL_SLAB, "any_slab"),
+                                     (1, oracle.CULL_AT_ACCEPT, "any_accept")):
+            o = np.zeros(4096, np.uint8)
+            orc.oracle_occluded(C.byref(d2), 4096, oracle.ptr(rays), oracle.ptr(o), any_hit, mode(d2), cull, 4)
+            occ[label] = digest(o)
+        out["c2_occluded" + name] = occ
         fbw = np.zeros((64 * 48, 7), np.float32)
         rw = orc.oracle_wpt_render_pass(C.byref(d2), 1, 50, 5, 1, 1, oracle.ptr(fbw), mode(d2), 4)
         out["c2_wpt_direct1_64x48" + name] = {"fb": digest(fbw), "rays": int(rw)}
