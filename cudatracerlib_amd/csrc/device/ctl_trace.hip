@@ -465,7 +465,8 @@ template <bool ANY, bool STATS, bool SINGLE, int WIDE>
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            int64_t n2, const ctl_ray* rays2, ctl_hit* hits2,
                                                            unsigned long long* cursor, unsigned long long* counters,
-                                                           const uint32_t* dcount, uint32_t band_w) {
+                                                           const uint32_t* dcount, uint32_t band_w,
+                                                           const uint32_t* order) {
     const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
     // dcount: the two segment sizes read from device memory (the WavefrontPathTracer's
     // queue counts, written by the previous bounce's scan: no host round trip); the
@@ -480,8 +481,8 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64
     TraceStats ts{0, 0, 0};
     Traverser<ANY ? 1 : 0, STATS, SINGLE, WIDE> T;
     T.done = true;
-    bool haveRay = false, exhausted = false, ovf = false;
-    int64_t ray = 0;
+    bool haveRay = false, exhausted = false, ovf = false, seg2 = false;
+    int64_t ray = 0;   // slot in its segment
     const int lane = threadIdx.x & 63;
     while (true) {
         if (haveRay && T.done) {
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64
                 uint16_t xd = (uint16_t)(T.h.u * 65535), yd = (uint16_t)(T.h.v * 65535);
                 res.w = ((uint32_t)yd << 16) | (uint32_t)xd;
             }
-            reinterpret_cast<uint4*>(ray < n ? hits + ray : hits2 + (ray - n))[0] = res;
+            reinterpret_cast<uint4*>(seg2 ? hits2 + ray : hits + ray)[0] = res;
             ovf |= st.overflow;
             haveRay = false;
         }
@@ -515,9 +516,16 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64
                         const int64_t bh = h - 8 * band < 8 ? h - 8 * band : 8, r = k - band * bw;
                         k = (8 * band + r % bh) * band_w + r / bh;
                     }
-                    ray = k;
+                    if (order) {   // ctl_set_ray_order: the k-th slot in key order (raysort.hip)
+                        const uint32_t v = order[k];
+                        seg2 = (v >> 31) != 0;
+                        ray = v & 0x7fffffffu;
+                    } else {
+                        seg2 = k >= n;
+                        ray = seg2 ? k - n : k;
+                    }
                     haveRay = true;
-                    const float4* r4 = reinterpret_cast<const float4*>(k < n ? rays + k : rays2 + (k - n));
+                    const float4* r4 = reinterpret_cast<const float4*>(seg2 ? rays2 + ray : rays + ray);
                     const float4 o = r4[0], d = r4[1];
                     T.init(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), o.w, o.w, d.w, st, &ts);
                 } else {
@@ -676,6 +684,7 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
     ctl::wavefront_free(c);
     ctl::wpt_free(c);
     ctl::anim_free(c);
+    ctl::raysort_free(c);
     if (c->d_mt1) (void)hipFree(c->d_mt1);
     if (c->d_mt2) (void)hipFree(c->d_mt2);
     if (c->d_slices) (void)hipFree(c->d_slices);
@@ -748,6 +757,14 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
     CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
     const bool single = c->scene.single != 0;
     const uint64_t want = ((uint64_t)(n + n2) + kBlock - 1) / kBlock;
+    // ctl_set_ray_order: visit the rays in key order (not a coherent camera image
+    // traced in 8 x 8 blocks, not the counting launches of the roofline)
+    const uint32_t* order = nullptr;
+    if (c->ray_order && !stats && !band_w) {
+        const int r = ctl::sort_rays(c, (uint32_t)n, rays, (uint32_t)n2, rays2, dcount, s);
+        if (r != CTL_OK) return (ctl_status)r;
+        order = c->rs_order;
+    }
 #ifndef CTL_INTERSECT_BPC
 #define CTL_INTERSECT_BPC 3   // resident blocks per CU of the batch traversal (0: occupancy limit)
 #endif
@@ -757,7 +774,7 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
         if (CTL_INTERSECT_BPC > 0) nb = std::min(nb, CTL_INTERSECT_BPC * c->cu_count);                          \
         hipLaunchKernelGGL((intersect_kernel<AN, ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)),     \
                            dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, n2, rays2, hits2, cursor,  \
-                           c->d_counters, dcount, band_w);                                                       \
+                           c->d_counters, dcount, band_w, order);                                                \
     } while (0)
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;
