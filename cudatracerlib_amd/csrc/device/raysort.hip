@@ -10,10 +10,13 @@
 // writes every hit to its own slot, so the results are the caller-order
 // results byte for byte (a ray's hit is a function of the ray alone).
 //
-// Keys: 31 bits, bit 31 clear (slots past the device-side segment counts get
-// 0xFFFFFFFF and sort last).  Mode 1: octant in bits 28-30, a 28-bit origin
-// Morton code below it (9-10 bits per axis); mode 2: the Morton code on top, the
-// octant in the 3 low bits.  Only the top `bits` bits take part in the sort.
+// Keys: the top `bits` bits of a 31-bit key, shifted down (slots past the
+// device-side segment counts get 2^bits and sort last).  Mode 1: octant in bits
+// 28-30 of the 31-bit key, a 28-bit origin Morton code below it (9-10 bits per
+// axis); mode 2: the Morton code on top, the octant in the 3 low bits.  The sort
+// covers bits [0, bits + 1): rocPRIM 7.2's radix sort returns no permutation
+// for inputs of at most 2^20 elements when begin_bit > 0
+// (probes/rocprim_sort_check.hip, profiles/r05_rocprim_sort_check.txt).
 // Order entries name slots: segment 1 slot i -> i, segment 2 slot j -> 2^31 | j.
 #include <hip/hip_runtime.h>
 
@@ -36,7 +39,7 @@ __device__ __forceinline__ uint32_t spread3(uint32_t x) {   // 10 bits -> every 
 
 __global__ __launch_bounds__(256) void ray_key_kernel(const ctl_ray* rays, uint32_t n, const ctl_ray* rays2, uint32_t n2,
                                                       const uint32_t* dcount, float3 lo, float3 scale, int mode,
-                                                      uint32_t* keys, uint32_t* vals) {
+                                                      uint32_t bits, uint32_t* keys, uint32_t* vals) {
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     if (k >= n + n2) return;
     const bool second = k >= n;
@@ -44,7 +47,7 @@ __global__ __launch_bounds__(256) void ray_key_kernel(const ctl_ray* rays, uint3
     const uint32_t live = dcount ? dcount[second ? 1 : 0] : (second ? n2 : n);
     vals[k] = second ? (0x80000000u | j) : j;
     if (j >= live) {
-        keys[k] = 0xffffffffu;
+        keys[k] = 1u << bits;
         return;
     }
     const float4* r4 = reinterpret_cast<const float4*>((second ? rays2 : rays) + j);
@@ -57,7 +60,8 @@ __global__ __launch_bounds__(256) void ray_key_kernel(const ctl_ray* rays, uint3
     const uint32_t m = spread3(q(o.x, lo.x, scale.x)) | (spread3(q(o.y, lo.y, scale.y)) << 1) |
                        (spread3(q(o.z, lo.z, scale.z)) << 2);   // 30 bits
     const uint32_t m28 = m >> 2;
-    keys[k] = mode == 2 ? ((m28 << 3) | oct) : ((oct << 28) | m28);
+    const uint32_t key31 = mode == 2 ? ((m28 << 3) | oct) : ((oct << 28) | m28);
+    keys[k] = key31 >> (31u - bits);
 }
 
 }  // namespace
@@ -86,29 +90,40 @@ int sort_rays(ctl_ctx* c, uint32_t n, const ctl_ray* rays, uint32_t n2, const ct
             c->err = "ray order: buffer allocation failed";
             return CTL_ERR_NOMEM;
         }
-        size_t tb = 0;
-        if (rocprim::radix_sort_pairs(nullptr, tb, c->rs_keys[0], c->rs_keys[1], c->rs_vals, c->rs_order,
-                                      (uint32_t)cap, 0u, 32u, s) != hipSuccess ||
-            hipMalloc(&c->rs_temp, tb) != hipSuccess) {
-            raysort_free(c);
+        c->rs_cap = (uint32_t)cap;
+    }
+    // the sort's temporary storage is laid out for the exact element count and
+    // bit range (one queried for another size sorts wrongly: probes/rocprim_sort_check.hip)
+    const uint32_t bits = (uint32_t)std::min(31, std::max(1, c->ray_order_bits));
+    size_t need = 0;
+    if (rocprim::radix_sort_pairs(nullptr, need, c->rs_keys[0], c->rs_keys[1], c->rs_vals, c->rs_order, total, 0u,
+                                  bits + 1u, s) != hipSuccess) {
+        c->err = "ray order: sort storage query failed";
+        return CTL_ERR_HIP;
+    }
+    if (need > c->rs_temp_bytes) {
+        if (c->rs_temp && (hipStreamSynchronize(s) != hipSuccess || hipFree(c->rs_temp) != hipSuccess)) {
+            c->err = "ray order: sort storage release failed";
+            return CTL_ERR_HIP;
+        }
+        c->rs_temp = nullptr;
+        c->rs_temp_bytes = 0;
+        if (hipMalloc(&c->rs_temp, need) != hipSuccess) {
             c->err = "ray order: sort storage allocation failed";
             return CTL_ERR_NOMEM;
         }
-        c->rs_temp_bytes = tb;
-        c->rs_cap = (uint32_t)cap;
+        c->rs_temp_bytes = need;
     }
     const float* b = c->scene_box;
     auto inv = [](float l, float h) { return h > l ? 1024.0f / (h - l) : 0.0f; };
     const float3 lo = make_float3(b[0], b[1], b[2]);
     const float3 sc = make_float3(inv(b[0], b[3]), inv(b[1], b[4]), inv(b[2], b[5]));
     hipLaunchKernelGGL(ray_key_kernel, dim3((total + 255) / 256), dim3(256), 0, s, rays, n, rays2, n2, dcount, lo, sc,
-                       c->ray_order, c->rs_keys[0], c->rs_vals);
+                       c->ray_order, bits, c->rs_keys[0], c->rs_vals);
     if (hipGetLastError() != hipSuccess) { c->err = "ray order: key launch failed"; return CTL_ERR_HIP; }
-    // the top `bits` key bits (bit 31 included: it orders the empty slots last)
-    const unsigned begin = 32u - (unsigned)std::min(32, std::max(1, c->ray_order_bits + 1));
-    size_t tb = c->rs_temp_bytes;
-    if (rocprim::radix_sort_pairs(c->rs_temp, tb, c->rs_keys[0], c->rs_keys[1], c->rs_vals, c->rs_order, total,
-                                  begin, 32u, s) != hipSuccess) {
+    // the key bits and the empty-slot bit above them
+    if (rocprim::radix_sort_pairs(c->rs_temp, need, c->rs_keys[0], c->rs_keys[1], c->rs_vals, c->rs_order, total,
+                                  0u, bits + 1u, s) != hipSuccess) {
         c->err = "ray order: radix sort failed";
         return CTL_ERR_HIP;
     }

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--wpt-passes", type=int, default=3)
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--variants", default="0:16,1:12,1:16,1:24,2:12,2:16,2:24", help="mode:bits,...")
+    ap.add_argument("--no-wpt", action="store_true")
     a = ap.parse_args()
     import torch
     import cudatracerlib_amd as ctl
@@ -33,7 +35,8 @@ def main():
     dev = torch.device("cuda:0")
     W, H = 1920, 1080
     t0 = time.time()
-    d = ctl.HostScene().generate(3, a.scale, W, H).compile(threads=int(os.environ.get("OMP_NUM_THREADS", "8")))
+    hs = ctl.HostScene().generate(3, a.scale, W, H)   # owns the desc's arrays: keep it alive
+    d = hs.compile(threads=int(os.environ.get("OMP_NUM_THREADS", "8")))
     print(f"scene {d.n_tri_data} tris in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     pt = ctl.PathTracer(0)
     pt.upload_scene(d)
@@ -51,7 +54,7 @@ def main():
     rng = np.random.default_rng(2024)
     bounce, shadow = secondary_rays(d, prim, ph, rng, 1_000_000)
     nee = nee_shadow_rays(d, prim, ph, rng, 1_000_000)
-    variants = [(0, 16), (1, 12), (1, 16), (1, 24), (2, 12), (2, 16), (2, 24)]
+    variants = [tuple(int(x) for x in v.split(":")) for v in a.variants.split(",")]
     out = {"scene": f"C3 {d.n_tri_data} tris", "launches": a.launches, "batches": {}}
     stream = torch.cuda.current_stream()
     for name, r, any_hit in (("camera", prim, False), ("bounce", bounce, False), ("shadow_segment_closest", shadow, False),
@@ -90,7 +93,7 @@ def main():
     import ctypes as C
     L = ctl.lib()
     wres, img0 = {}, None
-    for mode, bits in variants:
+    for mode, bits in ([] if a.no_wpt else variants):
         pt.set_ray_order(mode, bits)
         fb = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
         ms, rs = [], []
