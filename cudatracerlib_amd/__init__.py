@@ -335,10 +335,6 @@ class Tracer:
         _check(self._L.ctl_intersect(self._ctx, int(n), rays_ptr, hits_ptr, 1 if any_hit else 0, stream),
                self._ctx, "ctl_intersect")
 
-    def set_ray_order(self, mode, key_bits=16):
-        """Batch traversal visit order (ctl_set_ray_order): 0 caller's, 1 / 2 sorted."""
-        _check(self._L.ctl_set_ray_order(self._ctx, int(mode), int(key_bits)), self._ctx, "ctl_set_ray_order")
-
     def occluded(self, n, rays_ptr, out_ptr, any_hit=False, stream=0):
         """KernelDynamicScene::Occluded(ray, 0, ray.tmax) per ray into uint32 out
         (ctl_occluded): the reference's closest-hit form or the any-hit query."""

@@ -211,7 +211,6 @@ SYMBOLS = [
     ("ctl_sampler_upload", C.c_int32, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
     ("ctl_intersect", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, _vp]),
     ("ctl_occluded", C.c_int32, [_vp, C.c_int64, _vp, _vp, C.c_int32, _vp]),
-    ("ctl_set_ray_order", C.c_int32, [_vp, C.c_int32, C.c_int32]),
     ("ctl_render_pass", C.c_int32, [_vp, C.POINTER(PTParams), _vp, _vp]),
     ("ctl_render_passes", C.c_int32, [_vp, C.POINTER(PTParams), C.c_uint64, C.c_uint32, _vp, _vp]),
     ("ctl_wpt_render_pass", C.c_int32, [_vp, C.POINTER(WptParams), _vp, _vp]),

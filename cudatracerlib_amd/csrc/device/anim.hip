@@ -546,7 +546,6 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         }
         S.ray_eps = A->h_eps[6];
         for (int k = 0; k < 3; k++) S.cull_m[k] = A->h_eps[7 + k];
-        for (int k = 0; k < 6; k++) c->scene_box[k] = A->h_eps[k];
         c->device_eps = true;
     }
     c->device_edited = true;
@@ -599,7 +598,6 @@ CTL_API ctl_status ctl_scene_set_transform(ctl_ctx* c, uint32_t node, const ctl_
     }
     S.ray_eps = A->h_eps[6];
     for (int k = 0; k < 3; k++) S.cull_m[k] = A->h_eps[7 + k];
-    for (int k = 0; k < 6; k++) c->scene_box[k] = A->h_eps[k];
     c->device_eps = true;
     c->device_edited = true;
     return CTL_OK;

@@ -627,15 +627,6 @@ struct ctl_ctx {
     ctl::AnimState* anim = nullptr;             // animated meshes, refit plans (anim.hip)
     uint64_t n_tri_data = 0, n_woop = 0, n_bvh_nodes = 0, n_scene_bvh = 0;   // uploaded array lengths
     int cu_count = 256;
-    float scene_box[6] = {0, 0, 0, 0, 0, 0};    // world box (desc, or derived by set_transform / animate)
-    // batch traversal visit order (ctl_set_ray_order, raysort.hip): 0 = the caller's
-    int32_t ray_order = 0, ray_order_bits = 16;
-    uint32_t* rs_keys[2] = {nullptr, nullptr};
-    uint32_t* rs_vals = nullptr;
-    uint32_t* rs_order = nullptr;               // sorted slots of the last sort_rays
-    void* rs_temp = nullptr;
-    size_t rs_temp_bytes = 0;
-    uint32_t rs_cap = 0;
 };
 
 namespace ctl {
@@ -665,10 +656,6 @@ struct WideNode;
 int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>& wn, const std::vector<uint32_t>& wbase,
                const std::vector<WideNode>& sw, const std::vector<uint32_t>& wsrc, const std::vector<uint32_t>& ssrc);
 void anim_free(ctl_ctx* c);
-// raysort.hip
-int sort_rays(ctl_ctx* c, uint32_t n, const ctl_ray* rays, uint32_t n2, const ctl_ray* rays2, const uint32_t* dcount,
-              hipStream_t s);
-void raysort_free(ctl_ctx* c);
 // wpt.hip
 int wpt_pass(ctl_ctx* c, const ctl_wpt_params* p, ctl_pixel* fb, hipStream_t s);
 void wpt_free(ctl_ctx* c);

@@ -465,8 +465,7 @@ template <bool ANY, bool STATS, bool SINGLE, int WIDE>
 __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64_t n, const ctl_ray* rays, ctl_hit* hits,
                                                            int64_t n2, const ctl_ray* rays2, ctl_hit* hits2,
                                                            unsigned long long* cursor, unsigned long long* counters,
-                                                           const uint32_t* dcount, uint32_t band_w,
-                                                           const uint32_t* order) {
+                                                           const uint32_t* dcount, uint32_t band_w) {
     const DevScene& S = kernarg_ref<DevScene>(S_arg, 0);   // read in place (common.h kernarg_ref)
     // dcount: the two segment sizes read from device memory (the WavefrontPathTracer's
     // queue counts, written by the previous bounce's scan: no host round trip); the
@@ -516,14 +515,8 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64
                         const int64_t bh = h - 8 * band < 8 ? h - 8 * band : 8, r = k - band * bw;
                         k = (8 * band + r % bh) * band_w + r / bh;
                     }
-                    if (order) {   // ctl_set_ray_order: the k-th slot in key order (raysort.hip)
-                        const uint32_t v = order[k];
-                        seg2 = (v >> 31) != 0;
-                        ray = v & 0x7fffffffu;
-                    } else {
-                        seg2 = k >= n;
-                        ray = seg2 ? k - n : k;
-                    }
+                    seg2 = k >= n;
+                    ray = seg2 ? k - n : k;
                     haveRay = true;
                     const float4* r4 = reinterpret_cast<const float4*>(seg2 ? rays2 + ray : rays + ray);
                     const float4 o = r4[0], d = r4[1];
@@ -684,7 +677,6 @@ CTL_API void ctl_destroy(ctl_ctx* c) {
     ctl::wavefront_free(c);
     ctl::wpt_free(c);
     ctl::anim_free(c);
-    ctl::raysort_free(c);
     if (c->d_mt1) (void)hipFree(c->d_mt1);
     if (c->d_mt2) (void)hipFree(c->d_mt2);
     if (c->d_slices) (void)hipFree(c->d_slices);
@@ -757,14 +749,6 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
     CTL_HIP(c, hipMemsetAsync(cursor, 0, sizeof(unsigned long long), s));
     const bool single = c->scene.single != 0;
     const uint64_t want = ((uint64_t)(n + n2) + kBlock - 1) / kBlock;
-    // ctl_set_ray_order: visit the rays in key order (not a coherent camera image
-    // traced in 8 x 8 blocks, not the counting launches of the roofline)
-    const uint32_t* order = nullptr;
-    if (c->ray_order && !stats && !band_w) {
-        const int r = ctl::sort_rays(c, (uint32_t)n, rays, (uint32_t)n2, rays2, dcount, s);
-        if (r != CTL_OK) return (ctl_status)r;
-        order = c->rs_order;
-    }
 #ifndef CTL_INTERSECT_BPC
 #define CTL_INTERSECT_BPC 3   // resident blocks per CU of the batch traversal (0: occupancy limit)
 #endif
@@ -774,7 +758,7 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
         if (CTL_INTERSECT_BPC > 0) nb = std::min(nb, CTL_INTERSECT_BPC * c->cu_count);                          \
         hipLaunchKernelGGL((intersect_kernel<AN, ST, SG, WD>), dim3((unsigned)std::min<uint64_t>(nb, want)),     \
                            dim3(kBlock), kStackLdsBytes, s, c->scene, n, rays, hits, n2, rays2, hits2, cursor,  \
-                           c->d_counters, dcount, band_w, order);                                                \
+                           c->d_counters, dcount, band_w);                                                       \
     } while (0)
     // stats launches count the reference's binary traversal (the roofline's algorithmic bytes)
     const bool wide = c->scene.wide != 0 && !stats;

@@ -207,7 +207,6 @@ void set_constants(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty) {
     if (!c->device_eps || (dirty & CTL_DIRTY_NODES)) {
         S.ray_eps = d->ray_eps;
         cull_bound(d->box_min, d->box_max, d->mesh_boxes, d->n_meshes, S.cull_m);
-        for (int k = 0; k < 3; k++) { c->scene_box[k] = d->box_min[k]; c->scene_box[3 + k] = d->box_max[k]; }
         c->device_eps = false;
     }
     for (int i = 0; i < CTL_MAX_NUM_LIGHTS; i++) S.light_cdf[i] = d->light_cdf[i];

@@ -459,17 +459,6 @@ CTL_API ctl_status ctl_intersect(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays,
 CTL_API ctl_status ctl_occluded(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays, uint32_t* d_out, int32_t any_hit,
                                 void* stream);
 
-/* Visit order of the batch traversal (ctl_intersect and the
- * WavefrontPathTracer's per-bounce batches): mode 0 (default) fetches rays in
- * the caller's order, as intersectKernel (TraceHelper.cu:379-399); mode 1 / 2
- * first radix-sorts the launch's rays by a key of (direction octant, Morton
- * code of the origin in the scene box) -- octant major / origin major -- over
- * its top key_bits bits, and fetches them in key order.  Hits are written to
- * the caller's slots and are byte-identical in every mode (a ray's hit does
- * not depend on the rays around it); only the traversal's memory coherence and
- * the sort's cost change (csrc/device/raysort.hip). */
-CTL_API ctl_status ctl_set_ray_order(ctl_ctx* ctx, int32_t mode, int32_t key_bits);
-
 /* One progressive PathTracer pass (one sample per owned pixel) accumulated
  * into the caller's device framebuffer d_fb[width*height] (PixelData,
  * Engine/Image.cu:22-44).  Uses the tables from the last ctl_sampler_generate /

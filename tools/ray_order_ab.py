@@ -1,4 +1,4 @@
-"""A/B of the batch traversal's visit order (ctl_set_ray_order, raysort.hip) on
+"""A/B of the batch traversal's visit order (ctl_set_ray_order: probes/ray_order_experiment.patch applied) on
 C3 at full size: camera rays of a pass, a million bounce-like rays, a million
 shadow-segment rays and a million NEE shadow rays from their hits (the rays of
 tests/test_reference_order.py), each batch through ctl_intersect in the
