@@ -128,9 +128,13 @@ CTL_API ctl_status ctl_fb_reduce(ctl_ctx* c, void* comm, const ctl_pixel* d_fb, 
     if (!c || !comm || (!d_fb && n_pixels)) return CTL_ERR_INVALID;
     if (d_out && d_out == d_fb) { c->err = "fb_reduce: d_out must not alias d_fb"; return CTL_ERR_INVALID; }
     if (!have_rccl(c)) return CTL_ERR_NODEVICE;
-    if (!d_out && n_pixels) {   // the root needs a receive buffer (RCCL would get a null recvbuff)
+    if (!d_out && n_pixels) {
+        // the root needs a receive buffer (RCCL would get a null recvbuff); a NULL
+        // d_out is refused only where this rank is known to be the root: refusing it
+        // on a rank whose number cannot be read would leave the other ranks waiting
+        // in the collective
         int me = -1;
-        if (!rccl().user_rank || rccl().user_rank(reinterpret_cast<ncclComm_t>(comm), &me) != ncclSuccess || me == root) {
+        if (rccl().user_rank && rccl().user_rank(reinterpret_cast<ncclComm_t>(comm), &me) == ncclSuccess && me == root) {
             c->err = "fb_reduce: d_out is required on the root rank";
             return CTL_ERR_INVALID;
         }

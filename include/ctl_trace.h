@@ -514,8 +514,10 @@ CTL_API ctl_status ctl_comm_destroy(void* comm);
  * root (ncclReduce, fp32 sum).  d_fb is only read: each rank keeps
  * accumulating its own pixels into it, so the reduce may run after any step and
  * any number of times (d_out then holds the image of all passes so far; it must
- * not alias d_fb; it is required on the root (CTL_ERR_INVALID when NULL there)
- * and ignored on the other ranks).  Every rank calls it with
+ * not alias d_fb; it is required on the root and ignored on the other ranks: a
+ * NULL d_out is CTL_ERR_INVALID where the rank reads as the root through
+ * ncclCommUserRank, and passed to RCCL otherwise, so a rank whose number cannot
+ * be read never drops out of the collective).  Every rank calls it with
  * its own ctx and stream; asynchronous on `stream`.  RCCL is loaded on first
  * use (CTL_ERR_NODEVICE when it cannot be). */
 CTL_API ctl_status ctl_fb_reduce(ctl_ctx* ctx, void* comm, const ctl_pixel* d_fb, ctl_pixel* d_out,

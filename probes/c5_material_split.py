@@ -1,6 +1,7 @@
 """C5 shading cost by material class: the C5 scene (HostScene.generate(5)) with its
 rough-dielectric and / or textured materials swapped for constant diffuse ones of
-the same reflectance, 4 passes per ctl_render_passes launch each."""
+the same reflectance, 4 passes per ctl_render_passes launch each.  C5SPLIT_ONLY
+(';'-separated case names) runs a subset, e.g. under rocprofv3 --pmc."""
 import ctypes as C
 import os
 import sys
@@ -53,10 +54,14 @@ def with_unused_textured(mats):
     return (ctl.Material * (n + 1))(*out)
 
 
-for name, kr, kt, flt in (("C5", 1, 1, None), ("rough only", 1, 0, None), ("textures only", 0, 1, None),
-                          ("tex trilinear", 0, 1, ctl._abi.CTL_TEX_TRILINEAR), ("tex EWA", 0, 1, ctl._abi.CTL_TEX_EWA),
-                          ("tex bilinear", 0, 1, ctl._abi.CTL_TEX_BILINEAR), ("neither", 0, 0, None),
-                          ("neither, full", 0, 0, "full")):
+CASES = (("C5", 1, 1, None), ("rough only", 1, 0, None), ("textures only", 0, 1, None),
+         ("tex trilinear", 0, 1, ctl._abi.CTL_TEX_TRILINEAR), ("tex EWA", 0, 1, ctl._abi.CTL_TEX_EWA),
+         ("tex bilinear", 0, 1, ctl._abi.CTL_TEX_BILINEAR), ("neither", 0, 0, None),
+         ("neither, full", 0, 0, "full"))
+only = [x for x in os.environ.get("C5SPLIT_ONLY", "").split(";") if x]
+for name, kr, kt, flt in CASES:
+    if only and name not in only:
+        continue
     d = type(desc).from_buffer_copy(desc)
     mats = variant(kr, kt)
     if flt == "full":
