@@ -121,7 +121,7 @@ CTL_HD float unorm8(uint32_t b) {
     return fmaf(fmaf(-q0, 255.0f, x), c, q0);
 }
 
-CTL_HD spec tex_texel(const TexView& T, uint32_t level, f2 uv) {                     // MIPMap.cu:15-35
+CTL_HD spec tex_texel(TexView T, uint32_t level, f2 uv) {                     // MIPMap.cu:15-35
     const ctl_texture& t = *T.tex;
     f2 l;
     if (!tex_wrap(uv, mk2((float)(t.width >> level), (float)(t.height >> level)), t.wrap, l)) return mk3s(0.0f);
@@ -132,7 +132,7 @@ CTL_HD spec tex_texel(const TexView& T, uint32_t level, f2 uv) {                
     return mk3(unorm8(c & 0xffu), unorm8((c >> 8) & 0xffu), unorm8((c >> 16) & 0xffu));
 }
 
-CTL_TEX_FN spec tex_triangle(const TexView& T, uint32_t level, f2 uv) {                  // MIPMap.cu:37-48
+CTL_TEX_FN spec tex_triangle(TexView T, uint32_t level, f2 uv) {                  // MIPMap.cu:37-48
     const ctl_texture& t = *T.tex;
     level = clampu_ref(level, 0u, t.levels - 1);
     const f2 s = mk2((float)(t.width >> level), (float)(t.height >> level));
@@ -143,7 +143,7 @@ CTL_TEX_FN spec tex_triangle(const TexView& T, uint32_t level, f2 uv) {         
            ds * (1.f - dt) * tex_texel(T, level, uv + mk2(is.x, 0)) + ds * dt * tex_texel(T, level, uv + mk2(is.x, is.y));
 }
 
-CTL_TEX_FN spec tex_ewa(const TexView& T, uint32_t level, f2 uv, float A, float B, float C) {   // MIPMap.cu:50-111
+CTL_TEX_FN spec tex_ewa(TexView T, uint32_t level, f2 uv, float A, float B, float C) {   // MIPMap.cu:50-111
     const ctl_texture& t = *T.tex;
     if (level >= t.levels) return tex_texel(T, t.levels - 1, mk2(0.0f, 0.0f));
     const f2 size = mk2((float)(t.width >> level), (float)(t.height >> level));
@@ -184,7 +184,7 @@ CTL_TEX_FN spec tex_ewa(const TexView& T, uint32_t level, f2 uv, float A, float 
 }
 
 // KernelMIPMap::eval (MIPMap.cu:160-233): point / bilinear / trilinear / EWA
-CTL_HD spec tex_eval(const TexView& T, f2 uv, f2 d0, f2 d1) {
+CTL_HD spec tex_eval(TexView T, f2 uv, f2 d0, f2 d1) {
     const ctl_texture& t = *T.tex;
     const float dimx = (float)t.width - 1, dimy = (float)t.height - 1;   // m_fDim (MIPMap.cpp:108)
     const float du0 = d0.x * dimx, dv0 = d0.y * dimy, du1 = d1.x * dimx, dv1 = d1.y * dimy, du = (du0 + du1) / 2.0f,
@@ -235,16 +235,19 @@ CTL_HD spec tex_eval(const TexView& T, f2 uv, f2 d0, f2 d1) {
 // ImageTexture::Evaluate(const DifferentialGeometry&) (Texture.cu:16-31).
 // Out of line on the device: the MIP/EWA filter is large and would otherwise
 // be inlined at every BSDF call site (instruction-cache footprint).
-CTL_TEX_FN spec image_texture_eval(const TexView& T, const dgeom& dg) {
+// The differential geometry's uv and partials come by value (an argument
+// passed by reference to an out-of-line call lives in scratch for the call).
+CTL_TEX_FN spec image_texture_eval(TexView T, f2 duv, float dudx, float dudy, float dvdx, float dvdy,
+                                   bool has_partials) {
     const ctl_texture& t = *T.tex;
     spec r;
-    if (dg.has_partials) {
-        const f2 uv = mk2(t.m11 * dg.uv.x + t.m12 * dg.uv.y, t.m21 * dg.uv.x + t.m22 * dg.uv.y) + mk2(t.m13, t.m23);
-        const float dsdx = t.m11 * dg.dudx + t.m12 * dg.dvdx, dsdy = t.m11 * dg.dudy + t.m12 * dg.dvdy;
-        const float dtdx = t.m21 * dg.dudx + t.m22 * dg.dvdx, dtdy = t.m21 * dg.dudy + t.m22 * dg.dvdy;
+    if (has_partials) {
+        const f2 uv = mk2(t.m11 * duv.x + t.m12 * duv.y, t.m21 * duv.x + t.m22 * duv.y) + mk2(t.m13, t.m23);
+        const float dsdx = t.m11 * dudx + t.m12 * dvdx, dsdy = t.m11 * dudy + t.m12 * dvdy;
+        const float dtdx = t.m21 * dudx + t.m22 * dvdx, dtdy = t.m21 * dudy + t.m22 * dvdy;
         r = tex_eval(T, uv, mk2(dsdx, dtdx), mk2(dsdy, dtdy));
     } else {   // Evaluate(uv) -> Sample(uv)
-        const f2 uv = mk2(t.m11 * dg.uv.x + t.m12 * dg.uv.y, t.m21 * dg.uv.x + t.m22 * dg.uv.y) + mk2(t.m13, t.m23);
+        const f2 uv = mk2(t.m11 * duv.x + t.m12 * duv.y, t.m21 * duv.x + t.m22 * duv.y) + mk2(t.m13, t.m23);
         r = t.filter == CTL_TEX_POINT ? tex_texel(T, 0, uv) : tex_triangle(T, 0, uv);
     }
     return r * mk3(t.scale[0], t.scale[1], t.scale[2]);
@@ -253,7 +256,7 @@ CTL_TEX_FN spec image_texture_eval(const TexView& T, const dgeom& dg) {
 // KernelMIPMap::SampleAlpha (MIPMap.cu:123-139): level-0 texel alpha, no
 // filtering.  The reference indexes without clamping; the index is clamped
 // here (it can only differ where the reference would read out of bounds).
-CTL_HD float tex_sample_alpha(const TexView& T, f2 uv) {
+CTL_HD float tex_sample_alpha(TexView T, f2 uv) {
     const ctl_texture& t = *T.tex;
     f2 l;
     if (!tex_wrap(uv, mk2((float)t.width, (float)t.height), t.wrap, l)) return 0.0f;
@@ -268,7 +271,7 @@ CTL_HD f2 tex_map(const ctl_texture& t, f2 uv) {   // TextureMapping2D::Transfor
 
 // Material::AlphaTest (Engine/Material.cu:160-189) for image / constant
 // textures (sample_fast, :140-158), states without the Color compare.
-CTL_HD bool material_alpha_test(const ctl_material& m, const TexView& tex, f2 uv) {
+CTL_HD bool material_alpha_test(const ctl_material& m, TexView tex, f2 uv) {
     if (!m.alpha_state) return true;
     const bool reflImg = m.texture != 0xffffffffu;
     const bool alphaImg = m.alpha_texture != 0xffffffffu;
@@ -482,7 +485,11 @@ CTL_HD Microfacet rough_distr(const ctl_material& m) {
     return d;
 }
 
-CTL_TEX_FN float rough_pdf(const ctl_material& mat, const bsdf_rec& b) {
+// The rough-dielectric entry points are out of line on the device; the BSDF
+// record's fields travel by value and the material as a global pointer, so no
+// argument needs a scratch copy around the call.
+CTL_TEX_FN float rough_pdf(const ctl_material* matp, bsdf_rec b) {
+    const ctl_material& mat = *matp;
     const bool hasReflection = (b.type_mask & CTL_EGLOSSY_REFLECTION) != 0,
                hasTransmission = (b.type_mask & CTL_EGLOSSY_TRANSMISSION) != 0,
                reflect = b.wi.z * b.wo.z > 0;
@@ -516,7 +523,8 @@ CTL_TEX_FN float rough_pdf(const ctl_material& mat, const bsdf_rec& b) {
     return fabsf(prob * dwh_dwo);
 }
 
-CTL_TEX_FN spec rough_f(const ctl_material& mat, const bsdf_rec& b) {
+CTL_TEX_FN spec rough_f(const ctl_material* matp, bsdf_rec b) {
+    const ctl_material& mat = *matp;
     const bool reflect = b.wi.z * b.wo.z > 0;
     f3 H;
     if (reflect) {
@@ -544,7 +552,17 @@ CTL_TEX_FN spec rough_f(const ctl_material& mat, const bsdf_rec& b) {
     return mk3(mat.transmittance[0], mat.transmittance[1], mat.transmittance[2]) * fabsf(value * factor * factor);
 }
 
-CTL_TEX_FN spec rough_sample(const ctl_material& mat, bsdf_rec& b, float& pdf, f2 sample) {
+// roughdielectric::sample: returns the weight; `b` and `pdf` come back in
+// the result, changed only where the reference's sample writes them.
+struct RoughSample { spec w; f3 wo; float pdf; uint32_t sampled_type; };
+CTL_HD spec rough_sample_impl(const ctl_material& mat, bsdf_rec& b, float& pdf, f2 sample);
+CTL_TEX_FN RoughSample rough_sample(const ctl_material* matp, bsdf_rec b, float pdf, f2 sample) {
+    RoughSample r;
+    r.w = rough_sample_impl(*matp, b, pdf, sample);
+    r.wo = b.wo; r.pdf = pdf; r.sampled_type = b.sampled_type;
+    return r;
+}
+CTL_HD spec rough_sample_impl(const ctl_material& mat, bsdf_rec& b, float& pdf, f2 sample) {
     const bool hasReflection = (b.type_mask & CTL_EGLOSSY_REFLECTION) != 0,
                hasTransmission = (b.type_mask & CTL_EGLOSSY_TRANSMISSION) != 0;
     bool sampleReflection = hasReflection;
@@ -607,8 +625,8 @@ CTL_TEX_FN spec rough_sample(const ctl_material& mat, bsdf_rec& b, float& pdf, f
 // diffuse with an optional image texture for m_reflectance
 CTL_HD spec diffuse_reflectance(const ctl_material& m, const dgeom& dg, const TexView* tex) {
     if (m.texture != 0xffffffffu && tex) {
-        TexView T{tex->tex + m.texture, tex->data};
-        return image_texture_eval(T, dg);
+        return image_texture_eval(TexView{tex->tex + m.texture, tex->data}, dg.uv, dg.dudx, dg.dudy, dg.dvdx, dg.dvdy,
+                                  dg.has_partials);
     }
     return refl(m);
 }
@@ -618,40 +636,43 @@ CTL_HD spec diffuse_reflectance(const ctl_material& m, const dgeom& dg, const Te
 // diffuse reflectance at dg when the caller already evaluated it (a textured
 // diffuse hit samples and evaluates the same texture at the same dg for the
 // BSDF sample and for next-event estimation: one lookup serves both).
-// gm: the same material in global memory (the scene's array element), handed
-// to the out-of-line rough-dielectric calls so the caller's register copy of
-// the 80-B record need not be written to scratch for them.
+// gm: the same material in global memory (the scene's array element; required
+// for rough dielectrics), handed to the out-of-line rough-dielectric calls so
+// the caller's register copy of the 80-B record need not be written to scratch
+// for them.
 CTL_HD spec bsdf_sample(const ctl_material& m, bsdf_rec& b, float& pdf, f2 sample, const dgeom& dg, const TexView* tex,
-                        const spec* R = nullptr, const ctl_material* gm = nullptr) {
+                        const spec* R, const ctl_material* gm) {
     if (m.bsdf_type == CTL_BSDF_DIFFUSE) {
         if (!diffuse_sample_dir(m, b, pdf, sample)) return mk3s(0.0f);
         return (R ? *R : diffuse_reflectance(m, dg, tex)) * 1.0f;
     }
     const bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
-    spec res = rough_sample(gm ? *gm : m, b, pdf, sample);
+    const RoughSample rs = rough_sample(gm, b, pdf, sample);
+    b.wo = rs.wo; b.sampled_type = rs.sampled_type; pdf = rs.pdf;
+    const spec res = rs.w;
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
     return res;
 }
 
-CTL_HD spec bsdf_f(const ctl_material& m, bsdf_rec& b, const dgeom& dg, const TexView* tex, const spec* R = nullptr,
-                   const ctl_material* gm = nullptr) {
+CTL_HD spec bsdf_f(const ctl_material& m, bsdf_rec& b, const dgeom& dg, const TexView* tex, const spec* R,
+                   const ctl_material* gm) {
     if (m.bsdf_type == CTL_BSDF_DIFFUSE) {
         if (!(b.type_mask & m.combined_type)) return mk3s(0.0f);
         return diffuse_f_refl(m, b, R ? *R : diffuse_reflectance(m, dg, tex));
     }
     const bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
-    spec res = rough_f(gm ? *gm : m, b);
+    spec res = rough_f(gm, b);
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
     return res;
 }
 
-CTL_HD float bsdf_pdf(const ctl_material& m, bsdf_rec& b, const ctl_material* gm = nullptr) {
+CTL_HD float bsdf_pdf(const ctl_material& m, bsdf_rec& b, const ctl_material* gm) {
     if (m.bsdf_type == CTL_BSDF_DIFFUSE) return diffuse_pdf(m, b);
     const bool flip = b.wi.z < 0 && m.two_sided;
     if (flip) b.wi.z *= -1.0f;
-    float res = rough_pdf(gm ? *gm : m, b);
+    float res = rough_pdf(gm, b);
     if (flip) { b.wi.z *= -1.0f; b.wo.z *= -1.0f; }
     return res;
 }

@@ -89,7 +89,8 @@ void prim_kernel(DevScene S_arg, PathParams P_arg, PrimParams Q, const float* s1
                 b.sampled_type = 0;
                 b.type_mask = kEAll;
                 b.wi = to_local(dg.sys, -d);
-                const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N->material_offset];
+                const ctl_material* gmat = S.mats + (((td.w[1] >> 16) & 0xffu) + N->material_offset);
+                const ctl_material mat = *gmat;
                 if (mat.two_sided && b.wi.z < 0) {
                     dg.n = -dg.n;
                     dg.sys.n = -dg.sys.n;
@@ -118,7 +119,7 @@ void prim_kernel(DevScene S_arg, PathParams P_arg, PrimParams Q, const float* s1
                     // (PrimTracer.cu:61-67: isDelta is false)
                     b.wo = mk3(0.0f, 0.0f, 1.0f);
                     const TexView tex{S.textures, S.tex_data};
-                    const spec f_avg = FULL ? bsdf_f(mat, b, dg, &tex) : diffuse_f(mat, b);
+                    const spec f_avg = FULL ? bsdf_f(mat, b, dg, &tex, nullptr, gmat) : diffuse_f(mat, b);
                     spec Le = mk3s(0.0f);   // TraceResult::Le -> DiffuseLight::eval (Light.cu:67-82)
                     if (mat.node_light_index != 0xffffffffu) {
                         const ctl_light Lt = S.lights[N->lights[mat.node_light_index]];

@@ -175,7 +175,8 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S_arg, Wpt
             dg.dudx = dg.dudy = dg.dvdx = dg.dvdy = 0.0f;
             dg.has_partials = false;   // no ray differentials in the wavefront tracer
             b.wi = to_local(dg.sys, -rd);
-            const ctl_material mat = S.mats[((td.w[1] >> 16) & 0xffu) + N->material_offset];
+            const ctl_material* gmat = S.mats + (((td.w[1] >> 16) & 0xffu) + N->material_offset);
+            const ctl_material mat = *gmat;
             if (mat.two_sided && b.wi.z < 0) {
                 dg.n = -dg.n;
                 dg.sys.n = -dg.sys.n;
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S_arg, Wpt
                 spec Rtex = mk3s(0.0f);
                 if (texd) Rtex = diffuse_reflectance(mat, dg, &tex);
                 const spec* Rp = texd ? &Rtex : nullptr;
-                spec f = FULL ? bsdf_sample(mat, b, bpdf, rng.next2(), dg, &tex, Rp)
+                spec f = FULL ? bsdf_sample(mat, b, bpdf, rng.next2(), dg, &tex, Rp, gmat)
                               : diffuse_sample(mat, b, bpdf, rng.next2());
                 specular = (b.sampled_type & kEDelta) != 0;
                 const f3 out = to_world(dg.sys, b.wo);
@@ -234,8 +235,8 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S_arg, Wpt
                     if (!spec_zero(value)) {
                         b.type_mask = kEAll & ~kEDelta;
                         b.wo = to_local(dg.sys, dRec.d);
-                        spec bsdfVal = FULL ? bsdf_f(mat, b, dg, &tex, Rp) : diffuse_f(mat, b);
-                        const float bsdfPdf = FULL ? bsdf_pdf(mat, b) : diffuse_pdf(mat, b);
+                        spec bsdfVal = FULL ? bsdf_f(mat, b, dg, &tex, Rp, gmat) : diffuse_f(mat, b);
+                        const float bsdfPdf = FULL ? bsdf_pdf(mat, b, gmat) : diffuse_pdf(mat, b);
                         const float directPdf = dRec.pdf;   // measure is ESolidAngle after sampleDirect
                         const float weight = power_heuristic(directPdf, bsdfPdf);
                         const spec dF = tp * value * bsdfVal * weight;
