@@ -132,7 +132,28 @@ CTL_HD spec tex_texel(TexView T, uint32_t level, f2 uv) {                     //
     return mk3(unorm8(c & 0xffu), unorm8((c >> 8) & 0xffu), unorm8((c >> 16) & 0xffu));
 }
 
-CTL_TEX_FN spec tex_triangle(TexView T, uint32_t level, f2 uv) {                  // MIPMap.cu:37-48
+// One MIP level's fields, read once per EWA lookup (tex_texel reads them per texel).
+struct TexLevel {
+    const uint32_t* data;
+    uint32_t base, wl, hl;   // offsets[level], level size
+    f2 dim;                  // level size as floats
+};
+
+// tex_texel for a fixed wrap mode (WRAP outside 0..3: no texel, as tex_wrap).
+template <uint32_t WRAP>
+CTL_HD spec level_texel(const TexLevel& L, f2 uv) {
+    f2 l;
+    if (!tex_wrap(uv, L.dim, WRAP, l)) return mk3s(0.0f);
+    const int x = clampi_ref((int)l.x, 0, (int)L.wl - 1), y = clampi_ref((int)l.y, 0, (int)L.hl - 1);
+    const uint32_t c = L.data[L.base + (uint32_t)y * L.wl + (uint32_t)x];
+    return mk3(unorm8(c & 0xffu), unorm8((c >> 8) & 0xffu), unorm8((c >> 16) & 0xffu));
+}
+
+// tex_triangle with the texture's fields read per texel: fewer live registers
+// (up to v31) than tex_triangle's per-wrap-mode form, for the alpha test's
+// call inside the traversal loop, where a callee using v32..v39 costs the
+// caller spills.  Same arithmetic.
+CTL_TEX_FN spec tex_triangle_compact(TexView T, uint32_t level, f2 uv) {                  // MIPMap.cu:37-48
     const ctl_texture& t = *T.tex;
     level = clampu_ref(level, 0u, t.levels - 1);
     const f2 s = mk2((float)(t.width >> level), (float)(t.height >> level));
@@ -143,10 +164,64 @@ CTL_TEX_FN spec tex_triangle(TexView T, uint32_t level, f2 uv) {                
            ds * (1.f - dt) * tex_texel(T, level, uv + mk2(is.x, 0)) + ds * dt * tex_texel(T, level, uv + mk2(is.x, is.y));
 }
 
+template <uint32_t WRAP>
+CTL_HD spec level_bilerp(const TexLevel& L, f2 uv, f2 is, float ds, float dt) {
+    return (1.f - ds) * (1.f - dt) * level_texel<WRAP>(L, uv) + (1.f - ds) * dt * level_texel<WRAP>(L, uv + mk2(0, is.y)) +
+           ds * (1.f - dt) * level_texel<WRAP>(L, uv + mk2(is.x, 0)) + ds * dt * level_texel<WRAP>(L, uv + mk2(is.x, is.y));
+}
+
+CTL_TEX_FN spec tex_triangle(TexView T, uint32_t level, f2 uv) {                  // MIPMap.cu:37-48
+    const ctl_texture& t = *T.tex;
+    level = clampu_ref(level, 0u, t.levels - 1);
+    const uint32_t wl = t.width >> level, hl = t.height >> level;
+    const f2 s = mk2((float)wl, (float)hl);
+    const f2 is = mk2(1.0f / s.x, 1.0f / s.y);
+    const f2 l = mk2(uv.x * s.x, uv.y * s.y);
+    const float ds = fracf_ref(l.x), dt = fracf_ref(l.y);
+    const TexLevel L{T.data, t.offsets[level], wl, hl, s};
+    switch (t.wrap) {   // the level's fields and the wrap mode resolved once for the four texels
+        case CTL_WRAP_REPEAT: return level_bilerp<CTL_WRAP_REPEAT>(L, uv, is, ds, dt);
+        case CTL_WRAP_CLAMP: return level_bilerp<CTL_WRAP_CLAMP>(L, uv, is, ds, dt);
+        case CTL_WRAP_MIRROR: return level_bilerp<CTL_WRAP_MIRROR>(L, uv, is, ds, dt);
+        case CTL_WRAP_BLACK: return level_bilerp<CTL_WRAP_BLACK>(L, uv, is, ds, dt);
+        default: return level_bilerp<0xffffffffu>(L, uv, is, ds, dt);
+    }
+}
+
+// The EWA footprint loop of tex_ewa.  P2: both level sizes are powers of two,
+// so (float)ut / size.x is the exact product with the exact reciprocal (the
+// quotient's value, without a division per texel).
+template <uint32_t WRAP, bool P2>
+CTL_HD void ewa_footprint(const TexLevel& L, const float* lut, int u0, int u1, int v0, int v1, float u, float v,
+                          float As, float Bs, float Cs, spec& result, float& denominator) {
+    const f2 size = L.dim, inv = mk2(1.0f / size.x, 1.0f / size.y);
+    const float ddq = 2 * As, uu0 = u0 - u;
+    for (int vt = v0; vt <= v1; ++vt) {
+        const float vv = vt - v;
+        const float tv = P2 ? (float)vt * inv.y : (float)vt / size.y;
+        float q = As * uu0 * uu0 + (Bs * uu0 + Cs * vv) * vv;
+        float dq = As * (2 * uu0 + 1) + Bs * vv;
+        for (int ut = u0; ut <= u1; ++ut) {
+            if (q < 64) {
+                const uint32_t qi = (uint32_t)q;
+                if (qi < 64) {
+                    const float weight = lut[(int)q];
+                    const float tu = P2 ? (float)ut * inv.x : (float)ut / size.x;
+                    result = result + level_texel<WRAP>(L, mk2(tu, tv)) * weight;
+                    denominator += weight;
+                }
+            }
+            q += dq;
+            dq += ddq;
+        }
+    }
+}
+
 CTL_TEX_FN spec tex_ewa(TexView T, uint32_t level, f2 uv, float A, float B, float C) {   // MIPMap.cu:50-111
     const ctl_texture& t = *T.tex;
     if (level >= t.levels) return tex_texel(T, t.levels - 1, mk2(0.0f, 0.0f));
-    const f2 size = mk2((float)(t.width >> level), (float)(t.height >> level));
+    const uint32_t wl = t.width >> level, hl = t.height >> level;
+    const f2 size = mk2((float)wl, (float)hl);
     const float u = uv.x * size.x - 0.5f;
     const float v = uv.y * size.y - 0.5f;
     // KernelMIPMap::m_fDim = (width - 1, height - 1) (MIPMap.cpp:108)
@@ -161,24 +236,20 @@ CTL_TEX_FN spec tex_ewa(TexView T, uint32_t level, f2 uv, float A, float B, floa
     const float As = A * 64, Bs = B * 64, Cs = C * 64;
     spec result = mk3s(0.0f);
     float denominator = 0.0f;
-    const float ddq = 2 * As, uu0 = u0 - u;
-    for (int vt = v0; vt <= v1; ++vt) {
-        const float vv = vt - v;
-        float q = As * uu0 * uu0 + (Bs * uu0 + Cs * vv) * vv;
-        float dq = As * (2 * uu0 + 1) + Bs * vv;
-        for (int ut = u0; ut <= u1; ++ut) {
-            if (q < 64) {
-                const uint32_t qi = (uint32_t)q;
-                if (qi < 64) {
-                    const float weight = t.weight_lut[(int)q];
-                    result = result + tex_texel(T, level, mk2((float)ut / size.x, (float)vt / size.y)) * weight;
-                    denominator += weight;
-                }
-            }
-            q += dq;
-            dq += ddq;
-        }
+    const TexLevel L{T.data, t.offsets[level], wl, hl, size};
+    const float* lut = t.weight_lut;
+    const bool p2 = (wl & (wl - 1)) == 0 && (hl & (hl - 1)) == 0;
+#define CTL_EWA(W)                                                                                     \
+    (p2 ? ewa_footprint<W, true>(L, lut, u0, u1, v0, v1, u, v, As, Bs, Cs, result, denominator)        \
+        : ewa_footprint<W, false>(L, lut, u0, u1, v0, v1, u, v, As, Bs, Cs, result, denominator))
+    switch (t.wrap) {
+        case CTL_WRAP_REPEAT: CTL_EWA(CTL_WRAP_REPEAT); break;
+        case CTL_WRAP_CLAMP: CTL_EWA(CTL_WRAP_CLAMP); break;
+        case CTL_WRAP_MIRROR: CTL_EWA(CTL_WRAP_MIRROR); break;
+        case CTL_WRAP_BLACK: CTL_EWA(CTL_WRAP_BLACK); break;
+        default: CTL_EWA(0xffffffffu); break;   // no texel, the weights still count
     }
+#undef CTL_EWA
     if (denominator == 0) return tex_triangle(T, level, uv);
     return spec_div(result, denominator);
 }
@@ -286,7 +357,7 @@ CTL_HD bool material_alpha_test(const ctl_material& m, TexView tex, f2 uv) {
         const ctl_texture& t = tex.tex[src];
         const TexView T{&t, tex.data};
         const f2 u2 = tex_map(t, uv);
-        val = (t.filter == CTL_TEX_POINT ? tex_texel(T, 0, u2) : tex_triangle(T, 0, u2)) *
+        val = (t.filter == CTL_TEX_POINT ? tex_texel(T, 0, u2) : tex_triangle_compact(T, 0, u2)) *
               mk3(t.scale[0], t.scale[1], t.scale[2]);
     } else {                    // ConstantTexture (the diffuse reflectance)
         val = refl(m);

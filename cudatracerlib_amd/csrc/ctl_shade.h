@@ -124,37 +124,36 @@ CTL_HD bool solve2x2_ref(const float a[2][2], const float b[2], float x[2]) {
     return true;
 }
 CTL_HD void compute_partials(dgeom& dg, f3 rxo, f3 rxd, f3 ryo, f3 ryd) {
-    float A[2][2], Bx[2], By[2], x[2];
-    int axes[2];
+    // One exit, the four partials stored once in a fixed order: stores in the
+    // early-return branches made the compiler keep them in scratch, addressed
+    // through a selected offset.
+    float dudx = 0.0f, dvdx = 0.0f, dudy = 0.0f, dvdy = 0.0f;
     dg.has_partials = true;
-    if (dot(dg.dpdu, dg.dpdu) == 0 && dot(dg.dpdv, dg.dpdv) == 0) {
-        dg.dudx = dg.dvdx = dg.dudy = dg.dvdy = 0.0f;
-        return;
-    }
     const float pp = dot(dg.n, dg.P), pox = dot(dg.n, rxo), poy = dot(dg.n, ryo), prx = dot(dg.n, rxd),
                 pry = dot(dg.n, ryd);
-    if (prx == 0 || pry == 0) {
-        dg.dudx = dg.dvdx = dg.dudy = dg.dvdy = 0.0f;
-        return;
+    if (!(dot(dg.dpdu, dg.dpdu) == 0 && dot(dg.dpdv, dg.dpdv) == 0) && !(prx == 0 || pry == 0)) {
+        float A[2][2], Bx[2], By[2], x[2];
+        int axes[2];
+        const float tx = (pp - pox) / prx, ty = (pp - poy) / pry;
+        const float absX = fabsf(dg.n.x), absY = fabsf(dg.n.y), absZ = fabsf(dg.n.z);
+        if (absX > absY && absX > absZ) { axes[0] = 1; axes[1] = 2; }
+        else if (absY > absZ) { axes[0] = 0; axes[1] = 2; }
+        else { axes[0] = 0; axes[1] = 1; }
+        A[0][0] = comp(dg.dpdu, axes[0]);
+        A[0][1] = comp(dg.dpdv, axes[0]);
+        A[1][0] = comp(dg.dpdu, axes[1]);
+        A[1][1] = comp(dg.dpdv, axes[1]);
+        const f3 px = rxo + rxd * tx, py = ryo + ryd * ty;
+        Bx[0] = comp(px, axes[0]) - comp(dg.P, axes[0]);
+        Bx[1] = comp(px, axes[1]) - comp(dg.P, axes[1]);
+        By[0] = comp(py, axes[0]) - comp(dg.P, axes[0]);
+        By[1] = comp(py, axes[1]) - comp(dg.P, axes[1]);
+        const bool okx = solve2x2_ref(A, Bx, x);
+        dudx = okx ? x[0] : 1.0f; dvdx = okx ? x[1] : 0.0f;
+        const bool oky = solve2x2_ref(A, By, x);
+        dudy = oky ? x[0] : 0.0f; dvdy = oky ? x[1] : 1.0f;
     }
-    const float tx = (pp - pox) / prx, ty = (pp - poy) / pry;
-    const float absX = fabsf(dg.n.x), absY = fabsf(dg.n.y), absZ = fabsf(dg.n.z);
-    if (absX > absY && absX > absZ) { axes[0] = 1; axes[1] = 2; }
-    else if (absY > absZ) { axes[0] = 0; axes[1] = 2; }
-    else { axes[0] = 0; axes[1] = 1; }
-    A[0][0] = comp(dg.dpdu, axes[0]);
-    A[0][1] = comp(dg.dpdv, axes[0]);
-    A[1][0] = comp(dg.dpdu, axes[1]);
-    A[1][1] = comp(dg.dpdv, axes[1]);
-    const f3 px = rxo + rxd * tx, py = ryo + ryd * ty;
-    Bx[0] = comp(px, axes[0]) - comp(dg.P, axes[0]);
-    Bx[1] = comp(px, axes[1]) - comp(dg.P, axes[1]);
-    By[0] = comp(py, axes[0]) - comp(dg.P, axes[0]);
-    By[1] = comp(py, axes[1]) - comp(dg.P, axes[1]);
-    if (solve2x2_ref(A, Bx, x)) { dg.dudx = x[0]; dg.dvdx = x[1]; }
-    else { dg.dudx = 1; dg.dvdx = 0; }
-    if (solve2x2_ref(A, By, x)) { dg.dudy = x[0]; dg.dvdy = x[1]; }
-    else { dg.dudy = 0; dg.dvdy = 1; }
+    dg.dudx = dudx; dg.dudy = dudy; dg.dvdx = dvdx; dg.dvdy = dvdy;
 }
 
 struct bsdf_rec { f3 wi, wo; uint32_t sampled_type, type_mask; };

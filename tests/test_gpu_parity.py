@@ -323,15 +323,17 @@ def test_render_c5_bit_exact(ctl, orc, tracer, dev, mode, any_hit, bvh):
     assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
 
 
-def test_render_c5_textured_quad(ctl, orc, tracer, dev):
-    """A camera-facing textured quad per filter mode (point, bilinear,
-    trilinear, EWA) and wrap mode, plus rough Beckmann / GGX panels, lit by
-    an area light: exercises every texture path at the first hit."""
+@pytest.mark.parametrize("modes", [((0, 0), (1, 1), (3, 2), (2, 0), (2, 3)), ((2, 1), (2, 2), (3, 0), (1, 3), (0, 2))],
+                         ids=["set_a", "ewa_clamp_mirror"])
+def test_render_c5_textured_quad(ctl, orc, tracer, dev, modes):
+    """A camera-facing textured quad per (filter, wrap) pair -- point,
+    bilinear, trilinear, EWA; repeat, clamp, mirror, black -- plus rough
+    Beckmann / GGX panels, lit by an area light: exercises every texture path
+    at the first hit (EWA under every wrap mode across the two sets)."""
     s = ctl.HostScene()
     rng = np.random.default_rng(3)
     img = rng.integers(0, 2 ** 32, size=(64, 64), dtype=np.uint64).astype(np.uint32)
-    tex = [s.add_texture(img, filter=f, wrap=wr, mapping=(3.0, 0.5, 0.1, -0.2, 2.0, 0.3))
-           for f, wr in [(0, 0), (1, 1), (3, 2), (2, 0), (2, 3)]]
+    tex = [s.add_texture(img, filter=f, wrap=wr, mapping=(3.0, 0.5, 0.1, -0.2, 2.0, 0.3)) for f, wr in modes]
     mats = [ctl.diffuse_material(0.5, 0.5, 0.5, texture=t) for t in tex]
     mats += [ctl.roughdielectric_material(0, 1.5, 0.1), ctl.roughdielectric_material(1, 1.5, 0.3, 0.2)]
     mats += [ctl.diffuse_material(0.8, 0.8, 0.8)]
