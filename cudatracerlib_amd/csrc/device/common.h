@@ -29,32 +29,35 @@ struct PathParams {
     uint32_t apron;   // 2 * tile_size + 1 when num_ranks > 1, else 0
 };
 
+// d1 / d2: the 1D / 2D draw counters reduced modulo len -- the reference only
+// ever uses counter % len (the table row), and (d + 1) % len follows from
+// d % len with a compare, so no division (and no loop-held reciprocal) per draw.
 struct SamplerDev {   // SequenceSampler (Kernel/Sampler_device.h:59-113)
     const float* s1;
     const float2* s2;
     uint32_t nseq, len, a, b;   // a = idx % nseq, b = (idx / nseq) % nseq
-    uint32_t d1, d2;
+    uint32_t d1, d2;            // draw counters mod len
     __device__ __forceinline__ void init(const float* t1, const float2* t2, const PathParams& P, uint32_t idx,
                                          uint32_t c1, uint32_t c2) {
         s1 = t1; s2 = t2; nseq = P.nseq; len = P.len;
         a = idx % P.nseq; b = (idx / P.nseq) % P.nseq;
-        d1 = c1; d2 = c2;
+        d1 = c1 % len; d2 = c2 % len;
     }
     __device__ __forceinline__ float next1() {
-        uint32_t k = d1 % len;
+        const uint32_t k = d1;
         float val = 0.0f;
         val += s1[k * nseq + a];
         val += s1[k * nseq + b];
-        d1++;
+        d1 = d1 + 1 == len ? 0u : d1 + 1;
         return fracf_ref(val);
     }
     __device__ __forceinline__ f2 next2() {
-        uint32_t k = d2 % len;
+        const uint32_t k = d2;
         float2 p = s2[k * nseq + a], q = s2[k * nseq + b];
         float x = 0.0f, y = 0.0f;
         x += p.x; y += p.y;
         x += q.x; y += q.y;
-        d2++;
+        d2 = d2 + 1 == len ? 0u : d2 + 1;
         return mk2(fracf_ref(x), fracf_ref(y));
     }
 };
@@ -72,6 +75,21 @@ __device__ __forceinline__ m44 load_m44(const float4* M) {
     m.d[8] = r2.x; m.d[9] = r2.y; m.d[10] = r2.z; m.d[11] = r2.w;
     m.d[12] = r3.x; m.d[13] = r3.y; m.d[14] = r3.z; m.d[15] = r3.w;
     return m;
+}
+
+// Number of set bits of `mask` below the calling lane (mbcnt: no per-lane
+// mask register held for the kernel's lifetime).
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// The same pointer, opaque to the optimiser: reads through it (and the
+// integer-division reciprocals of the fields read) stay where they are used
+// instead of being hoisted out of a loop into registers held for its lifetime.
+template <class T>
+__device__ __forceinline__ const T* opaque_ptr(const T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
 }
 
 __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, uint64_t v) {
@@ -354,11 +372,13 @@ __device__ __forceinline__ spec env_miss(const DevScene& S, const PathParams& P,
 // draws the light choice and the light position, and when both the light
 // sample and the BSDF value are non-zero fills the shadow ray and, in sh.add,
 // EstimateDirect(...) / pdf -- the value UniformSampleOneLight returns when the
-// shadow ray is unoccluded (it returns +0 otherwise).
+// shadow ray is unoccluded (it returns +0 otherwise).  gm: the material's
+// record in the scene array (the rough-dielectric calls read it there; required
+// for FULL), R: the diffuse reflectance when already evaluated (or null).
 template <int FULL>
 __device__ __forceinline__ void nee_sample(const DevScene& S, SamplerDev& rng, const ctl_material& mat,
                                            const bsdf_rec& b, const dgeom& dg, const TexView& tex, ShadowReq& sh,
-                                           const spec* R = nullptr, const ctl_material* gm = nullptr) {
+                                           const spec* R, const ctl_material* gm) {
     f2 sample = rng.next2();
     const uint32_t nl = S.n_lights < CTL_MAX_NUM_LIGHTS ? S.n_lights : CTL_MAX_NUM_LIGHTS;
     uint32_t first = 0, cnt = nl;   // STL_upper_bound

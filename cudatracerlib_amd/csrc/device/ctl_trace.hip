@@ -93,6 +93,15 @@ struct Park {
         put3(16, sh.add);
         puti(19, rng.a); puti(20, rng.b); puti(21, rng.d1); puti(22, rng.d2);
     }
+    // a new path (refill): everything but the shadow contribution, which only the
+    // shadow phase reads and store_shaded always writes first -- so the previous
+    // path's value is not carried through the loop just to be written here
+    __device__ __forceinline__ void begin(const PathVars& v, const SamplerDev& rng) const {
+        put3(0, v.cl); put3(3, v.cf); put3(6, v.last_nor); put3(9, v.wo);
+        put(12, v.pX.x); put(13, v.pX.y); put(14, v.brdf_pdf);
+        puti(15, ((uint32_t)v.depth << 1) | (v.specular ? 1u : 0u));
+        puti(19, rng.a); puti(20, rng.b); puti(21, rng.d1); puti(22, rng.d2);
+    }
     __device__ __forceinline__ void load(PathVars& v, ShadowReq& sh, SamplerDev& rng) const {
         v.cl = get3(0); v.cf = get3(3); v.last_nor = get3(6); v.wo = get3(9);
         v.pX.x = get(12); v.pX.y = get(13); v.brdf_pdf = get(14);
@@ -333,18 +342,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             if (lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
             base = __shfl(base, leader);
             if (need) {
-                const uint64_t k64 = base + (uint64_t)__popcll(mask & ((1ull << lane) - 1ull));
+                const uint64_t k64 = base + (uint64_t)lanes_below(mask);
                 if (k64 >= items) {
                     exhausted = true;
                 } else {
                     const uint32_t k = (uint32_t)k64;   // items < 2^32 (checked on the host)
                     uint32_t px, py, ps, kk;
                     split(k, ps, kk);
-                    if (work_pixel(P, kk, px, py)) {
-                        const uint32_t idx = py * P.width + px;
+                    // the pass record read through an opaque pointer here: the divisions
+                    // by its fields keep their reciprocals local to the refill (hoisted,
+                    // they held VGPRs spilled for the kernel's lifetime)
+                    const PathParams& Pw = *opaque_ptr(&P);
+                    if (work_pixel(Pw, kk, px, py)) {
+                        const uint32_t idx = py * Pw.width + px;
                         // the pass slot's tables start ps * tbl elements in: folded into
                         // the two sequence offsets so the table bases stay kernel-uniform
-                        rng.a = idx % P.nseq + ps * tbl; rng.b = (idx / P.nseq) % P.nseq + ps * tbl;
+                        rng.a = idx % Pw.nseq + ps * tbl; rng.b = (idx / Pw.nseq) % Pw.nseq + ps * tbl;
                         rng.d1 = 0; rng.d2 = 0;
                         *pkw = (int)k;
                         f3 o, dw;
@@ -353,10 +366,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                         shadowPhase = false;
                         ending = false;
                         // loop head of PathTrace: `while (depth++ < MaxPathLength)`
-                        if (!apron_keep(P, kk, pX)) PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                        if (!apron_keep(Pw, kk, pX)) PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                         else if (v.depth++ < P.max_path_length) active = true;
                         else store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
-                        if (active) park.store(v, sh, rng);
+                        if (active) park.begin(v, rng);
                     } else {
                         PS.s[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // work item outside the image: no sample
                     }
@@ -417,9 +430,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             if (!cont) {
                 uint32_t px, py, ps, kk;
                 split((uint32_t)*pkw, ps, kk);
-                work_pixel(P, kk, px, py);
+                const PathParams& Pw = *opaque_ptr(&P);   // as at the refill
+                work_pixel(Pw, kk, px, py);
                 if (lazy) park.load_px(v);
-                store_sample(P, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
+                store_sample(Pw, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
                 active = false;
             } else if (!lazy) {
                 park.store(v, sh, rng);
@@ -504,7 +518,7 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64
             if (lane == leader) base = atomicAdd(cursor, (unsigned long long)__popcll(mask));
             base = __shfl(base, leader);
             if (need) {
-                int64_t k = (int64_t)base + __popcll(mask & ((1ull << lane) - 1ull));
+                int64_t k = (int64_t)base + (int64_t)lanes_below(mask);
                 if (k < total) {
                     // band_w: the first segment is a row-major image of that width (the
                     // WavefrontPathTracer's camera rays); trace it in 8-row bands, column by

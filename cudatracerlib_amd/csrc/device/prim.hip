@@ -135,7 +135,7 @@ void prim_kernel(DevScene S_arg, PathParams P_arg, PrimParams Q, const float* s1
                         if (S.n_lights) {
                             ShadowReq sh;
                             sh.valid = false;
-                            nee_sample<FULL>(S, rng, mat, b, dg, tex, sh);
+                            nee_sample<FULL>(S, rng, mat, b, dg, tex, sh, nullptr, gmat);
                             if (sh.valid) {
                                 // KernelDynamicScene::Occluded (KernelDynamicScene.cu:70-80)
                                 HitRec hs;

@@ -37,7 +37,7 @@ __device__ __forceinline__ uint32_t queue_push(uint32_t* count, bool want) {
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(mask));
     base = __shfl(base, leader);
-    const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    const uint32_t rank = lanes_below(mask);
     return want ? base + rank : 0xffffffffu;
 }
 
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(kBlock) void wf_trace_kernel(DevScene S_arg, WfStat
             if (lane == leader) base = atomicAdd(cursor, (uint32_t)__popcll(mask));
             base = __shfl(base, leader);
             if (need) {
-                const uint32_t k = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                const uint32_t k = base + lanes_below(mask);
                 if (k < count) {
                     ray = queue[k];
                     haveRay = true;

@@ -81,7 +81,7 @@ __device__ __forceinline__ SamplerDev wpt_rng(const float* s1, const float2* s2,
     SamplerDev r;
     r.s1 = s1; r.s2 = s2; r.nseq = A.nseq; r.len = A.len;
     r.a = idx % A.nseq; r.b = (idx / A.nseq) % A.nseq;
-    r.d1 = skip; r.d2 = skip;
+    r.d1 = skip % A.len; r.d2 = skip % A.len;   // draw counters mod len (SamplerDev)
     return r;
 }
 
