@@ -349,10 +349,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
                     const uint32_t k = (uint32_t)k64;   // items < 2^32 (checked on the host)
                     uint32_t px, py, ps, kk;
                     split(k, ps, kk);
-                    // the pass record read through an opaque pointer here: the divisions
-                    // by its fields keep their reciprocals local to the refill (hoisted,
-                    // they held VGPRs spilled for the kernel's lifetime)
-                    const PathParams& Pw = *opaque_ptr(&P);
+                    // FULL: the pass record read through an opaque pointer here, so the
+                    // divisions by its fields keep their reciprocals local to the refill
+                    // (hoisted, they held VGPRs the FULL kernel spilled for its lifetime;
+                    // the lean kernel has the registers and keeps them hoisted)
+                    const PathParams& Pw = FULL ? *opaque_ptr(&P) : P;
                     if (work_pixel(Pw, kk, px, py)) {
                         const uint32_t idx = py * Pw.width + px;
                         // the pass slot's tables start ps * tbl elements in: folded into
@@ -430,7 +431,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
             if (!cont) {
                 uint32_t px, py, ps, kk;
                 split((uint32_t)*pkw, ps, kk);
-                const PathParams& Pw = *opaque_ptr(&P);   // as at the refill
+                const PathParams& Pw = FULL ? *opaque_ptr(&P) : P;   // as at the refill
                 work_pixel(Pw, kk, px, py);
                 if (lazy) park.load_px(v);
                 store_sample(Pw, PS, ps, kk, px, py, v.pX, mk3s(1.0f) * v.cl);
