@@ -169,7 +169,7 @@ def test_update_switches_tree_format(ctl, orc, dev):
 
 @pytest.mark.parametrize("bvh", ["wide"])
 def test_update_tri_indices_alone_rebuilds_trees(ctl, orc, dev, bvh):
-    """CTL_DIRTY_TRI_INDICES alone, same size: the 4-wide (and 8-wide) trees
+    """CTL_DIRTY_TRI_INDICES alone, same size: the 4-wide trees
     carry per-leaf entry counts and relaid entries derived from the
     TriIntersectorData2 flags, so they are rebuilt.  The update merges leaves
     (a cleared last-in-leaf flag) and renames triangles; the image equals the
