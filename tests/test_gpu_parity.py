@@ -132,9 +132,11 @@ def test_render_direct0_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, mo
     assert wrays < 2 * wrays1
 
 
-@pytest.mark.parametrize("mpl,rr", [(1, 5), (3, 1), (8, 2)])
+@pytest.mark.parametrize("mpl,rr", [(1, 5), (3, 1), (8, 2), (50, 50)])
 def test_render_short_paths_and_rr(ctl, orc, tracer, dev, mpl, rr):
-    """MaxPathLength / RRStartDepth edge values (PathTracer.h:16-19)."""
+    """MaxPathLength / RRStartDepth edge values (PathTracer.h:16-19); (50, 50):
+    no Russian roulette in the closed box, so paths run far past the sampler's
+    30-row tables (the draw counters wrap, SamplerDev keeps them mod len)."""
     d = scene(ctl, 1, 1.0, 64, 64)
     p = ctl.PTParams(1, mpl, rr, 1, 64, 1, 0, 0)
     want, wrays = oracle_render(orc, d, p, 2, 64, 64)
