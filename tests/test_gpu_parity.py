@@ -132,6 +132,18 @@ def test_render_direct0_bit_exact(ctl, orc, tracer, dev, config, scale, w, h, mo
     assert wrays < 2 * wrays1
 
 
+@pytest.mark.parametrize("mode", ["megakernel", "wavefront"])
+def test_render_long_paths_other_schedules(ctl, orc, tracer, dev, mode):
+    """50 bounces without Russian roulette through the megakernel and wavefront
+    schedules (their samplers wrap the 30-row tables as the persistent one does)."""
+    d = scene(ctl, 1, 1.0, 64, 64)
+    p = ctl.PTParams(1, 50, 50, 1, 64, 1, 0, ctl.CTL_PT_MEGAKERNEL if mode == "megakernel" else ctl.CTL_PT_WAVEFRONT)
+    want, wrays = oracle_render(orc, d, p, 2, 64, 64)
+    got, grays = render_gpu(ctl, tracer, d, p, 2, 64, 64, dev)
+    assert grays == wrays
+    assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
+
+
 @pytest.mark.parametrize("mpl,rr", [(1, 5), (3, 1), (8, 2), (50, 50)])
 def test_render_short_paths_and_rr(ctl, orc, tracer, dev, mpl, rr):
     """MaxPathLength / RRStartDepth edge values (PathTracer.h:16-19); (50, 50):
@@ -496,7 +508,7 @@ def test_wpt_pass_bit_exact(ctl, orc, dev, config, scale, w, h, direct, bvh):
     assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
 
 
-@pytest.mark.parametrize("mpl,rr", [(1, 5), (2, 1), (7, 2)])
+@pytest.mark.parametrize("mpl,rr", [(1, 5), (2, 1), (7, 2), (50, 50)])
 def test_wpt_short_paths(ctl, orc, dev, mpl, rr):
     d = scene(ctl, 2, 0.25, 96, 64)
     want, wrays = wpt_oracle(orc, d, 1, 2, 96, 64, mpl, rr, first_pass=3)
