@@ -30,6 +30,7 @@ namespace ctl {
 void sampler_tables(uint64_t pass, uint32_t nseq, uint32_t len, float* seq1d, float* seq2d);
 void sampler_pass_state(uint64_t pass, uint32_t nseq, uint32_t len, uint32_t v[5], uint32_t* d);
 void sampler_step_powers(uint32_t* out, int kmax);
+void sampler_seq_powers(uint32_t* out, uint32_t len);
 }
 
 using namespace ctl;
@@ -199,33 +200,63 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
     return x;
 }
 
-__global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict__ powers, XorwowDev base,
-                                                      uint32_t nseq, uint32_t len, float* s1, float2* s2) {
+// powers: [kJumpBits] M^(2^k), then (sampler_seq_powers) [64] A^ql and
+// [64] A^(64 qh) with A = M^(3 len), then M^len and M^(len + 2 (len / 2)), all 800 words.
+// Sequence q < 4096 jumps in two rounds (A^ql, A^(64 qh)); a larger q by the
+// binary powers of its offset.  The rounds are dependent memory round trips,
+// so two instead of the ~10 set bits of q * 3 len is what the kernel's time is
+// made of (30.6 -> 18.4 us per pass).  Then three lanes draw a third of the
+// sequence each, from the states len and len + 2 (len / 2) steps on (one more round each,
+// independent of each other): lane 0 the 1-D values, lanes 1 and 2 the first
+// and second half of the 2-D pairs.
+constexpr int kSeqPowBase = kJumpBits * 800;
+// v <- M v over the wave (lane j holds input bits j, j + 64, j + 128)
+__device__ __forceinline__ void wave_apply(const uint32_t* __restrict__ M, uint32_t v[5], int lane) {
+    const bool lo = lane < 32;
+    const uint32_t sh = (uint32_t)(lane & 31);
+    const uint32_t w0 = lo ? v[0] : v[1], w1 = lo ? v[2] : v[3];
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+    auto col = [&](uint32_t word, int b) {
+        if ((word >> sh) & 1u) {
+            const uint32_t* c = M + b * 5;
+            r0 ^= c[0]; r1 ^= c[1]; r2 ^= c[2]; r3 ^= c[3]; r4 ^= c[4];
+        }
+    };
+    col(w0, lane);
+    col(w1, lane + 64);
+    if (lo) col(v[4], lane + 128);
+    v[0] = wave_xor(r0); v[1] = wave_xor(r1); v[2] = wave_xor(r2); v[3] = wave_xor(r3); v[4] = wave_xor(r4);
+}
+
+__device__ __forceinline__ void sampler_sequence(const uint32_t* __restrict__ powers, const XorwowDev& base,
+                                                 uint32_t nseq, uint32_t len, float* s1, float2* s2) {
     const uint32_t q = blockIdx.x * 4u + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (q >= nseq) return;   // whole wave
     const uint32_t off = q * len * 3;
     uint32_t v[5] = {base.v[0], base.v[1], base.v[2], base.v[3], base.v[4]};
-    for (int k = 0; k < kJumpBits; k++) {
-        if (!((off >> k) & 1u)) continue;   // uniform over the wave
-        const uint32_t* M = powers + k * 800;
-        const bool lo = lane < 32;
-        const uint32_t sh = (uint32_t)(lane & 31);
-        const uint32_t w0 = lo ? v[0] : v[1], w1 = lo ? v[2] : v[3];
-        uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
-        auto col = [&](uint32_t word, int b) {
-            if ((word >> sh) & 1u) {
-                const uint32_t* c = M + b * 5;
-                r0 ^= c[0]; r1 ^= c[1]; r2 ^= c[2]; r3 ^= c[3]; r4 ^= c[4];
-            }
-        };
-        col(w0, lane);
-        col(w1, lane + 64);
-        if (lo) col(v[4], lane + 128);
-        v[0] = wave_xor(r0); v[1] = wave_xor(r1); v[2] = wave_xor(r2); v[3] = wave_xor(r3); v[4] = wave_xor(r4);
+    const bool twoStep = q < 4096u;
+    for (int k = 0; k < (twoStep ? 2 : kJumpBits); k++) {
+        const uint32_t* M;
+        if (twoStep) {
+            const uint32_t digit = k == 0 ? (q & 63u) : (q >> 6);
+            if (!digit) continue;   // identity; uniform over the wave
+            M = powers + kSeqPowBase + (k * 64 + digit) * 800;
+        } else {
+            if (!((off >> k) & 1u)) continue;   // uniform over the wave
+            M = powers + k * 800;
+        }
+        wave_apply(M, v, lane);
     }
-    if (lane != 0) return;
-    uint32_t d = base.d + 362437u * off;
+    // the states len and len + 2 (len / 2) draws on, for lanes 1 and 2
+    uint32_t va[5] = {v[0], v[1], v[2], v[3], v[4]}, vb[5] = {v[0], v[1], v[2], v[3], v[4]};
+    wave_apply(powers + kSeqPowBase + 128 * 800, va, lane);
+    wave_apply(powers + kSeqPowBase + 129 * 800, vb, lane);
+    if (lane > 2) return;
+    uint32_t start = 0;
+    if (lane == 1) { for (int w = 0; w < 5; w++) v[w] = va[w]; start = len; }
+    if (lane == 2) { for (int w = 0; w < 5; w++) v[w] = vb[w]; start = len + 2 * (len / 2); }
+    uint32_t d = base.d + 362437u * (off + start);
     auto next = [&]() -> float {
         uint32_t t = v[0] ^ (v[0] >> 2);
         v[0] = v[1]; v[1] = v[2]; v[2] = v[3]; v[3] = v[4];
@@ -235,12 +266,36 @@ __global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict
         float f = (float)(v[4] + d) * kInv + (kInv / 2.0f);
         return f * (1 - 1e-5f);
     };
-    for (uint32_t i = 0; i < len; i++) s1[i * nseq + q] = next();
-    for (uint32_t i = 0; i < len; i++) {
-        float x = next();
-        float y = next();
-        s2[i * nseq + q] = make_float2(x, y);
+    if (lane == 0) {
+        for (uint32_t i = 0; i < len; i++) s1[i * nseq + q] = next();
+    } else {
+        // lane 1: pairs 0 .. len/2 - 1 (draws len .. len + 2 (len / 2) - 1); lane 2: the rest
+        const uint32_t i0 = lane == 1 ? 0u : len / 2, i1 = lane == 1 ? len / 2 : len;
+        for (uint32_t i = i0; i < i1; i++) {
+            float x = next();
+            float y = next();
+            s2[i * nseq + q] = make_float2(x, y);
+        }
     }
+}
+
+__global__ __launch_bounds__(256) void sampler_kernel(const uint32_t* __restrict__ powers, XorwowDev base,
+                                                      uint32_t nseq, uint32_t len, float* s1, float2* s2) {
+    sampler_sequence(powers, base, nseq, len, s1, s2);
+}
+
+// The tables of up to kSamplerBatch passes in one launch (ctl_render_passes):
+// blockIdx.y = pass slot, whose first state is B.b[slot] and whose tables
+// start slot * tbl elements in.  One launch keeps the GPU busier than a chain
+// of single-pass launches of 4096 waves each (latency-bound jump rounds).
+constexpr uint32_t kSamplerBatch = 128;
+struct SamplerBases { XorwowDev b[kSamplerBatch]; };
+static_assert(sizeof(SamplerBases) <= 3584, "sampler bases must fit the 4 KB kernel-argument segment");
+__global__ __launch_bounds__(256) void sampler_batch_kernel(const uint32_t* __restrict__ powers, SamplerBases B,
+                                                            uint32_t nseq, uint32_t len, float* s1, float2* s2,
+                                                            uint64_t tbl) {
+    const uint32_t slot = blockIdx.y;
+    sampler_sequence(powers, B.b[slot], nseq, len, s1 + slot * tbl, s2 + slot * tbl);
 }
 
 // One path per thread (the reference's pathKernel2 launch shape).
@@ -662,8 +717,9 @@ CTL_API ctl_ctx* ctl_create(int32_t device) {
         return fail("ctl_create: cursor/event allocation failed");
     }
     {
-        std::vector<uint32_t> pw((size_t)kJumpBits * 800);
+        std::vector<uint32_t> pw((size_t)kJumpBits * 800 + 130 * 800);
         ctl::sampler_step_powers(pw.data(), kJumpBits);
+        ctl::sampler_seq_powers(pw.data() + kSeqPowBase, c->len);
         if (hipMalloc(&c->d_powers, pw.size() * 4) != hipSuccess ||
             hipMemcpy(c->d_powers, pw.data(), pw.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
             ctl_destroy(c);
@@ -1047,11 +1103,13 @@ CTL_API ctl_status ctl_render_passes(ctl_ctx* c, const ctl_pt_params* params, ui
         c->mt_cap = n_passes;
     }
     CTL_HIP(c, hipEventRecord(c->pass_ev[0], s));
-    for (uint32_t i = 0; i < n_passes; i++) {
-        XorwowDev base;
-        ctl::sampler_pass_state(first_pass + i, c->nseq, c->len, base.v, &base.d);
-        hipLaunchKernelGGL(sampler_kernel, dim3((c->nseq + 3) / 4), dim3(256), 0, s, c->d_powers, base, c->nseq, c->len,
-                           c->d_mt1 + i * tbl, c->d_mt2 + i * tbl);
+    for (uint32_t i0 = 0; i0 < n_passes; i0 += kSamplerBatch) {
+        const uint32_t nb = std::min(kSamplerBatch, n_passes - i0);
+        SamplerBases B;
+        for (uint32_t i = 0; i < nb; i++)
+            ctl::sampler_pass_state(first_pass + i0 + i, c->nseq, c->len, B.b[i].v, &B.b[i].d);
+        hipLaunchKernelGGL(sampler_batch_kernel, dim3((c->nseq + 3) / 4, nb), dim3(256), 0, s, c->d_powers, B, c->nseq,
+                           c->len, c->d_mt1 + i0 * tbl, c->d_mt2 + i0 * tbl, (uint64_t)tbl);
     }
     r = prepare_slots(c, items, s);
     if (r != CTL_OK) return r;

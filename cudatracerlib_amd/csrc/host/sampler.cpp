@@ -103,6 +103,53 @@ void sampler_step_powers(uint32_t* out, int kmax) {
     for (int k = 0; k < kmax; k++) memcpy(out + (size_t)k * 800, P[k].col, 800 * sizeof(uint32_t));
 }
 
+// Jumps to a sequence's first draw in two steps: with A = M^(3 len) (one
+// sequence's draws), sequence q = 64 qh + ql starts at A^ql A^(64 qh) times the
+// pass's first state.  out: [ql = 0..63] A^ql, then [qh = 0..63] A^(64 qh),
+// then M^len and M^(len + 2 floor(len / 2)) (where a sequence's 2-D pairs and
+// their second half start), 160 columns x 5 words each (130 x 800 words; index
+// 0 of each half of the first 128 is the identity).
+void sampler_seq_powers(uint32_t* out, uint32_t len) {
+    const auto& P = step_powers();
+    for (int m = 1; m <= 2; m++) {
+        const uint64_t st = m == 1 ? (uint64_t)len : (uint64_t)len + 2ull * (len / 2);
+        uint32_t* dst = out + (size_t)(127 + m) * 800;
+        for (int j = 0; j < 160; j++) {
+            uint32_t v[5] = {0, 0, 0, 0, 0};
+            v[j >> 5] = 1u << (j & 31);
+            for (int b = 0; b < 64; b++)
+                if ((st >> b) & 1) apply(P[b], v);
+            memcpy(dst + j * 5, v, sizeof(v));
+        }
+    }
+    const uint64_t steps = 3ull * len;
+    Gf2Matrix A, cur, next;
+    for (int j = 0; j < 160; j++) {
+        uint32_t v[5] = {0, 0, 0, 0, 0};
+        v[j >> 5] = 1u << (j & 31);
+        for (int b = 0; b < 64; b++)
+            if ((steps >> b) & 1) apply(P[b], v);
+        memcpy(A.col[j], v, sizeof(v));
+    }
+    for (int half = 0; half < 2; half++) {
+        // step matrix of this half: A, then A^64
+        Gf2Matrix S = A;
+        if (half == 1)
+            for (int j = 0; j < 160; j++)
+                for (int r = 1; r < 64; r++) apply(A, S.col[j]);
+        memset(&cur, 0, sizeof(cur));
+        for (int j = 0; j < 160; j++) cur.col[j][j >> 5] = 1u << (j & 31);   // identity
+        for (int i = 0; i < 64; i++) {
+            memcpy(out + ((size_t)half * 64 + i) * 800, cur.col, 800 * sizeof(uint32_t));
+            for (int j = 0; j < 160; j++) {
+                memcpy(next.col[j], cur.col[j], sizeof(next.col[j]));
+                apply(S, next.col[j]);
+            }
+            cur = next;
+        }
+    }
+}
+
 void sampler_tables(uint64_t pass, uint32_t nseq, uint32_t len, float* seq1d, float* seq2d) {
     const uint64_t per_pass = (uint64_t)nseq * len * 3;
     XorwowState s = xorwow_at(1234, 7539414, pass * per_pass);
