@@ -464,13 +464,14 @@ def reference_order_record():
     return out
 
 
-def wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_index, passes):
+def wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_index, passes, flags=0):
     """WavefrontPathTracer::DoRender (ctl_wpt_render_pass) on the same context and
     scene: the batch traversal's second caller.  The first
-    pass allocates the queues and is not counted."""
+    pass allocates the queues and is not counted.  flags: ctl_wpt_params.flags
+    (CTL_WPT_SHADOW_ANY_HIT: shadow rays as the any-hit query)."""
     import ctypes as C
     fb = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
-    prm = ctl.WptParams(1, 50, 5, 0, 0)
+    prm = ctl.WptParams(1, 50, 5, 0, flags)
     L = ctl.lib()
     ms, rays = [], []
     for k in range(passes + 1):
@@ -484,6 +485,7 @@ def wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_index, passes):
             rays.append(pt.rays_traced())
     per = sum(ms) / len(ms)
     return {"integrator": "WavefrontPathTracer (DoubleRayBuffer queues + batch traversal)",
+            "shadow_rays": "any-hit query" if flags & 1 else "closest hit + distance compare (reference)",
             "passes": passes, "ms_per_pass": round(per, 3), "rays_per_pass": int(sum(rays) / len(rays)),
             "mrays_s": round(sum(rays) / (sum(ms) * 1e-3) / 1e6, 2)}
 
@@ -783,6 +785,8 @@ def main(argv=None):
     prim = primary_ray_leg(pt, dev, stream, sptr, torch, nxt, prof) if rank == 0 else None
     wpt = (wpt_leg(ctl, pt, dev, sptr, torch, W, H, nxt + 1, a.wpt_passes)
            if rank == 0 and a.wpt_passes > 0 else None)
+    if wpt is not None:   # the same integrator with the any-hit shadow query (CTL_WPT_SHADOW_ANY_HIT)
+        wpt["shadow_any_hit"] = wpt_leg(ctl, pt, dev, sptr, torch, W, H, nxt + 1, a.wpt_passes, flags=1)
     c1 = None
     if rank == 0 and a.prim_passes > 0:
         try:   # a side leg: its failure is reported in the line, not fatal to the headline

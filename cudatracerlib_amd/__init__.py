@@ -502,9 +502,10 @@ class WavefrontPathTracer(Tracer):
     tracing over a DoubleRayBuffer, the batch traversal's second caller.  Defaults
     Direct=1, MaxPathLength=50, RRStartDepth=5 (WavefrontPathTracer.h:32-37)."""
 
-    def __init__(self, device=0, direct=True, max_path_length=50, rr_start_depth=5):
+    def __init__(self, device=0, direct=True, max_path_length=50, rr_start_depth=5, shadow_any_hit=False):
         super().__init__(device)
-        self.params = WptParams(1 if direct else 0, max_path_length, rr_start_depth, 0, 0)
+        self.params = WptParams(1 if direct else 0, max_path_length, rr_start_depth, 0,
+                                _abi.CTL_WPT_SHADOW_ANY_HIT if shadow_any_hit else 0)
         self.passes_done = 0
 
     def do_pass(self, fb_ptr, pass_index, new_trace=False, stream=0):

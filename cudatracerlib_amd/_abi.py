@@ -192,6 +192,9 @@ PRIM_DRAW_MODES = ["linear_depth", "D3D_depth", "v_absdot_n_geo", "v_dot_n_geo",
                    "first_non_delta_Le", "first_non_delta_f", "first_non_delta_f_direct"]
 
 
+CTL_WPT_SHADOW_ANY_HIT = 1 << 0   # ctl_wpt_params.flags
+
+
 class WptParams(C.Structure):
     _fields_ = [("direct", C.c_int32), ("max_path_length", C.c_int32), ("rr_start_depth", C.c_int32),
                 ("passes_done", C.c_uint32), ("flags", C.c_uint32)]

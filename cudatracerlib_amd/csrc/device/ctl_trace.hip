@@ -524,10 +524,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
 // grid; lanes whose ray finished take the next ray from a wave-aggregated
 // atomic cursor between traversal rounds (the reference fetches per warp per
 // batch of 32 rays, :379-399), so waves stay full on incoherent rays.
-template <bool ANY, bool STATS, bool SINGLE, int WIDE>
+template <int ANY, bool STATS, bool SINGLE, int WIDE>
 // Two segments (rays, hits)[0, n) then (rays2, hits2)[0, n2) in one launch: the
 // wavefront tracer's payload and secondary batches share one resident grid and
-// one tail.
+// one tail.  ANY: 0 closest hit, 1 any hit (intersectKernel<true>, culled at the
+// ray's tmax), 2 closest hit for the first segment and, for the second, the
+// shadow query (any hit below tmax, boxes culled at tmax + slab_slack: the
+// WavefrontPathTracer's CTL_WPT_SHADOW_ANY_HIT).
 #ifndef CTL_REFILL_MIN
 #define CTL_REFILL_MIN 40   // batch traversal: refill once at least this many lanes of the wave wait for a ray
                            // (C3 WPT sweep 1/8/24/32/40/48/56: 1093/1222/1505/1563/1564/1569/1545 Mrays/s)
@@ -548,7 +551,7 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64
     const int64_t total = n + n2;
     CTL_LANE_STACK(st);
     TraceStats ts{0, 0, 0};
-    Traverser<ANY ? 1 : 0, STATS, SINGLE, WIDE> T;
+    Traverser<ANY, STATS, SINGLE, WIDE> T;
     T.done = true;
     bool haveRay = false, exhausted = false, ovf = false, seg2 = false;
     int64_t ray = 0;   // slot in its segment
@@ -590,7 +593,9 @@ __global__ __launch_bounds__(kBlock) void intersect_kernel(DevScene S_arg, int64
                     haveRay = true;
                     const float4* r4 = reinterpret_cast<const float4*>(seg2 ? rays2 + ray : rays + ray);
                     const float4 o = r4[0], d = r4[1];
-                    T.init(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), o.w, o.w, d.w, st, &ts);
+                    if (ANY == 2) T.anyhit = seg2;
+                    T.init(S, mk3(o.x, o.y, o.z), mk3(d.x, d.y, d.z), o.w, o.w, d.w, st, &ts,
+                           ANY == 2 && seg2 ? d.w : -1.0f);
                 } else {
                     exhausted = true;
                 }
@@ -839,8 +844,9 @@ static ctl_status launch_intersect(ctl_ctx* c, int64_t n, const ctl_ray* rays, c
         else if (wide) { if (single) IK(AN, false, true, 1); else IK(AN, false, false, 1); } \
         else { if (single) IK(AN, false, true, 0); else IK(AN, false, false, 0); } \
     } while (0)
-    if (stats) { if (any_hit) IK2(true, true); else IK2(false, true); }
-    else { if (any_hit) IK2(true, false); else IK2(false, false); }
+    if (stats) { if (any_hit) IK2(1, true); else IK2(0, true); }
+    else if (any_hit == 2) IK2(2, false);   // internal: the WavefrontPathTracer's shadow query segment
+    else { if (any_hit) IK2(1, false); else IK2(0, false); }
 #undef IK2
 #undef IK
     CTL_HIP(c, hipGetLastError());
@@ -851,7 +857,7 @@ static ctl_status add_rays(ctl_ctx* c, uint64_t n, hipStream_t s);
 
 CTL_API ctl_status ctl_intersect(ctl_ctx* c, int64_t n, const ctl_ray* d_rays, ctl_hit* d_hits, int32_t any_hit,
                                  void* stream) {
-    ctl_status r = launch_intersect(c, n, d_rays, d_hits, any_hit, false, stream);
+    ctl_status r = launch_intersect(c, n, d_rays, d_hits, any_hit ? 1 : 0, false, stream);
     if (r != CTL_OK) return r;
     // the batch call counts N rays (g_RayTracedCounterHost += N, TraceHelper.cu:745)
     return add_rays(c, (uint64_t)n, reinterpret_cast<hipStream_t>(stream));
@@ -1250,7 +1256,7 @@ CTL_API ctl_status ctl_intersect_stats(ctl_ctx* c, int64_t n, const ctl_ray* d_r
     CTL_HIP(c, hipStreamSynchronize(s));
     CTL_HIP(c, hipMemset(c->d_counters + 2, 0, 3 * sizeof(unsigned long long)));
     CTL_HIP(c, hipMemcpy(&before, c->d_counters, sizeof(before), hipMemcpyDeviceToHost));
-    ctl_status r = launch_intersect(c, n, d_rays, d_hits, any_hit, true, stream);
+    ctl_status r = launch_intersect(c, n, d_rays, d_hits, any_hit ? 1 : 0, true, stream);
     if (r != CTL_OK) return r;
     if ((r = add_rays(c, (uint64_t)n, s)) != CTL_OK) return r;
     return read_stats(c, out, before, s);

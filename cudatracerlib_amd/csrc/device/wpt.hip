@@ -73,6 +73,7 @@ struct WptArgs {
     int32_t depth, max_path_length, rr_start_depth;
     uint32_t skip;       // rng.skip(iterationIdx + 2), iterationIdx = m_uPassesDone
     bool half_quirk;
+    bool shadow_any;     // CTL_WPT_SHADOW_ANY_HIT: shadow rays as the any-hit query to dist (1 - eps)
     float4* samples;     // non-null: samples go to per-source slots, folded by wpt_fold_kernel
 };
 
@@ -244,7 +245,10 @@ __global__ __launch_bounds__(kBlock) void wpt_iterate_kernel(DevScene S_arg, Wpt
                         p.b.w = dRec.dist;
                         ctl_ray sr;
                         sr.o[0] = dg.P.x; sr.o[1] = dg.P.y; sr.o[2] = dg.P.z; sr.tmin = S.ray_eps;
-                        sr.d[0] = dRec.d.x; sr.d[1] = dRec.d.y; sr.d[2] = dRec.d.z; sr.tmax = FLT_MAX;
+                        // any-hit form: accept t < dist (1 - eps), the bound the compare
+                        // in the next iteration tests the closest hit against
+                        sr.d[0] = dRec.d.x; sr.d[1] = dRec.d.y; sr.d[2] = dRec.d.z;
+                        sr.tmax = A.shadow_any ? p.b.w * (1 - S.ray_eps) : FLT_MAX;
                         sec_tmp[j] = sr;
                         shadow = true;   // dIdx = its slot, set by the scatter
                     }
@@ -467,6 +471,7 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
     A.rr_start_depth = prm->rr_start_depth;
     A.skip = prm->passes_done + 2u;
     A.half_quirk = c->half_quirk;
+    A.shadow_any = (prm->flags & CTL_WPT_SHADOW_ANY_HIT) != 0;
     A.depth = 0;
     A.samples = nullptr;
     if (cam.width > 2048u || cam.height > 2048u) {
@@ -534,7 +539,7 @@ int wpt_pass(ctl_ctx* c, const ctl_wpt_params* prm, ctl_pixel* fb, hipStream_t s
         // hit), as one launch over both batches (one resident grid, one tail);
         // the kernel counts the rays it traces
         // bounce 0: the camera rays, one per pixel in row order, traced in 8 x 8 blocks
-        int r = intersect_launch(c, ub, B->rays[cur], B->hits, 0, s, depth ? ub : 0, B->sec, B->sec_hits, cnt,
+        int r = intersect_launch(c, ub, B->rays[cur], B->hits, A.shadow_any ? 2 : 0, s, depth ? ub : 0, B->sec, B->sec_hits, cnt,
                                  depth == 0 && (uint64_t)n0 == (uint64_t)A.width * A.height ? A.width : 0u);
         if (r != CTL_OK) return r;
         A.depth = depth;

@@ -617,8 +617,17 @@ typedef struct {
     int32_t rr_start_depth;    /* KEY_RRStartDepth, default 5                    */
     uint32_t passes_done;      /* Tracer::m_uPassesDone inside this DoRender: 1  */
                                /* for the first pass of a trace (Tracer.h:231)   */
-    uint32_t flags;            /* reserved, 0                                    */
+    uint32_t flags;            /* CTL_WPT_* below, else 0                        */
 } ctl_wpt_params;
+
+/* ctl_wpt_params.flags.  CTL_WPT_SHADOW_ANY_HIT: trace the secondary (shadow)
+ * rays as the any-hit query over (eps, dist (1 - eps)), boxes culled at that
+ * bound + slab_slack(ray) (the path tracer's shadow_any_hit query),
+ * instead of the reference's closest hit and distance compare
+ * (WavefrontPathTracer.cu:58-63).  The visibility is the same wherever the
+ * slab slack bounds the rounding (measured: tests/test_gpu_parity.py); the
+ * default (0) is the reference's query. */
+enum { CTL_WPT_SHADOW_ANY_HIT = 1u << 0 };
 
 /* One WavefrontPathTracer::DoRender (WavefrontPathTracer.cu:152-189) into
  * d_fb[width*height]: pathCreateKernelWPT (one camera ray per pixel, the

@@ -468,8 +468,9 @@ def test_render_alpha_tested_traversal(ctl, orc, tracer, dev, mode, bvh):
 
 # ---- WavefrontPathTracer over the batch traversal ----------
 
-def wpt_gpu(ctl, desc, direct, passes, w, h, dev, max_path_length=50, rr=5, first_pass=1):
-    wt = ctl.WavefrontPathTracer(0, direct=direct, max_path_length=max_path_length, rr_start_depth=rr)
+def wpt_gpu(ctl, desc, direct, passes, w, h, dev, max_path_length=50, rr=5, first_pass=1, shadow_any_hit=False):
+    wt = ctl.WavefrontPathTracer(0, direct=direct, max_path_length=max_path_length, rr_start_depth=rr,
+                                 shadow_any_hit=shadow_any_hit)
     wt.upload_scene(desc)
     fb = torch.zeros((w * h, 7), dtype=torch.float32, device=dev)
     wt.reset_rays()
@@ -506,6 +507,20 @@ def test_wpt_pass_bit_exact(ctl, orc, dev, config, scale, w, h, direct, bvh):
     assert want[:, 6].min() == 2 and np.isfinite(got).all()
     bad = np.nonzero((want.view(np.uint32) != got.view(np.uint32)).any(axis=1))[0]
     assert bad.size == 0, (bad[:10], want[bad[:3]], got[bad[:3]])
+
+
+@pytest.mark.parametrize("config,scale,w,h", [(1, 1.0, 64, 64), (2, 0.25, 96, 64), (3, 0.003, 64, 48),
+                                              (5, 0.003, 64, 48)])
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_wpt_shadow_any_hit_equals_reference(ctl, orc, dev, config, scale, w, h, bvh):
+    """CTL_WPT_SHADOW_ANY_HIT: the secondary rays as the any-hit shadow query
+    (tmax = dist (1 - eps), culled at tmax + slab slack) give the image of the
+    reference's closest hit + distance compare (the oracle), bit for bit."""
+    d = select_bvh(scene(ctl, config, scale, w, h), bvh)
+    want, wrays = wpt_oracle(orc, d, 1, 2, w, h, first_pass=5)
+    got, grays = wpt_gpu(ctl, d, 1, 2, w, h, dev, first_pass=5, shadow_any_hit=True)
+    assert grays == wrays
+    assert np.array_equal(want.view(np.uint32), got.view(np.uint32))
 
 
 @pytest.mark.parametrize("mpl,rr", [(1, 5), (2, 1), (7, 2), (50, 50)])
