@@ -33,7 +33,7 @@ PASSES = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 FAMILIES = {
     "path_kernel": "path_kernel_persistent<false, true, 1, 0>",
     "path_kernel_full": "path_kernel_persistent<false, true, 1, 1>",
-    "primary_intersect": "intersect_kernel<false, false, true, 1>",
+    "primary_intersect": "intersect_kernel<0, false, true, 1>",
     "prim_kernel": "prim_kernel<",
     "fold_samples": "fold_samples_kernel",
     "sampler": "sampler_kernel",
@@ -50,6 +50,9 @@ for f in sorted(glob.glob(os.path.join(root, "g*", "**", "*counter_collection.cs
         agg[fam][c] += float(row.get("Counter_Value", 0))
         disp[fam][c].add((f, row.get("Dispatch_Id")))
 
+missing = [k for k in ("path_kernel", "primary_intersect") if k not in agg]
+if missing:   # a renamed template must not silently drop a roofline (it did once: bool -> int ANY)
+    raise SystemExit(f"no counter rows matched families {missing}; check FAMILIES against the kernel names")
 here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # the repo root
 sys.path.insert(0, here)
 from buildid import source_fingerprint  # noqa: E402
