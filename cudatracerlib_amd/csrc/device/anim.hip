@@ -4,12 +4,15 @@
 //   skin     g_ComputeVertices (AnimatedMesh.cu:29-43): per vertex, two 8-bone
 //            matrix blends, TransformPoint / TransformDirection, lerp
 //   tris     g_ComputeTriangles -> TriangleData::setData (TriangleData.cu:35-63)
-//   entries  per BVH entry: Woop data (AnimProvider::setObject, AnimatedMesh.cpp:
-//            113-117) and the triangle's box
-//   refit    bottom-up box refit of the mesh's binary tree, one launch per wide
-//            level (deepest first) and one single-block launch for the narrow
-//            top levels; the 4-wide copy then gathers its boxes from the binary
-//            children they came from
+//   leaves   per leaf of the mesh tree, its entries' Woop data (AnimProvider::
+//            setObject, AnimatedMesh.cpp:113-117) and the union of their
+//            triangles' boxes, stored straight into the parent's child slot
+//   refit    bottom-up box refit of the mesh's inner children: the subtrees of at
+//            most kSubMax inner nodes in one launch, one block each, level by
+//            level between block barriers; the nodes above them one launch per
+//            wide level (deepest first) and one single-block launch for the
+//            narrow top levels; the 4-wide copy then gathers its boxes from the
+//            binary children they came from
 //   scene    instance boxes (mesh box x node transform), refit of the scene's
 //            binary tree + gather into its 4-wide copy, scene box -> m_rayTraceEps
 //
@@ -35,10 +38,22 @@ namespace ctl {
 
 struct AnimTree {
     uint32_t base = 0;                  // float4 offset of the tree's node 0
-    std::vector<uint32_t> level_off;    // [levels + 1] offsets into order, deepest level first
+    // The nodes refit by one block (refit_block_kernel): a record {node, child 0,
+    // child 1} per node, grouped in block sets, each set's levels deepest first.
+    struct Blocks {
+        uint32_t n_sets = 0, max_nodes = 0;
+        uint4* d_rec = nullptr;
+        uint32_t* d_lvl = nullptr;      // [levels + 1] level offsets into d_rec, all sets
+        uint32_t* d_first = nullptr;    // [n_sets + 1] first level of each set
+    };
+    Blocks sub;                         // the subtrees below the cut, one set each
+    Blocks top;                         // the narrow levels at the top of the tree, one set
+    // the levels in between, too wide for one block: one launch each, deepest first
+    std::vector<uint32_t> level_off;    // [levels + 1] offsets into d_order
     uint32_t* d_order = nullptr;        // node indices relative to base
-    uint32_t* d_level_off = nullptr;
-    uint32_t top_first = 0;             // levels from here on are small: one single-block launch
+    // mesh trees: the leaves, boxed by anim_leaf_kernel
+    uint32_t n_leaf = 0;
+    uint4* d_leaf = nullptr;            // {node << 1 | child, first entry, entries, 0}
     bool valid = false;
 };
 
@@ -71,7 +86,6 @@ struct AnimState {
     float* h_eps = nullptr;             // pinned
     float4* d_P = nullptr;
     float4* d_N = nullptr;
-    float4* d_ebox = nullptr;           // 2 per BVH entry
     size_t tmp_cap = 0;
     float* d_bones[2] = {nullptr, nullptr};
     size_t bones_cap = 0;
@@ -83,7 +97,14 @@ namespace {
 
 constexpr int32_t kSent = 0x76543210;
 constexpr int kAB = 256;
-constexpr uint32_t kTopMax = 512;    // levels at most this wide go to the single-block refit
+constexpr uint32_t kTopMax = 512;    // levels at most this wide go to the single-block top set ...
+constexpr uint32_t kTopLds = 1536;   // ... of at most this many nodes (boxes + records in LDS: 60 KB)
+constexpr uint32_t kSubMax = 511;    // inner nodes of a subtree refit by one block
+// child references of a block record: an LDS slot (the set's own node), or
+constexpr uint32_t kRefGlobal = 0x40000000u;   // | node: a node refit earlier (its child slots in memory)
+constexpr uint32_t kRefInst = 0x80000000u;     // | instance: a scene-tree leaf
+constexpr uint32_t kRefLeafSlot = 0xfffffffeu; // a mesh leaf, its slot written by anim_leaf_kernel
+constexpr uint32_t kRefNone = 0xffffffffu;     // an empty child
 
 __device__ __forceinline__ void box_empty(float lo[3], float hi[3]) {
     lo[0] = lo[1] = lo[2] = FLT_MAX;
@@ -128,48 +149,6 @@ __global__ __launch_bounds__(kAB) void anim_tri_kernel(const uint32_t* __restric
     td[t] = r;
 }
 
-// Per BVH entry: its Woop data (AnimProvider::setObject, AnimatedMesh.cpp:113-117)
-// and its triangle's box, one thread per entry.
-__global__ __launch_bounds__(kAB) void anim_entry_kernel(const uint32_t* __restrict__ idx, uint32_t n,
-                                                        const uint32_t* __restrict__ tris,
-                                                        const float4* __restrict__ P, float4* woop, float4* ebox) {
-    const uint32_t e = blockIdx.x * kAB + threadIdx.x;
-    if (e >= n) return;
-    const uint32_t t = idx[e] >> 1;
-    const f3 a = ld3(P, tris[3 * t]), b = ld3(P, tris[3 * t + 1]), c = ld3(P, tris[3 * t + 2]);
-    float w[12];
-    woop_set_hd(a, b, c, w);
-    woop[3 * e] = make_float4(w[0], w[1], w[2], w[3]);
-    woop[3 * e + 1] = make_float4(w[4], w[5], w[6], w[7]);
-    woop[3 * e + 2] = make_float4(w[8], w[9], w[10], w[11]);
-    ebox[2 * e] = make_float4(tmin(tmin(a.x, b.x), c.x), tmin(tmin(a.y, b.y), c.y), tmin(tmin(a.z, b.z), c.z), 0.0f);
-    ebox[2 * e + 1] = make_float4(tmax(tmax(a.x, b.x), c.x), tmax(tmax(a.y, b.y), c.y), tmax(tmax(a.z, b.z), c.z), 0.0f);
-}
-
-// Box of a leaf value: mesh trees (SCENE = false) take the union of their entry
-// run's triangle boxes; the scene tree's leaves are instances (~node).
-struct LeafCtx {
-    const uint32_t* idx;     // mesh entries (TriIntersectorData2), relative to the mesh
-    const float4* ebox;      // entry triangle boxes (lo, hi)
-    const float* inst;       // instance boxes (scene)
-};
-
-template <bool SCENE>
-__device__ __forceinline__ void leaf_box(const LeafCtx& L, int32_t v, float lo[3], float hi[3]) {
-    if (SCENE) {
-        const float* b = L.inst + 6 * (uint32_t)~v;
-        for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
-        return;
-    }
-    box_empty(lo, hi);
-    for (uint32_t e = (uint32_t)~v;; e++) {
-        const float4 a = L.ebox[2 * e], b = L.ebox[2 * e + 1];
-        const float q0[3] = {a.x, a.y, a.z}, q1[3] = {b.x, b.y, b.z};
-        box_extend(lo, hi, q0, q1);
-        if (L.idx[e] & 1) break;
-    }
-}
-
 // BVHNodeData child boxes (the reference layout, TriIntersectorData.h:44-50)
 __device__ __forceinline__ void bin_child_box(const float* nd, int c, float lo[3], float hi[3]) {
     const int o = c ? 4 : 0, z = c ? 10 : 8;
@@ -179,13 +158,75 @@ __device__ __forceinline__ void bin_set_child_box(float* nd, int c, const float 
     const int o = c ? 4 : 0, z = c ? 10 : 8;
     nd[o] = lo[0]; nd[o + 1] = hi[0]; nd[o + 2] = lo[1]; nd[o + 3] = hi[1]; nd[z] = lo[2]; nd[z + 1] = hi[2];
 }
-__device__ __forceinline__ void bin_node_box(const float* nd, float lo[3], float hi[3]) {
+// Per leaf of a mesh tree (one thread): each entry of its run gets its Woop
+// data (AnimProvider::setObject, AnimatedMesh.cpp:113-117), and the union of
+// the entries' triangle boxes, in entry order, goes into the parent's child
+// slot.  The leaves cover every entry once (checked by the plan), and the plan
+// counts each run, so an entry's loads do not wait for the previous end bit.
+__global__ __launch_bounds__(kAB) void anim_leaf_kernel(const uint4* __restrict__ leaves, uint32_t n,
+                                                       const uint32_t* __restrict__ idx, const uint32_t* __restrict__ tris,
+                                                       const float4* __restrict__ P, float4* woop, float* nodes) {
+    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
+    if (i >= n) return;
+    const uint4 lf = leaves[i];
+    float lo[3], hi[3];
     box_empty(lo, hi);
-    for (int c = 0; c < 2; c++) {
-        if (__float_as_int(nd[12 + c]) == kSent) continue;
-        float a[3], b[3];
-        bin_child_box(nd, c, a, b);
+#pragma unroll 2
+    for (uint32_t e = lf.y; e < lf.y + lf.z; e++) {
+        const uint32_t t = idx[e] >> 1;
+        const f3 a = ld3(P, tris[3 * t]), b = ld3(P, tris[3 * t + 1]), c = ld3(P, tris[3 * t + 2]);
+        float w[12];
+        woop_set_hd(a, b, c, w);
+        woop[3 * e] = make_float4(w[0], w[1], w[2], w[3]);
+        woop[3 * e + 1] = make_float4(w[4], w[5], w[6], w[7]);
+        woop[3 * e + 2] = make_float4(w[8], w[9], w[10], w[11]);
+        const float q0[3] = {tmin(tmin(a.x, b.x), c.x), tmin(tmin(a.y, b.y), c.y), tmin(tmin(a.z, b.z), c.z)};
+        const float q1[3] = {tmax(tmax(a.x, b.x), c.x), tmax(tmax(a.y, b.y), c.y), tmax(tmax(a.z, b.z), c.z)};
+        box_extend(lo, hi, q0, q1);
+    }
+    bin_set_child_box(nodes + 16 * (size_t)(lf.x >> 1), (int)(lf.x & 1u), lo, hi);
+}
+
+// Leaf boxes of the scene tree: its leaves are instances (~node).  Mesh trees
+// (SCENE = false) have their leaf slots written by anim_leaf_kernel.
+struct LeafCtx {
+    const float* inst;       // instance boxes (scene)
+};
+
+// The node's box: the union of its non-empty child slots, in slot order.  The
+// whole 64-B node is loaded up front (four 16-B loads in flight, `nd` 16-B
+// aligned) rather than a slot after its sentinel test.
+__device__ __forceinline__ void bin_node_box(const float* nd, float lo[3], float hi[3]) {
+    const float4* n4 = reinterpret_cast<const float4*>(nd);
+    const float4 q0 = n4[0], q1 = n4[1], q2 = n4[2], q3 = n4[3];
+    box_empty(lo, hi);
+    if (__float_as_int(q3.x) != kSent) {
+        const float a[3] = {q0.x, q0.z, q2.x}, b[3] = {q0.y, q0.w, q2.y};
         box_extend(lo, hi, a, b);
+    }
+    if (__float_as_int(q3.y) != kSent) {
+        const float a[3] = {q1.x, q1.z, q2.z}, b[3] = {q1.y, q1.w, q2.w};
+        box_extend(lo, hi, a, b);
+    }
+}
+
+// One node: its children's boxes from their leaves or from the children's own
+// (already refit) child boxes.
+template <bool SCENE>
+__device__ __forceinline__ void refit_node(float* nodes, uint32_t k, const LeafCtx& L) {
+    float* nd = nodes + 16 * (size_t)k;
+    for (int c = 0; c < 2; c++) {
+        const int32_t v = __float_as_int(nd[12 + c]);
+        if (v == kSent) continue;
+        float lo[3], hi[3];
+        if (v < 0) {
+            if (!SCENE) continue;   // written by anim_leaf_kernel
+            const float* b = L.inst + 6 * (uint32_t)~v;
+            for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
+        } else {
+            bin_node_box(nodes + 16 * (size_t)(v >> 2), lo, hi);
+        }
+        bin_set_child_box(nd, c, lo, hi);
     }
 }
 
@@ -194,36 +235,61 @@ __global__ __launch_bounds__(kAB) void refit_bin_kernel(float* nodes, const uint
                                                        LeafCtx L) {
     const uint32_t i = blockIdx.x * kAB + threadIdx.x;
     if (i >= n) return;
-    float* nd = nodes + 16 * (size_t)order[i];
-    for (int c = 0; c < 2; c++) {
-        const int32_t v = __float_as_int(nd[12 + c]);
-        if (v == kSent) continue;
-        float lo[3], hi[3];
-        if (v < 0) leaf_box<SCENE>(L, v, lo, hi);
-        else bin_node_box(nodes + 16 * (size_t)(v >> 2), lo, hi);
-        bin_set_child_box(nd, c, lo, hi);
-    }
+    refit_node<SCENE>(nodes, order[i], L);
 }
 
-// The levels that hold few nodes (the top of the tree) in one block, level by
-// level with a barrier in between, instead of one launch each.
+// One node of a block set: each child slot from its reference, and the node's
+// own box (the union of its slots, in slot order as bin_node_box takes it) into
+// LDS for its parent in the same set.
 template <bool SCENE>
-__global__ __launch_bounds__(1024) void refit_bin_top_kernel(float* nodes, const uint32_t* __restrict__ order,
-                                                            const uint32_t* __restrict__ level_off, uint32_t n_levels,
-                                                            LeafCtx L) {
-    for (uint32_t l = 0; l < n_levels; l++) {
-        for (uint32_t i = level_off[l] + threadIdx.x; i < level_off[l + 1]; i += 1024) {
-            float* nd = nodes + 16 * (size_t)order[i];
-            for (int c = 0; c < 2; c++) {
-                const int32_t v = __float_as_int(nd[12 + c]);
-                if (v == kSent) continue;
-                float lo[3], hi[3];
-                if (v < 0) leaf_box<SCENE>(L, v, lo, hi);
-                else bin_node_box(nodes + 16 * (size_t)(v >> 2), lo, hi);
-                bin_set_child_box(nd, c, lo, hi);
+__device__ __forceinline__ void refit_rec(float* nodes, const uint4 q, float* sbox, uint32_t self, const LeafCtx& L) {
+    float* nd = nodes + 16 * (size_t)q.x;
+    float ulo[3], uhi[3];
+    box_empty(ulo, uhi);
+    for (int c = 0; c < 2; c++) {
+        const uint32_t r = c ? q.z : q.y;
+        if (r == kRefNone) continue;
+        float lo[3], hi[3];
+        if (r == kRefLeafSlot) {
+            bin_child_box(nd, c, lo, hi);
+        } else {
+            if (r < kRefGlobal) {
+                const float* b = sbox + 6 * r;
+                for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
+            } else if (r < kRefInst) {
+                bin_node_box(nodes + 16 * (size_t)(r - kRefGlobal), lo, hi);
+            } else {
+                const float* b = L.inst + 6 * (size_t)(r - kRefInst);
+                for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
             }
+            bin_set_child_box(nd, c, lo, hi);
         }
-        __syncthreads();
+        box_extend(ulo, uhi, lo, hi);
+    }
+    float* o = sbox + 6 * self;
+    for (int k = 0; k < 3; k++) { o[k] = ulo[k]; o[3 + k] = uhi[k]; }
+}
+
+// Block sets (the subtrees below the cut, one per block; the narrow top of the
+// tree in one block): the set's records staged in LDS once, then level after
+// level with the boxes handed up through LDS.  The barrier between levels waits
+// for this wave's LDS traffic only: the node stores are read by no one in this
+// launch.  LDS: max_nodes (even) x (6 floats + one record).
+template <bool SCENE, int NT>
+__global__ __launch_bounds__(NT) void refit_block_kernel(float* nodes, const uint4* __restrict__ rec,
+                                                        const uint32_t* __restrict__ lvl,
+                                                        const uint32_t* __restrict__ first, uint32_t max_nodes,
+                                                        LeafCtx L) {
+    extern __shared__ float sbox[];
+    uint4* srec = reinterpret_cast<uint4*>(sbox + 6 * max_nodes);
+    const uint32_t l0 = first[blockIdx.x], l1 = first[blockIdx.x + 1];
+    const uint32_t base = lvl[l0], end = lvl[l1];
+    for (uint32_t i = base + threadIdx.x; i < end; i += NT) srec[i - base] = rec[i];
+    __syncthreads();
+    for (uint32_t l = l0; l < l1; l++) {
+        for (uint32_t i = lvl[l] - base + threadIdx.x; i < lvl[l + 1] - base; i += NT)
+            refit_rec<SCENE>(nodes, srec[i], sbox, i, L);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 }
 
@@ -317,59 +383,172 @@ bool anim_upload(AnimState* A, T** dst, const T* src, size_t n) {
     return n == 0 || hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
 }
 
-// Level plan of a tree: depth of every inner node by DFS from its root,
-// grouped deepest first.  `kids(k, out)` lists the inner children of node k.
-template <class KIDS>
-bool plan_tree(AnimState* A, AnimTree& T, uint32_t base, uint32_t n_nodes, uint32_t root, KIDS kids, std::string& err) {
-    T.base = base;
+bool upload_blocks(AnimState* A, AnimTree::Blocks& B, const std::vector<uint4>& rec, const std::vector<uint32_t>& lvl,
+                   const std::vector<uint32_t>& first) {
+    B.n_sets = (uint32_t)first.size() - 1;
+    B.max_nodes += B.max_nodes & 1u;   // even: the records after the boxes stay 16-B aligned
+    return anim_upload(A, &B.d_rec, rec.data(), rec.size()) && anim_upload(A, &B.d_lvl, lvl.data(), lvl.size()) &&
+           anim_upload(A, &B.d_first, first.data(), first.size());
+}
+
+// Refit plan of a binary tree (BVHNodeData, TriIntersectorData.h:44-50).
+//   - the cut: the subtrees of at most kSubMax inner nodes hanging off the
+//     nodes above them, one block set each;
+//   - above the cut, by depth from the root, deepest first: the narrow levels
+//     at the top (each at most kTopMax wide, together at most kTopLds) in one
+//     block set, the wider levels below them one launch each.
+// A mesh tree (n_entries > 0, `idx` its entries' TriIntersectorData2 words) also
+// lists its leaves for anim_leaf_kernel, which writes their slots; a node with
+// only leaf children is then in no list.  Every entry must lie in exactly one leaf.
+bool plan_binary(AnimState* A, AnimTree& T, const ctl_bvh_node* nodes, uint32_t n_nodes, uint32_t base_f4,
+                 uint32_t root, uint32_t n_entries, const uint32_t* idx, std::string& err) {
+    T.base = base_f4;
     if (n_nodes == 0 || root >= n_nodes) { err = "refit plan: empty tree"; return false; }
+    const bool mesh = n_entries > 0;
+    auto child = [&](uint32_t k, int c) {
+        int32_t v;
+        memcpy(&v, &nodes[k].v[12 + c], 4);
+        return v;
+    };
+    auto kids = [&](uint32_t k, uint32_t* out) {
+        int n = 0;
+        for (int c = 0; c < 2; c++) {
+            const int32_t v = child(k, c);
+            if (v >= 0 && v != kSent) out[n++] = (uint32_t)v >> 2;
+        }
+        return n;
+    };
+    // depth of every node reachable from the root, and a pre-order
     std::vector<int> depth(n_nodes, -1);
-    std::vector<uint32_t> st{root};
+    std::vector<uint32_t> pre, st{root};
     depth[root] = 0;
-    int maxd = 0;
     while (!st.empty()) {
         const uint32_t k = st.back();
         st.pop_back();
-        uint32_t ch[4];
+        pre.push_back(k);
+        uint32_t ch[2];
         const int nc = kids(k, ch);
         for (int i = 0; i < nc; i++) {
             if (ch[i] >= n_nodes || depth[ch[i]] >= 0) { err = "refit plan: malformed tree"; return false; }
             depth[ch[i]] = depth[k] + 1;
-            maxd = std::max(maxd, depth[ch[i]]);
             st.push_back(ch[i]);
         }
     }
-    std::vector<uint32_t> order;
-    T.level_off.clear();
-    for (int d = maxd; d >= 0; d--) {
-        T.level_off.push_back((uint32_t)order.size());
-        for (uint32_t k = 0; k < n_nodes; k++)
-            if (depth[k] == d) order.push_back(k);
+    if (pre.size() >= kRefGlobal) { err = "refit plan: tree too large"; return false; }
+    // inner nodes per subtree (reverse pre-order: children first)
+    std::vector<uint32_t> size(n_nodes, 0);
+    for (size_t i = pre.size(); i-- > 0;) {
+        uint32_t ch[2];
+        const int nc = kids(pre[i], ch);
+        size[pre[i]] = 1;
+        for (int c = 0; c < nc; c++) size[pre[i]] += size[ch[c]];
     }
-    T.level_off.push_back((uint32_t)order.size());
-    const uint32_t nl = (uint32_t)T.level_off.size() - 1;
-    T.top_first = nl;
-    while (T.top_first > 0 && T.level_off[T.top_first] - T.level_off[T.top_first - 1] <= kTopMax) T.top_first--;
-    if (!anim_upload(A, &T.d_order, order.data(), order.size()) ||
-        !anim_upload(A, &T.d_level_off, T.level_off.data(), T.level_off.size())) {
-        err = "refit plan: upload failed";
-        return false;
-    }
-    T.valid = true;
-    return true;
-}
-
-bool plan_binary(AnimState* A, AnimTree& T, const ctl_bvh_node* nodes, uint32_t n_nodes, uint32_t base_f4,
-                 uint32_t root, std::string& err) {
-    return plan_tree(A, T, base_f4, n_nodes, root, [&](uint32_t k, uint32_t* out) {
-        int n = 0;
+    std::vector<int32_t> loc(n_nodes, -1);   // LDS slot of a node of the set being planned
+    auto record = [&](uint32_t k) {
+        uint32_t r[2];
         for (int c = 0; c < 2; c++) {
-            int32_t v;
-            memcpy(&v, &nodes[k].v[12 + c], 4);
-            if (v >= 0 && v != kSent) out[n++] = (uint32_t)v >> 2;
+            const int32_t v = child(k, c);
+            if (v == kSent) r[c] = kRefNone;
+            else if (v < 0) r[c] = mesh ? kRefLeafSlot : kRefInst + (uint32_t)~v;
+            else if (loc[(uint32_t)v >> 2] >= 0) r[c] = (uint32_t)loc[(uint32_t)v >> 2];
+            else r[c] = kRefGlobal + ((uint32_t)v >> 2);
         }
-        return n;
-    }, err);
+        return make_uint4(k, r[0], r[1], 0u);
+    };
+    // a block set from its nodes grouped by level, deepest first
+    auto add_set = [&](const std::vector<std::vector<uint32_t>>& lv, std::vector<uint4>& rec, std::vector<uint32_t>& lvl,
+                       std::vector<uint32_t>& first, uint32_t& max_nodes) {
+        first.push_back((uint32_t)lvl.size());
+        const size_t r0 = rec.size();
+        for (const auto& level : lv) {
+            if (level.empty()) continue;
+            lvl.push_back((uint32_t)rec.size());
+            for (uint32_t k : level) rec.push_back(record(k));
+            for (size_t q = 0; q < level.size(); q++) loc[level[q]] = (int32_t)(rec.size() - level.size() - r0 + q);
+        }
+        max_nodes = std::max<uint32_t>(max_nodes, (uint32_t)(rec.size() - r0));
+        for (size_t q = r0; q < rec.size(); q++) loc[rec[q].x] = -1;
+    };
+    // the cut
+    std::vector<uint32_t> top, cuts;
+    st.assign(1, root);
+    while (!st.empty()) {
+        const uint32_t k = st.back();
+        st.pop_back();
+        if (size[k] <= kSubMax) { cuts.push_back(k); continue; }
+        top.push_back(k);   // more than one inner node at and below it: an inner child
+        uint32_t ch[2];
+        const int nc = kids(k, ch);
+        for (int c = 0; c < nc; c++) st.push_back(ch[c]);
+    }
+    std::sort(cuts.begin(), cuts.end());
+    std::vector<uint4> rec;
+    std::vector<uint32_t> lvl, first;
+    std::vector<std::vector<uint32_t>> lv;
+    for (uint32_t r : cuts) {
+        lv.clear();
+        st.assign(1, r);
+        while (!st.empty()) {
+            const uint32_t k = st.back();
+            st.pop_back();
+            uint32_t ch[2];
+            const int nc = kids(k, ch);
+            for (int c = 0; c < nc; c++) st.push_back(ch[c]);
+            if (mesh && nc == 0) continue;   // leaf slots only: anim_leaf_kernel
+            const size_t d = (size_t)(depth[k] - depth[r]);
+            if (lv.size() <= d) lv.resize(d + 1);
+            lv[d].push_back(k);
+        }
+        if (lv.empty()) continue;
+        std::reverse(lv.begin(), lv.end());
+        for (auto& level : lv) std::sort(level.begin(), level.end());
+        add_set(lv, rec, lvl, first, T.sub.max_nodes);
+    }
+    lvl.push_back((uint32_t)rec.size());
+    if (first.empty()) first.push_back(0);
+    else first.push_back((uint32_t)lvl.size() - 1);
+    if (!upload_blocks(A, T.sub, rec, lvl, first)) { err = "refit plan: upload failed"; return false; }
+    // above the cut, deepest first; the top levels that fit one block
+    std::sort(top.begin(), top.end(), [&](uint32_t a, uint32_t b) {
+        return depth[a] != depth[b] ? depth[a] > depth[b] : a < b;
+    });
+    std::vector<uint32_t> off;
+    for (size_t i = 0; i < top.size(); i++)
+        if (i == 0 || depth[top[i]] != depth[top[i - 1]]) off.push_back((uint32_t)i);
+    off.push_back((uint32_t)top.size());
+    size_t split = off.size() - 1;   // levels [split, end) go to the top block set
+    while (split > 0 && off[split] - off[split - 1] <= kTopMax && top.size() - off[split - 1] <= kTopLds) split--;
+    T.level_off.assign(off.begin(), off.begin() + split + 1);
+    lv.clear();
+    for (size_t l = split; l + 1 < off.size(); l++) lv.emplace_back(top.begin() + off[l], top.begin() + off[l + 1]);
+    rec.clear(); lvl.clear(); first.clear();
+    if (!lv.empty()) add_set(lv, rec, lvl, first, T.top.max_nodes);
+    lvl.push_back((uint32_t)rec.size());
+    first.push_back((uint32_t)lvl.size() - 1);
+    if (!upload_blocks(A, T.top, rec, lvl, first) ||
+        !anim_upload(A, &T.d_order, top.data(), off[split])) { err = "refit plan: upload failed"; return false; }
+    T.valid = true;
+    if (!mesh) return true;
+    // the leaves of a mesh tree, in entry order
+    std::vector<uint4> leaves;
+    std::vector<uint8_t> seen(n_entries, 0);
+    for (uint32_t k : pre)
+        for (int c = 0; c < 2; c++) {
+            const int32_t v = child(k, c);
+            if (v >= 0 || v == kSent) continue;
+            uint32_t e = (uint32_t)~v;
+            for (;; e++) {
+                if (e >= n_entries || seen[e]) { err = "refit plan: a leaf's entries overrun or overlap"; return false; }
+                seen[e] = 1;
+                if (idx[e] & 1) break;
+            }
+            leaves.push_back(make_uint4(k << 1 | (uint32_t)c, (uint32_t)~v, e + 1 - (uint32_t)~v, 0u));
+        }
+    if (std::find(seen.begin(), seen.end(), 0) != seen.end()) { err = "refit plan: an entry lies in no leaf"; return false; }
+    std::sort(leaves.begin(), leaves.end(), [](uint4 a, uint4 b) { return a.y < b.y; });
+    T.n_leaf = (uint32_t)leaves.size();
+    if (!anim_upload(A, &T.d_leaf, leaves.data(), leaves.size())) { err = "refit plan: upload failed"; return false; }
+    return true;
 }
 
 bool plan_gather(AnimState* A, WideGather& G, const uint32_t* src, uint32_t n_nodes, uint32_t base, std::string& err) {
@@ -382,16 +561,18 @@ bool plan_gather(AnimState* A, WideGather& G, const uint32_t* src, uint32_t n_no
 
 template <bool SCENE>
 void launch_refit(hipStream_t s, const AnimTree& T, float* bin_base, const LeafCtx& L) {
-    for (uint32_t l = 0; l < T.top_first; l++) {
+    const size_t per = 6 * sizeof(float) + sizeof(uint4);
+    if (T.sub.n_sets)
+        hipLaunchKernelGGL((refit_block_kernel<SCENE, kAB>), dim3(T.sub.n_sets), dim3(kAB), per * T.sub.max_nodes, s,
+                           bin_base, T.sub.d_rec, T.sub.d_lvl, T.sub.d_first, T.sub.max_nodes, L);
+    for (size_t l = 0; l + 1 < T.level_off.size(); l++) {
         const uint32_t first = T.level_off[l], cnt = T.level_off[l + 1] - first;
-        if (!cnt) continue;
         hipLaunchKernelGGL(refit_bin_kernel<SCENE>, dim3((cnt + kAB - 1) / kAB), dim3(kAB), 0, s, bin_base,
                            T.d_order + first, cnt, L);
     }
-    const uint32_t nl = (uint32_t)T.level_off.size() - 1;
-    if (T.top_first < nl)
-        hipLaunchKernelGGL(refit_bin_top_kernel<SCENE>, dim3(1), dim3(1024), 0, s, bin_base, T.d_order,
-                           T.d_level_off + T.top_first, nl - T.top_first, L);
+    if (T.top.n_sets)
+        hipLaunchKernelGGL((refit_block_kernel<SCENE, 1024>), dim3(1), dim3(1024), per * T.top.max_nodes, s,
+                           bin_base, T.top.d_rec, T.top.d_lvl, T.top.d_first, T.top.max_nodes, L);
 }
 
 void launch_gather(hipStream_t s, const WideGather& G, WideNode* wide_base, const float* bin_base) {
@@ -432,7 +613,7 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
     // the instance tree's refit plan: animated meshes and moved nodes (ctl_scene_set_transform)
     if (d->n_nodes > 0 && d->scene_start_node >= 0 && d->n_scene_bvh_nodes > 0) {
         if (!plan_binary(A, A->scene_bin, d->scene_bvh_nodes, d->n_scene_bvh_nodes, 0,
-                         (uint32_t)d->scene_start_node >> 2, err))
+                         (uint32_t)d->scene_start_node >> 2, 0, nullptr, err))
             return fail(err);
         if (wide && !sw.empty()) {
             if (ssrc.size() != 4 * sw.size()) return fail("wide source map missing");
@@ -443,7 +624,7 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
     if (!anim_upload(A, (ctl_anim_vertex**)&A->d_verts, d->anim_vertices, d->n_anim_vertices) ||
         !anim_upload(A, (uint32_t**)&A->d_tris, d->anim_triangles, 3ull * d->n_anim_triangles))
         return fail("animation upload failed");
-    size_t tmp = 0, etmp = 0;
+    size_t tmp = 0;
     for (uint32_t a = 0; a < d->n_anim_meshes; a++) {
         AnimMeshPlan P;
         P.am = d->anim_meshes[a];
@@ -465,7 +646,9 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
         for (uint64_t e = e0; e < e1; e++)
             if ((d->tri_indices[e] >> 1) >= P.am.tri_count) return fail("animated mesh entry out of range");
         P.n_entries = (uint32_t)(e1 - e0);
-        if (!plan_binary(A, P.bin, d->bvh_nodes + n0, (uint32_t)(n1 - n0), P.km.bvh_node_offset, 0, err)) return fail(err);
+        if (!plan_binary(A, P.bin, d->bvh_nodes + n0, (uint32_t)(n1 - n0), P.km.bvh_node_offset, 0, P.n_entries,
+                         d->tri_indices + e0, err))
+            return fail(err);
         if (wide) {
             const uint32_t wb = wbase[P.am.mesh];
             const uint32_t we = P.am.mesh + 1 < wbase.size() ? wbase[P.am.mesh + 1] : (uint32_t)wn.size();
@@ -473,10 +656,9 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
             if (!plan_gather(A, P.wide, wsrc.data() + 4ull * wb, we - wb, wb, err)) return fail(err);
         }
         tmp = std::max<size_t>(tmp, P.am.vertex_count);
-        etmp = std::max<size_t>(etmp, P.n_entries);
         A->meshes.push_back(std::move(P));
     }
-    if (!anim_alloc(A, &A->d_P, tmp) || !anim_alloc(A, &A->d_N, tmp) || !anim_alloc(A, &A->d_ebox, 2 * etmp))
+    if (!anim_alloc(A, &A->d_P, tmp) || !anim_alloc(A, &A->d_N, tmp))
         return fail("animation buffers allocation failed");
     A->tmp_cap = tmp;
     return CTL_OK;
@@ -514,7 +696,7 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         return CTL_ERR_HIP;
     }
     DevScene& S = c->scene;
-    const uint32_t nv = P.am.vertex_count, nt = P.am.tri_count, ne = P.n_entries;
+    const uint32_t nv = P.am.vertex_count, nt = P.am.tri_count;
     const uint32_t* tris = A->d_tris + 3ull * P.am.tri_first;
     if (nv) hipLaunchKernelGGL(anim_skin_kernel, dim3((nv + kAB - 1) / kAB), dim3(kAB), 34 * n_bones * sizeof(float), s,
                                A->d_verts + P.am.vertex_first, nv, A->d_bones[0], A->d_bones[1], n_bones, lerp, A->d_P,
@@ -522,18 +704,18 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
     if (nt) hipLaunchKernelGGL(anim_tri_kernel, dim3((nt + kAB - 1) / kAB), dim3(kAB), 0, s, tris, nt, A->d_P, A->d_N,
                                const_cast<ctl_triangle_data*>(S.tri_data) + P.km.triangle_offset);
     const uint32_t* idx = S.tri_idx + P.km.bvh_indices_offset;
-    if (ne) hipLaunchKernelGGL(anim_entry_kernel, dim3((ne + kAB - 1) / kAB), dim3(kAB), 0, s, idx, ne, tris, A->d_P,
-                               const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset, A->d_ebox);
-    LeafCtx L{idx, A->d_ebox, nullptr};
     float* bin = reinterpret_cast<float*>(const_cast<float4*>(S.bvh) + P.bin.base);
-    launch_refit<false>(s, P.bin, bin, L);
+    if (P.bin.n_leaf)
+        hipLaunchKernelGGL(anim_leaf_kernel, dim3((P.bin.n_leaf + kAB - 1) / kAB), dim3(kAB), 0, s, P.bin.d_leaf,
+                           P.bin.n_leaf, idx, tris, A->d_P, const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset, bin);
+    launch_refit<false>(s, P.bin, bin, LeafCtx{nullptr});
     launch_gather(s, P.wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.wbvh)), bin);
     hipLaunchKernelGGL(mesh_box_kernel, dim3(1), dim3(1), 0, s, bin, A->d_mesh_boxes + 6 * P.am.mesh);
     // instances, scene trees, epsilon
     if (A->n_nodes) {
         hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf,
                            A->n_nodes, A->d_mesh_boxes, A->d_inst_boxes);
-        LeafCtx LS{nullptr, nullptr, A->d_inst_boxes};
+        LeafCtx LS{A->d_inst_boxes};
         float* sbin = reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh));
         if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
         launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);
@@ -584,7 +766,7 @@ CTL_API ctl_status ctl_scene_set_transform(ctl_ctx* c, uint32_t node, const ctl_
                            S.tri_data, S.xf, node);
     hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf, A->n_nodes,
                        A->d_mesh_boxes, A->d_inst_boxes);
-    LeafCtx LS{nullptr, nullptr, A->d_inst_boxes};
+    LeafCtx LS{A->d_inst_boxes};
     float* sbin = reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh));
     if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
     if (S.wide) launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);

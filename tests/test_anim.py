@@ -263,6 +263,86 @@ def test_animated_traversal_and_render_bit_exact(ctl, orc, dev, bvh):
     pt.close()
 
 
+def skinned_grid(n, bones=16):
+    """n x n quads in the xz plane (2 n^2 triangles), 4 random bone influences per
+    vertex: a mesh tree deep and wide enough for every refit stage (one-block
+    subtrees, per-level launches above them, the single-block top)."""
+    xs = np.linspace(-10, 10, n + 1, dtype=np.float32)
+    X, Z = np.meshgrid(xs, xs, indexing="xy")
+    V = np.stack([X.ravel(), np.zeros(X.size, np.float32), Z.ravel()], 1).astype(np.float32)
+    N = np.tile(np.array([[0, 1, 0]], np.float32), (V.shape[0], 1))
+    rng = np.random.default_rng(0)
+    BI = np.zeros((V.shape[0], 8), np.uint8)
+    BI[:, :4] = rng.integers(0, bones, size=(V.shape[0], 4), dtype=np.uint8)
+    BW = np.zeros((V.shape[0], 8), np.uint8)
+    BW[:, :4] = [64, 64, 64, 63]
+    q = np.arange(n * n, dtype=np.uint32)
+    i, j = q // n, q % n
+    a = i * (n + 1) + j
+    b, c, d = a + 1, a + n + 1, a + n + 2
+    T = np.concatenate([np.stack([a, c, b], 1), np.stack([b, c, d], 1)]).astype(np.uint32)
+    UV = np.stack([(X.ravel() + 10) / 20, (Z.ravel() + 10) / 20], 1).astype(np.float32)
+    return V, N, BI, BW, T, UV
+
+
+def grid_frames(bones, t):
+    out = []
+    for k in range(bones):
+        a = math.radians(5 * math.sin(t + k))
+        m = np.eye(4, dtype=np.float32)
+        m[0, 0], m[0, 1], m[1, 0], m[1, 1] = math.cos(a), -math.sin(a), math.sin(a), math.cos(a)
+        m[1, 3] = 0.2 * math.sin(t * 0.5 + k)
+        out.append(m)
+    return np.stack(out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_animate_large_grid_bit_exact(ctl, orc, dev, bvh):
+    """The 2 M-triangle skinned grid of tools/tools_anim_bench.py: ~1 M binary nodes,
+    so the refit runs all three stages (thousands of one-block subtrees, a
+    1024-node level launched on its own, the single-block top); every array
+    equals the oracle's bit for bit."""
+    A = ctl._abi
+    V, N, BI, BW, T, UV = skinned_grid(1024)
+    s = ctl.HostScene()
+    s.add_animated_mesh(V, N, BI, BW, T, [ctl.diffuse_material(0.5, 0.5, 0.5)], uvs=UV)
+    s.add_node(0)
+    s.add_node(0, [1, 0, 0, 25, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1])
+    s.set_camera([0, 8, -20], [0, 0, 0], [0, 1, 0], 50, 16, 16)
+    d = s.compile()
+    assert d.n_bvh_nodes > 500000
+    if bvh == "binary":
+        d = binary_bvh(d)
+    f0, f1 = grid_frames(16, 0.0), grid_frames(16, 1.0)
+    pt = ctl.PathTracer(0)
+    pt.upload_scene(d)
+    pt.animate(0, f0, f1, 0.3)
+    pt.animate(0, f0, f1, 0.7)
+    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.7)
+    tri, woop, nodes, scene, boxes = keep
+    got = pt.read_array(A.CTL_ARRAY_BVH_NODES, 0, d.n_bvh_nodes, np.uint32, 16)
+    assert np.array_equal(got.ravel(), nodes.view(np.uint32))
+    assert not np.array_equal(nodes.view(np.uint32), _arr(d.bvh_nodes, C.c_uint32, d.n_bvh_nodes * 16))   # it moved
+    got = pt.read_array(A.CTL_ARRAY_WOOP, 0, d.n_woop_tris, np.uint32, 12)
+    assert np.array_equal(got.ravel(), woop.view(np.uint32))
+    got = pt.read_array(A.CTL_ARRAY_SCENE_BVH, 0, d.n_scene_bvh_nodes, np.uint32, 16)
+    assert np.array_equal(got.ravel(), scene[:d.n_scene_bvh_nodes * 16].view(np.uint32))
+    got = pt.read_array(A.CTL_ARRAY_MESH_BOXES, 0, d.n_meshes, np.float32, 6)
+    assert np.array_equal(got.ravel().view(np.uint32), boxes.view(np.uint32))
+    if bvh == "wide":   # the 4-wide copy gathers the refit binary boxes
+        trees = device_wide_trees(pt, d)
+        rays = random_rays(d2, 20000, seed=7, tmin=d2.ray_eps)
+        want = oracle_intersect(orc, d2, rays, trees=trees)
+        r = torch.from_numpy(rays).to(dev)
+        hits = torch.zeros((rays.shape[0], 4), dtype=torch.int32, device=dev)
+        pt.intersect_buffers(rays.shape[0], r.data_ptr(), hits.data_ptr(), False)
+        torch.cuda.synchronize()
+        assert np.array_equal(hits.cpu().numpy(), want)
+        assert (want[:, 2] != -1).sum() > 1000
+    pt.close()
+
+
 @pytest.mark.gpu
 def test_animate_rejects_bad_bones(ctl, dev):
     s = build_scene(ctl)
