@@ -41,7 +41,7 @@ struct AnimTree {
     // The nodes refit by one block (refit_block_kernel): a record {node, child 0,
     // child 1} per node, grouped in block sets, each set's levels deepest first.
     struct Blocks {
-        uint32_t n_sets = 0, max_nodes = 0;
+        uint32_t n_sets = 0, max_nodes = 0, max_levels = 0;
         uint4* d_rec = nullptr;
         uint32_t* d_lvl = nullptr;      // [levels + 1] level offsets into d_rec, all sets
         uint32_t* d_first = nullptr;    // [n_sets + 1] first level of each set
@@ -98,7 +98,7 @@ namespace {
 constexpr int32_t kSent = 0x76543210;
 constexpr int kAB = 256;
 constexpr uint32_t kTopMax = 512;    // levels at most this wide go to the single-block top set ...
-constexpr uint32_t kTopLds = 1536;   // ... of at most this many nodes (boxes + records in LDS: 60 KB)
+constexpr uint32_t kTopLds = 1400;   // ... of at most this many nodes (boxes, records, level offsets in LDS: < 62 KB)
 constexpr uint32_t kSubMax = 511;    // inner nodes of a subtree refit by one block
 // child references of a block record: an LDS slot (the set's own node), or
 constexpr uint32_t kRefGlobal = 0x40000000u;   // | node: a node refit earlier (its child slots in memory)
@@ -271,10 +271,11 @@ __device__ __forceinline__ void refit_rec(float* nodes, const uint4 q, float* sb
 }
 
 // Block sets (the subtrees below the cut, one per block; the narrow top of the
-// tree in one block): the set's records staged in LDS once, then level after
-// level with the boxes handed up through LDS.  The barrier between levels waits
-// for this wave's LDS traffic only: the node stores are read by no one in this
-// launch.  LDS: max_nodes (even) x (6 floats + one record).
+// tree in one block): the set's records and level offsets staged in LDS once,
+// then level after level with the boxes handed up through LDS.  The barrier
+// between levels waits for this wave's LDS traffic only: the node stores are
+// read by no one in this launch.  LDS: max_nodes (even) x (6 floats + one
+// record) + max_levels + 1 offsets.
 template <bool SCENE, int NT>
 __global__ __launch_bounds__(NT) void refit_block_kernel(float* nodes, const uint4* __restrict__ rec,
                                                         const uint32_t* __restrict__ lvl,
@@ -282,13 +283,15 @@ __global__ __launch_bounds__(NT) void refit_block_kernel(float* nodes, const uin
                                                         LeafCtx L) {
     extern __shared__ float sbox[];
     uint4* srec = reinterpret_cast<uint4*>(sbox + 6 * max_nodes);
-    const uint32_t l0 = first[blockIdx.x], l1 = first[blockIdx.x + 1];
-    const uint32_t base = lvl[l0], end = lvl[l1];
+    uint32_t* slvl = reinterpret_cast<uint32_t*>(srec + max_nodes);
+    const uint32_t l0 = first[blockIdx.x], nl = first[blockIdx.x + 1] - l0;
+    const uint32_t base = lvl[l0], end = lvl[l0 + nl];
     for (uint32_t i = base + threadIdx.x; i < end; i += NT) srec[i - base] = rec[i];
+    for (uint32_t l = threadIdx.x; l <= nl; l += NT) slvl[l] = lvl[l0 + l] - base;
     __syncthreads();
-    for (uint32_t l = l0; l < l1; l++) {
-        for (uint32_t i = lvl[l] - base + threadIdx.x; i < lvl[l + 1] - base; i += NT)
-            refit_rec<SCENE>(nodes, srec[i], sbox, i, L);
+    for (uint32_t l = 0; l < nl; l++) {
+        const uint32_t e = slvl[l + 1];
+        for (uint32_t i = slvl[l] + threadIdx.x; i < e; i += NT) refit_rec<SCENE>(nodes, srec[i], sbox, i, L);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 }
@@ -457,9 +460,9 @@ bool plan_binary(AnimState* A, AnimTree& T, const ctl_bvh_node* nodes, uint32_t 
     };
     // a block set from its nodes grouped by level, deepest first
     auto add_set = [&](const std::vector<std::vector<uint32_t>>& lv, std::vector<uint4>& rec, std::vector<uint32_t>& lvl,
-                       std::vector<uint32_t>& first, uint32_t& max_nodes) {
+                       std::vector<uint32_t>& first, uint32_t& max_nodes, uint32_t& max_levels) {
         first.push_back((uint32_t)lvl.size());
-        const size_t r0 = rec.size();
+        const size_t r0 = rec.size(), v0 = lvl.size();
         for (const auto& level : lv) {
             if (level.empty()) continue;
             lvl.push_back((uint32_t)rec.size());
@@ -467,6 +470,7 @@ bool plan_binary(AnimState* A, AnimTree& T, const ctl_bvh_node* nodes, uint32_t 
             for (size_t q = 0; q < level.size(); q++) loc[level[q]] = (int32_t)(rec.size() - level.size() - r0 + q);
         }
         max_nodes = std::max<uint32_t>(max_nodes, (uint32_t)(rec.size() - r0));
+        max_levels = std::max<uint32_t>(max_levels, (uint32_t)(lvl.size() - v0));
         for (size_t q = r0; q < rec.size(); q++) loc[rec[q].x] = -1;
     };
     // the cut
@@ -502,7 +506,7 @@ bool plan_binary(AnimState* A, AnimTree& T, const ctl_bvh_node* nodes, uint32_t 
         if (lv.empty()) continue;
         std::reverse(lv.begin(), lv.end());
         for (auto& level : lv) std::sort(level.begin(), level.end());
-        add_set(lv, rec, lvl, first, T.sub.max_nodes);
+        add_set(lv, rec, lvl, first, T.sub.max_nodes, T.sub.max_levels);
     }
     lvl.push_back((uint32_t)rec.size());
     if (first.empty()) first.push_back(0);
@@ -522,7 +526,7 @@ bool plan_binary(AnimState* A, AnimTree& T, const ctl_bvh_node* nodes, uint32_t 
     lv.clear();
     for (size_t l = split; l + 1 < off.size(); l++) lv.emplace_back(top.begin() + off[l], top.begin() + off[l + 1]);
     rec.clear(); lvl.clear(); first.clear();
-    if (!lv.empty()) add_set(lv, rec, lvl, first, T.top.max_nodes);
+    if (!lv.empty()) add_set(lv, rec, lvl, first, T.top.max_nodes, T.top.max_levels);
     lvl.push_back((uint32_t)rec.size());
     first.push_back((uint32_t)lvl.size() - 1);
     if (!upload_blocks(A, T.top, rec, lvl, first) ||
@@ -563,7 +567,8 @@ template <bool SCENE>
 void launch_refit(hipStream_t s, const AnimTree& T, float* bin_base, const LeafCtx& L) {
     const size_t per = 6 * sizeof(float) + sizeof(uint4);
     if (T.sub.n_sets)
-        hipLaunchKernelGGL((refit_block_kernel<SCENE, kAB>), dim3(T.sub.n_sets), dim3(kAB), per * T.sub.max_nodes, s,
+        hipLaunchKernelGGL((refit_block_kernel<SCENE, kAB>), dim3(T.sub.n_sets), dim3(kAB),
+                           per * T.sub.max_nodes + 4 * (T.sub.max_levels + 1), s,
                            bin_base, T.sub.d_rec, T.sub.d_lvl, T.sub.d_first, T.sub.max_nodes, L);
     for (size_t l = 0; l + 1 < T.level_off.size(); l++) {
         const uint32_t first = T.level_off[l], cnt = T.level_off[l + 1] - first;
@@ -571,7 +576,8 @@ void launch_refit(hipStream_t s, const AnimTree& T, float* bin_base, const LeafC
                            T.d_order + first, cnt, L);
     }
     if (T.top.n_sets)
-        hipLaunchKernelGGL((refit_block_kernel<SCENE, 1024>), dim3(1), dim3(1024), per * T.top.max_nodes, s,
+        hipLaunchKernelGGL((refit_block_kernel<SCENE, 1024>), dim3(1), dim3(1024),
+                           per * T.top.max_nodes + 4 * (T.top.max_levels + 1), s,
                            bin_base, T.top.d_rec, T.top.d_lvl, T.top.d_first, T.top.max_nodes, L);
 }
 
