@@ -92,6 +92,9 @@ def parse(argv=None):
                          "ctl_render_pass per pass; 0: skip)")
     ap.add_argument("--c5-passes", type=int, default=16,
                     help="C5 (textured scene, full-shading kernel) leg passes (0: skip; skipped when --config 5)")
+    ap.add_argument("--ceiling", type=int, default=1,
+                    help="measure the HBM-read and dependent node-chain ceilings (libctl_ceiling.so) on rank 0 "
+                         "after the timed region and report the path kernel against them (0: skip)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal: the ranks join the process group and count themselves; no GPU, "
                          "no scene (tests/test_bench_launch.py)")
@@ -150,17 +153,26 @@ PEAK_L2 = 34500.0    # GB/s, aggregate L2 rate, MI355X_MICROARCH.md (L2)
 def pmc_profile():
     """Newest committed rocprofv3 counter summary (profiles/rNN_pmc.json,
     tools_pmc.sh + tools_pmc_summary.py) and whether it was measured on the
-    libctl_trace.so this run loads."""
+    libctl_trace.so this run loads.  CTL_PMC_PROFILE names another summary
+    explicitly (a box-local one, tools/round_measure.sh); nothing outside the
+    committed rNN files is picked up by the glob."""
     import glob
+    import re
     here = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(here, "profiles", "r[0-9][0-9]*_pmc.json")))
+    explicit = os.environ.get("CTL_PMC_PROFILE")
+    if explicit:
+        files = [explicit]
+    else:
+        files = [f for f in glob.glob(os.path.join(here, "profiles", "r[0-9][0-9]*_pmc.json"))
+                 if re.fullmatch(r"r\d\d(_[a-z0-9]+)?_pmc\.json", os.path.basename(f))]
+        files.sort(key=lambda f: os.path.basename(f))
     if not files:
         return None, None, False
     j = json.load(open(files[-1]))
-    return j, os.path.relpath(files[-1], here), build_match(j, here)
+    return j, os.path.relpath(os.path.abspath(files[-1]), here), build_match(j, here)
 
 
-def roofline(prof, fam, ms, alg_bytes, kernel, units=None):
+def roofline(prof, fam, ms, alg_bytes, kernel, units=None, unit_key="units_per_launch"):
     """Roofline of one kernel: physical HBM bytes (PMC counters of the same
     binary) over its live per-launch time against the HBM peak, plus the L2 and
     vector-memory-address-unit fractions that actually bind it.  The
@@ -171,23 +183,27 @@ def roofline(prof, fam, ms, alg_bytes, kernel, units=None):
     units: the work units (render passes) of one timed launch.  A profile that
     records its counters per unit ("per_unit", tools_pmc_summary.py) is scaled
     to this launch shape, so any --steps / launch grouping gets its bytes;
-    otherwise the profile's per-launch counters apply as they are."""
+    otherwise the profile's per-launch counters apply as they are.  unit_key
+    names the profile's unit count: "units_per_launch" (passes, rays of a
+    primary batch) or "rays_per_launch" (rays a path-kernel launch traced, so a
+    rank's 1/N-image launch gets the bytes per ray of the 1-GPU profile)."""
     j, path, match = prof
     k = (j or {}).get("kernels", {}).get(fam, {})
     scale = 1.0
-    if units is not None and k.get("units_per_launch"):
-        scale = units / k["units_per_launch"]
+    if units is not None and k.get(unit_key):
+        scale = units / k[unit_key]
     elif units is not None and k:
         # counters of another launch shape without its unit count cannot be scaled to this one
         k = {}
-        match = "profile has no units_per_launch for " + fam
+        match = f"profile has no {unit_key} for " + fam
     hbm = k.get("hbm_bytes")
     hbm = hbm * scale if hbm else hbm
     r = {"bound": "hbm", "achieved": None, "peak": PEAK_HBM, "unit": "GB/s", "frac": None, "traffic": hbm,
          "kernel": kernel, "per_launch_ms": round(ms, 4)}
-    if units is not None and k.get("units_per_launch"):
-        r["traffic_per_unit"] = k["hbm_bytes"] / k["units_per_launch"] if k.get("hbm_bytes") else None
-        r["profile_units_per_launch"] = k["units_per_launch"]
+    if units is not None and k.get(unit_key):
+        r["traffic_per_unit"] = k["hbm_bytes"] / k[unit_key] if k.get("hbm_bytes") else None
+        r["profile_units_per_launch"] = k[unit_key]
+        r["scaled_by"] = unit_key
     if hbm:
         ach = hbm / (ms * 1e-3) / 1e9
         r["achieved"] = round(ach, 2)
@@ -213,6 +229,40 @@ def roofline(prof, fam, ms, alg_bytes, kernel, units=None):
                               "instance entry of the reference's binary traversal of the same rays; L2-served, "
                               "not a bound"}
     return r
+
+
+def measure_ceilings(device, lanes):
+    """Measured ceilings of the resources the traversal uses (libctl_ceiling.so,
+    csrc/device/ceiling.hip), on this run's GPU after its timed region:
+    hbm_read_gbs  STREAM-like read of 8 GiB (best of 10), the practical HBM
+                  ceiling SURVEY 8(d) asks for beside the 8 TB/s spec;
+    node_chain    lane node steps per second of dependent walks over random
+                  128-B nodes, seven 16-B loads per step (the wide node fetch),
+                  4 waves per SIMD (the path kernel's occupancy), `lanes` active
+                  lanes per wave (its measured VALU lane use), with the nodes
+                  L2-resident (2 MiB; the path kernel hits L2 99 %) and spread
+                  over 0.54 GB (every step a far fetch), and with all 64 lanes."""
+    import ctypes as C
+    here = os.path.dirname(os.path.abspath(__file__))
+    L = C.CDLL(os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_ceiling.so"))
+    L.ctl_ceiling_hbm_read.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
+    L.ctl_ceiling_node_chain.argtypes = [C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.POINTER(C.c_double)]
+    out = {"source": "cudatracerlib_amd/csrc/device/ceiling.hip"}
+    o = (C.c_double * 3)()
+    if L.ctl_ceiling_hbm_read(device, 8 << 30, 10, o) != 0:
+        raise RuntimeError("ctl_ceiling_hbm_read failed")
+    out["hbm_read_gbs"] = round(o[0], 1)
+    out["hbm_read_gbs_mean"] = round(o[1], 1)
+    chain = {}
+    for name, nbytes, act, steps in (("l2_resident", 2 << 20, lanes, 4000), ("l2_resident_64_lanes", 2 << 20, 64, 4000),
+                                     ("far_0p54gb", 650 << 20, lanes, 400)):
+        if L.ctl_ceiling_node_chain(device, nbytes, act, 4, steps, 5, o) != 0:
+            raise RuntimeError("ctl_ceiling_node_chain failed")
+        chain[name] = {"lane_steps_per_s": round(o[0], 1), "ns_per_wave_step_per_simd": round(o[1], 2),
+                       "active_lanes": act, "waves_per_simd": 4, "node_bytes": int(o[2])}
+    out["node_chain"] = chain
+    return out
 
 
 def cpu_cores():
@@ -435,33 +485,58 @@ def build_match(j, here):
 
 def reference_order_record():
     """The newest committed distance of the shipped default from the reference's
-    CPU path (profiles/rNN_reference_order.json, written by
-    tests/test_reference_order.py::test_full_size_c3_reference_order_distance):
-    per-ray order classes, NEE visibility flips of the any-hit shadow query
-    against the reference's closest-hit Occluded, and one full pass against the
-    oracle's render of the reference's CPU path; `record_matches_binary` ties it
-    to this run's library."""
+    CPU path, one entry per PathTracer config (profiles/rNN_reference_order_<cfg>.json,
+    written by tests/test_reference_order.py::test_full_size_reference_order_distance;
+    a round-5 profiles/rNN_reference_order.json counts as C3): per-ray order
+    classes, NEE visibility flips of the any-hit shadow query against the
+    reference's closest-hit Occluded, and one full pass against the oracle's
+    render of the reference's CPU path; `record_matches_binary` ties each to this
+    run's library.  Plus the adversarial shadow-ray rooms
+    (profiles/rNN_shadow_query_rooms.json, tests/test_shadow_query.py): where the
+    any-hit query departs from the reference's Occluded."""
     import glob
+    import re
     here = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(here, "profiles", "r[0-9][0-9]*_reference_order.json")))
-    if not files:
-        return None
-    j = json.load(open(files[-1]))
-    t = j.get("total", {})
-    ps = j.get("pass") or {}
-    ref = ps.get("reference_cpu_path", ps)   # round 4 records: one comparison, any-hit on both sides
-    out = {"rays": t.get("rays"), "differing_rays": t.get("differ"), "ties": t.get("ties"),
-           "reference_culled": t.get("ref_culled"), "wide_culled": t.get("other_culled"),
-           "pixels": ref.get("pixels"), "pixels_over_1e-4_rel": ref.get("pixels_over_1e-4_rel"),
-           "pixels_differing": ref.get("pixels_differing"),
-           "vs": ("the reference CPU path (binary order, closest-hit Occluded)" if "reference_cpu_path" in ps
-                  else "binary order with any-hit shadows"),
-           "source": os.path.relpath(files[-1], here),
-           "record_matches_binary": build_match(j.get("build", {}), here) if j.get("build") else False}
-    if j.get("nee_visibility"):
-        out["nee_visibility_flips"] = j["nee_visibility"].get("visibility_flips")
-        out["nee_rays"] = j["nee_visibility"].get("rays")
-    return out
+    newest = {}
+    for f in sorted(glob.glob(os.path.join(here, "profiles", "r[0-9][0-9]*_reference_order*.json"))):
+        m = re.fullmatch(r"(r\d\d)_reference_order(?:_(c\d))?\.json", os.path.basename(f))
+        if m:
+            newest[m.group(2) or "c3"] = f     # sorted: a later round wins
+    out = {}
+    for cfg, path in sorted(newest.items()):
+        j = json.load(open(path))
+        t = j.get("total", {})
+        ps = j.get("pass") or {}
+        ref = ps.get("reference_cpu_path", ps)   # round 4 records: one comparison, any-hit on both sides
+        e = {"rays": t.get("rays"), "differing_rays": t.get("differ"), "ties": t.get("ties"),
+             "reference_culled": t.get("ref_culled"), "wide_culled": t.get("other_culled"),
+             "ray_classes": sorted((j.get("classes") or {}).keys()),
+             "pixels": ref.get("pixels"), "pixels_over_1e-4_rel": ref.get("pixels_over_1e-4_rel"),
+             "pixels_differing": ref.get("pixels_differing"), "max_rel": ref.get("max_rel"),
+             "vs": ("the reference CPU path (binary order, closest-hit Occluded)" if "reference_cpu_path" in ps
+                    else "binary order with any-hit shadows"),
+             "source": os.path.relpath(path, here),
+             "record_matches_binary": build_match(j.get("build", {}), here) if j.get("build") else False}
+        if j.get("nee_visibility"):
+            e["nee_visibility_flips"] = j["nee_visibility"].get("visibility_flips")
+            e["nee_rays"] = j["nee_visibility"].get("rays")
+        out[cfg] = e
+    rooms = sorted(glob.glob(os.path.join(here, "profiles", "r[0-9][0-9]_shadow_query_rooms.json")))
+    if rooms:
+        j = json.load(open(rooms[-1]))
+        recs = [(k, kind, c) for k, v in j.items() if k != "build" for kind, c in v.items()]
+        out["shadow_query_rooms"] = {
+            "rays": sum(c["rays"] for _, _, c in recs),
+            "flips": sum(c["flips"] for _, _, c in recs),
+            "flips_no_cull": sum(c["flips_no_cull"] for _, _, c in recs),
+            "flips_query_misses_occluder": sum(c["flips_query_misses_occluder"] for _, _, c in recs),
+            "per_room": {f"{k}/{kind}": [c["flips"], c["rays"]] for k, kind, c in recs},
+            "note": ("adversarial grazing shadow rays on grid walls at the origin, 1e4 and 5e4 away: every flip is "
+                     "an occluder the any-hit query finds that the reference's own closest-hit cull skips "
+                     "(flips == flips_no_cull); shipped shadow_any_hit = 1 departs from Occluded on these rays only"),
+            "source": os.path.relpath(rooms[-1], here),
+            "record_matches_binary": build_match(j["build"], here) if j.get("build") else False}
+    return out or None
 
 
 def wpt_leg(ctl, pt, dev, sptr, torch, W, H, pass_index, passes, flags=0):
@@ -837,18 +912,49 @@ def main(argv=None):
         per_launch_ms = kernel_ms / launches
         passes_per_launch = passes / launches   # this rank's passes (tiles of them when sharded) per launch
         fam = "path_kernel_full" if a.config == 5 else "path_kernel"
-        # the profile's counters are per pass (units_per_launch), so they scale to this
-        # run's launch shape; only the workload (scene, resolution, schedule, shards) must match
+        # the profile's counters are per traced ray (rays_per_launch) and per pass, so
+        # they scale to this run's launch shape, a rank's share of a sharded image
+        # included (its launches trace 1/N of the image's rays of N passes); only the
+        # workload (scene, resolution, schedule, tree) must match
         pj = prof[0] or {}
         same_workload = ("passes_per_launch" in pj and list(pj.get("config", []))[:4] == [a.config, a.scale, W, H]
-                         and pj.get("shards", 1) == shards and a.schedule == "persistent" and a.bvh == "wide")
-        rl = roofline(prof if same_workload else (None, None, False), fam, per_launch_ms,
-                      alg_bytes_per_pass * passes_per_launch, KERNEL_NAME[a.schedule], units=passes_per_launch)
+                         and a.schedule == "persistent" and a.bvh == "wide")
+        pk = (pj.get("kernels") or {}).get(fam, {})
+        if pk.get("rays_per_launch"):
+            rl = roofline(prof if same_workload else (None, None, False), fam, per_launch_ms,
+                          alg_bytes_per_pass * passes_per_launch, KERNEL_NAME[a.schedule], units=rays / launches,
+                          unit_key="rays_per_launch")
+        else:
+            rl = roofline(prof if same_workload and pj.get("shards", 1) == shards else (None, None, False), fam,
+                          per_launch_ms, alg_bytes_per_pass * passes_per_launch, KERNEL_NAME[a.schedule],
+                          units=passes_per_launch)
         rl.update({"launches_timed": launches, "gpu_step_ms": round(step_ms / a.steps, 3),
                    "passes_per_launch": round(passes_per_launch, 4),
                    "steps_per_launch": launch_groups(a.steps, G),
                    "visits_per_launch": {"inner_nodes": int(st[1]), "tri_tests": int(st[2]),
                                          "instances": int(st[3]), "rays": int(st[0])}})
+        if a.ceiling and rank == 0:
+            # the binding resources against their measured ceilings on this GPU
+            lanes = int(round(64 * rl["valu_lane_util"])) if rl.get("valu_lane_util") else 26
+            ce = measure_ceilings(local, lanes)
+            node_steps_s = st[1] * passes_per_launch / (per_launch_ms * 1e-3)
+            ce["path_kernel_node_steps_per_s"] = round(node_steps_s, 1)
+            ce["frac_chain"] = round(node_steps_s / ce["node_chain"]["l2_resident"]["lane_steps_per_s"], 4)
+            ce["frac_chain_64_lanes"] = round(node_steps_s / ce["node_chain"]["l2_resident_64_lanes"]["lane_steps_per_s"],
+                                              4)
+            # triangle tests are dependent fetches too (three 16-B loads against the node's seven)
+            ce["frac_chain_with_tri_fetches"] = round(
+                (st[1] + st[2] * 3.0 / 7.0) * passes_per_launch / (per_launch_ms * 1e-3)
+                / ce["node_chain"]["l2_resident"]["lane_steps_per_s"], 4)
+            if rl.get("achieved"):
+                ce["frac_hbm_of_measured_read"] = round(rl["achieved"] / ce["hbm_read_gbs"], 4)
+            ce["note"] = ("frac_chain = the path kernel's 4-wide node steps per second (STATS pass x passes per "
+                          "launch / its HIP-event launch time) over the L2-resident dependent-chain ceiling at "
+                          "the kernel's lane activity and occupancy; the kernel also shades, tests triangles "
+                          "and idles in divergence, which the probe does not")
+            rl["ceilings"] = ce
+            rl["hbm_ceiling_gbs"] = ce["hbm_read_gbs"]
+            rl["frac_chain"] = ce["frac_chain"]
         if passes_per_launch > 1:
             rl["launch"] = ("ctl_render_passes: the launch's sampler tables, one path-kernel launch over all its "
                             "passes, slice fold (all inside the bracket)")
@@ -910,6 +1016,21 @@ def main(argv=None):
             out["cpu_baseline"].update({k: v for k, v in cc.items() if k != "threads"})
             out["cpu_baseline"]["bvh"] = ("SBVH, leaves <= 8 (the reference's SplitBVHBuilder configuration), binary "
                                           "visit order, closest-hit Occluded shadow rays: the reference's CPU path")
+            anchor = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06_cpu_anchor.json")
+            if os.path.exists(anchor):
+                aj = json.load(open(anchor))
+                w = aj["workloads"].get("soup_edge_0.01", {})
+                out["cpu_baseline"]["per_thread_vs_reference"] = (w.get("threads_1") or {}).get("ratio_to_reference")
+                out["cpu_baseline"]["anchor"] = {
+                    "source": "profiles/r06_cpu_anchor.json (tools/cpu_anchor.py, this repo's container)",
+                    "workload": "SURVEY 6: 1 M-triangle random soup, SBVH leaves <= 8, 2 M rays from one point",
+                    "reference_mrays_s": aj["reference_mrays_s"],
+                    "oracle_mrays_s_1_thread": {k: v["threads_1"]["mrays_s"] for k, v in aj["workloads"].items()},
+                    "work_per_ray": {k: [v["threads_1"]["inner_visits_per_ray"], v["threads_1"]["tri_tests_per_ray"]]
+                                     for k, v in aj["workloads"].items()},
+                    "note": ("SURVEY did not record the soup's triangle size; the rate moves 14x with it (inner "
+                             "visits and triangle tests per ray listed). per_thread_vs_reference is the soup where "
+                             "every ray hits, as SURVEY records, and the work per ray is least (edge 0.01)")}
             out["cpu_baseline"]["note"] = (
                 "threads = min(affinity set, cgroup quota, the job's CPU share OMP_NUM_THREADS); the oracle's "
                 "rays are independent, so the rate scales about linearly with threads (per_thread_mrays_s)")

@@ -43,7 +43,7 @@ CTL_DIRTY_TEXTURES, CTL_DIRTY_ENV, CTL_DIRTY_ALL = 256, 512, 1023
 (CTL_ARRAY_TRI_DATA, CTL_ARRAY_WOOP, CTL_ARRAY_BVH_NODES, CTL_ARRAY_SCENE_BVH, CTL_ARRAY_MESH_BOXES, CTL_ARRAY_RAY_EPS,
  CTL_ARRAY_SAMPLES_1D, CTL_ARRAY_SAMPLES_2D, CTL_ARRAY_NODE_XF, CTL_ARRAY_NODE_INV_XF, CTL_ARRAY_LIGHTS,
  CTL_ARRAY_LIGHT_TRIS, CTL_ARRAY_LIGHT_CDF, CTL_ARRAY_SCENE_BOX, CTL_ARRAY_ENV, CTL_ARRAY_WIDE_BVH,
- CTL_ARRAY_SCENE_WIDE_BVH, CTL_ARRAY_MESH_WIDE_BASE) = range(18)
+ CTL_ARRAY_SCENE_WIDE_BVH, CTL_ARRAY_MESH_WIDE_BASE, CTL_ARRAY_CULL_BOUND) = range(19)
 
 
 class BVHNode(C.Structure):          # BVHNodeData, 64 B

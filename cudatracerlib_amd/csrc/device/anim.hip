@@ -244,28 +244,37 @@ __global__ __launch_bounds__(kAB) void refit_bin_kernel(float* nodes, const uint
 template <bool SCENE>
 __device__ __forceinline__ void refit_rec(float* nodes, const uint4 q, float* sbox, uint32_t self, const LeafCtx& L) {
     float* nd = nodes + 16 * (size_t)q.x;
-    float ulo[3], uhi[3];
-    box_empty(ulo, uhi);
+    float lo[2][3], hi[2][3];
+    bool set[2];
     for (int c = 0; c < 2; c++) {
         const uint32_t r = c ? q.z : q.y;
+        set[c] = r != kRefNone && r != kRefLeafSlot;
         if (r == kRefNone) continue;
-        float lo[3], hi[3];
         if (r == kRefLeafSlot) {
-            bin_child_box(nd, c, lo, hi);
+            bin_child_box(nd, c, lo[c], hi[c]);
+        } else if (r < kRefGlobal) {
+            const float* b = sbox + 6 * r;
+            for (int k = 0; k < 3; k++) { lo[c][k] = b[k]; hi[c][k] = b[3 + k]; }
+        } else if (r < kRefInst) {
+            bin_node_box(nodes + 16 * (size_t)(r - kRefGlobal), lo[c], hi[c]);
         } else {
-            if (r < kRefGlobal) {
-                const float* b = sbox + 6 * r;
-                for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
-            } else if (r < kRefInst) {
-                bin_node_box(nodes + 16 * (size_t)(r - kRefGlobal), lo, hi);
-            } else {
-                const float* b = L.inst + 6 * (size_t)(r - kRefInst);
-                for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
-            }
-            bin_set_child_box(nd, c, lo, hi);
+            const float* b = L.inst + 6 * (size_t)(r - kRefInst);
+            for (int k = 0; k < 3; k++) { lo[c][k] = b[k]; hi[c][k] = b[3 + k]; }
         }
-        box_extend(ulo, uhi, lo, hi);
     }
+    if (set[0] && set[1]) {   // both slots: the node's first 48 B as three whole 16-B stores
+        float4* n4 = reinterpret_cast<float4*>(nd);
+        n4[0] = make_float4(lo[0][0], hi[0][0], lo[0][1], hi[0][1]);
+        n4[1] = make_float4(lo[1][0], hi[1][0], lo[1][1], hi[1][1]);
+        n4[2] = make_float4(lo[0][2], hi[0][2], lo[1][2], hi[1][2]);
+    } else {
+        for (int c = 0; c < 2; c++)
+            if (set[c]) bin_set_child_box(nd, c, lo[c], hi[c]);
+    }
+    float ulo[3], uhi[3];
+    box_empty(ulo, uhi);
+    if (q.y != kRefNone) box_extend(ulo, uhi, lo[0], hi[0]);
+    if (q.z != kRefNone) box_extend(ulo, uhi, lo[1], hi[1]);
     float* o = sbox + 6 * self;
     for (int k = 0; k < 3; k++) { o[k] = ulo[k]; o[3 + k] = uhi[k]; }
 }
@@ -734,6 +743,10 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         }
         S.ray_eps = A->h_eps[6];
         for (int k = 0; k < 3; k++) S.cull_m[k] = A->h_eps[7 + k];
+        // a bound on every mesh box now on the device (cull_bound took them all),
+        // kept past an instance-only update (set_constants)
+        for (int k = 0; k < 3; k++) c->moved_cull_m[k] = S.cull_m[k];
+        c->mesh_moved = true;
         c->device_eps = true;
     }
     c->device_edited = true;
@@ -828,6 +841,10 @@ CTL_API ctl_status ctl_scene_read(ctl_ctx* c, uint32_t array, uint64_t first, ui
         case CTL_ARRAY_SCENE_BOX:
             if (!c->anim || !c->device_eps) { c->err = "scene_read: the scene box is derived by set_transform / animate"; return CTL_ERR_STATE; }
             src = c->anim->d_eps; elem = 6 * sizeof(float); n = 1; break;
+        case CTL_ARRAY_CULL_BOUND:
+            if (first != 0 || count > 1) { c->err = "scene_read: the cull bound is one record of 3 floats"; return CTL_ERR_INVALID; }
+            if (count) memcpy(dst, S.cull_m, 3 * sizeof(float));
+            return CTL_OK;
         case CTL_ARRAY_ENV:
             if (!S.env) { c->err = "scene_read: no environment light"; return CTL_ERR_STATE; }
             src = S.env; elem = sizeof(ctl_env_light); n = 1; break;

@@ -608,6 +608,11 @@ struct ctl_ctx {
     uint32_t n_anim_meshes = 0;
     bool device_eps = false;                    // ray_eps derived on the device (set_transform / animate)
     bool device_edited = false;                 // set_transform / animate rewrote device arrays since the upload
+    // ctl_scene_animate moved mesh trees on the device: a bound (DevScene::cull_m
+    // of the animated scene) on their boxes, kept until the mesh trees are uploaded
+    // again, so a later instance-only update cannot shrink cull_m below them
+    bool mesh_moved = false;
+    float moved_cull_m[3] = {0.0f, 0.0f, 0.0f};
     ctl::DevScene scene{};
     bool has_scene = false;
     bool half_quirk = false;

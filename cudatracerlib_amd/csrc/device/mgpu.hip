@@ -35,7 +35,7 @@ struct Rccl {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
-    decltype(&ncclCommUserRank) user_rank = nullptr;   // optional: checks d_out on the root
+    decltype(&ncclCommUserRank) user_rank = nullptr;   // required: tells a rank whether it is the root
     std::string err;
     bool ok = false;
 };
@@ -61,8 +61,11 @@ const Rccl& rccl() {
         sym(R.group_start, "ncclGroupStart");
         sym(R.group_end, "ncclGroupEnd");
         sym(R.error_string, "ncclGetErrorString");
+        // every rank of a collective must be able to tell whether a NULL d_out
+        // would reach RCCL as the root's receive buffer (ctl_fb_reduce): without
+        // ncclCommUserRank all ranks refuse alike (CTL_ERR_NODEVICE), none waits
+        sym(R.user_rank, "ncclCommUserRank");
         if (!all) { R.err = "RCCL: missing entry points"; return; }
-        R.user_rank = reinterpret_cast<decltype(&ncclCommUserRank)>(dlsym(h, "ncclCommUserRank"));
         R.ok = true;
     });
     return R;
@@ -129,12 +132,16 @@ CTL_API ctl_status ctl_fb_reduce(ctl_ctx* c, void* comm, const ctl_pixel* d_fb, 
     if (d_out && d_out == d_fb) { c->err = "fb_reduce: d_out must not alias d_fb"; return CTL_ERR_INVALID; }
     if (!have_rccl(c)) return CTL_ERR_NODEVICE;
     if (!d_out && n_pixels) {
-        // the root needs a receive buffer (RCCL would get a null recvbuff); a NULL
-        // d_out is refused only where this rank is known to be the root: refusing it
-        // on a rank whose number cannot be read would leave the other ranks waiting
-        // in the collective
+        // the root needs a receive buffer: a NULL d_out never reaches RCCL as the
+        // root's recvbuff.  A non-root rank may pass NULL.  A rank whose number
+        // cannot be read refuses too (its peers then fail in the collective rather
+        // than the root writing through a null pointer).
         int me = -1;
-        if (rccl().user_rank && rccl().user_rank(reinterpret_cast<ncclComm_t>(comm), &me) == ncclSuccess && me == root) {
+        if (rccl().user_rank(reinterpret_cast<ncclComm_t>(comm), &me) != ncclSuccess) {
+            c->err = "fb_reduce: the rank cannot be read (ncclCommUserRank) and d_out is NULL";
+            return CTL_ERR_INVALID;
+        }
+        if (me == root) {
             c->err = "fb_reduce: d_out is required on the root rank";
             return CTL_ERR_INVALID;
         }

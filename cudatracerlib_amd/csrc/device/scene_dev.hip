@@ -204,9 +204,14 @@ void set_constants(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty) {
     // After ctl_scene_set_transform / ctl_scene_animate the device holds the
     // scene box the reference's getSceneBox would return (DynamicScene.cpp:583-587),
     // and its epsilon wins over the desc's until the instances are uploaded again.
+    // mesh trees uploaded again: their boxes are the desc's
+    if (dirty & CTL_DIRTY_BVH) c->mesh_moved = false;
     if (!c->device_eps || (dirty & CTL_DIRTY_NODES)) {
         S.ray_eps = d->ray_eps;
         cull_bound(d->box_min, d->box_max, d->mesh_boxes, d->n_meshes, S.cull_m);
+        // animated mesh trees still on the device may reach past the desc's mesh boxes
+        if (c->mesh_moved)
+            for (int k = 0; k < 3; k++) S.cull_m[k] = S.cull_m[k] > c->moved_cull_m[k] ? S.cull_m[k] : c->moved_cull_m[k];
         c->device_eps = false;
     }
     for (int i = 0; i < CTL_MAX_NUM_LIGHTS; i++) S.light_cdf[i] = d->light_cdf[i];
@@ -452,6 +457,7 @@ void free_scene(ctl_ctx* c) {
     c->tree_flags = 0xffffffffu;
     c->device_eps = false;
     c->device_edited = false;
+    c->mesh_moved = false;
     c->scene = DevScene{};
     c->scene.env_index = 0xffffffffu;
 }

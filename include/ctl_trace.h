@@ -451,7 +451,8 @@ CTL_API ctl_status ctl_intersect(ctl_ctx* ctx, int64_t n, const ctl_ray* d_rays,
  * d_out[i] = 1 when occluded.  any_hit = 0: the reference's form, a closest-hit
  * traceRay and eps < t < tmax - eps (a miss with tmax = inf is not occluded);
  * any_hit = 1: the query ctl_pt_params.shadow_any_hit = 1 runs in the path
- * kernels, any hit with eps < t < tmax - eps, boxes culled at tmax.  traceRay's
+ * kernels, any hit with eps < t < tmax - eps, boxes culled at tmax +
+ * slab_slack(ray) (traverse.h: a per-ray bound on the slab rounding).  traceRay's
  * traversal (span tmin 0, the alpha test in scenes with alpha maps) in the
  * scene's tree order (CTL_SCENE_BINARY_BVH: the reference's).  Counts n rays
  * (each Occluded is one traceRay).  How often the two forms disagree is
@@ -573,7 +574,13 @@ enum {
      * more); instance tree: ~node), 0x76543210 an empty slot.                */
     CTL_ARRAY_WIDE_BVH = 15,       /* all mesh trees                          */
     CTL_ARRAY_SCENE_WIDE_BVH = 16, /* the instance tree (root at node 0)      */
-    CTL_ARRAY_MESH_WIDE_BASE = 17  /* uint32 per mesh: its tree's first node  */
+    CTL_ARRAY_MESH_WIDE_BASE = 17, /* uint32 per mesh: its tree's first node  */
+    /* 3 floats: per axis, the bound on every box coordinate the any-hit shadow
+     * query's cull slack uses (DevScene::cull_m, traverse.h slab_slack): the
+     * scene box and mesh boxes of the desc, and of the device after
+     * set_transform / animate (an animated mesh's boxes are kept in it until
+     * its tree is uploaded again).                                           */
+    CTL_ARRAY_CULL_BOUND = 18
 };
 CTL_API ctl_status ctl_scene_read(ctl_ctx* ctx, uint32_t array, uint64_t first, uint64_t count, void* host_dst);
 

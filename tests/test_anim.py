@@ -263,6 +263,40 @@ def test_animated_traversal_and_render_bit_exact(ctl, orc, dev, bvh):
     pt.close()
 
 
+@pytest.mark.gpu
+def test_cull_bound_keeps_animated_mesh_boxes_after_instance_update(ctl, orc, dev):
+    """DevScene::cull_m bounds every box the any-hit shadow query tests (the
+    slack of traverse.h slab_slack).  The tube is animated past its rest box;
+    an instance-only ctl_scene_update (CTL_DIRTY_NODES) refreshes the constants
+    from the desc, whose mesh boxes are the rest pose, while the animated mesh
+    trees stay on the device: the bound must still cover them.  A re-upload of
+    the mesh trees returns it to the desc's."""
+    A = ctl._abi
+    s = build_scene(ctl)
+    d = s.compile()
+    f0, f1 = frames()
+    bump = np.stack([np.eye(4, dtype=np.float32)] * 2)
+    bump[:, 0, 3] = 40.0                                     # both bones: the tube moves 40 along x
+    pt = ctl.PathTracer(0)
+    try:
+        pt.upload_scene(d)
+        rest = pt.read_array(A.CTL_ARRAY_CULL_BOUND, 0, 1, np.float32, 3)[0].copy()
+        pt.animate(0, bump, bump, 0.0)
+        boxes = pt.read_array(A.CTL_ARRAY_MESH_BOXES, 0, d.n_meshes, np.float32, 6)
+        moved = np.abs(boxes).reshape(-1, 2, 3).max(axis=(0, 1))
+        assert moved[0] > 40.0 > rest[0]
+        after_anim = pt.read_array(A.CTL_ARRAY_CULL_BOUND, 0, 1, np.float32, 3)[0].copy()
+        assert (after_anim >= moved).all()
+        pt.update_scene(d, A.CTL_DIRTY_NODES)
+        after_nodes = pt.read_array(A.CTL_ARRAY_CULL_BOUND, 0, 1, np.float32, 3)[0].copy()
+        assert (after_nodes >= moved).all() and (after_nodes >= rest).all(), (after_nodes, moved, rest)
+        pt.update_scene(d, A.CTL_DIRTY_BVH | A.CTL_DIRTY_WOOP | A.CTL_DIRTY_NODES)
+        again = pt.read_array(A.CTL_ARRAY_CULL_BOUND, 0, 1, np.float32, 3)[0]
+        assert np.array_equal(again, rest)
+    finally:
+        pt.close()
+
+
 def skinned_grid(n, bones=16):
     """n x n quads in the xz plane (2 n^2 triangles), 4 random bone influences per
     vertex: a mesh tree deep and wide enough for every refit stage (one-block

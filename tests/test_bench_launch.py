@@ -60,6 +60,27 @@ def test_roofline_scales_per_unit_counters():
     assert none["traffic"] is None and none["frac"] is None and "no units_per_launch" in str(none["profile_matches_binary"])
 
 
+def test_roofline_of_a_sharded_launch_scales_per_ray():
+    """A path-kernel profile of a 1-GPU 8-pass launch carries its traced rays
+    (rays_per_launch, tools_pmc_summary.py); rank r of an 8-GPU job traces 1/8
+    of the image's rays per pass in its N-pass launch, and its line gets the
+    same HBM bytes per ray, so a non-null frac and traffic."""
+    prof = {"kernels": {"path_kernel": {"units_per_launch": 8, "rays_per_launch": 150_000_000.0,
+                                        "hbm_bytes": 1.77e9, "l2_read_bytes": 2.0e11, "ta_busy": 0.9}}}
+    one = bench.roofline((prof, "p", True), "path_kernel", 46.4, 4e11, "k", units=150_000_000.0,
+                         unit_key="rays_per_launch")
+    rank5 = bench.roofline((prof, "p", True), "path_kernel", 46.4 / 8 * 1.02, 4e11 / 8, "k", units=18_900_000.0,
+                           unit_key="rays_per_launch")
+    assert rank5["traffic"] is not None and rank5["frac"] is not None
+    assert rank5["traffic_per_unit"] == one["traffic_per_unit"] == 1.77e9 / 150_000_000.0
+    assert abs(rank5["traffic"] / 18_900_000.0 - one["traffic"] / 150_000_000.0) < 1e-9
+    # a profile without rays per launch is not applied by rays
+    prof["kernels"]["path_kernel"].pop("rays_per_launch")
+    none = bench.roofline((prof, "p", True), "path_kernel", 5.8, 5e10, "k", units=18_900_000.0,
+                          unit_key="rays_per_launch")
+    assert none["traffic"] is None and "no rays_per_launch" in str(none["profile_matches_binary"])
+
+
 def test_mismatched_launcher_world_size_fails():
     r = _run(["--gpus", "4", "--launch-check"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0

@@ -91,6 +91,23 @@ def test_wide_order_vs_reference_order_grazing_translated(ctl, orc, offset):
     assert c["hit_miss"] == 0, c
 
 
+def test_refraction_rays_wide_vs_reference_order_small(ctl, orc):
+    """The C5 ray class refraction adds (transmitted-like rays that start on a
+    roughdielectric surface and cross it), on a small C5 scene: the 4-wide order
+    against the reference order."""
+    d = scene(ctl, 5, 0.003, 192, 128)
+    prim = camera_rays(d, 192, 128, seed=5)
+    ph = oracle_intersect(orc, d, prim)
+    refr = refraction_rays(d, prim, ph, np.random.default_rng(3), 20000)
+    assert refr.shape[0] > 1000
+    ref = oracle_intersect(orc, d, refr, tie=0)
+    wide = oracle_intersect(orc, d, refr)
+    c = classify_orders(ref, wide)
+    assert (ref[:, 2] >= 0).sum() > 300          # an open scene: most transmitted rays leave it
+    assert c["differ"] <= MAX_DIFFER_FRAC * c["rays"], c
+    assert c["hit_miss"] == 0, c
+
+
 def test_host_wide_trees_shape(ctl):
     d = scene(ctl, 2, 0.25)
     mesh, wbase, sc = ctl.host_wide_trees(d)
@@ -253,24 +270,80 @@ def build_stamp():
     return {"lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(), "src_sha256": source_fingerprint(ROOT)}
 
 
+def refraction_rays(desc, prim, hits, rng, n):
+    """Transmitted-like rays from camera-ray hits on roughdielectric triangles
+    (the C5 population that refraction adds, BSDF_Simple.cu:491-615): origin
+    o + t d (fp32), direction Snell-refracted (eta 1.5, entering or leaving by
+    the side the ray arrives from) about a microfacet normal tilted from the
+    triangle's plane normal (the Woop row a, TriIntersectorData.cu:5-18) by a
+    random alpha in [0.05, 0.5]; total internal reflection reflects.  tmin =
+    eps, as traceRay's; the ray crosses the surface it starts on."""
+    A = __import__("cudatracerlib_amd")._abi
+    nt, ni, nw = int(desc.n_tri_data), int(desc.n_tri_indices), int(desc.n_woop_tris)
+    td = np.ctypeslib.as_array(C.cast(desc.tri_data, C.POINTER(C.c_uint32)), shape=(nt * 8,)).reshape(nt, 8)
+    idx = np.ctypeslib.as_array(C.cast(desc.tri_indices, C.POINTER(C.c_uint32)), shape=(ni,))
+    woop = np.ctypeslib.as_array(C.cast(desc.woop_tris, C.POINTER(C.c_float)), shape=(nw * 12,)).reshape(nw, 12)
+    assert desc.n_meshes == 1 and desc.meshes[0].triangle_offset == 0 and desc.meshes[0].bvh_indices_offset == 0
+    mats = np.array([desc.materials[i].bsdf_type for i in range(desc.n_materials)])
+    mat_off = desc.nodes[0].material_offset if desc.n_nodes else 0
+    hit = np.nonzero(hits[:, 2] >= 0)[0]
+    tri = hits[hit, 2].astype(np.int64)
+    m = ((td[tri, 1] >> 16) & 0xFF).astype(np.int64) + mat_off
+    hit = hit[mats[m] == A.CTL_BSDF_ROUGHDIELECTRIC]
+    sel = rng.choice(hit, size=min(n, hit.size), replace=False)
+    slot = np.empty(nt, np.int64)
+    slot[idx >> 1] = np.arange(ni)
+    a = woop[slot[hits[sel, 2]], 0:3].astype(np.float64)
+    ng = a / np.linalg.norm(a, axis=1, keepdims=True)
+    d = prim[sel, 4:7].astype(np.float64)
+    t = hits[sel, 0].view(np.float32)[:, None]
+    p = (prim[sel, 0:3] + t * prim[sel, 4:7]).astype(np.float32)
+    front = (d * ng).sum(1) < 0
+    eta = np.where(front, 1.0 / 1.5, 1.5)[:, None]
+    ng = np.where(front[:, None], ng, -ng)                       # facing the incoming ray
+    alpha = rng.uniform(0.05, 0.5, size=(sel.size, 1))
+    mn = ng + alpha * rng.normal(size=(sel.size, 3))
+    mn /= np.linalg.norm(mn, axis=1, keepdims=True)
+    ci = -(d * mn).sum(1, keepdims=True)
+    bad = ci[:, 0] <= 0
+    mn[bad], ci[bad] = ng[bad], -(d[bad] * ng[bad]).sum(1, keepdims=True)
+    k = 1.0 - eta ** 2 * (1.0 - ci ** 2)
+    refr = eta * d + (eta * ci - np.sqrt(np.maximum(k, 0.0))) * mn
+    refl = d + 2.0 * ci * mn
+    w = np.where(k >= 0, refr, refl)
+    w /= np.linalg.norm(w, axis=1, keepdims=True)
+    r = np.zeros((sel.size, 8), np.float32)
+    r[:, 0:3] = p
+    r[:, 3] = np.float32(desc.ray_eps)
+    r[:, 4:7] = w
+    r[:, 7] = 3.0e38
+    return r
+
+
+# BASELINE configs of the PathTracer at their full size: (generate config, width, height)
+FULL = {"c2": (2, 1280, 720), "c3": (3, 1920, 1080), "c5": (5, 1920, 1080)}
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(1200)
-def test_full_size_c3_reference_order_distance(ctl, orc, dev):
-    """C3 at full size (10 M triangles, 1080p) against the reference's own CPU
-    path.  (1) One pass's camera rays plus a million bounce-like and a million
-    shadow-like rays from their hits, through ctl_intersect (default 4-wide
-    order): bit-exact to the oracle's statement of that order, classified
-    against the reference's binary order.  (2) A million NEE shadow rays to
-    points on the lights: the shipped any-hit query (ctl_occluded) against the
-    reference's closest-hit Occluded in its binary order (visibility flips).
-    (3) One full PathTracer pass of the shipped default (4-wide order, any-hit
-    shadow rays) against the oracle's render of the reference's CPU path
-    (binary order, closest-hit Occluded) and against the same order with
-    any-hit shadows, per pixel at 1e-4 relative.  The counts and the build's
-    hashes go to gpurun_out/reference_order.json (bench.py reports the
-    committed copy under profiles/)."""
-    W, H = 1920, 1080
-    hs = ctl.HostScene().generate(3, 1.0, W, H)
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
+def test_full_size_reference_order_distance(ctl, orc, dev, cfg):
+    """C2 / C3 / C5 at full size against the reference's own CPU path.  (1) One
+    pass's camera rays plus a million bounce-like and a million shadow-like rays
+    from their hits (C5: and a million transmitted-like rays through its
+    roughdielectric surfaces), through ctl_intersect (default 4-wide order):
+    bit-exact to the oracle's statement of that order, classified against the
+    reference's binary order.  (2) A million NEE shadow rays to points on the
+    lights: the shipped any-hit query (ctl_occluded) against the reference's
+    closest-hit Occluded in its binary order (visibility flips).  (3) One full
+    PathTracer pass of the shipped default (4-wide order, any-hit shadow rays)
+    against the oracle's render of the reference's CPU path (binary order,
+    closest-hit Occluded, KernelDynamicScene.cu:70-80) and against the binary
+    order with any-hit shadows, per pixel at 1e-4 relative.  The counts and the
+    build's hashes go to gpurun_out/reference_order_<cfg>.json (bench.py reports
+    the committed copies under profiles/)."""
+    config, W, H = FULL[cfg]
+    hs = ctl.HostScene().generate(config, 1.0, W, H)
     d = hs.compile()
     rng = np.random.default_rng(2024)
     pt = ctl.PathTracer(0)
@@ -282,17 +355,22 @@ def test_full_size_c3_reference_order_distance(ctl, orc, dev):
         pt.camera_rays(rays.data_ptr(), n)
         torch.cuda.synchronize()
         prim = rays.cpu().numpy()
+        del rays
         prim = prim[prim[:, 7] > 0]
         ph = gpu_hits(pt, prim, dev)
         bounce, shadow = secondary_rays(d, prim, ph, rng, 1_000_000)
-        bh = gpu_hits(pt, bounce, dev)
-        sh = gpu_hits(pt, shadow, dev)
+        classes = [("camera", prim, ph), ("bounce", bounce, gpu_hits(pt, bounce, dev)),
+                   ("shadow_closest", shadow, gpu_hits(pt, shadow, dev))]
+        if config == 5:
+            refr = refraction_rays(d, prim, ph, rng, 1_000_000)
+            classes.append(("refraction", refr, gpu_hits(pt, refr, dev)))
         nee = nee_shadow_rays(d, prim, ph, rng, 1_000_000)
         nr = torch.from_numpy(nee).to(dev)
         occ = torch.zeros(nee.shape[0], dtype=torch.int32, device=dev)
         pt.occluded(nee.shape[0], nr.data_ptr(), occ.data_ptr(), True)
         torch.cuda.synchronize()
         nee_any = occ.cpu().numpy().astype(np.uint8)
+        del nr, occ
         # one full pass, default schedule, order and shadow query
         pt.params = ctl.PTParams(1, 50, 5, 1, 64, 1, 0, 0)
         fb = torch.zeros((W * H, 7), dtype=torch.float32, device=dev)
@@ -302,8 +380,9 @@ def test_full_size_c3_reference_order_distance(ctl, orc, dev):
         img, grays = fb.cpu().numpy(), pt.rays_traced()
     finally:
         pt.close()
-    out = {"scene": f"C3 {d.n_tri_data} tris, {W}x{H}", "build": build_stamp(), "classes": {}}
-    for name, r, g in (("camera", prim, ph), ("bounce", bounce, bh), ("shadow_closest", shadow, sh)):
+    out = {"config": cfg, "scene": f"{cfg.upper()} {d.n_tri_data} tris, {W}x{H}", "build": build_stamp(),
+           "classes": {}}
+    for name, r, g in classes:
         wide = oracle_intersect(orc, d, r, threads=16)
         bad = np.nonzero((wide != g).any(axis=1))[0]
         assert bad.size == 0, (name, bad[:10], wide[bad[:3]], g[bad[:3]])
@@ -333,8 +412,9 @@ def test_full_size_c3_reference_order_distance(ctl, orc, dev):
         renders[key]["rays_reference"] = int(wr)
     renders["rays_gpu"] = int(grays)
     out["pass"] = renders
+    hs.close()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "reference_order.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", f"reference_order_{cfg}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
     assert tot["hit_miss"] == 0 and tot["same_hit_other_fields"] == 0, out

@@ -146,6 +146,8 @@ def test_any_hit_vs_closest_hit_occluded_rooms(ctl, key):
     path = os.path.join(ROOT, "gpurun_out", "shadow_query.json")
     allrec = json.load(open(path)) if os.path.exists(path) else {}
     allrec[key] = rec
+    from test_reference_order import build_stamp
+    allrec["build"] = build_stamp()   # the oracle states the product's query (held to it by test_gpu_occluded_equals_oracle)
     json.dump(allrec, open(path, "w"), indent=1)
 
 

@@ -9,14 +9,15 @@ mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 # Stages (one gpurun call each fits the call limit): "profile" = kernel trace + PMC
 # passes; "bench" = the bench runs, reading the newest committed profiles/rNN_pmc.json
-# (copy gpurun_out/pmc/pmc.json there after the profile stage); no argument = both.
+# (copy gpurun_out/pmc/pmc.json there after the profile stage); no argument = both,
+# the bench runs reading the fresh gpurun_out/pmc/pmc.json through CTL_PMC_PROFILE.
 STAGE=${1:-all}
 if [ "$STAGE" != bench ]; then
 bash tools/tools_profile.sh > gpurun_out/profile.log 2>&1 || { echo "PROFILE FAILED"; tail -20 gpurun_out/profile.log; exit 1; }
 bash tools/tools_pmc.sh > gpurun_out/pmc.log 2>&1 || { echo "PMC FAILED"; tail -20 gpurun_out/pmc.log; exit 1; }
 cat gpurun_out/pmc/summary.txt
 [ "$STAGE" = profile ] && exit 0
-cp gpurun_out/pmc/pmc.json profiles/r99_pmc.json   # box-local: the runs below read the newest profile
+export CTL_PMC_PROFILE=gpurun_out/pmc/pmc.json   # box-local: the runs below read this profile
 fi
 timeout -k 10 900 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { echo "BENCH FAILED"; tail -20 gpurun_out/bench_full.err; exit 1; }
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --emulate-ranks 8 --emulate-rank 5 --no-cpu-baseline \

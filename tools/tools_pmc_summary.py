@@ -13,7 +13,9 @@ profiles/rNN_pmc.json) for the roofline fractions of the same binary:
   cycles         GRBM_GUI_ACTIVE / 8 per launch (kernel cycles of one XCD)
 
 The path-kernel families also carry units_per_launch (render passes per
-profiled launch; tools_pmc.sh profiles one 8-pass ctl_render_passes launch),
+profiled launch; tools_pmc.sh profiles one 8-pass ctl_render_passes launch)
+and rays_per_launch (the rays that launch traced, from the bench line), so a
+sharded launch (1/N of the image) is scaled by its rays,
 and primary_intersect its rays per launch (the profiled runs' bench lines,
 primary_rays.rays_per_launch), so bench.py scales the counters to whatever
 launch shape it times (a rank's 1/N image included).
@@ -36,7 +38,7 @@ FAMILIES = {
     "primary_intersect": "intersect_kernel<0, false, true, 1>",
     "prim_kernel": "prim_kernel<",
     "fold_samples": "fold_samples_kernel",
-    "sampler": "sampler_kernel",
+    "sampler": "sampler_",          # sampler_kernel (ctl_sampler_generate) and sampler_batch_kernel (render_passes)
 }
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(lambda: collections.defaultdict(set))
@@ -50,7 +52,7 @@ for f in sorted(glob.glob(os.path.join(root, "g*", "**", "*counter_collection.cs
         agg[fam][c] += float(row.get("Counter_Value", 0))
         disp[fam][c].add((f, row.get("Dispatch_Id")))
 
-missing = [k for k in ("path_kernel", "primary_intersect") if k not in agg]
+missing = [k for k in ("path_kernel", "primary_intersect", "sampler") if k not in agg]
 if missing:   # a renamed template must not silently drop a roofline (it did once: bool -> int ANY)
     raise SystemExit(f"no counter rows matched families {missing}; check FAMILIES against the kernel names")
 here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # the repo root
@@ -65,22 +67,32 @@ try:
                                               stderr=subprocess.DEVNULL).decode().strip()
 except Exception:
     out["git_head"] = None
-# rays per primary_intersect launch, from the bench lines of the profiled runs
-prim_rays = set()
+# rays per primary_intersect launch and rays per path-kernel launch (the timed
+# region's traced rays over its path-kernel launches), from the bench lines of
+# the profiled runs
+prim_rays, path_rays = set(), set()
 for f in glob.glob(os.path.join(root, "g*.json")):
     for line in open(f):
         if line.startswith("{"):
-            pr = (json.loads(line).get("primary_rays") or {}).get("rays_per_launch")
+            j = json.loads(line)
+            pr = (j.get("primary_rays") or {}).get("rays_per_launch")
             if pr:
                 prim_rays.add(int(pr))
+            tr, nl = (j.get("config") or {}).get("total_rays"), (j.get("roofline") or {}).get("launches_timed")
+            if tr and nl:
+                path_rays.add(tr / nl)
 if len(prim_rays) > 1:
     raise SystemExit(f"profiled runs disagree on primary rays per launch: {sorted(prim_rays)}")
+if len(path_rays) > 1:
+    raise SystemExit(f"profiled runs disagree on rays per path-kernel launch: {sorted(path_rays)}")
 for fam, a in sorted(agg.items()):
     n = {c: max(1, len(d)) for c, d in disp[fam].items()}
     per = {c: v / n[c] for c, v in a.items()}
     k = {"launches": max(n.values()), "counters_per_launch": {c: round(v, 1) for c, v in sorted(per.items())}}
     if fam.startswith("path_kernel"):
         k["units_per_launch"] = PASSES
+        if fam == "path_kernel" and path_rays:
+            k["rays_per_launch"] = next(iter(path_rays))
     if fam == "primary_intersect" and prim_rays:
         k["units_per_launch"] = prim_rays.pop()   # rays
     if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
