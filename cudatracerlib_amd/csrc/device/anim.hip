@@ -1,26 +1,31 @@
 // anim.hip — animated (skinned) meshes on the device: AnimatedMesh::k_ComputeState
-// (Engine/AnimatedMesh.cpp:163-184) as a chain of data-parallel kernels.
+// (Engine/AnimatedMesh.cpp:163-184) as a chain of data-parallel kernels, and the
+// instance tree after ctl_scene_animate / ctl_scene_set_transform.
 //
 //   skin     g_ComputeVertices (AnimatedMesh.cu:29-43): per vertex, two 8-bone
 //            matrix blends, TransformPoint / TransformDirection, lerp
 //   tris     g_ComputeTriangles -> TriangleData::setData (TriangleData.cu:35-63)
-//   leaves   per leaf of the mesh tree, its entries' Woop data (AnimProvider::
+//   rebuild  the mesh tree as BVHRebuilder::Build(&p, true) leaves it
+//            (AnimatedMesh.cpp:174-176, BVHRebuilder.cpp:281-340, 365-450): one
+//            thread per leaf writes its entries' Woop data (AnimProvider::
 //            setObject, AnimatedMesh.cpp:113-117) and the union of their
-//            triangles' boxes, stored straight into the parent's child slot
-//   refit    bottom-up box refit of the mesh's inner children: the subtrees of at
-//            most kSubMax inner nodes in one launch, one block each, level by
-//            level between block barriers; the nodes above them one launch per
-//            wide level (deepest first) and one single-block launch for the
-//            narrow top levels; the 4-wide copy then gathers its boxes from the
-//            binary children they came from
-//   scene    instance boxes (mesh box x node transform), refit of the scene's
-//            binary tree + gather into its 4-wide copy, scene box -> m_rayTraceEps
-//
-// The reference re-derives the mesh tree on the host with BVHRebuilder (refit
-// plus subtree rotations, BVHRebuilder.cpp:281-340); the tree shape is not
-// observable through traversal, so the compiled topology is kept and only the
-// boxes move.  A box is a min/max over the same vertices whatever the order,
-// so the refit boxes are exact and the CPU oracle reproduces them bit for bit.
+//            triangles' boxes into the slot that holds the leaf, then climbs:
+//            the last of a node's children to arrive (an atomic counter per
+//            node) recomputes the node -- its inner children's boxes, the best
+//            of the four child/grandchild rotations by SAH if strictly cheaper
+//            (host/bvh_rebuild.h states the rules), the moved subtrees' parent
+//            words and leaf records -- and moves on to its parent.  A node is
+//            recomputed after its whole subtree, as in the reference's
+//            post-order recursion, and nodes of disjoint subtrees never touch
+//            the same words, so the result is the recursion's.  The tree's
+//            shape persists from frame to frame, as the reference's does.  The
+//            4-wide copy keeps the topology the upload collapsed and is refit in
+//            the same launch, bottom-up by arrival counts from the same leaves.
+//   scene    instance boxes (mesh box x node transform) and the scene box ->
+//            m_rayTraceEps on the device; the instance tree rebuilt on the host
+//            along the moved instances' paths (SceneBVH::Build, the same
+//            BVHRebuilder without invalidateAll), its 4-wide copy refit in its
+//            topology, both uploaded.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,64 +37,57 @@
 #include "../ctl_anim.h"
 #include "../ctl_shade.h"
 #include "../host/bvh_wide.h"
+#include "../host/bvh_rebuild.h"
 #include "../ctl_qnode.h"
 
 namespace ctl {
 
-struct AnimTree {
-    uint32_t base = 0;                  // float4 offset of the tree's node 0
-    // The nodes refit by one block (refit_block_kernel): a record {node, child 0,
-    // child 1} per node, grouped in block sets, each set's levels deepest first.
-    struct Blocks {
-        uint32_t n_sets = 0, max_nodes = 0, max_levels = 0;
-        uint4* d_rec = nullptr;
-        uint32_t* d_lvl = nullptr;      // [levels + 1] level offsets into d_rec, all sets
-        uint32_t* d_first = nullptr;    // [n_sets + 1] first level of each set
-    };
-    Blocks sub;                         // the subtrees below the cut, one set each
-    Blocks top;                         // the narrow levels at the top of the tree, one set
-    // the levels in between, too wide for one block: one launch each, deepest first
-    std::vector<uint32_t> level_off;    // [levels + 1] offsets into d_order
-    uint32_t* d_order = nullptr;        // node indices relative to base
-    // mesh trees: the leaves, boxed by anim_leaf_kernel
+// The rebuild of one animated mesh's trees.
+struct MeshRebuild {
+    uint32_t n_nodes = 0;               // binary nodes of the mesh tree
     uint32_t n_leaf = 0;
-    uint4* d_leaf = nullptr;            // {node << 1 | child, first entry, entries, 0}
-    bool valid = false;
-};
-
-// A 4-wide copy's boxes after the binary refit: slot q of the wide tree takes
-// the box of binary (node, child) src[q] (recorded by collapse_wide).
-struct WideGather {
-    uint32_t base = 0;                  // wide-node index of the tree's node 0
-    uint32_t n_slots = 0;               // 4 x nodes
-    uint32_t* d_src = nullptr;
-    bool valid = false;
+    uint4* d_leaf = nullptr;            // {holder << 1 | slot, first entry, entries, wide node << 2 | slot}
+    uint32_t* d_leaf_of = nullptr;      // per entry of the mesh: the record of the leaf starting there
+    int32_t* d_objects = nullptr;       // numLeafs (bvhNodeData) per binary node
+    uint32_t* d_cnt = nullptr;          // arrival counters per binary node (0 between launches)
+    uint32_t n_wide = 0;                // 4-wide nodes of the mesh (0: binary scene)
+    uint32_t* d_wup = nullptr;          // per wide node: parent << 2 | slot (0xffffffff: the root)
+    uint32_t* d_wcnt = nullptr;         // arrival counters per wide node
 };
 
 struct AnimMeshPlan {
     ctl_anim_mesh am;
     ctl_kernel_mesh km;
     uint32_t n_entries = 0;
-    AnimTree bin;
-    WideGather wide;
+    uint32_t wide_base = 0;             // the mesh's first wide node
+    MeshRebuild rb;
+};
+
+// Host copies of the instance trees: the rebuild changes their shape, so each
+// call starts from the last one's.
+struct SceneTrees {
+    std::vector<ctl_bvh_node> bin;
+    int32_t root = -1;                  // start node (float4 offset); < 0: no instance tree
+    std::vector<WideNode> wide;
+    std::vector<uint32_t> wide_post;    // wide nodes, children before parents
 };
 
 struct AnimState {
     std::vector<AnimMeshPlan> meshes;
-    AnimTree scene_bin;
-    WideGather scene_wide;
+    SceneTrees scene;
     const ctl_anim_vertex* d_verts = nullptr;
     const uint32_t* d_tris = nullptr;
     float* d_mesh_boxes = nullptr;      // 6 per mesh
     float* d_inst_boxes = nullptr;      // 6 per node
     float* d_eps = nullptr;             // scene box (6) + eps + cull_m (3)
-    float* h_eps = nullptr;             // pinned
+    float* h_eps = nullptr;             // pinned: the same 10 floats, then 6 per node (instance boxes)
     float4* d_P = nullptr;
     float4* d_N = nullptr;
     size_t tmp_cap = 0;
     float* d_bones[2] = {nullptr, nullptr};
     size_t bones_cap = 0;
     uint32_t n_meshes = 0, n_nodes = 0;
+    std::vector<uint32_t> node_mesh;    // Node::m_uMeshIndex per node
     std::vector<void*> allocs;
 };
 
@@ -97,14 +95,6 @@ namespace {
 
 constexpr int32_t kSent = 0x76543210;
 constexpr int kAB = 256;
-constexpr uint32_t kTopMax = 512;    // levels at most this wide go to the single-block top set ...
-constexpr uint32_t kTopLds = 1400;   // ... of at most this many nodes (boxes, records, level offsets in LDS: < 62 KB)
-constexpr uint32_t kSubMax = 511;    // inner nodes of a subtree refit by one block
-// child references of a block record: an LDS slot (the set's own node), or
-constexpr uint32_t kRefGlobal = 0x40000000u;   // | node: a node refit earlier (its child slots in memory)
-constexpr uint32_t kRefInst = 0x80000000u;     // | instance: a scene-tree leaf
-constexpr uint32_t kRefLeafSlot = 0xfffffffeu; // a mesh leaf, its slot written by anim_leaf_kernel
-constexpr uint32_t kRefNone = 0xffffffffu;     // an empty child
 
 __device__ __forceinline__ void box_empty(float lo[3], float hi[3]) {
     lo[0] = lo[1] = lo[2] = FLT_MAX;
@@ -149,181 +139,202 @@ __global__ __launch_bounds__(kAB) void anim_tri_kernel(const uint32_t* __restric
     td[t] = r;
 }
 
-// BVHNodeData child boxes (the reference layout, TriIntersectorData.h:44-50)
-__device__ __forceinline__ void bin_child_box(const float* nd, int c, float lo[3], float hi[3]) {
-    const int o = c ? 4 : 0, z = c ? 10 : 8;
-    lo[0] = nd[o]; hi[0] = nd[o + 1]; lo[1] = nd[o + 2]; hi[1] = nd[o + 3]; lo[2] = nd[z]; hi[2] = nd[z + 1];
+// ---------------------------------------------------------------------------
+// Mesh tree rebuild (one launch per animated mesh)
+// ---------------------------------------------------------------------------
+struct DBox {
+    float lo[3], hi[3];
+};
+
+__device__ __forceinline__ DBox dbox_identity() {
+    return DBox{{FLT_MAX, FLT_MAX, FLT_MAX}, {-FLT_MAX, -FLT_MAX, -FLT_MAX}};
 }
-__device__ __forceinline__ void bin_set_child_box(float* nd, int c, const float lo[3], const float hi[3]) {
-    const int o = c ? 4 : 0, z = c ? 10 : 8;
-    nd[o] = lo[0]; nd[o + 1] = hi[0]; nd[o + 2] = lo[1]; nd[o + 3] = hi[1]; nd[z] = lo[2]; nd[z + 1] = hi[2];
+// AABB::Extend (Math/AABB.h:72-78), this box first
+__device__ __forceinline__ DBox dbox_union(const DBox& a, const DBox& b) {
+    DBox r;
+    for (int k = 0; k < 3; k++) { r.lo[k] = tmin(a.lo[k], b.lo[k]); r.hi[k] = tmax(a.hi[k], b.hi[k]); }
+    return r;
 }
-// Per leaf of a mesh tree (one thread): each entry of its run gets its Woop
-// data (AnimProvider::setObject, AnimatedMesh.cpp:113-117), and the union of
-// the entries' triangle boxes, in entry order, goes into the parent's child
-// slot.  The leaves cover every entry once (checked by the plan), and the plan
-// counts each run, so an entry's loads do not wait for the previous end bit.
-__global__ __launch_bounds__(kAB) void anim_leaf_kernel(const uint4* __restrict__ leaves, uint32_t n,
-                                                       const uint32_t* __restrict__ idx, const uint32_t* __restrict__ tris,
-                                                       const float4* __restrict__ P, float4* woop, float* nodes) {
+// AABB::Area (Math/AABB.h:19-23); no contraction (-ffp-contract=off)
+__device__ __forceinline__ float dbox_area(const DBox& b) {
+    const float x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
+    return 2.0f * (x * y + x * z + y * z);
+}
+// BVHNodeData child slots (TriIntersectorData.h:44-88)
+__device__ __forceinline__ DBox slot_box(const float* nd, int c) {
+    const float4 q = reinterpret_cast<const float4*>(nd)[c];
+    const float2 z = reinterpret_cast<const float2*>(nd + 8)[c];
+    return DBox{{q.x, q.z, z.x}, {q.y, q.w, z.y}};
+}
+__device__ __forceinline__ void set_slot(float* nd, int c, const DBox& b) {
+    reinterpret_cast<float4*>(nd)[c] = make_float4(b.lo[0], b.hi[0], b.lo[1], b.hi[1]);
+    reinterpret_cast<float2*>(nd + 8)[c] = make_float2(b.lo[2], b.hi[2]);
+}
+__device__ __forceinline__ int32_t kid(const float* nd, int c) { return __float_as_int(nd[12 + c]); }
+
+struct RebuildArgs {
+    float* bin;                 // the mesh tree's node 0
+    WideNode* wide;             // its first 4-wide node (nullptr: no wide copy)
+    const uint32_t* idx;        // the mesh's TriIntersectorData2 entries
+    const uint32_t* tris;       // the mesh's triangles (skinned vertex indices)
+    const float4* P;            // skinned positions
+    float4* woop;               // the mesh's TriIntersectorData entries
+    uint4* leaf;
+    const uint32_t* leaf_of;
+    int32_t* objects;
+    uint32_t* cnt;
+    const uint32_t* wup;
+    uint32_t* wcnt;
+    float* mesh_box;            // m_sLocalBox: 6 floats
+    uint32_t n_leaf;
+};
+
+// The last of `need` arrivals at counter k goes on (and leaves the counter at
+// 0 for the next launch).  Release: this thread's node writes before the
+// arrival; acquire: the other arrivals' writes before this thread's reads.
+__device__ __forceinline__ bool arrive(uint32_t* cnt, uint32_t k, uint32_t need) {
+    const uint32_t old = __hip_atomic_fetch_add(cnt + k, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 < need) return false;
+    __hip_atomic_store(cnt + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+__device__ __forceinline__ int leaf_objects(const uint32_t* idx, uint32_t first) {
+    int n = 1;
+    while (!(idx[first + n - 1] & 1u)) n++;
+    return n;
+}
+
+// getBox / numLeafs of child value v held in slot c of node `holder`
+__device__ __forceinline__ void child_info(const RebuildArgs& A, const float* holder, int c, int32_t v, DBox& b,
+                                           int& n) {
+    if (v == kSent) { b = dbox_identity(); n = 0; }
+    else if (v < 0) { b = slot_box(holder, c); n = leaf_objects(A.idx, (uint32_t)~v); }
+    else {
+        const float* y = A.bin + 16 * (size_t)((uint32_t)v >> 2);
+        b = dbox_union(slot_box(y, 0), slot_box(y, 1));
+        n = A.objects[(uint32_t)v >> 2];
+    }
+}
+
+// BVHRebuilder::setChild's array writes for a moved child: the parent word of
+// an inner node, the holder of a leaf's record
+__device__ __forceinline__ void moved_to(const RebuildArgs& A, int32_t v, uint32_t node, int slot) {
+    if (v == kSent) return;
+    if (v >= 0) A.bin[16 * (size_t)((uint32_t)v >> 2) + 14] = __int_as_float((int32_t)(node << 2));
+    else A.leaf[A.leaf_of[(uint32_t)~v]].x = node << 1 | (uint32_t)slot;
+}
+
+// recomputeNode (BVHRebuilder.cpp:281-340) of node x, its subtree done
+__device__ void rebuild_node(const RebuildArgs& A, uint32_t x) {
+    float* X = A.bin + 16 * (size_t)x;
+    const int32_t c[2] = {kid(X, 0), kid(X, 1)};
+    DBox cb[2], gb[2][2];
+    int cn[2], gn[2][2];
+    int32_t g[2][2];
+    bool can[2];
+    for (int i = 0; i < 2; i++) {
+        child_info(A, X, i, c[i], cb[i], cn[i]);
+        if (c[i] >= 0 && c[i] != kSent) set_slot(X, i, cb[i]);   // node->setLeft / setRight(newBox)
+        can[i] = false;
+        if (c[i] >= 0 && c[i] != kSent) {
+            const float* Y = A.bin + 16 * (size_t)((uint32_t)c[i] >> 2);
+            for (int j = 0; j < 2; j++) {
+                g[i][j] = kid(Y, j);
+                child_info(A, Y, j, g[i][j], gb[i][j], gn[i][j]);
+            }
+            can[i] = g[i][0] != kSent && g[i][1] != kSent;   // numberGrandchildren == 2
+        }
+    }
+    // sah(idx, child, grandchild) (:624-638) for the four rotations
+    float rot[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+    if (can[0]) {
+        rot[0] = dbox_area(dbox_union(cb[1], gb[0][1])) * (float)(cn[1] + gn[0][1]) + dbox_area(gb[0][0]) * (float)gn[0][0];
+        rot[1] = dbox_area(dbox_union(cb[1], gb[0][0])) * (float)(cn[1] + gn[0][0]) + dbox_area(gb[0][1]) * (float)gn[0][1];
+    }
+    if (can[1]) {
+        rot[2] = dbox_area(dbox_union(cb[0], gb[1][0])) * (float)(cn[0] + gn[1][0]) + dbox_area(gb[1][1]) * (float)gn[1][1];
+        rot[3] = dbox_area(dbox_union(cb[0], gb[1][1])) * (float)(cn[0] + gn[1][1]) + dbox_area(gb[1][0]) * (float)gn[1][0];
+    }
+    int best = 0;
+    for (int i = 1; i < 4; i++)
+        if (rot[i] < rot[best]) best = i;   // std::min_element: the first smallest
+    const float now = dbox_area(cb[0]) * (float)cn[0] + dbox_area(cb[1]) * (float)cn[1];
+    if (!(rot[best] < now)) return;
+    // swapChildren(idx, lc, lg) (:691-702): child c[lc] and grandchild g[1-lc][lg] trade places
+    const int lc = best < 2 ? 1 : 0, lg = (best == 1 || best == 2) ? 1 : 0, o = 1 - lc;
+    const uint32_t other = (uint32_t)c[o] >> 2;
+    float* O = A.bin + 16 * (size_t)other;
+    O[12 + lg] = __int_as_float(c[lc]);
+    set_slot(O, lg, cb[lc]);
+    moved_to(A, c[lc], other, lg);
+    // propagateBBChange(other -> x): the other child's box, its slots in order
+    const DBox ob = lg == 0 ? dbox_union(cb[lc], gb[o][1]) : dbox_union(gb[o][0], cb[lc]);
+    set_slot(X, o, ob);
+    X[12 + lc] = __int_as_float(g[o][lg]);
+    set_slot(X, lc, gb[o][lg]);
+    moved_to(A, g[o][lg], x, lc);
+    A.objects[other] += cn[lc] - gn[o][lg];   // BVHNodeInfo::changeCount, net
+}
+
+// One thread per leaf: Woop data and the leaf's box, then up both trees.
+__global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
     const uint32_t i = blockIdx.x * kAB + threadIdx.x;
-    if (i >= n) return;
-    const uint4 lf = leaves[i];
+    if (i >= A.n_leaf) return;
+    const uint4 lf = A.leaf[i];
     float lo[3], hi[3];
     box_empty(lo, hi);
 #pragma unroll 2
     for (uint32_t e = lf.y; e < lf.y + lf.z; e++) {
-        const uint32_t t = idx[e] >> 1;
-        const f3 a = ld3(P, tris[3 * t]), b = ld3(P, tris[3 * t + 1]), c = ld3(P, tris[3 * t + 2]);
+        const uint32_t t = A.idx[e] >> 1;
+        const f3 a = ld3(A.P, A.tris[3 * t]), b = ld3(A.P, A.tris[3 * t + 1]), c = ld3(A.P, A.tris[3 * t + 2]);
         float w[12];
         woop_set_hd(a, b, c, w);
-        woop[3 * e] = make_float4(w[0], w[1], w[2], w[3]);
-        woop[3 * e + 1] = make_float4(w[4], w[5], w[6], w[7]);
-        woop[3 * e + 2] = make_float4(w[8], w[9], w[10], w[11]);
+        A.woop[3 * e] = make_float4(w[0], w[1], w[2], w[3]);
+        A.woop[3 * e + 1] = make_float4(w[4], w[5], w[6], w[7]);
+        A.woop[3 * e + 2] = make_float4(w[8], w[9], w[10], w[11]);
         const float q0[3] = {tmin(tmin(a.x, b.x), c.x), tmin(tmin(a.y, b.y), c.y), tmin(tmin(a.z, b.z), c.z)};
         const float q1[3] = {tmax(tmax(a.x, b.x), c.x), tmax(tmax(a.y, b.y), c.y), tmax(tmax(a.z, b.z), c.z)};
         box_extend(lo, hi, q0, q1);
     }
-    bin_set_child_box(nodes + 16 * (size_t)(lf.x >> 1), (int)(lf.x & 1u), lo, hi);
-}
-
-// Leaf boxes of the scene tree: its leaves are instances (~node).  Mesh trees
-// (SCENE = false) have their leaf slots written by anim_leaf_kernel.
-struct LeafCtx {
-    const float* inst;       // instance boxes (scene)
-};
-
-// The node's box: the union of its non-empty child slots, in slot order.  The
-// whole 64-B node is loaded up front (four 16-B loads in flight, `nd` 16-B
-// aligned) rather than a slot after its sentinel test.
-__device__ __forceinline__ void bin_node_box(const float* nd, float lo[3], float hi[3]) {
-    const float4* n4 = reinterpret_cast<const float4*>(nd);
-    const float4 q0 = n4[0], q1 = n4[1], q2 = n4[2], q3 = n4[3];
-    box_empty(lo, hi);
-    if (__float_as_int(q3.x) != kSent) {
-        const float a[3] = {q0.x, q0.z, q2.x}, b[3] = {q0.y, q0.w, q2.y};
-        box_extend(lo, hi, a, b);
-    }
-    if (__float_as_int(q3.y) != kSent) {
-        const float a[3] = {q1.x, q1.z, q2.z}, b[3] = {q1.y, q1.w, q2.w};
-        box_extend(lo, hi, a, b);
-    }
-}
-
-// One node: its children's boxes from their leaves or from the children's own
-// (already refit) child boxes.
-template <bool SCENE>
-__device__ __forceinline__ void refit_node(float* nodes, uint32_t k, const LeafCtx& L) {
-    float* nd = nodes + 16 * (size_t)k;
-    for (int c = 0; c < 2; c++) {
-        const int32_t v = __float_as_int(nd[12 + c]);
-        if (v == kSent) continue;
-        float lo[3], hi[3];
-        if (v < 0) {
-            if (!SCENE) continue;   // written by anim_leaf_kernel
-            const float* b = L.inst + 6 * (uint32_t)~v;
-            for (int k = 0; k < 3; k++) { lo[k] = b[k]; hi[k] = b[3 + k]; }
-        } else {
-            bin_node_box(nodes + 16 * (size_t)(v >> 2), lo, hi);
-        }
-        bin_set_child_box(nd, c, lo, hi);
-    }
-}
-
-template <bool SCENE>
-__global__ __launch_bounds__(kAB) void refit_bin_kernel(float* nodes, const uint32_t* __restrict__ order, uint32_t n,
-                                                       LeafCtx L) {
-    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
-    if (i >= n) return;
-    refit_node<SCENE>(nodes, order[i], L);
-}
-
-// One node of a block set: each child slot from its reference, and the node's
-// own box (the union of its slots, in slot order as bin_node_box takes it) into
-// LDS for its parent in the same set.
-template <bool SCENE>
-__device__ __forceinline__ void refit_rec(float* nodes, const uint4 q, float* sbox, uint32_t self, const LeafCtx& L) {
-    float* nd = nodes + 16 * (size_t)q.x;
-    float lo[2][3], hi[2][3];
-    bool set[2];
-    for (int c = 0; c < 2; c++) {
-        const uint32_t r = c ? q.z : q.y;
-        set[c] = r != kRefNone && r != kRefLeafSlot;
-        if (r == kRefNone) continue;
-        if (r == kRefLeafSlot) {
-            bin_child_box(nd, c, lo[c], hi[c]);
-        } else if (r < kRefGlobal) {
-            const float* b = sbox + 6 * r;
-            for (int k = 0; k < 3; k++) { lo[c][k] = b[k]; hi[c][k] = b[3 + k]; }
-        } else if (r < kRefInst) {
-            bin_node_box(nodes + 16 * (size_t)(r - kRefGlobal), lo[c], hi[c]);
-        } else {
-            const float* b = L.inst + 6 * (size_t)(r - kRefInst);
-            for (int k = 0; k < 3; k++) { lo[c][k] = b[k]; hi[c][k] = b[3 + k]; }
+    const DBox lb{{lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}};
+    // the 4-wide copy: its leaf slot, then every node whose slots have all arrived
+    if (A.wide) {
+        uint32_t w = lf.w >> 2, sl = lf.w & 3u;
+        DBox b = lb;
+        for (;;) {
+            WideNode& W = A.wide[w];
+            W.lo_x[sl] = b.lo[0]; W.lo_y[sl] = b.lo[1]; W.lo_z[sl] = b.lo[2];
+            W.hi_x[sl] = b.hi[0]; W.hi_y[sl] = b.hi[1]; W.hi_z[sl] = b.hi[2];
+            uint32_t need = 0;
+            for (int k = 0; k < 4; k++) need += W.child[k] != kSent;
+            if (!arrive(A.wcnt, w, need)) break;
+            const uint32_t up = A.wup[w];
+            if (up == 0xffffffffu) break;
+            b = dbox_identity();
+            for (int k = 0; k < 4; k++)
+                if (W.child[k] != kSent)
+                    b = dbox_union(b, DBox{{W.lo_x[k], W.lo_y[k], W.lo_z[k]}, {W.hi_x[k], W.hi_y[k], W.hi_z[k]}});
+            w = up >> 2;
+            sl = up & 3u;
         }
     }
-    if (set[0] && set[1]) {   // both slots: the node's first 48 B as three whole 16-B stores
-        float4* n4 = reinterpret_cast<float4*>(nd);
-        n4[0] = make_float4(lo[0][0], hi[0][0], lo[0][1], hi[0][1]);
-        n4[1] = make_float4(lo[1][0], hi[1][0], lo[1][1], hi[1][1]);
-        n4[2] = make_float4(lo[0][2], hi[0][2], lo[1][2], hi[1][2]);
-    } else {
-        for (int c = 0; c < 2; c++)
-            if (set[c]) bin_set_child_box(nd, c, lo[c], hi[c]);
+    // the binary tree: the leaf's slot, then each node whose children have all arrived
+    uint32_t x = lf.x >> 1;
+    set_slot(A.bin + 16 * (size_t)x, (int)(lf.x & 1u), lb);
+    for (;;) {
+        float* X = A.bin + 16 * (size_t)x;
+        const uint32_t need = (kid(X, 0) != kSent) + (kid(X, 1) != kSent);
+        if (!arrive(A.cnt, x, need)) return;
+        rebuild_node(A, x);
+        const int32_t p = __float_as_int(X[14]);
+        if (p < 0) {   // the root: m_sLocalBox = BVHNodeData::getBox, both slots
+            const DBox r = dbox_union(slot_box(X, 0), slot_box(X, 1));
+            for (int k = 0; k < 3; k++) { A.mesh_box[k] = r.lo[k]; A.mesh_box[3 + k] = r.hi[k]; }
+            return;
+        }
+        x = (uint32_t)p >> 2;
     }
-    float ulo[3], uhi[3];
-    box_empty(ulo, uhi);
-    if (q.y != kRefNone) box_extend(ulo, uhi, lo[0], hi[0]);
-    if (q.z != kRefNone) box_extend(ulo, uhi, lo[1], hi[1]);
-    float* o = sbox + 6 * self;
-    for (int k = 0; k < 3; k++) { o[k] = ulo[k]; o[3 + k] = uhi[k]; }
-}
-
-// Block sets (the subtrees below the cut, one per block; the narrow top of the
-// tree in one block): the set's records and level offsets staged in LDS once,
-// then level after level with the boxes handed up through LDS.  The barrier
-// between levels waits for this wave's LDS traffic only: the node stores are
-// read by no one in this launch.  LDS: max_nodes (even) x (6 floats + one
-// record) + max_levels + 1 offsets.
-template <bool SCENE, int NT>
-__global__ __launch_bounds__(NT) void refit_block_kernel(float* nodes, const uint4* __restrict__ rec,
-                                                        const uint32_t* __restrict__ lvl,
-                                                        const uint32_t* __restrict__ first, uint32_t max_nodes,
-                                                        LeafCtx L) {
-    extern __shared__ float sbox[];
-    uint4* srec = reinterpret_cast<uint4*>(sbox + 6 * max_nodes);
-    uint32_t* slvl = reinterpret_cast<uint32_t*>(srec + max_nodes);
-    const uint32_t l0 = first[blockIdx.x], nl = first[blockIdx.x + 1] - l0;
-    const uint32_t base = lvl[l0], end = lvl[l0 + nl];
-    for (uint32_t i = base + threadIdx.x; i < end; i += NT) srec[i - base] = rec[i];
-    for (uint32_t l = threadIdx.x; l <= nl; l += NT) slvl[l] = lvl[l0 + l] - base;
-    __syncthreads();
-    for (uint32_t l = 0; l < nl; l++) {
-        const uint32_t e = slvl[l + 1];
-        for (uint32_t i = slvl[l] + threadIdx.x; i < e; i += NT) refit_rec<SCENE>(nodes, srec[i], sbox, i, L);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-}
-
-__global__ __launch_bounds__(kAB) void wide_gather_kernel(WideNode* wide, const uint32_t* __restrict__ src,
-                                                         uint32_t n_slots, const float* __restrict__ bin) {
-    const uint32_t q = blockIdx.x * kAB + threadIdx.x;
-    if (q >= n_slots) return;
-    const uint32_t sidx = src[q];
-    if (sidx == 0xffffffffu) return;
-    float lo[3], hi[3];
-    bin_child_box(bin + 16 * (size_t)(sidx >> 1), (int)(sidx & 1u), lo, hi);
-    WideNode& w = wide[q >> 2];
-    const uint32_t sl = q & 3u;
-    w.lo_x[sl] = lo[0]; w.lo_y[sl] = lo[1]; w.lo_z[sl] = lo[2];
-    w.hi_x[sl] = hi[0]; w.hi_y[sl] = hi[1]; w.hi_z[sl] = hi[2];
-}
-
-// m_sLocalBox of the refit mesh: the union of its root's children.
-__global__ void mesh_box_kernel(const float* root, float* out) {
-    float lo[3], hi[3];
-    bin_node_box(root, lo, hi);
-    for (int k = 0; k < 3; k++) { out[k] = lo[k]; out[3 + k] = hi[k]; }
 }
 
 __global__ __launch_bounds__(kAB) void inst_box_kernel(const ctl_node* __restrict__ nodes, const float4* __restrict__ xf,
@@ -395,205 +406,169 @@ bool anim_upload(AnimState* A, T** dst, const T* src, size_t n) {
     return n == 0 || hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
 }
 
-bool upload_blocks(AnimState* A, AnimTree::Blocks& B, const std::vector<uint4>& rec, const std::vector<uint32_t>& lvl,
-                   const std::vector<uint32_t>& first) {
-    B.n_sets = (uint32_t)first.size() - 1;
-    B.max_nodes += B.max_nodes & 1u;   // even: the records after the boxes stay 16-B aligned
-    return anim_upload(A, &B.d_rec, rec.data(), rec.size()) && anim_upload(A, &B.d_lvl, lvl.data(), lvl.size()) &&
-           anim_upload(A, &B.d_first, first.data(), first.size());
-}
-
-// Refit plan of a binary tree (BVHNodeData, TriIntersectorData.h:44-50).
-//   - the cut: the subtrees of at most kSubMax inner nodes hanging off the
-//     nodes above them, one block set each;
-//   - above the cut, by depth from the root, deepest first: the narrow levels
-//     at the top (each at most kTopMax wide, together at most kTopLds) in one
-//     block set, the wider levels below them one launch each.
-// A mesh tree (n_entries > 0, `idx` its entries' TriIntersectorData2 words) also
-// lists its leaves for anim_leaf_kernel, which writes their slots; a node with
-// only leaf children is then in no list.  Every entry must lie in exactly one leaf.
-bool plan_binary(AnimState* A, AnimTree& T, const ctl_bvh_node* nodes, uint32_t n_nodes, uint32_t base_f4,
-                 uint32_t root, uint32_t n_entries, const uint32_t* idx, std::string& err) {
-    T.base = base_f4;
-    if (n_nodes == 0 || root >= n_nodes) { err = "refit plan: empty tree"; return false; }
-    const bool mesh = n_entries > 0;
-    auto child = [&](uint32_t k, int c) {
-        int32_t v;
-        memcpy(&v, &nodes[k].v[12 + c], 4);
-        return v;
-    };
-    auto kids = [&](uint32_t k, uint32_t* out) {
-        int n = 0;
-        for (int c = 0; c < 2; c++) {
-            const int32_t v = child(k, c);
-            if (v >= 0 && v != kSent) out[n++] = (uint32_t)v >> 2;
-        }
-        return n;
-    };
-    // depth of every node reachable from the root, and a pre-order
-    std::vector<int> depth(n_nodes, -1);
-    std::vector<uint32_t> pre, st{root};
-    depth[root] = 0;
+// The rebuild plan of a mesh tree (the compiled tree the upload put on the
+// device): its leaves with the slots that hold them, the objects under every
+// node, and the 4-wide copy's parent links and leaf slots.
+bool plan_mesh(AnimState* A, MeshRebuild& R, const ctl_bvh_node* nodes, uint32_t n_nodes, uint32_t n_entries,
+               const uint32_t* idx, const WideNode* wn, uint32_t n_wide, std::string& err) {
+    R.n_nodes = n_nodes;
+    if (n_nodes == 0) { err = "rebuild plan: empty tree"; return false; }
+    std::vector<uint4> leaves;
+    std::vector<int32_t> objects(n_nodes, 0);
+    std::vector<uint8_t> seen(n_entries, 0), node_seen(n_nodes, 0);
+    // pre-order from the root, then the objects children first
+    std::vector<uint32_t> pre, st{0};
+    node_seen[0] = 1;
     while (!st.empty()) {
         const uint32_t k = st.back();
         st.pop_back();
         pre.push_back(k);
-        uint32_t ch[2];
-        const int nc = kids(k, ch);
-        for (int i = 0; i < nc; i++) {
-            if (ch[i] >= n_nodes || depth[ch[i]] >= 0) { err = "refit plan: malformed tree"; return false; }
-            depth[ch[i]] = depth[k] + 1;
-            st.push_back(ch[i]);
-        }
-    }
-    if (pre.size() >= kRefGlobal) { err = "refit plan: tree too large"; return false; }
-    // inner nodes per subtree (reverse pre-order: children first)
-    std::vector<uint32_t> size(n_nodes, 0);
-    for (size_t i = pre.size(); i-- > 0;) {
-        uint32_t ch[2];
-        const int nc = kids(pre[i], ch);
-        size[pre[i]] = 1;
-        for (int c = 0; c < nc; c++) size[pre[i]] += size[ch[c]];
-    }
-    std::vector<int32_t> loc(n_nodes, -1);   // LDS slot of a node of the set being planned
-    auto record = [&](uint32_t k) {
-        uint32_t r[2];
         for (int c = 0; c < 2; c++) {
-            const int32_t v = child(k, c);
-            if (v == kSent) r[c] = kRefNone;
-            else if (v < 0) r[c] = mesh ? kRefLeafSlot : kRefInst + (uint32_t)~v;
-            else if (loc[(uint32_t)v >> 2] >= 0) r[c] = (uint32_t)loc[(uint32_t)v >> 2];
-            else r[c] = kRefGlobal + ((uint32_t)v >> 2);
-        }
-        return make_uint4(k, r[0], r[1], 0u);
-    };
-    // a block set from its nodes grouped by level, deepest first
-    auto add_set = [&](const std::vector<std::vector<uint32_t>>& lv, std::vector<uint4>& rec, std::vector<uint32_t>& lvl,
-                       std::vector<uint32_t>& first, uint32_t& max_nodes, uint32_t& max_levels) {
-        first.push_back((uint32_t)lvl.size());
-        const size_t r0 = rec.size(), v0 = lvl.size();
-        for (const auto& level : lv) {
-            if (level.empty()) continue;
-            lvl.push_back((uint32_t)rec.size());
-            for (uint32_t k : level) rec.push_back(record(k));
-            for (size_t q = 0; q < level.size(); q++) loc[level[q]] = (int32_t)(rec.size() - level.size() - r0 + q);
-        }
-        max_nodes = std::max<uint32_t>(max_nodes, (uint32_t)(rec.size() - r0));
-        max_levels = std::max<uint32_t>(max_levels, (uint32_t)(lvl.size() - v0));
-        for (size_t q = r0; q < rec.size(); q++) loc[rec[q].x] = -1;
-    };
-    // the cut
-    std::vector<uint32_t> top, cuts;
-    st.assign(1, root);
-    while (!st.empty()) {
-        const uint32_t k = st.back();
-        st.pop_back();
-        if (size[k] <= kSubMax) { cuts.push_back(k); continue; }
-        top.push_back(k);   // more than one inner node at and below it: an inner child
-        uint32_t ch[2];
-        const int nc = kids(k, ch);
-        for (int c = 0; c < nc; c++) st.push_back(ch[c]);
-    }
-    std::sort(cuts.begin(), cuts.end());
-    std::vector<uint4> rec;
-    std::vector<uint32_t> lvl, first;
-    std::vector<std::vector<uint32_t>> lv;
-    for (uint32_t r : cuts) {
-        lv.clear();
-        st.assign(1, r);
-        while (!st.empty()) {
-            const uint32_t k = st.back();
-            st.pop_back();
-            uint32_t ch[2];
-            const int nc = kids(k, ch);
-            for (int c = 0; c < nc; c++) st.push_back(ch[c]);
-            if (mesh && nc == 0) continue;   // leaf slots only: anim_leaf_kernel
-            const size_t d = (size_t)(depth[k] - depth[r]);
-            if (lv.size() <= d) lv.resize(d + 1);
-            lv[d].push_back(k);
-        }
-        if (lv.empty()) continue;
-        std::reverse(lv.begin(), lv.end());
-        for (auto& level : lv) std::sort(level.begin(), level.end());
-        add_set(lv, rec, lvl, first, T.sub.max_nodes, T.sub.max_levels);
-    }
-    lvl.push_back((uint32_t)rec.size());
-    if (first.empty()) first.push_back(0);
-    else first.push_back((uint32_t)lvl.size() - 1);
-    if (!upload_blocks(A, T.sub, rec, lvl, first)) { err = "refit plan: upload failed"; return false; }
-    // above the cut, deepest first; the top levels that fit one block
-    std::sort(top.begin(), top.end(), [&](uint32_t a, uint32_t b) {
-        return depth[a] != depth[b] ? depth[a] > depth[b] : a < b;
-    });
-    std::vector<uint32_t> off;
-    for (size_t i = 0; i < top.size(); i++)
-        if (i == 0 || depth[top[i]] != depth[top[i - 1]]) off.push_back((uint32_t)i);
-    off.push_back((uint32_t)top.size());
-    size_t split = off.size() - 1;   // levels [split, end) go to the top block set
-    while (split > 0 && off[split] - off[split - 1] <= kTopMax && top.size() - off[split - 1] <= kTopLds) split--;
-    T.level_off.assign(off.begin(), off.begin() + split + 1);
-    lv.clear();
-    for (size_t l = split; l + 1 < off.size(); l++) lv.emplace_back(top.begin() + off[l], top.begin() + off[l + 1]);
-    rec.clear(); lvl.clear(); first.clear();
-    if (!lv.empty()) add_set(lv, rec, lvl, first, T.top.max_nodes, T.top.max_levels);
-    lvl.push_back((uint32_t)rec.size());
-    first.push_back((uint32_t)lvl.size() - 1);
-    if (!upload_blocks(A, T.top, rec, lvl, first) ||
-        !anim_upload(A, &T.d_order, top.data(), off[split])) { err = "refit plan: upload failed"; return false; }
-    T.valid = true;
-    if (!mesh) return true;
-    // the leaves of a mesh tree, in entry order
-    std::vector<uint4> leaves;
-    std::vector<uint8_t> seen(n_entries, 0);
-    for (uint32_t k : pre)
-        for (int c = 0; c < 2; c++) {
-            const int32_t v = child(k, c);
-            if (v >= 0 || v == kSent) continue;
+            const int32_t v = rb_kid(nodes[k], c);
+            if (v == kSent) continue;
+            if (v >= 0) {
+                const uint32_t ch = (uint32_t)v >> 2;
+                if (ch >= n_nodes || node_seen[ch] || rb_parent(nodes[ch]) != (int32_t)(k << 2)) {
+                    err = "rebuild plan: malformed tree (child range, repeat or parent word)";
+                    return false;
+                }
+                node_seen[ch] = 1;
+                st.push_back(ch);
+                continue;
+            }
             uint32_t e = (uint32_t)~v;
             for (;; e++) {
-                if (e >= n_entries || seen[e]) { err = "refit plan: a leaf's entries overrun or overlap"; return false; }
+                if (e >= n_entries || seen[e]) { err = "rebuild plan: a leaf's entries overrun or overlap"; return false; }
                 seen[e] = 1;
                 if (idx[e] & 1) break;
             }
-            leaves.push_back(make_uint4(k << 1 | (uint32_t)c, (uint32_t)~v, e + 1 - (uint32_t)~v, 0u));
+            leaves.push_back(make_uint4(k << 1 | (uint32_t)c, (uint32_t)~v, e + 1 - (uint32_t)~v, 0xffffffffu));
         }
-    if (std::find(seen.begin(), seen.end(), 0) != seen.end()) { err = "refit plan: an entry lies in no leaf"; return false; }
-    std::sort(leaves.begin(), leaves.end(), [](uint4 a, uint4 b) { return a.y < b.y; });
-    T.n_leaf = (uint32_t)leaves.size();
-    if (!anim_upload(A, &T.d_leaf, leaves.data(), leaves.size())) { err = "refit plan: upload failed"; return false; }
-    return true;
-}
-
-bool plan_gather(AnimState* A, WideGather& G, const uint32_t* src, uint32_t n_nodes, uint32_t base, std::string& err) {
-    G.base = base;
-    G.n_slots = 4 * n_nodes;
-    if (!anim_upload(A, &G.d_src, src, G.n_slots)) { err = "refit plan: upload failed"; return false; }
-    G.valid = true;
-    return true;
-}
-
-template <bool SCENE>
-void launch_refit(hipStream_t s, const AnimTree& T, float* bin_base, const LeafCtx& L) {
-    const size_t per = 6 * sizeof(float) + sizeof(uint4);
-    if (T.sub.n_sets)
-        hipLaunchKernelGGL((refit_block_kernel<SCENE, kAB>), dim3(T.sub.n_sets), dim3(kAB),
-                           per * T.sub.max_nodes + 4 * (T.sub.max_levels + 1), s,
-                           bin_base, T.sub.d_rec, T.sub.d_lvl, T.sub.d_first, T.sub.max_nodes, L);
-    for (size_t l = 0; l + 1 < T.level_off.size(); l++) {
-        const uint32_t first = T.level_off[l], cnt = T.level_off[l + 1] - first;
-        hipLaunchKernelGGL(refit_bin_kernel<SCENE>, dim3((cnt + kAB - 1) / kAB), dim3(kAB), 0, s, bin_base,
-                           T.d_order + first, cnt, L);
     }
-    if (T.top.n_sets)
-        hipLaunchKernelGGL((refit_block_kernel<SCENE, 1024>), dim3(1), dim3(1024),
-                           per * T.top.max_nodes + 4 * (T.top.max_levels + 1), s,
-                           bin_base, T.top.d_rec, T.top.d_lvl, T.top.d_first, T.top.max_nodes, L);
+    if (rb_parent(nodes[0]) >= 0) { err = "rebuild plan: the root has a parent word"; return false; }
+    if (std::find(seen.begin(), seen.end(), 0) != seen.end()) { err = "rebuild plan: an entry lies in no leaf"; return false; }
+    for (size_t i = pre.size(); i-- > 0;) {
+        const uint32_t k = pre[i];
+        for (int c = 0; c < 2; c++) {
+            const int32_t v = rb_kid(nodes[k], c);
+            if (v == kSent) continue;
+            if (v >= 0) objects[k] += objects[(uint32_t)v >> 2];
+            else for (uint32_t e = (uint32_t)~v;; e++) { objects[k]++; if (idx[e] & 1) break; }
+        }
+    }
+    std::sort(leaves.begin(), leaves.end(), [](uint4 a, uint4 b) { return a.y < b.y; });
+    std::vector<uint32_t> leaf_of(n_entries, 0xffffffffu);
+    for (size_t i = 0; i < leaves.size(); i++) leaf_of[leaves[i].y] = (uint32_t)i;
+    // the 4-wide copy: every leaf slot is one binary leaf (counted: first entry << 3 | count)
+    std::vector<uint32_t> wup(n_wide, 0xffffffffu);
+    if (n_wide) {
+        std::vector<uint32_t> wide_leaf(n_entries, 0xffffffffu);
+        for (uint32_t i = 0; i < n_wide; i++)
+            for (int q = 0; q < 4; q++) {
+                const int32_t v = wn[i].child[q];
+                if (v == kSent) continue;
+                if (v >= 0) {
+                    if ((uint32_t)v >= n_wide || wup[v] != 0xffffffffu) { err = "rebuild plan: malformed 4-wide tree"; return false; }
+                    wup[v] = i << 2 | (uint32_t)q;
+                } else {
+                    const uint32_t first = (uint32_t)~v >> 3;
+                    if (first >= n_entries || leaf_of[first] == 0xffffffffu) {
+                        err = "rebuild plan: a 4-wide leaf is no binary leaf";
+                        return false;
+                    }
+                    wide_leaf[first] = i << 2 | (uint32_t)q;
+                }
+            }
+        for (uint4& l : leaves) {
+            l.w = wide_leaf[l.y];
+            if (l.w == 0xffffffffu) { err = "rebuild plan: a binary leaf is in no 4-wide leaf slot"; return false; }
+        }
+    }
+    R.n_leaf = (uint32_t)leaves.size();
+    R.n_wide = n_wide;
+    if (!anim_upload(A, &R.d_leaf, leaves.data(), leaves.size()) ||
+        !anim_upload(A, &R.d_leaf_of, leaf_of.data(), leaf_of.size()) ||
+        !anim_upload(A, &R.d_objects, objects.data(), objects.size()) || !anim_alloc(A, &R.d_cnt, n_nodes) ||
+        hipMemset(R.d_cnt, 0, n_nodes * sizeof(uint32_t)) != hipSuccess ||
+        (n_wide && (!anim_upload(A, &R.d_wup, wup.data(), wup.size()) || !anim_alloc(A, &R.d_wcnt, n_wide) ||
+                    hipMemset(R.d_wcnt, 0, n_wide * sizeof(uint32_t)) != hipSuccess))) {
+        err = "rebuild plan: upload failed";
+        return false;
+    }
+    return true;
 }
 
-void launch_gather(hipStream_t s, const WideGather& G, WideNode* wide_base, const float* bin_base) {
-    if (!G.valid || !G.n_slots) return;
-    hipLaunchKernelGGL(wide_gather_kernel, dim3((G.n_slots + kAB - 1) / kAB), dim3(kAB), 0, s, wide_base + G.base,
-                       G.d_src, G.n_slots, bin_base);
+// The instance tree along the moved instances' paths (host/bvh_rebuild.h), its
+// 4-wide copy refit in its topology, both uploaded; inst = 6 floats per node.
+bool rebuild_scene(AnimState* A, DevScene& S, const float* inst, const std::vector<uint32_t>& moved, hipStream_t s) {
+    SceneTrees& T = A->scene;
+    if (T.root < 0 || T.bin.empty()) return true;
+    auto hit = [&](int32_t v) { return std::find(moved.begin(), moved.end(), (uint32_t)~v) != moved.end(); };
+    const std::vector<uint8_t> flag = flag_paths(T.bin.data(), T.bin.size(), hit);
+    auto leaf_box = [&](int32_t v) {
+        const float* b = inst + 6 * (size_t)(uint32_t)~v;
+        return RbBox{{b[0], b[1], b[2]}, {b[3], b[4], b[5]}};
+    };
+    auto one = [](int32_t) { return 1; };
+    auto R = make_tree_rebuild(T.bin.data(), leaf_box, one, &flag);
+    R.run(T.root, T.bin.size());
+    if (hipMemcpyAsync(const_cast<float4*>(S.scene_bvh), T.bin.data(), T.bin.size() * sizeof(ctl_bvh_node),
+                       hipMemcpyHostToDevice, s) != hipSuccess)
+        return false;
+    if (S.wide && !T.wide.empty()) {
+        for (uint32_t i : T.wide_post) {
+            WideNode& w = T.wide[i];
+            for (int q = 0; q < 4; q++) {
+                const int32_t v = w.child[q];
+                if (v == kSent) continue;
+                RbBox b;
+                if (v < 0) {
+                    b = leaf_box(v);
+                } else {
+                    const WideNode& ch = T.wide[(uint32_t)v];
+                    b = rb_identity();
+                    for (int k = 0; k < 4; k++)
+                        if (ch.child[k] != kSent)
+                            b = rb_union(b, RbBox{{ch.lo_x[k], ch.lo_y[k], ch.lo_z[k]}, {ch.hi_x[k], ch.hi_y[k], ch.hi_z[k]}});
+                }
+                w.lo_x[q] = b.lo[0]; w.lo_y[q] = b.lo[1]; w.lo_z[q] = b.lo[2];
+                w.hi_x[q] = b.hi[0]; w.hi_y[q] = b.hi[1]; w.hi_z[q] = b.hi[2];
+            }
+        }
+        if (hipMemcpyAsync(const_cast<float4*>(S.scene_wbvh), T.wide.data(), T.wide.size() * sizeof(WideNode),
+                           hipMemcpyHostToDevice, s) != hipSuccess)
+            return false;
+    }
+    return hipStreamSynchronize(s) == hipSuccess;   // the host trees are read by the copies
+}
+
+// Instance boxes and the scene box / epsilon on the device (inst_box_kernel,
+// scene_eps_kernel), read back with the instance boxes for the host rebuild of
+// the instance tree.
+ctl_status scene_after_move(ctl_ctx* c, const std::vector<uint32_t>& moved, hipStream_t s, const char* what) {
+    AnimState* A = c->anim;
+    DevScene& S = c->scene;
+    hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf, A->n_nodes,
+                       A->d_mesh_boxes, A->d_inst_boxes);
+    hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps,
+                       const_cast<ctl_env_light*>(S.env), A->d_mesh_boxes, A->n_meshes);
+    if (hipGetLastError() != hipSuccess) { c->err = std::string(what) + ": launch failed"; return CTL_ERR_HIP; }
+    if (hipMemcpyAsync(A->h_eps, A->d_eps, 10 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(A->h_eps + 10, A->d_inst_boxes, 6 * sizeof(float) * A->n_nodes, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        c->err = std::string(what) + ": readback failed";
+        return CTL_ERR_HIP;
+    }
+    if (!rebuild_scene(A, S, A->h_eps + 10, moved, s)) {
+        c->err = std::string(what) + ": instance tree upload failed";
+        return CTL_ERR_HIP;
+    }
+    S.ray_eps = A->h_eps[6];
+    for (int k = 0; k < 3; k++) S.cull_m[k] = A->h_eps[7 + k];
+    c->device_eps = true;
+    c->device_edited = true;
+    return CTL_OK;
 }
 
 }  // namespace
@@ -610,8 +585,7 @@ void anim_free(ctl_ctx* c) {
 // Called by ctl_scene_upload once the scene arrays are on the device.
 // wn / wbase / sw: the 4-wide trees built on upload (empty for binary scenes).
 int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>& wn,
-               const std::vector<uint32_t>& wbase, const std::vector<WideNode>& sw,
-               const std::vector<uint32_t>& wsrc, const std::vector<uint32_t>& ssrc) {
+               const std::vector<uint32_t>& wbase, const std::vector<WideNode>& sw) {
     anim_free(c);
     if (!d->mesh_boxes) return CTL_OK;
     c->anim = new AnimState();
@@ -620,25 +594,40 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
     auto fail = [&](const std::string& m) { c->err = "scene_upload: " + m; anim_free(c); return (int)CTL_ERR_INVALID; };
     A->n_meshes = d->n_meshes;
     A->n_nodes = d->n_nodes;
+    for (uint32_t i = 0; i < d->n_nodes; i++) A->node_mesh.push_back(d->nodes[i].mesh_index);
     if (!anim_upload(A, &A->d_mesh_boxes, d->mesh_boxes, 6ull * d->n_meshes) ||
         !anim_alloc(A, &A->d_inst_boxes, 6ull * std::max(1u, d->n_nodes)) || !anim_alloc(A, &A->d_eps, 10) ||
-        hipHostMalloc((void**)&A->h_eps, 10 * sizeof(float), hipHostMallocDefault) != hipSuccess)
+        hipHostMalloc((void**)&A->h_eps, (10 + 6ull * std::max(1u, d->n_nodes)) * sizeof(float), hipHostMallocDefault) !=
+            hipSuccess)
         return fail("animation state allocation failed");
-    const bool wide = !wn.empty() || !sw.empty();
-    // the instance tree's refit plan: animated meshes and moved nodes (ctl_scene_set_transform)
+    // the instance trees' host copies (ctl_scene_set_transform / animate rebuild them)
     if (d->n_nodes > 0 && d->scene_start_node >= 0 && d->n_scene_bvh_nodes > 0) {
-        if (!plan_binary(A, A->scene_bin, d->scene_bvh_nodes, d->n_scene_bvh_nodes, 0,
-                         (uint32_t)d->scene_start_node >> 2, 0, nullptr, err))
-            return fail(err);
-        if (wide && !sw.empty()) {
-            if (ssrc.size() != 4 * sw.size()) return fail("wide source map missing");
-            if (!plan_gather(A, A->scene_wide, ssrc.data(), (uint32_t)sw.size(), 0, err)) return fail(err);
+        SceneTrees& T = A->scene;
+        T.bin.assign(d->scene_bvh_nodes, d->scene_bvh_nodes + d->n_scene_bvh_nodes);
+        T.root = d->scene_start_node;
+        T.wide = sw;
+        // children before parents: reverse pre-order from node 0
+        std::vector<uint32_t> st;
+        if (!T.wide.empty()) st.push_back(0);
+        while (!st.empty()) {
+            const uint32_t k = st.back();
+            st.pop_back();
+            T.wide_post.push_back(k);
+            for (int q = 0; q < 4; q++) {
+                const int32_t v = T.wide[k].child[q];
+                if (v >= 0 && v != kSent) {
+                    if ((size_t)v >= T.wide.size() || T.wide_post.size() > T.wide.size()) return fail("malformed instance 4-wide tree");
+                    st.push_back((uint32_t)v);
+                }
+            }
         }
+        std::reverse(T.wide_post.begin(), T.wide_post.end());
     }
     if (d->n_anim_meshes == 0) return CTL_OK;
     if (!anim_upload(A, (ctl_anim_vertex**)&A->d_verts, d->anim_vertices, d->n_anim_vertices) ||
         !anim_upload(A, (uint32_t**)&A->d_tris, d->anim_triangles, 3ull * d->n_anim_triangles))
         return fail("animation upload failed");
+    const bool wide = !wn.empty();
     size_t tmp = 0;
     for (uint32_t a = 0; a < d->n_anim_meshes; a++) {
         AnimMeshPlan P;
@@ -661,15 +650,15 @@ int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>&
         for (uint64_t e = e0; e < e1; e++)
             if ((d->tri_indices[e] >> 1) >= P.am.tri_count) return fail("animated mesh entry out of range");
         P.n_entries = (uint32_t)(e1 - e0);
-        if (!plan_binary(A, P.bin, d->bvh_nodes + n0, (uint32_t)(n1 - n0), P.km.bvh_node_offset, 0, P.n_entries,
-                         d->tri_indices + e0, err))
-            return fail(err);
+        uint32_t wb = 0, we = 0;
         if (wide) {
-            const uint32_t wb = wbase[P.am.mesh];
-            const uint32_t we = P.am.mesh + 1 < wbase.size() ? wbase[P.am.mesh + 1] : (uint32_t)wn.size();
-            if (wsrc.size() != 4 * wn.size()) return fail("wide source map missing");
-            if (!plan_gather(A, P.wide, wsrc.data() + 4ull * wb, we - wb, wb, err)) return fail(err);
+            wb = wbase[P.am.mesh];
+            we = P.am.mesh + 1 < wbase.size() ? wbase[P.am.mesh + 1] : (uint32_t)wn.size();
         }
+        P.wide_base = wb;
+        if (!plan_mesh(A, P.rb, d->bvh_nodes + n0, (uint32_t)(n1 - n0), P.n_entries, d->tri_indices + e0,
+                       wide ? wn.data() + wb : nullptr, we - wb, err))
+            return fail(err);
         tmp = std::max<size_t>(tmp, P.am.vertex_count);
         A->meshes.push_back(std::move(P));
     }
@@ -718,39 +707,34 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
                                A->d_N);
     if (nt) hipLaunchKernelGGL(anim_tri_kernel, dim3((nt + kAB - 1) / kAB), dim3(kAB), 0, s, tris, nt, A->d_P, A->d_N,
                                const_cast<ctl_triangle_data*>(S.tri_data) + P.km.triangle_offset);
-    const uint32_t* idx = S.tri_idx + P.km.bvh_indices_offset;
-    float* bin = reinterpret_cast<float*>(const_cast<float4*>(S.bvh) + P.bin.base);
-    if (P.bin.n_leaf)
-        hipLaunchKernelGGL(anim_leaf_kernel, dim3((P.bin.n_leaf + kAB - 1) / kAB), dim3(kAB), 0, s, P.bin.d_leaf,
-                           P.bin.n_leaf, idx, tris, A->d_P, const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset, bin);
-    launch_refit<false>(s, P.bin, bin, LeafCtx{nullptr});
-    launch_gather(s, P.wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.wbvh)), bin);
-    hipLaunchKernelGGL(mesh_box_kernel, dim3(1), dim3(1), 0, s, bin, A->d_mesh_boxes + 6 * P.am.mesh);
-    // instances, scene trees, epsilon
+    if (P.rb.n_leaf) {
+        RebuildArgs R;
+        R.bin = reinterpret_cast<float*>(const_cast<float4*>(S.bvh)) + 4ull * P.km.bvh_node_offset;
+        R.wide = S.wide && P.rb.n_wide ? reinterpret_cast<WideNode*>(const_cast<float4*>(S.wbvh)) + P.wide_base : nullptr;
+        R.idx = S.tri_idx + P.km.bvh_indices_offset;
+        R.tris = tris;
+        R.P = A->d_P;
+        R.woop = const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset;
+        R.leaf = P.rb.d_leaf;
+        R.leaf_of = P.rb.d_leaf_of;
+        R.objects = P.rb.d_objects;
+        R.cnt = P.rb.d_cnt;
+        R.wup = P.rb.d_wup;
+        R.wcnt = P.rb.d_wcnt;
+        R.mesh_box = A->d_mesh_boxes + 6 * P.am.mesh;
+        R.n_leaf = P.rb.n_leaf;
+        hipLaunchKernelGGL(anim_rebuild_kernel, dim3((P.rb.n_leaf + kAB - 1) / kAB), dim3(kAB), 0, s, R);
+    }
+    if (hipGetLastError() != hipSuccess) { c->err = "scene_animate: launch failed"; return CTL_ERR_HIP; }
+    // instances of the mesh, the instance tree, epsilon (DynamicScene::AnimateMesh invalidates the node)
     if (A->n_nodes) {
-        hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf,
-                           A->n_nodes, A->d_mesh_boxes, A->d_inst_boxes);
-        LeafCtx LS{A->d_inst_boxes};
-        float* sbin = reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh));
-        if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
-        launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);
-        hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps,
-                           const_cast<ctl_env_light*>(S.env), A->d_mesh_boxes, A->n_meshes);
-        if (hipMemcpyAsync(A->h_eps, A->d_eps, 10 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
-            c->err = "scene_animate: epsilon readback failed";
-            return CTL_ERR_HIP;
-        }
-        S.ray_eps = A->h_eps[6];
-        for (int k = 0; k < 3; k++) S.cull_m[k] = A->h_eps[7 + k];
-        // a bound on every mesh box now on the device (cull_bound took them all),
-        // kept past an instance-only update (set_constants)
-        for (int k = 0; k < 3; k++) c->moved_cull_m[k] = S.cull_m[k];
-        c->mesh_moved = true;
-        c->device_eps = true;
+        std::vector<uint32_t> moved;
+        for (uint32_t i = 0; i < A->n_nodes; i++)
+            if (A->node_mesh[i] == P.am.mesh) moved.push_back(i);
+        const ctl_status r = scene_after_move(c, moved, s, "scene_animate");
+        if (r != CTL_OK) return r;
     }
     c->device_edited = true;
-    if (hipGetLastError() != hipSuccess) { c->err = "scene_animate: launch failed"; return CTL_ERR_HIP; }
     return CTL_OK;
 }
 
@@ -760,7 +744,7 @@ CTL_API ctl_status ctl_scene_set_transform(ctl_ctx* c, uint32_t node, const ctl_
     AnimState* A = c->anim;
     DevScene& S = c->scene;
     if (node >= S.n_nodes) { c->err = "scene_set_transform: node index out of range"; return CTL_ERR_INVALID; }
-    if (S.wide && S.quant && A->scene_bin.valid) {
+    if (S.wide && S.quant && A->scene.root >= 0) {
         c->err = "scene_set_transform: 64-B quantized trees are not refit (upload without CTL_SCENE_WIDE_QUANT)";
         return CTL_ERR_STATE;
     }
@@ -783,25 +767,7 @@ CTL_API ctl_status ctl_scene_set_transform(ctl_ctx* c, uint32_t node, const ctl_
         hipLaunchKernelGGL(light_recalc_kernel, dim3(1), dim3(64), 0, s, const_cast<ctl_light*>(S.lights), S.n_lights,
                            const_cast<ctl_light_tri*>(S.light_tris), const_cast<float*>(S.light_tri_cdf), S.woop,
                            S.tri_data, S.xf, node);
-    hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf, A->n_nodes,
-                       A->d_mesh_boxes, A->d_inst_boxes);
-    LeafCtx LS{A->d_inst_boxes};
-    float* sbin = reinterpret_cast<float*>(const_cast<float4*>(S.scene_bvh));
-    if (A->scene_bin.valid) launch_refit<true>(s, A->scene_bin, sbin, LS);
-    if (S.wide) launch_gather(s, A->scene_wide, reinterpret_cast<WideNode*>(const_cast<float4*>(S.scene_wbvh)), sbin);
-    hipLaunchKernelGGL(scene_eps_kernel, dim3(1), dim3(1), 0, s, A->d_inst_boxes, A->n_nodes, A->d_eps,
-                       const_cast<ctl_env_light*>(S.env), A->d_mesh_boxes, A->n_meshes);
-    if (hipGetLastError() != hipSuccess) { c->err = "scene_set_transform: launch failed"; return CTL_ERR_HIP; }
-    if (hipMemcpyAsync(A->h_eps, A->d_eps, 10 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
-        c->err = "scene_set_transform: epsilon readback failed";
-        return CTL_ERR_HIP;
-    }
-    S.ray_eps = A->h_eps[6];
-    for (int k = 0; k < 3; k++) S.cull_m[k] = A->h_eps[7 + k];
-    c->device_eps = true;
-    c->device_edited = true;
-    return CTL_OK;
+    return scene_after_move(c, std::vector<uint32_t>{node}, s, "scene_set_transform");
 }
 
 CTL_API ctl_status ctl_scene_read(ctl_ctx* c, uint32_t array, uint64_t first, uint64_t count, void* dst) {

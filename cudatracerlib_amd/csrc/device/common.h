@@ -608,11 +608,6 @@ struct ctl_ctx {
     uint32_t n_anim_meshes = 0;
     bool device_eps = false;                    // ray_eps derived on the device (set_transform / animate)
     bool device_edited = false;                 // set_transform / animate rewrote device arrays since the upload
-    // ctl_scene_animate moved mesh trees on the device: a bound (DevScene::cull_m
-    // of the animated scene) on their boxes, kept until the mesh trees are uploaded
-    // again, so a later instance-only update cannot shrink cull_m below them
-    bool mesh_moved = false;
-    float moved_cull_m[3] = {0.0f, 0.0f, 0.0f};
     ctl::DevScene scene{};
     bool has_scene = false;
     bool half_quirk = false;
@@ -679,7 +674,7 @@ void wavefront_free(ctl_ctx* c);
 // anim.hip
 struct WideNode;
 int anim_setup(ctl_ctx* c, const ctl_scene_desc* d, const std::vector<WideNode>& wn, const std::vector<uint32_t>& wbase,
-               const std::vector<WideNode>& sw, const std::vector<uint32_t>& wsrc, const std::vector<uint32_t>& ssrc);
+               const std::vector<WideNode>& sw);
 void anim_free(ctl_ctx* c);
 // wpt.hip
 int wpt_pass(ctl_ctx* c, const ctl_wpt_params* p, ctl_pixel* fb, hipStream_t s);

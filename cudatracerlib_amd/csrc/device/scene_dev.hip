@@ -204,14 +204,12 @@ void set_constants(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty) {
     // After ctl_scene_set_transform / ctl_scene_animate the device holds the
     // scene box the reference's getSceneBox would return (DynamicScene.cpp:583-587),
     // and its epsilon wins over the desc's until the instances are uploaded again.
-    // mesh trees uploaded again: their boxes are the desc's
-    if (dirty & CTL_DIRTY_BVH) c->mesh_moved = false;
     if (!c->device_eps || (dirty & CTL_DIRTY_NODES)) {
         S.ray_eps = d->ray_eps;
         cull_bound(d->box_min, d->box_max, d->mesh_boxes, d->n_meshes, S.cull_m);
-        // animated mesh trees still on the device may reach past the desc's mesh boxes
-        if (c->mesh_moved)
-            for (int k = 0; k < 3; k++) S.cull_m[k] = S.cull_m[k] > c->moved_cull_m[k] ? S.cull_m[k] : c->moved_cull_m[k];
+        // the desc's boxes bound the device's trees here: after set_transform /
+        // animate (device_edited) an instance update re-uploads every edited array
+        // with the trees (commit), so no moved box outlives this bound
         c->device_eps = false;
     }
     for (int i = 0; i < CTL_MAX_NUM_LIGHTS; i++) S.light_cdf[i] = d->light_cdf[i];
@@ -225,10 +223,11 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
     if ((d->flags & tree_bits) != c->tree_flags) dirty |= kDirtyTrees;
     // quantized trees are encoded together
     if ((d->flags & CTL_SCENE_WIDE_QUANT) && (dirty & kDirtyTrees)) dirty |= kDirtyTrees;
-    // animated meshes: their refit plans hold the wide trees' source maps
+    // animated meshes: their rebuild plans describe the trees on the device (shape,
+    // leaf holders, 4-wide links), so a tree update re-uploads every tree with them
     if (d->n_anim_meshes > 0 && (dirty & (kDirtyTrees | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES)))
         dirty |= kDirtyTrees | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES;
-    // the refit plans (anim_setup) are rebuilt with the instance tree's wide copy
+    // the rebuild plans (anim_setup) keep host copies of the instance trees
     if (dirty & (kDirtyTrees | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES)) dirty |= CTL_DIRTY_NODES;
     // after set_transform / animate, re-uploading any tree group returns every
     // device-edited array to the desc (geometry, instances, their area lights,
@@ -278,9 +277,8 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
     // 4-wide trees (host/bvh_wide.h) for the device traversal, unless the caller
     // asks for the reference's binary visit order
     const bool wide = (d->flags & CTL_SCENE_BINARY_BVH) == 0 && d->n_bvh_nodes > 0;
-    const bool want_src = d->n_anim_meshes > 0;
+    const bool animated = d->n_anim_meshes > 0;
     std::vector<WideNode> wn, sw;
-    std::vector<uint32_t> wsrc, ssrc;
     // the 4-wide mesh trees read the binary nodes, the leaf entries' last-in-leaf
     // flags (counted leaves) and the per-mesh offsets
     const bool mesh_trees = (dirty & (CTL_DIRTY_BVH | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES)) != 0;
@@ -289,7 +287,6 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
         if (mesh_trees) {
             c->h_wbase.assign(d->n_meshes, 0);
             int mesh_bin = 0, mesh_wide = 0;
-            std::vector<uint32_t> ms;
             for (uint32_t m = 0; m < d->n_meshes && d->n_bvh_nodes > 0; m++) {
                 const size_t first = d->meshes[m].bvh_node_offset / 4;
                 if (first >= d->n_bvh_nodes) throw std::runtime_error("mesh BVH offset out of range");
@@ -300,9 +297,8 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
                 // order); leaf children carry counts, each leaf bounded by its last-in-leaf flag
                 const uint64_t e0 = d->meshes[m].bvh_indices_offset;
                 if (e0 > d->n_tri_indices) throw std::runtime_error("mesh entry offset out of range");
-                collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn, want_src ? &ms : nullptr,
-                              d->tri_indices + e0, (size_t)(d->n_tri_indices - e0));
-                if (want_src) wsrc.insert(wsrc.end(), ms.begin(), ms.end());
+                collapse_wide(d->bvh_nodes + first, d->n_bvh_nodes - first, 0, wn, nullptr, d->tri_indices + e0,
+                              (size_t)(d->n_tri_indices - e0));
                 mesh_wide = std::max(mesh_wide, wide_stack_bound(wn.data() + c->h_wbase[m], wn.size() - c->h_wbase[m], 0, kStackMax));
             }
             c->stack_mesh_bin = mesh_bin;
@@ -313,7 +309,7 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
             if (d->n_nodes > 0 && d->scene_start_node >= 0) {
                 c->stack_top_bin = binary_stack_bound(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, kStackMax);
                 if (wide) {
-                    collapse_wide(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, sw, &ssrc);
+                    collapse_wide(d->scene_bvh_nodes, d->n_scene_bvh_nodes, d->scene_start_node, sw);
                     c->stack_top_wide = wide_stack_bound(sw.data(), sw.size(), 0, kStackMax);
                 }
             }
@@ -340,7 +336,7 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
     }
     if (wide && (mesh_trees || top_tree)) {
         // 64-B quantized nodes on request (not when the refit will rewrite float nodes)
-        const bool quant = (d->flags & CTL_SCENE_WIDE_QUANT) != 0 && !want_src;
+        const bool quant = (d->flags & CTL_SCENE_WIDE_QUANT) != 0 && !animated;
         auto encode = [](const std::vector<WideNode>& in, std::vector<QWideNode>& out) {
             out.resize(in.size());
             for (size_t i = 0; i < in.size(); i++) {
@@ -437,7 +433,7 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
     c->n_scene_bvh = d->n_scene_bvh_nodes;
     if (dirty & (kDirtyTrees | CTL_DIRTY_TRI_INDICES | CTL_DIRTY_MESHES)) {
         // instance-tree refit plan (moved nodes) and animated meshes' plans
-        int ar = anim_setup(c, d, wn, c->h_wbase, sw, wsrc, ssrc);
+        int ar = anim_setup(c, d, wn, c->h_wbase, sw);
         if (ar != CTL_OK) return (ctl_status)ar;
         SD_HIP(c, hipStreamSynchronize(s));
     }
@@ -457,7 +453,6 @@ void free_scene(ctl_ctx* c) {
     c->tree_flags = 0xffffffffu;
     c->device_eps = false;
     c->device_edited = false;
-    c->mesh_moved = false;
     c->scene = DevScene{};
     c->scene.env_index = 0xffffffffu;
 }

@@ -54,6 +54,7 @@ def load():
         "oracle_prim_pass": (C.c_uint64, [C.POINTER(SceneDesc), C.POINTER(PrimParams), C.c_uint64, vp, vp, C.c_int32,
                                           C.c_int32]),
         "oracle_animate": (None, [C.POINTER(SceneDesc), C.c_uint32, vp, vp, C.c_float, vp, vp, vp, vp, vp, vp]),
+        "oracle_scene_set_transform": (None, [C.POINTER(SceneDesc), vp, vp, vp, C.c_uint32, vp]),
         "oracle_wpt_render_pass": (C.c_uint64, [C.POINTER(SceneDesc), C.c_int32, C.c_int32, C.c_int32, C.c_uint32,
                                                 C.c_uint64, vp, C.c_int32, C.c_int32]),
         "oracle_image_resolve": (None, [vp, C.c_uint32, C.c_uint32, C.c_float, vp]),

@@ -26,6 +26,7 @@
 #include "../include/ctl_trace.h"
 
 #include <vector>
+#include <functional>
 #include <thread>
 #include <atomic>
 #include <mutex>
@@ -1512,6 +1513,127 @@ Box6 refit(ctl_bvh_node* nodes, uint32_t k, const LEAF& leaf) {
     return all;
 }
 
+// ---------------------------------------------------------------------------
+// BVHRebuilder::recomputeNode with its tree rotations
+// (Engine/SpatialStructures/BVH/BVHRebuilder.cpp:281-340; the rotations of the
+// paper cited at :12-13), as AnimatedMesh::k_ComputeState runs it on a mesh
+// tree every frame (AnimatedMesh.cpp:174-176: Build(&p, true), recomputeAll)
+// and SceneBVH::Build on the instance tree for the nodes DynamicScene
+// invalidated (DynamicScene.cpp:447,564; SceneBVH.cpp:43; only the flagged
+// path, :431-438).  The tree state persists: each call starts from the tree
+// the last one left.
+//   getBox (:598-609): NO_NODE = AABB::Identity; a leaf = its objects' boxes
+//     extended from the identity; an inner node = BVHNodeData::getBox, the
+//     union of BOTH stored child slots (an empty slot's stored box included)
+//   numLeafs (:645-657): objects under the node (bvhNodeData, BuildInfoTree)
+//   sah (:624-638), numberGrandchildren (:612-622), swapChildren (:691-702),
+//     setChild (:665-681): child value, slot box, parent (BVHNodeData d.z,
+//     native) of a moved inner node; propagateBBChange's writes to the
+//     ancestors are overwritten when the recursion returns to them
+//   AABB::Area (Math/AABB.h:19-23): 2 (x y + x z + y z) of max - min
+// ---------------------------------------------------------------------------
+constexpr int32_t kNoNode = 0x76543210;
+
+float box_area(const Box6& b) {
+    const float x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
+    return 2.0f * (x * y + x * z + y * z);
+}
+Box6 box_union(Box6 a, const Box6& b) { box_add(a, b); return a; }
+void node_set_kid(ctl_bvh_node& n, int c, int32_t v) { std::memcpy(&n.v[12 + c], &v, 4); }
+void node_set_parent(ctl_bvh_node& n, int32_t p) { std::memcpy(&n.v[14], &p, 4); }
+
+struct Rebuilder {
+    ctl_bvh_node* N;
+    std::function<Box6(int32_t)> leaf_box;     // union of the leaf's objects' boxes (from the identity)
+    std::function<int(int32_t)> leaf_count;    // objects in the leaf
+    std::function<void(int32_t)> leaf_set;     // setObject for the leaf's entries (may be empty)
+    const std::vector<uint8_t>* flagged = nullptr;   // inner nodes to recompute; null: recomputeAll
+    std::vector<int32_t> nleaf;
+
+    static bool inner(int32_t v) { return v >= 0 && v != kNoNode; }
+    int count(int32_t v) {   // BuildInfoTree (:476-495)
+        int s = 0;
+        for (int c = 0; c < 2; c++) {
+            const int32_t k = node_kid(N[v >> 2], c);
+            if (k < 0) s += leaf_count(k);
+            else if (k != kNoNode) s += count(k);
+        }
+        return nleaf[v >> 2] = s;
+    }
+    int num_leafs(int32_t v) { return v == kNoNode ? 0 : v < 0 ? leaf_count(v) : nleaf[v >> 2]; }
+    Box6 get_box(int32_t v) {
+        if (v == kNoNode) return box_empty();
+        if (v < 0) return leaf_box(v);
+        return box_union(node_child(N[v >> 2], 0), node_child(N[v >> 2], 1));
+    }
+    int32_t kid(int32_t v, int c) { return node_kid(N[v >> 2], c); }
+    int grandchildren(int32_t v, int c) {
+        const int32_t k = kid(v, c);
+        if (!inner(k)) return 0;
+        return (kid(k, 0) != kNoNode) + (kid(k, 1) != kNoNode);
+    }
+    float sah(int32_t v, int lc, int lg) {
+        const int32_t child = kid(v, lc), other = kid(v, 1 - lc);
+        const int32_t grand = kid(other, lg), og = kid(other, 1 - lg);
+        const float rhs_area = box_area(get_box(grand));
+        const int rhs_num = num_leafs(grand);
+        const Box6 lhs = box_union(get_box(child), get_box(og));
+        const int n1 = num_leafs(child), n2 = num_leafs(og);
+        return box_area(lhs) * (float)(n1 + n2) + rhs_area * (float)rhs_num;
+    }
+    void set_child(int32_t v, int c, int32_t k) {   // setChild's array writes
+        node_set_kid(N[v >> 2], c, k);
+        node_set_child(N[v >> 2], c, get_box(k));
+        if (inner(k)) node_set_parent(N[k >> 2], v);
+    }
+    void swap(int32_t v, int lc, int lg) {
+        const int32_t child = kid(v, lc), other = kid(v, 1 - lc);
+        const int32_t grand = kid(other, lg);
+        set_child(other, lg, child);
+        node_set_child(N[v >> 2], 1 - lc, get_box(other));   // propagateBBChange(other -> v)
+        set_child(v, lc, grand);
+        nleaf[other >> 2] += num_leafs(child) - num_leafs(grand);
+    }
+    Box6 recompute(int32_t v) {
+        const int32_t c[2] = {kid(v, 0), kid(v, 1)};
+        bool modified = false;
+        for (int i = 0; i < 2; i++) {
+            if (c[i] < 0 || (c[i] != kNoNode && (!flagged || (*flagged)[c[i] >> 2]))) {
+                modified = true;
+                Box6 b;
+                if (c[i] < 0) {
+                    if (leaf_set) leaf_set(c[i]);
+                    b = get_box(c[i]);
+                } else {
+                    b = recompute(c[i]);
+                }
+                node_set_child(N[v >> 2], i, b);
+            }
+        }
+        if (modified) {
+            const bool ab = grandchildren(v, 0) == 2, cd = grandchildren(v, 1) == 2;
+            float rot[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+            if (ab) { rot[0] = sah(v, 1, 0); rot[1] = sah(v, 1, 1); }
+            if (cd) { rot[2] = sah(v, 0, 1); rot[3] = sah(v, 0, 0); }
+            int best = 0;
+            for (int i = 1; i < 4; i++)
+                if (rot[i] < rot[best]) best = i;   // std::min_element: the first smallest
+            const float cur = box_area(get_box(c[0])) * (float)num_leafs(c[0]) +
+                              box_area(get_box(c[1])) * (float)num_leafs(c[1]);
+            if (rot[best] < cur) {
+                static const int lc[4] = {1, 1, 0, 0}, lg[4] = {0, 1, 1, 0};
+                swap(v, lc[best], lg[best]);
+            }
+        }
+        return get_box(v);
+    }
+    Box6 run(int32_t root) {
+        nleaf.assign(nleaf.size(), 0);
+        count(root);
+        return recompute(root);
+    }
+};
+
 void instance_box(const M44& xf, const float lo[3], const float hi[3], Box6& o) {   // scene compile's node box
     o = box_empty();
     for (int c = 0; c < 8; c++) {
@@ -1523,6 +1645,48 @@ void instance_box(const M44& xf, const float lo[3], const float hi[3], Box6& o) 
         float ext = omax(std::fabs(o.lo[k]), std::fabs(o.hi[k])) * 1e-6f + 1e-30f;
         o.lo[k] -= ext; o.hi[k] += ext;
     }
+}
+
+// The instance tree after nodes `moved` changed (SceneBVH::Build ->
+// BVHRebuilder::Build without invalidateAll: only the flagged path, with
+// rotations): instance boxes from the mesh boxes and the transforms (xf16 per
+// node, or the desc's), the scene box's epsilon (DynamicScene.cpp:587).
+void scene_rebuild(const ctl_scene_desc* d, ctl_bvh_node* scene, const float* mesh_boxes, const float* xf16,
+                   const std::vector<uint32_t>& moved, float* eps) {
+    std::vector<Box6> inst(d->n_nodes);
+    Box6 sb = box_empty();
+    for (uint32_t i = 0; i < d->n_nodes; i++) {
+        M44 xf; std::memcpy(xf.d, xf16 ? xf16 + 16 * i : d->node_xf[i].m, 64);
+        const float* m = mesh_boxes + 6 * d->nodes[i].mesh_index;
+        instance_box(xf, m, m + 3, inst[i]);
+        box_add(sb, inst[i]);
+    }
+    if (d->n_nodes && d->scene_start_node >= 0 && d->n_scene_bvh_nodes) {
+        const uint32_t ns = d->n_scene_bvh_nodes;
+        // propagateFlag (:343-362): each moved instance's holder and its ancestors
+        std::vector<uint8_t> flag(ns, 0);
+        for (uint32_t k = 0; k < ns; k++)
+            for (int c = 0; c < 2; c++) {
+                const int32_t v = node_kid(scene[k], c);
+                if (v >= 0 || v == kNoNode || std::find(moved.begin(), moved.end(), (uint32_t)~v) == moved.end()) continue;
+                for (int32_t a = (int32_t)(k * 4); a != -1 && !flag[a >> 2];) {
+                    flag[a >> 2] = 1;
+                    std::memcpy(&a, &scene[a >> 2].v[14], 4);
+                }
+            }
+        Rebuilder R;
+        R.N = scene;
+        R.nleaf.assign(ns, 0);
+        R.flagged = &flag;
+        R.leaf_box = [&](int32_t v) { return box_union(box_empty(), inst[(uint32_t)~v]); };
+        R.leaf_count = [](int32_t) { return 1; };
+        const int32_t root = d->scene_start_node;
+        R.nleaf.assign(ns, 0);
+        R.count(root);
+        if (flag[root >> 2]) R.recompute(root);
+    }
+    V3 size = v3(sb.hi[0] - sb.lo[0], sb.hi[1] - sb.lo[1], sb.hi[2] - sb.lo[2]);
+    *eps = 1e-4f * length(size);
 }
 
 void animate(const ctl_scene_desc* d, uint32_t anim, const float* b0, const float* b1, float t, ctl_triangle_data* tri,
@@ -1553,9 +1717,16 @@ void animate(const ctl_scene_desc* d, uint32_t anim, const float* b0, const floa
         uint32_t i = d->tri_indices[e] >> 1;
         woop_set(P[T[3 * i]], P[T[3 * i + 1]], P[T[3 * i + 2]], woop + 12 * e);
     }
-    // refit of the mesh tree; leaves = the triangles of their entry run
+    // BVHRebuilder over the mesh tree (recomputeAll, with rotations); leaves =
+    // the triangles of their entry run, each triangle's box from its vertices
+    // (AnimProvider::getBox, AnimatedMesh.cpp:106-114)
     const uint32_t* idx = d->tri_indices + km.bvh_indices_offset;
-    auto leaf = [&](int32_t v) {
+    const uint32_t n0 = km.bvh_node_offset / 4;
+    const uint64_t n1 = last ? d->n_bvh_nodes : d->meshes[am.mesh + 1].bvh_node_offset / 4;
+    Rebuilder R;
+    R.N = nodes + n0;
+    R.nleaf.assign(n1 - n0, 0);
+    R.leaf_box = [&](int32_t v) {
         Box6 b = box_empty();
         for (uint32_t e = (uint32_t)~v;; e++) {
             uint32_t i = idx[e] >> 1;
@@ -1564,21 +1735,18 @@ void animate(const ctl_scene_desc* d, uint32_t anim, const float* b0, const floa
         }
         return b;
     };
-    Box6 mb = refit(nodes + km.bvh_node_offset / 4, 0, leaf);
+    R.leaf_count = [&](int32_t v) {
+        int n = 1;
+        for (uint32_t e = (uint32_t)~v; !(idx[e] & 1); e++) n++;
+        return n;
+    };
+    Box6 mb = R.run(0);
     for (int k = 0; k < 3; k++) { mesh_boxes[6 * am.mesh + k] = mb.lo[k]; mesh_boxes[6 * am.mesh + 3 + k] = mb.hi[k]; }
-    // instances, scene tree, epsilon (DynamicScene.cpp:587)
-    std::vector<Box6> inst(d->n_nodes);
-    Box6 sb = box_empty();
-    for (uint32_t i = 0; i < d->n_nodes; i++) {
-        M44 xf; std::memcpy(xf.d, d->node_xf[i].m, 64);
-        const float* m = mesh_boxes + 6 * d->nodes[i].mesh_index;
-        instance_box(xf, m, m + 3, inst[i]);
-        box_add(sb, inst[i]);
-    }
-    if (d->n_nodes && d->scene_start_node >= 0 && d->n_scene_bvh_nodes)
-        refit(scene, (uint32_t)d->scene_start_node >> 2, [&](int32_t v) { return inst[(uint32_t)~v]; });
-    V3 size = v3(sb.hi[0] - sb.lo[0], sb.hi[1] - sb.lo[1], sb.hi[2] - sb.lo[2]);
-    *eps = 1e-4f * length(size);
+    // instances, scene tree (the animated mesh's instances invalidated), epsilon (DynamicScene.cpp:587)
+    std::vector<uint32_t> moved;
+    for (uint32_t i = 0; i < d->n_nodes; i++)
+        if (d->nodes[i].mesh_index == am.mesh) moved.push_back(i);
+    scene_rebuild(d, scene, mesh_boxes, nullptr, moved, eps);
 }
 
 }  // namespace
@@ -2006,6 +2174,15 @@ void oracle_animate(const ctl_scene_desc* desc, uint32_t anim, const float* bone
                     ctl_triangle_data* tri, float* woop, ctl_bvh_node* nodes, ctl_bvh_node* scene, float* mesh_boxes,
                     float* eps) {
     animate(desc, anim, bones0, bones1, lerp, tri, woop, nodes, scene, mesh_boxes, eps);
+}
+
+// SceneBVH::setTransform + SceneBVH::Build for one moved node (SceneBVH.cpp:77-89,
+// DynamicScene.cpp:433-447): the instance tree `scene` (in/out, its state kept
+// between calls) rebuilt along the node's path with rotations, from the
+// transforms xf16 (16 per node) and the mesh boxes; eps out.
+void oracle_scene_set_transform(const ctl_scene_desc* desc, ctl_bvh_node* scene, const float* mesh_boxes,
+                                const float* xf16, uint32_t node, float* eps) {
+    scene_rebuild(desc, scene, mesh_boxes, xf16, std::vector<uint32_t>{node}, eps);
 }
 
 // Host-side compile pieces, for checking the product's scene compiler.

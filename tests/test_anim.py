@@ -76,14 +76,19 @@ def _arr(ptr, ctype, n):
     return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=(n,)).copy()
 
 
-def oracle_animated(ctl, orc, d, f0, f1, lerp):
-    """Arrays after k_ComputeState, and a desc pointing at them."""
+def oracle_animated(ctl, orc, d, f0, f1, lerp, state=None):
+    """Arrays after k_ComputeState, and a desc pointing at them.  The trees'
+    shape persists between frames (BVHRebuilder rotates the tree it is given):
+    pass the `keep` of the previous frame as `state` to continue from it."""
     A = ctl._abi
     tri = _arr(d.tri_data, C.c_uint32, d.n_tri_data * 8)
     woop = _arr(d.woop_tris, C.c_float, d.n_woop_tris * 12)
-    nodes = _arr(d.bvh_nodes, C.c_float, d.n_bvh_nodes * 16)
-    scene = _arr(d.scene_bvh_nodes, C.c_float, max(1, d.n_scene_bvh_nodes) * 16)
-    boxes = _arr(d.mesh_boxes, C.c_float, d.n_meshes * 6)
+    if state is None:
+        nodes = _arr(d.bvh_nodes, C.c_float, d.n_bvh_nodes * 16)
+        scene = _arr(d.scene_bvh_nodes, C.c_float, max(1, d.n_scene_bvh_nodes) * 16)
+        boxes = _arr(d.mesh_boxes, C.c_float, d.n_meshes * 6)
+    else:
+        nodes, scene, boxes = state[2].copy(), state[3].copy(), state[4].copy()
     eps = np.zeros(1, np.float32)
     b0 = np.ascontiguousarray(f0, np.float32)
     b1 = np.ascontiguousarray(f1, np.float32)
@@ -98,6 +103,45 @@ def oracle_animated(ctl, orc, d, f0, f1, lerp):
     d2.ray_eps = float(eps[0])
     keep = (tri, woop, nodes, scene, boxes)
     return d2, keep, eps[0]
+
+
+def check_tree(nodes, n_nodes, idx, root=0):
+    """BVHRebuilder::validateTree (BVHRebuilder.cpp:575-606) on a mesh tree in
+    the reference layout: parent words, every entry in exactly one leaf, every
+    slot box containing what it bounds (leaf slots: the leaf's entries are
+    checked by traversal elsewhere).  Returns the objects under the root."""
+    n = nodes.view(np.int32).reshape(-1, 16)
+    f = nodes.view(np.float32).reshape(-1, 16)
+    seen = np.zeros(idx.size, bool)
+
+    def walk(k, parent):
+        assert n[k, 14] == parent
+        total = 0
+        for c in range(2):
+            v = n[k, 12 + c]
+            if v == 0x76543210:
+                continue
+            if v < 0:
+                e = ~v
+                while True:
+                    assert not seen[e]
+                    seen[e] = True
+                    total += 1
+                    if idx[e] & 1:
+                        break
+                    e += 1
+            else:
+                ch = v >> 2
+                lo = np.array([f[ch, [0, 2, 8]], f[ch, [4, 6, 10]]]).min(0)
+                hi = np.array([f[ch, [1, 3, 9]], f[ch, [5, 7, 11]]]).max(0)
+                slot = f[k, [0, 2, 8]] if c == 0 else f[k, [4, 6, 10]]
+                sloth = f[k, [1, 3, 9]] if c == 0 else f[k, [5, 7, 11]]
+                assert (slot <= lo).all() and (sloth >= hi).all()
+                total += walk(ch, k * 4)
+        return total
+    total = walk(root, -1)
+    assert seen.all()
+    return total
 
 
 # ---------------------------------------------------------------------------- CPU
@@ -175,6 +219,57 @@ def test_oracle_refit_traversal_matches_brute_force(ctl, orc):
     assert np.array_equal(t, bt) and np.array_equal(tri, btri)
 
 
+def test_oracle_rebuild_rotates_and_keeps_a_valid_tree(ctl, orc):
+    """BVHRebuilder's rotations (BVHRebuilder.cpp:306-334) on the animated tube,
+    frame after frame from the last frame's tree: subtrees move (children and
+    parent words change), the tree stays valid (validateTree) and traversal
+    over it still finds what a scan over every triangle finds."""
+    from helpers import oracle_trace
+    s = build_scene(ctl)
+    d = s.compile()
+    f0, f1 = frames()
+    idx = _arr(d.tri_indices, C.c_uint32, d.n_tri_indices)
+    k0 = d.meshes[0].bvh_indices_offset
+    k1 = d.meshes[1].bvh_indices_offset
+    n1 = d.meshes[1].bvh_node_offset // 4
+    rest = _arr(d.bvh_nodes, C.c_int32, d.n_bvh_nodes * 16).reshape(-1, 16)
+    keep = None
+    moved = 0
+    for lerp in (0.2, 0.5, 0.9, 0.3):
+        d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, lerp, keep)
+        tube = keep[2][:n1 * 16].view(np.int32)
+        assert check_tree(tube, n1, idx[k0:k1]) == k1 - k0
+        moved = max(moved, int((tube.reshape(-1, 16)[:, 12:14] != rest[:n1, 12:14]).any(1).sum()))
+        rays = random_rays(d2, 5000, seed=int(lerp * 10))
+        t, u, v, tri, node, st = oracle_trace(orc, d2, rays, mode=0)
+        bt = np.zeros(rays.shape[0], np.float32)
+        btri = np.zeros(rays.shape[0], np.uint32)
+        orc.oracle_brute_force(C.byref(d2), rays.shape[0], oracle.ptr(rays), oracle.ptr(bt), oracle.ptr(btri), 0)
+        assert np.array_equal(t, bt) and np.array_equal(tri, btri)
+    assert moved > 20
+
+
+def test_oracle_rebuild_grid_moves_inner_nodes(ctl, orc):
+    """On a deeper tree (a skinned grid) rotations move inner subtrees too: their
+    parent words change, and the tree stays valid."""
+    V, N, BI, BW, T, UV = skinned_grid(64)
+    s = ctl.HostScene()
+    s.add_animated_mesh(V, N, BI, BW, T, [ctl.diffuse_material(0.5, 0.5, 0.5)], uvs=UV)
+    s.add_node(0)
+    s.add_node(0, [1, 0, 0, 25, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1])
+    s.set_camera([0, 8, -20], [0, 0, 0], [0, 1, 0], 50, 16, 16)
+    d = s.compile()
+    idx = _arr(d.tri_indices, C.c_uint32, d.n_tri_indices)
+    rest = _arr(d.bvh_nodes, C.c_int32, d.n_bvh_nodes * 16).reshape(-1, 16)
+    keep = None
+    for t in (0.5, 1.5, 2.5):
+        d2, keep, eps = oracle_animated(ctl, orc, d, grid_frames(16, 0.0), grid_frames(16, t), 1.0, keep)
+        nodes = keep[2].view(np.int32)
+        assert check_tree(nodes, d.n_bvh_nodes, idx) == d.n_tri_indices
+    parents = int((nodes.reshape(-1, 16)[:, 14] != rest[:, 14]).sum())
+    assert parents > 10
+
+
 # ---------------------------------------------------------------------------- GPU
 
 torch = pytest.importorskip("torch")
@@ -198,9 +293,10 @@ def test_animate_arrays_bit_exact(ctl, orc, dev, bvh):
     f0, f1 = frames()
     pt = ctl.PathTracer(0)
     pt.upload_scene(d)
-    pt.animate(0, f0, f1, 0.25)      # a first pose, then the one compared: each call starts from the rest pose
+    pt.animate(0, f0, f1, 0.25)      # a first pose, then the one compared: the tree's shape carries over
     pt.animate(0, f0, f1, 0.4)
-    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.4)
+    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.25)
+    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.4, keep)
     tri, woop, nodes, scene, boxes = keep
     got = pt.read_array(A.CTL_ARRAY_TRI_DATA, 0, d.n_tri_data, np.uint32, 8)
     assert np.array_equal(got.ravel(), tri)
@@ -264,23 +360,25 @@ def test_animated_traversal_and_render_bit_exact(ctl, orc, dev, bvh):
 
 
 @pytest.mark.gpu
-def test_cull_bound_keeps_animated_mesh_boxes_after_instance_update(ctl, orc, dev):
+def test_cull_bound_covers_animated_boxes_and_follows_instance_update(ctl, orc, dev):
     """DevScene::cull_m bounds every box the any-hit shadow query tests (the
-    slack of traverse.h slab_slack).  The tube is animated past its rest box;
-    an instance-only ctl_scene_update (CTL_DIRTY_NODES) refreshes the constants
-    from the desc, whose mesh boxes are the rest pose, while the animated mesh
-    trees stay on the device: the bound must still cover them.  A re-upload of
-    the mesh trees returns it to the desc's."""
+    slack of traverse.h slab_slack).  The tube is moved 40 along x: after
+    ctl_scene_animate the bound covers the moved mesh boxes.  An instance-only
+    ctl_scene_update (CTL_DIRTY_NODES) re-derives the bound from the desc; it
+    also returns every device-edited array to the desc (commit re-uploads the
+    trees with the instances), so the boxes on the device are the rest pose's
+    again and the desc's bound holds for them (advisor round 5: a NODES-only
+    update never leaves moved trees behind a rest-pose bound)."""
     A = ctl._abi
     s = build_scene(ctl)
     d = s.compile()
-    f0, f1 = frames()
     bump = np.stack([np.eye(4, dtype=np.float32)] * 2)
     bump[:, 0, 3] = 40.0                                     # both bones: the tube moves 40 along x
     pt = ctl.PathTracer(0)
     try:
         pt.upload_scene(d)
         rest = pt.read_array(A.CTL_ARRAY_CULL_BOUND, 0, 1, np.float32, 3)[0].copy()
+        rest_boxes = pt.read_array(A.CTL_ARRAY_MESH_BOXES, 0, d.n_meshes, np.float32, 6)
         pt.animate(0, bump, bump, 0.0)
         boxes = pt.read_array(A.CTL_ARRAY_MESH_BOXES, 0, d.n_meshes, np.float32, 6)
         moved = np.abs(boxes).reshape(-1, 2, 3).max(axis=(0, 1))
@@ -288,11 +386,13 @@ def test_cull_bound_keeps_animated_mesh_boxes_after_instance_update(ctl, orc, de
         after_anim = pt.read_array(A.CTL_ARRAY_CULL_BOUND, 0, 1, np.float32, 3)[0].copy()
         assert (after_anim >= moved).all()
         pt.update_scene(d, A.CTL_DIRTY_NODES)
-        after_nodes = pt.read_array(A.CTL_ARRAY_CULL_BOUND, 0, 1, np.float32, 3)[0].copy()
-        assert (after_nodes >= moved).all() and (after_nodes >= rest).all(), (after_nodes, moved, rest)
-        pt.update_scene(d, A.CTL_DIRTY_BVH | A.CTL_DIRTY_WOOP | A.CTL_DIRTY_NODES)
-        again = pt.read_array(A.CTL_ARRAY_CULL_BOUND, 0, 1, np.float32, 3)[0]
-        assert np.array_equal(again, rest)
+        back = pt.read_array(A.CTL_ARRAY_MESH_BOXES, 0, d.n_meshes, np.float32, 6)
+        assert np.array_equal(back.view(np.uint32), rest_boxes.view(np.uint32))
+        nodes = pt.read_array(A.CTL_ARRAY_BVH_NODES, 0, d.n_bvh_nodes, np.uint32, 16)
+        assert np.array_equal(nodes.ravel(), _arr(d.bvh_nodes, C.c_uint32, d.n_bvh_nodes * 16))
+        after_nodes = pt.read_array(A.CTL_ARRAY_CULL_BOUND, 0, 1, np.float32, 3)[0]
+        assert np.array_equal(after_nodes, rest)
+        assert (after_nodes >= np.abs(back).reshape(-1, 2, 3).max(axis=(0, 1))).all()
     finally:
         pt.close()
 
@@ -333,10 +433,11 @@ def grid_frames(bones, t):
 @pytest.mark.gpu
 @pytest.mark.parametrize("bvh", ["wide", "binary"])
 def test_animate_large_grid_bit_exact(ctl, orc, dev, bvh):
-    """The 2 M-triangle skinned grid of tools/tools_anim_bench.py: ~1 M binary nodes,
-    so the refit runs all three stages (thousands of one-block subtrees, a
-    1024-node level launched on its own, the single-block top); every array
-    equals the oracle's bit for bit."""
+    """The 2 M-triangle skinned grid of tools/tools_anim_bench.py: ~1 M binary
+    nodes rebuilt by ~0.5 M leaf threads climbing with arrival counters and
+    rotating on the way (two frames, the second from the first's tree); every
+    array equals the oracle's bit for bit, and traversal over the 4-wide copy
+    (refit in its upload topology) equals the oracle's over the same trees."""
     A = ctl._abi
     V, N, BI, BW, T, UV = skinned_grid(1024)
     s = ctl.HostScene()
@@ -353,7 +454,8 @@ def test_animate_large_grid_bit_exact(ctl, orc, dev, bvh):
     pt.upload_scene(d)
     pt.animate(0, f0, f1, 0.3)
     pt.animate(0, f0, f1, 0.7)
-    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.7)
+    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.3)
+    d2, keep, eps = oracle_animated(ctl, orc, d, f0, f1, 0.7, keep)
     tri, woop, nodes, scene, boxes = keep
     got = pt.read_array(A.CTL_ARRAY_BVH_NODES, 0, d.n_bvh_nodes, np.uint32, 16)
     assert np.array_equal(got.ravel(), nodes.view(np.uint32))
@@ -364,7 +466,7 @@ def test_animate_large_grid_bit_exact(ctl, orc, dev, bvh):
     assert np.array_equal(got.ravel(), scene[:d.n_scene_bvh_nodes * 16].view(np.uint32))
     got = pt.read_array(A.CTL_ARRAY_MESH_BOXES, 0, d.n_meshes, np.float32, 6)
     assert np.array_equal(got.ravel().view(np.uint32), boxes.view(np.uint32))
-    if bvh == "wide":   # the 4-wide copy gathers the refit binary boxes
+    if bvh == "wide":   # the 4-wide copy, refit in the topology the upload collapsed
         trees = device_wide_trees(pt, d)
         rays = random_rays(d2, 20000, seed=7, tmin=d2.ray_eps)
         want = oracle_intersect(orc, d2, rays, trees=trees)

@@ -9,6 +9,8 @@ import ctypes as C
 import numpy as np
 import pytest
 
+import oracle
+
 from helpers import binary_bvh, device_wide_trees, oracle_intersect, oracle_render, random_rays
 
 pytestmark = pytest.mark.gpu
@@ -190,6 +192,7 @@ def test_set_transform_on_device_matches_recompiled_scene(ctl, orc, dev, bvh):
         lights = pt.read_array(A.CTL_ARRAY_LIGHTS, 0, d2.n_lights, np.uint32, 12)
         eps = pt.read_array(A.CTL_ARRAY_RAY_EPS, 0, 1, np.float32, 1)
         box = pt.read_array(A.CTL_ARRAY_SCENE_BOX, 0, 1, np.float32, 6)
+        sbvh = pt.read_array(A.CTL_ARRAY_SCENE_BVH, 0, d.n_scene_bvh_nodes, np.uint32, 16)
         trees = None if bvh == "binary" else device_wide_trees(pt, d)   # instance tree refit on the device
         fb = torch.zeros((w * h, 7), dtype=torch.float32, device=dev)
         pt.reset_rays()
@@ -210,6 +213,18 @@ def test_set_transform_on_device_matches_recompiled_scene(ctl, orc, dev, bvh):
     assert np.array_equal(lights, arr(d2.lights, d2.n_lights, np.uint32, 12))
     assert eps.view(np.uint32)[0, 0] == np.float32(d2.ray_eps).view(np.uint32)
     assert np.array_equal(box.view(np.uint32)[0], np.array(list(d2.box_min) + list(d2.box_max), np.float32).view(np.uint32))
+    # the instance tree: SceneBVH::Build after each SetNodeTransform, along the moved
+    # node's path with BVHRebuilder's rotations, from the previous call's tree
+    scene = arr(d.scene_bvh_nodes, d.n_scene_bvh_nodes, np.float32, 16).copy()
+    xfs = arr(d.node_xf, d.n_nodes, np.float32, 16).copy()
+    mb = arr(d.mesh_boxes, d.n_meshes, np.float32, 6).copy()
+    oeps = np.zeros(1, np.float32)
+    for node, m in MOVES.items():
+        xfs[node] = np.asarray(m, np.float32).reshape(16)
+        orc.oracle_scene_set_transform(C.byref(d), oracle.ptr(scene), oracle.ptr(mb), oracle.ptr(xfs), node,
+                                       oracle.ptr(oeps))
+    assert np.array_equal(sbvh, scene.view(np.uint32))
+    assert oeps[0] == eps[0, 0]
     want, wrays = oracle_render(orc, d2, p, 3, w, h, trees=trees)
     old, _ = oracle_render(orc, d, p, 3, w, h)
     assert not np.array_equal(old.view(np.uint32), want.view(np.uint32))   # the move is visible
