@@ -383,34 +383,53 @@ def single_pass_leg(pt, fb, stream, sptr, torch, pass_index, passes):
                     "--steps-per-launch steps per ctl_render_passes launch"}
 
 
-def reference_dopass_leg(pt, desc, fb, stream, sptr, torch, pass_index, passes):
+def reference_dopass_leg(pt, desc, fb, stream, sptr, torch, pass_index, passes, ahead=False):
     """The reference's own pass loop as a drop-in drives it: Tracer::DoPass =
     UpdateKernel (ctl_scene_update on the unchanged scene: constants only, no
     copy, no sync) + the sampler tables + one render pass
     (Kernel/Tracer.h:209-248, TraceHelper.cu:182-217).  Device time of the loop
-    between HIP events on the pass stream, and the host time of the update calls."""
-    pt.generate_samples(pass_index, sptr)
-    pt.render_pass(fb.data_ptr(), sptr)   # warm-up
-    torch.cuda.synchronize()
-    pt.reset_rays(sptr)
-    upd = 0.0
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for k in range(passes):
-        t0 = time.perf_counter()
-        pt.update_scene(desc, 0, sptr)
-        upd += time.perf_counter() - t0
-        pt.generate_samples(pass_index + 1 + k, sptr)
-        pt.render_pass(fb.data_ptr(), sptr)
-    e1.record(stream)
-    pt.sync(sptr)
-    ms = e0.elapsed_time(e1)
-    rays = pt.rays_traced()
-    return {"passes": passes, "ms_per_pass": round(ms / passes, 3), "mrays_s": round(rays / ms / 1e3, 1),
-            "update_host_ms_per_call": round(upd * 1e3 / passes, 4),
-            "note": "per pass: ctl_scene_update(dirty=0) + ctl_sampler_generate + ctl_render_pass (reference "
-                    "DoPass: UpdateKernel + DoRender)"}
+    between HIP events on the pass stream, and the host time of the update calls.
+    ahead: the same calls with CTL_PT_RENDER_AHEAD (ctl_render_pass renders the
+    loop's next passes in one launch and folds them call by call): 7 untimed
+    calls reach the 8-pass windows, the timed calls are whole windows, so every
+    ray counted belongs to a pass the loop folded."""
+    import cudatracerlib_amd as ctl
+    old = pt.params.flags
+    if ahead:
+        pt.params.flags = old | ctl.CTL_PT_RENDER_AHEAD
+        passes = max(8, passes - passes % 8)
+    try:
+        warm = 7 if ahead else 1
+        for k in range(warm):
+            pt.update_scene(desc, 0, sptr)
+            pt.generate_samples(pass_index + k, sptr)
+            pt.render_pass(fb.data_ptr(), sptr)
+        torch.cuda.synchronize()
+        pt.reset_rays(sptr)
+        upd = 0.0
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for k in range(passes):
+            t0 = time.perf_counter()
+            pt.update_scene(desc, 0, sptr)
+            upd += time.perf_counter() - t0
+            pt.generate_samples(pass_index + warm + k, sptr)
+            pt.render_pass(fb.data_ptr(), sptr)
+        e1.record(stream)
+        pt.sync(sptr)
+        ms = e0.elapsed_time(e1)
+        rays = pt.rays_traced()
+    finally:
+        pt.params.flags = old
+    out = {"passes": passes, "ms_per_pass": round(ms / passes, 3), "mrays_s": round(rays / ms / 1e3, 1),
+           "update_host_ms_per_call": round(upd * 1e3 / passes, 4),
+           "note": "per pass: ctl_scene_update(dirty=0) + ctl_sampler_generate + ctl_render_pass (reference "
+                   "DoPass: UpdateKernel + DoRender)"}
+    if ahead:
+        out["note"] += ("; CTL_PT_RENDER_AHEAD: each 8th call renders 8 passes in one launch, the others fold "
+                        "(bit-exact to one pass per call, tests/test_gpu_render_ahead.py)")
+    return out
 
 
 def closest_shadow_leg(pt, fb, stream, sptr, torch, pass_index, passes):
@@ -874,6 +893,8 @@ def main(argv=None):
     dopass = None
     if rank == 0 and shards == 1 and a.dopass_leg > 0:
         dopass = reference_dopass_leg(pt, desc, fb, stream, sptr, torch, nxt + 60, a.dopass_leg)
+        dopass["render_ahead"] = reference_dopass_leg(pt, desc, fb, stream, sptr, torch, nxt + 100,
+                                                      max(16, a.dopass_leg), ahead=True)
     closest = None
     if rank == 0 and a.closest_shadow_passes > 0 and shards == 1:
         scratch = torch.zeros_like(fb)

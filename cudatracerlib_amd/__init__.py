@@ -26,12 +26,13 @@ import numpy as np
 
 from . import _abi
 from ._abi import (PTParams, WptParams, PrimParams, SceneDesc, Material, Pixel, Ray, Hit, CTL_SCENE_HALF_HOST_QUIRK, CTL_SCENE_BINARY_BVH,
-                   CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT, CTL_COMM_ID_BYTES)
+                   CTL_BSDF_DIFFUSE, CTL_EDIFFUSE_REFLECTION, CTL_PT_MEGAKERNEL, CTL_PT_WAVEFRONT, CTL_PT_RENDER_AHEAD,
+                   CTL_COMM_ID_BYTES)
 
 __all__ = ["HostScene", "Tracer", "PathTracer", "WavefrontPathTracer", "PrimTracer", "PrimParams", "WptParams", "PTParams", "SceneDesc", "Material", "Pixel", "Ray", "Hit",
            "roughdielectric_material", "set_alpha_map", "comm_unique_id", "comm_init_rank", "comm_init_all",
            "comm_destroy",
-           "CTL_SCENE_HALF_HOST_QUIRK", "CTL_SCENE_BINARY_BVH", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "lib", "diffuse_material"]
+           "CTL_SCENE_HALF_HOST_QUIRK", "CTL_SCENE_BINARY_BVH", "CTL_PT_MEGAKERNEL", "CTL_PT_WAVEFRONT", "CTL_PT_RENDER_AHEAD", "lib", "diffuse_material"]
 
 
 def lib():

@@ -35,6 +35,7 @@ CTL_WRAP_REPEAT, CTL_WRAP_CLAMP, CTL_WRAP_MIRROR, CTL_WRAP_BLACK = 0, 1, 2, 3
 CTL_MAX_NUM_LIGHTS = 16
 CTL_PT_MEGAKERNEL = 1
 CTL_PT_WAVEFRONT = 2
+CTL_PT_RENDER_AHEAD = 4
 # ctl_scene_update dirty groups (DynamicScene streams)
 CTL_DIRTY_TRI_DATA, CTL_DIRTY_WOOP, CTL_DIRTY_BVH, CTL_DIRTY_TRI_INDICES = 1, 2, 4, 8
 CTL_DIRTY_MATERIALS, CTL_DIRTY_MESHES, CTL_DIRTY_NODES, CTL_DIRTY_LIGHTS = 16, 32, 64, 128

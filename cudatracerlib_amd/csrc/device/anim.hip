@@ -160,17 +160,52 @@ __device__ __forceinline__ float dbox_area(const DBox& b) {
     const float x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
     return 2.0f * (x * y + x * z + y * z);
 }
+// Words another thread of the same launch reads or writes go through
+// agent-scope relaxed atomics (global_load / global_store with sc1 on gfx950):
+// each access is coherent across the XCDs' L2s by itself.  An acquire /
+// release at agent scope would instead write back and invalidate the whole L2
+// at every arrival (buffer_wbl2 / buffer_inv sc1), which made the rebuild 30x
+// slower than the refit it replaced.  The arrival orders the accesses instead:
+// a thread's coherent stores complete (s_waitcnt vmcnt(0)) before its arrival
+// increments the counter, and the last arriver's loads are issued after the
+// counter's value came back.
+__device__ __forceinline__ float2 cld2(const float* p) {
+    const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float2(__uint_as_float((uint32_t)v), __uint_as_float((uint32_t)(v >> 32)));
+}
+__device__ __forceinline__ void cst2(float* p, float a, float b) {
+    const uint64_t v = (uint64_t)__float_as_uint(a) | ((uint64_t)__float_as_uint(b) << 32);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float cld(const float* p) {
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void cst(float* p, float a) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int32_t cldi(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void csti(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // BVHNodeData child slots (TriIntersectorData.h:44-88)
 __device__ __forceinline__ DBox slot_box(const float* nd, int c) {
-    const float4 q = reinterpret_cast<const float4*>(nd)[c];
-    const float2 z = reinterpret_cast<const float2*>(nd + 8)[c];
-    return DBox{{q.x, q.z, z.x}, {q.y, q.w, z.y}};
+    const float2 a = cld2(nd + 4 * c), b = cld2(nd + 4 * c + 2), z = cld2(nd + 8 + 2 * c);
+    return DBox{{a.x, b.x, z.x}, {a.y, b.y, z.y}};
 }
 __device__ __forceinline__ void set_slot(float* nd, int c, const DBox& b) {
-    reinterpret_cast<float4*>(nd)[c] = make_float4(b.lo[0], b.hi[0], b.lo[1], b.hi[1]);
-    reinterpret_cast<float2*>(nd + 8)[c] = make_float2(b.lo[2], b.hi[2]);
+    cst2(nd + 4 * c, b.lo[0], b.hi[0]);
+    cst2(nd + 4 * c + 2, b.lo[1], b.hi[1]);
+    cst2(nd + 8 + 2 * c, b.lo[2], b.hi[2]);
 }
-__device__ __forceinline__ int32_t kid(const float* nd, int c) { return __float_as_int(nd[12 + c]); }
+__device__ __forceinline__ void kids(const float* nd, int32_t k[2]) {
+    const float2 v = cld2(nd + 12);
+    k[0] = __float_as_int(v.x);
+    k[1] = __float_as_int(v.y);
+}
+__device__ __forceinline__ void set_kid(float* nd, int c, int32_t v) { cst(nd + 12 + c, __int_as_float(v)); }
 
 struct RebuildArgs {
     float* bin;                 // the mesh tree's node 0
@@ -190,10 +225,11 @@ struct RebuildArgs {
 };
 
 // The last of `need` arrivals at counter k goes on (and leaves the counter at
-// 0 for the next launch).  Release: this thread's node writes before the
-// arrival; acquire: the other arrivals' writes before this thread's reads.
+// 0 for the next launch).  The caller's coherent stores complete first.
 __device__ __forceinline__ bool arrive(uint32_t* cnt, uint32_t k, uint32_t need) {
-    const uint32_t old = __hip_atomic_fetch_add(cnt + k, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(cnt + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::: "memory");   // no load of the arrivals' words is hoisted above the counter
     if (old + 1 < need) return false;
     __hip_atomic_store(cnt + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
@@ -213,22 +249,23 @@ __device__ __forceinline__ void child_info(const RebuildArgs& A, const float* ho
     else {
         const float* y = A.bin + 16 * (size_t)((uint32_t)v >> 2);
         b = dbox_union(slot_box(y, 0), slot_box(y, 1));
-        n = A.objects[(uint32_t)v >> 2];
+        n = cldi(A.objects + ((uint32_t)v >> 2));
     }
 }
 
 // BVHRebuilder::setChild's array writes for a moved child: the parent word of
-// an inner node, the holder of a leaf's record
+// an inner node, the holder of a leaf's record (read by the next launch)
 __device__ __forceinline__ void moved_to(const RebuildArgs& A, int32_t v, uint32_t node, int slot) {
     if (v == kSent) return;
-    if (v >= 0) A.bin[16 * (size_t)((uint32_t)v >> 2) + 14] = __int_as_float((int32_t)(node << 2));
+    if (v >= 0) cst(A.bin + 16 * (size_t)((uint32_t)v >> 2) + 14, __int_as_float((int32_t)(node << 2)));
     else A.leaf[A.leaf_of[(uint32_t)~v]].x = node << 1 | (uint32_t)slot;
 }
 
 // recomputeNode (BVHRebuilder.cpp:281-340) of node x, its subtree done
 __device__ void rebuild_node(const RebuildArgs& A, uint32_t x) {
     float* X = A.bin + 16 * (size_t)x;
-    const int32_t c[2] = {kid(X, 0), kid(X, 1)};
+    int32_t c[2];
+    kids(X, c);
     DBox cb[2], gb[2][2];
     int cn[2], gn[2][2];
     int32_t g[2][2];
@@ -239,10 +276,8 @@ __device__ void rebuild_node(const RebuildArgs& A, uint32_t x) {
         can[i] = false;
         if (c[i] >= 0 && c[i] != kSent) {
             const float* Y = A.bin + 16 * (size_t)((uint32_t)c[i] >> 2);
-            for (int j = 0; j < 2; j++) {
-                g[i][j] = kid(Y, j);
-                child_info(A, Y, j, g[i][j], gb[i][j], gn[i][j]);
-            }
+            kids(Y, g[i]);
+            for (int j = 0; j < 2; j++) child_info(A, Y, j, g[i][j], gb[i][j], gn[i][j]);
             can[i] = g[i][0] != kSent && g[i][1] != kSent;   // numberGrandchildren == 2
         }
     }
@@ -265,16 +300,16 @@ __device__ void rebuild_node(const RebuildArgs& A, uint32_t x) {
     const int lc = best < 2 ? 1 : 0, lg = (best == 1 || best == 2) ? 1 : 0, o = 1 - lc;
     const uint32_t other = (uint32_t)c[o] >> 2;
     float* O = A.bin + 16 * (size_t)other;
-    O[12 + lg] = __int_as_float(c[lc]);
+    set_kid(O, lg, c[lc]);
     set_slot(O, lg, cb[lc]);
     moved_to(A, c[lc], other, lg);
     // propagateBBChange(other -> x): the other child's box, its slots in order
     const DBox ob = lg == 0 ? dbox_union(cb[lc], gb[o][1]) : dbox_union(gb[o][0], cb[lc]);
     set_slot(X, o, ob);
-    X[12 + lc] = __int_as_float(g[o][lg]);
+    set_kid(X, lc, g[o][lg]);
     set_slot(X, lc, gb[o][lg]);
     moved_to(A, g[o][lg], x, lc);
-    A.objects[other] += cn[lc] - gn[o][lg];   // BVHNodeInfo::changeCount, net
+    csti(A.objects + other, cldi(A.objects + other) + cn[lc] - gn[o][lg]);   // BVHNodeInfo::changeCount, net
 }
 
 // One thread per leaf: Woop data and the leaf's box, then up both trees.
@@ -304,17 +339,19 @@ __global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
         DBox b = lb;
         for (;;) {
             WideNode& W = A.wide[w];
-            W.lo_x[sl] = b.lo[0]; W.lo_y[sl] = b.lo[1]; W.lo_z[sl] = b.lo[2];
-            W.hi_x[sl] = b.hi[0]; W.hi_y[sl] = b.hi[1]; W.hi_z[sl] = b.hi[2];
-            uint32_t need = 0;
-            for (int k = 0; k < 4; k++) need += W.child[k] != kSent;
+            cst(&W.lo_x[sl], b.lo[0]); cst(&W.lo_y[sl], b.lo[1]); cst(&W.lo_z[sl], b.lo[2]);
+            cst(&W.hi_x[sl], b.hi[0]); cst(&W.hi_y[sl], b.hi[1]); cst(&W.hi_z[sl], b.hi[2]);
+            const int4 ch = *reinterpret_cast<const int4*>(W.child);   // the topology: fixed since the upload
+            const uint32_t need = (ch.x != kSent) + (ch.y != kSent) + (ch.z != kSent) + (ch.w != kSent);
             if (!arrive(A.wcnt, w, need)) break;
             const uint32_t up = A.wup[w];
             if (up == 0xffffffffu) break;
+            const int32_t chk[4] = {ch.x, ch.y, ch.z, ch.w};
             b = dbox_identity();
             for (int k = 0; k < 4; k++)
-                if (W.child[k] != kSent)
-                    b = dbox_union(b, DBox{{W.lo_x[k], W.lo_y[k], W.lo_z[k]}, {W.hi_x[k], W.hi_y[k], W.hi_z[k]}});
+                if (chk[k] != kSent)
+                    b = dbox_union(b, DBox{{cld(&W.lo_x[k]), cld(&W.lo_y[k]), cld(&W.lo_z[k])},
+                                           {cld(&W.hi_x[k]), cld(&W.hi_y[k]), cld(&W.hi_z[k])}});
             w = up >> 2;
             sl = up & 3u;
         }
@@ -324,10 +361,12 @@ __global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
     set_slot(A.bin + 16 * (size_t)x, (int)(lf.x & 1u), lb);
     for (;;) {
         float* X = A.bin + 16 * (size_t)x;
-        const uint32_t need = (kid(X, 0) != kSent) + (kid(X, 1) != kSent);
+        int32_t k[2];
+        kids(X, k);   // unchanged until this node is rebuilt (by the last arrival)
+        const uint32_t need = (k[0] != kSent) + (k[1] != kSent);
         if (!arrive(A.cnt, x, need)) return;
         rebuild_node(A, x);
-        const int32_t p = __float_as_int(X[14]);
+        const int32_t p = __float_as_int(cld(X + 14));
         if (p < 0) {   // the root: m_sLocalBox = BVHNodeData::getBox, both slots
             const DBox r = dbox_union(slot_box(X, 0), slot_box(X, 1));
             for (int k = 0; k < 3; k++) { A.mesh_box[k] = r.lo[k]; A.mesh_box[3 + k] = r.hi[k]; }
@@ -547,6 +586,7 @@ bool rebuild_scene(AnimState* A, DevScene& S, const float* inst, const std::vect
 // the instance tree.
 ctl_status scene_after_move(ctl_ctx* c, const std::vector<uint32_t>& moved, hipStream_t s, const char* what) {
     AnimState* A = c->anim;
+    c->scene_epoch++;
     DevScene& S = c->scene;
     hipLaunchKernelGGL(inst_box_kernel, dim3((A->n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, S.nodes, S.xf, A->n_nodes,
                        A->d_mesh_boxes, A->d_inst_boxes);
@@ -700,6 +740,7 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         return CTL_ERR_HIP;
     }
     DevScene& S = c->scene;
+    c->scene_epoch++;   // the geometry moves (render-ahead passes are dropped)
     const uint32_t nv = P.am.vertex_count, nt = P.am.tri_count;
     const uint32_t* tris = A->d_tris + 3ull * P.am.tri_first;
     if (nv) hipLaunchKernelGGL(anim_skin_kernel, dim3((nv + kAB - 1) / kAB), dim3(kAB), 34 * n_bones * sizeof(float), s,

@@ -647,6 +647,27 @@ struct ctl_ctx {
     ctl::AnimState* anim = nullptr;             // animated meshes, refit plans (anim.hip)
     uint64_t n_tri_data = 0, n_woop = 0, n_bvh_nodes = 0, n_scene_bvh = 0;   // uploaded array lengths
     int cu_count = 256;
+    // Speculative DoPass windows (ctl_render_pass): the reference's host loop
+    // renders one pass per call (Tracer.h:209-248); once the calls follow each
+    // other with consecutive sampler passes and nothing else changing, one call
+    // renders the next passes too in one launch (their samples wait in the sample
+    // slots) and the following calls only fold them.  Anything that changes the
+    // scene, the tables, the parameters, the framebuffer or the stream, or uses
+    // the slots, drops the pending passes.
+    uint64_t scene_epoch = 0;                   // bumped by every scene / table change
+    int64_t tables_pass = -1;                   // pass of the active sampler tables (-1: uploaded tables)
+    struct Spec {
+        bool pending = false;                   // slots hold passes [next, end) of the window
+        int64_t first = 0, next = 0, end = 0;
+        bool last_valid = false;                // the previous ctl_render_pass call, for the pattern
+        int64_t last_pass = 0;
+        ctl_pt_params params{};
+        const void* fb = nullptr;
+        const void* stream = nullptr;
+        uint64_t epoch = 0;
+        uint32_t streak = 0;                    // windows consumed in a row: their length doubles up to 8
+        uint64_t per_pass = 0;
+    } spec;
 };
 
 namespace ctl {

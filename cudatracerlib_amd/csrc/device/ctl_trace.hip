@@ -789,6 +789,8 @@ CTL_API ctl_status ctl_sampler_upload(ctl_ctx* c, const float* seq1d, const floa
     CTL_HIP(c, hipEventRecord(c->ev[b], s));
     c->active = b;
     c->next_buf = 1 - b;
+    c->tables_pass = -1;   // caller's tables: no pass index to render ahead from
+    c->scene_epoch++;
     return CTL_OK;
 }
 
@@ -806,6 +808,7 @@ CTL_API ctl_status ctl_sampler_generate(ctl_ctx* c, uint64_t pass_index, void* s
     CTL_HIP(c, hipGetLastError());
     c->active = b;
     c->next_buf = 1 - b;
+    c->tables_pass = (int64_t)std::min<uint64_t>(pass_index, (uint64_t)INT64_MAX - 16);
     return CTL_OK;
 }
 
@@ -931,7 +934,8 @@ static ctl_status launch_schedule(ctl_ctx* c, const ctl_pt_params* p, const Path
                                   SampleSlots PS = make_slots(nullptr, 0), uint32_t tbl = 0);
 
 static ctl_status prepare_slots(ctl_ctx* c, uint64_t items, hipStream_t s);
-static void launch_fold(ctl_ctx* c, const PathParams& P, uint32_t per_pass, uint32_t n, ctl_pixel* fb, hipStream_t s);
+static void launch_fold(ctl_ctx* c, const PathParams& P, uint32_t per_pass, uint32_t n, ctl_pixel* fb, hipStream_t s,
+                        uint32_t first_slice);
 
 static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb, bool stats, void* stream) {
     PathParams P;
@@ -950,7 +954,7 @@ static ctl_status launch_pass(ctl_ctx* c, const ctl_pt_params* p, ctl_pixel* fb,
     ctl_status r2 = launch_schedule(c, p, P, fb, stats, s, threads, grid, s1, s2,
                                     make_slots(c->d_slices, (uint32_t)threads), 0);
     if (r2 != CTL_OK) return r2;
-    launch_fold(c, P, (uint32_t)threads, 1, fb, s);
+    launch_fold(c, P, (uint32_t)threads, 1, fb, s, 0);
     CTL_HIP(c, hipEventRecord(c->pass_ev[1], s));
     c->pass_timed = true;
     return CTL_OK;
@@ -1054,6 +1058,7 @@ __global__ __launch_bounds__(kBlock) void fold_samples_kernel(PathParams P, cons
 // work item writes its slot (code 0 when it has no pixel or AddSample would
 // drop the sample), so no clearing is needed.
 static ctl_status prepare_slots(ctl_ctx* c, uint64_t items, hipStream_t s) {
+    c->spec.pending = false;   // the slots are about to be overwritten
     if (c->slices_cap < items) {
         CTL_HIP(c, hipStreamSynchronize(s));
         if (c->d_slices) (void)hipFree(c->d_slices);
@@ -1067,16 +1072,29 @@ static ctl_status prepare_slots(ctl_ctx* c, uint64_t items, hipStream_t s) {
     return CTL_OK;
 }
 
-static void launch_fold(ctl_ctx* c, const PathParams& P, uint32_t per_pass, uint32_t n, ctl_pixel* fb, hipStream_t s) {
+static void launch_fold(ctl_ctx* c, const PathParams& P, uint32_t per_pass, uint32_t n, ctl_pixel* fb, hipStream_t s,
+                        uint32_t first_slice = 0) {
     const uint64_t px = (uint64_t)P.width * P.height;
     hipLaunchKernelGGL(fold_samples_kernel, dim3((unsigned)((px + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, P,
-                       c->d_slices, per_pass, n, fb);
+                       c->d_slices + (size_t)first_slice * per_pass, per_pass, n, fb);
 }
+
+// n_passes consecutive passes in one persistent launch; the first n_fold of them
+// are folded into d_fb, the rest stay in the sample slots (a speculative window).
+static ctl_status launch_window(ctl_ctx* c, const ctl_pt_params* params, uint64_t first_pass, uint32_t n_passes,
+                                uint32_t n_fold, ctl_pixel* d_fb, hipStream_t s, uint64_t* per_pass_out);
 
 CTL_API ctl_status ctl_render_passes(ctl_ctx* c, const ctl_pt_params* params, uint64_t first_pass, uint32_t n_passes,
                                      ctl_pixel* d_fb, void* stream) {
     if (!c || !params || !d_fb) return CTL_ERR_INVALID;
     if (n_passes == 0) return CTL_OK;
+    c->spec.last_valid = false;
+    return launch_window(c, params, first_pass, n_passes, n_passes, d_fb, reinterpret_cast<hipStream_t>(stream), nullptr);
+}
+
+static ctl_status launch_window(ctl_ctx* c, const ctl_pt_params* params, uint64_t first_pass, uint32_t n_passes,
+                                uint32_t n_fold, ctl_pixel* d_fb, hipStream_t s, uint64_t* per_pass_out) {
+    void* stream = reinterpret_cast<void*>(s);
     if (params->flags & (CTL_PT_WAVEFRONT | CTL_PT_MEGAKERNEL)) {
         // the other schedules: one pass at a time
         for (uint32_t i = 0; i < n_passes; i++) {
@@ -1090,8 +1108,8 @@ CTL_API ctl_status ctl_render_passes(ctl_ctx* c, const ctl_pt_params* params, ui
     ctl_status r = prepare_pass(c, params, d_fb, P, false);
     if (r != CTL_OK) return r;
     CTL_HIP(c, hipSetDevice(c->device));
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const uint64_t per_pass = pass_items_of(P);   // owned pixels + apron items
+    if (per_pass_out) *per_pass_out = per_pass;
     if (per_pass == 0) return CTL_OK;
     const uint64_t items = per_pass * n_passes;
     if (items >= 0xffffffffull) { c->err = "render_passes: 2^32-1 or more work items"; return CTL_ERR_INVALID; }
@@ -1122,10 +1140,70 @@ CTL_API ctl_status ctl_render_passes(ctl_ctx* c, const ctl_pt_params* params, ui
     r = launch_schedule(c, params, P, d_fb, false, s, items, dim3(1), c->d_mt1, c->d_mt2,
                         make_slots(c->d_slices, (uint32_t)per_pass), (uint32_t)tbl);
     if (r != CTL_OK) return r;
-    launch_fold(c, P, (uint32_t)per_pass, n_passes, d_fb, s);
+    launch_fold(c, P, (uint32_t)per_pass, n_fold, d_fb, s, 0);
     CTL_HIP(c, hipGetLastError());
     CTL_HIP(c, hipEventRecord(c->pass_ev[1], s));
     c->pass_timed = true;
+    return CTL_OK;
+}
+
+// Tracer::DoPass through the C ABI with CTL_PT_RENDER_AHEAD (see ctl_ctx::Spec):
+// a call whose pass was rendered ahead by an earlier call of the same window
+// only folds its samples; a call that continues a steady loop renders a window
+// of 2, 4, then 8 passes and folds the first.  Bit-exact to one launch per pass (the fold adds pass by
+// pass in the same order); ctl_rays_traced counts a window's rays when it is
+// launched, ctl_last_pass_ms times the call's own device work.
+static ctl_status render_pass_speculative(ctl_ctx* c, const ctl_pt_params* params, ctl_pixel* d_fb, void* stream) {
+    if (!c || !params || !d_fb) return CTL_ERR_INVALID;
+    ctl_ctx::Spec& W = c->spec;
+    const bool same_state = W.last_valid && std::memcmp(&W.params, params, sizeof(ctl_pt_params)) == 0 && W.fb == d_fb &&
+                            W.stream == stream && W.epoch == c->scene_epoch && c->tables_pass >= 0;
+    const bool next_pass = same_state && c->tables_pass == W.last_pass + 1;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (W.pending && next_pass && c->tables_pass == W.next && !c->overflow_seen) {
+        // rendered ahead: fold its slice
+        PathParams P;
+        ctl_status r = prepare_pass(c, params, d_fb, P);
+        if (r != CTL_OK) return r;
+        CTL_HIP(c, hipSetDevice(c->device));
+        CTL_HIP(c, hipEventRecord(c->pass_ev[0], s));
+        launch_fold(c, P, (uint32_t)W.per_pass, 1, d_fb, s, (uint32_t)(W.next - W.first));
+        CTL_HIP(c, hipGetLastError());
+        CTL_HIP(c, hipEventRecord(c->pass_ev[1], s));
+        c->pass_timed = true;
+        W.last_pass = W.next++;
+        if (W.next == W.end) { W.pending = false; W.streak++; }
+        return CTL_OK;
+    }
+    if (W.pending) W.streak = 0;   // the loop left the window: its passes are dropped
+    W.pending = false;
+    const bool speculate = next_pass && (params->flags & CTL_PT_RENDER_AHEAD) &&
+                           !(params->flags & (CTL_PT_WAVEFRONT | CTL_PT_MEGAKERNEL));
+    if (!speculate) W.streak = 0;
+    const uint32_t n = speculate ? (W.streak >= 2 ? 8u : W.streak == 1 ? 4u : 2u) : 1u;
+    ctl_status r;
+    uint64_t per_pass = 0;
+    if (n == 1) {
+        r = launch_pass(c, params, d_fb, false, stream);
+    } else {
+        PathParams P;
+        r = prepare_pass(c, params, d_fb, P);   // the tables of this pass are there; refusals as launch_pass's
+        if (r == CTL_OK) r = launch_window(c, params, (uint64_t)c->tables_pass, n, 1, d_fb, s, &per_pass);
+    }
+    if (r != CTL_OK) { W.last_valid = false; return r; }
+    W.last_valid = c->tables_pass >= 0;
+    W.last_pass = c->tables_pass;
+    W.params = *params;
+    W.fb = d_fb;
+    W.stream = stream;
+    W.epoch = c->scene_epoch;
+    if (n > 1 && per_pass > 0) {
+        W.pending = true;
+        W.per_pass = per_pass;
+        W.first = c->tables_pass;
+        W.next = c->tables_pass + 1;
+        W.end = c->tables_pass + n;
+    }
     return CTL_OK;
 }
 
@@ -1145,7 +1223,7 @@ CTL_API ctl_status ctl_render_pass(ctl_ctx* c, const ctl_pt_params* params, ctl_
     }
     return r;
 #else
-    return launch_pass(c, params, d_fb, false, stream);
+    return render_pass_speculative(c, params, d_fb, stream);
 #endif
 }
 

@@ -217,7 +217,19 @@ void set_constants(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty) {
     c->half_quirk = (d->flags & CTL_SCENE_HALF_HOST_QUIRK) != 0;
 }
 
+ctl_status commit_arrays(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream_t s);
+
+// Every commit that changes the device scene (an array, or a constant such as
+// the camera) moves the scene epoch: render-ahead passes (ctl_render_pass)
+// belong to the epoch they were rendered in.
 ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream_t s) {
+    DevScene before = c->scene;
+    const ctl_status r = commit_arrays(c, d, dirty, s);
+    if (r != CTL_OK || dirty != 0 || std::memcmp(&before, &c->scene, sizeof(DevScene)) != 0) c->scene_epoch++;
+    return r;
+}
+
+ctl_status commit_arrays(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream_t s) {
     // a change of the device tree format rebuilds the trees
     const uint32_t tree_bits = CTL_SCENE_BINARY_BVH | CTL_SCENE_WIDE_QUANT;
     if ((d->flags & tree_bits) != c->tree_flags) dirty |= kDirtyTrees;
@@ -446,6 +458,8 @@ ctl_status commit(ctl_ctx* c, const ctl_scene_desc* d, uint32_t dirty, hipStream
 
 namespace ctl {
 void free_scene(ctl_ctx* c) {
+    c->scene_epoch++;
+    c->spec.pending = false;
     free_arrays(c);
     anim_free(c);
     c->has_scene = false;

@@ -354,7 +354,16 @@ enum {
      * CTL_PT_WAVEFRONT: wavefront pipeline (gen / trace / shade / shadow /
      *                   resolve kernels per bounce over compacted queues)   */
     CTL_PT_MEGAKERNEL = 1u << 0,
-    CTL_PT_WAVEFRONT = 1u << 1
+    CTL_PT_WAVEFRONT = 1u << 1,
+    /* ctl_render_pass may render ahead (persistent schedule only): once the
+     * calls follow each other with consecutive ctl_sampler_generate passes and
+     * nothing changing (scene, tables, parameters, framebuffer, stream), a call
+     * renders a window of the next 2, 4, then 8 passes in one launch and folds
+     * its own; the next calls of the window only fold theirs.  The
+     * framebuffer after each call is bit-identical to one pass per call; a
+     * change drops the pending passes.  ctl_rays_traced counts a window's
+     * rays when it is launched (rays of dropped passes included).            */
+    CTL_PT_RENDER_AHEAD = 1u << 2
 };
 
 /* ------------------------------------------------------------------------ */

@@ -290,7 +290,8 @@ def refraction_rays(desc, prim, hits, rng, n):
     tri = hits[hit, 2].astype(np.int64)
     m = ((td[tri, 1] >> 16) & 0xFF).astype(np.int64) + mat_off
     hit = hit[mats[m] == A.CTL_BSDF_ROUGHDIELECTRIC]
-    sel = rng.choice(hit, size=min(n, hit.size), replace=False)
+    # fewer dielectric hits than rays wanted: hit points repeat, each with its own microfacet normal
+    sel = rng.choice(hit, size=n, replace=True) if hit.size < n else rng.choice(hit, size=n, replace=False)
     slot = np.empty(nt, np.int64)
     slot[idx >> 1] = np.arange(ni)
     a = woop[slot[hits[sel, 2]], 0:3].astype(np.float64)
