@@ -95,6 +95,12 @@ def parse(argv=None):
     ap.add_argument("--ceiling", type=int, default=1,
                     help="measure the HBM-read and dependent node-chain ceilings (libctl_ceiling.so) on rank 0 "
                          "after the timed region and report the path kernel against them (0: skip)")
+    ap.add_argument("--launch-check-scene", action="store_true",
+                    help="with --launch-check: also rehearse the build-once scene path on a small scene")
+    ap.add_argument("--no-build-once", action="store_true",
+                    help="every rank compiles the scene (default: local rank 0 compiles, the others map its cache)")
+    ap.add_argument("--scene-cache-dir", default="/dev/shm",
+                    help="where the build-once scene cache is written (shared by the ranks of a node)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher rehearsal: the ranks join the process group and count themselves; no GPU, "
                          "no scene (tests/test_bench_launch.py)")
@@ -246,7 +252,7 @@ def measure_ceilings(device, lanes):
     here = os.path.dirname(os.path.abspath(__file__))
     L = C.CDLL(os.path.join(here, "cudatracerlib_amd", "_lib", "libctl_ceiling.so"))
     L.ctl_ceiling_hbm_read.argtypes = [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double)]
-    L.ctl_ceiling_node_chain.argtypes = [C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int,
+    L.ctl_ceiling_node_chain.argtypes = [C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.POINTER(C.c_double)]
     out = {"source": "cudatracerlib_amd/csrc/device/ceiling.hip"}
     o = (C.c_double * 3)()
@@ -255,12 +261,15 @@ def measure_ceilings(device, lanes):
     out["hbm_read_gbs"] = round(o[0], 1)
     out["hbm_read_gbs_mean"] = round(o[1], 1)
     chain = {}
-    for name, nbytes, act, steps in (("l2_resident", 2 << 20, lanes, 4000), ("l2_resident_64_lanes", 2 << 20, 64, 4000),
-                                     ("far_0p54gb", 650 << 20, lanes, 400)):
-        if L.ctl_ceiling_node_chain(device, nbytes, act, 4, steps, 5, o) != 0:
+    for name, nbytes, act, share, steps in (("l2_resident", 2 << 20, lanes, 1, 4000),
+                                            ("l2_resident_64_lanes", 2 << 20, 64, 1, 4000),
+                                            ("far_0p54gb", 650 << 20, lanes, 1, 400),
+                                            ("l2_resident_coherent", 2 << 20, lanes, 64, 4000),
+                                            ("l1_resident_coherent", 16 << 10, lanes, 64, 4000)):
+        if L.ctl_ceiling_node_chain(device, nbytes, act, share, 4, steps, 5, o) != 0:
             raise RuntimeError("ctl_ceiling_node_chain failed")
         chain[name] = {"lane_steps_per_s": round(o[0], 1), "ns_per_wave_step_per_simd": round(o[1], 2),
-                       "active_lanes": act, "waves_per_simd": 4, "node_bytes": int(o[2])}
+                       "active_lanes": act, "lanes_per_chain": share, "waves_per_simd": 4, "node_bytes": int(o[2])}
     out["node_chain"] = chain
     return out
 
@@ -655,20 +664,86 @@ def c5_leg(ctl, dev, torch, stream, sptr, a, threads):
             "scene_build_s": round(t_build, 1)}
 
 
+def compile_scene(ctl, a, threads):
+    hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
+    if a.split_alpha is not None or a.bins or a.max_leaf:
+        hs.set_bvh_params(a.split_alpha, a.split_depth, a.bins, a.max_leaf)
+    hs.set_bvh_builder(a.builder, a.sbvh_alpha)
+    return hs, hs.compile(threads=threads)
+
+
+def build_scene_once(ctl, a, rank, world, dist, threads):
+    """The scene of this run.  One rank per node compiles it (the SBVH build:
+    ~36 s on 16 threads and a 3.5 GB host scene at C3 size) and writes the
+    compiled desc to a cache file in /dev/shm (cudatracerlib_amd/scene_cache);
+    the other ranks wait at a CPU (gloo) barrier and map that file, so the node
+    builds once and holds one shared host copy.  Without a process group, or
+    with --no-build-once, every rank compiles.  Returns (owner, desc, source):
+    owner keeps the desc's arrays alive (a HostScene or a mapped cache)."""
+    from cudatracerlib_amd import scene_cache
+    if world == 1 or a.no_build_once:
+        hs, desc = compile_scene(ctl, a, threads)
+        return hs, desc, "compiled"
+    cpu = dist.new_group(backend="gloo")
+    key = f"c{a.config}_s{a.scale:g}_{a.width}x{a.height}_{a.builder}_{a.sbvh_alpha:g}_{a.split_alpha}_{a.bins}_" \
+          f"{a.max_leaf}_{os.environ.get('MASTER_PORT', '0')}"
+    path = os.path.join(a.scene_cache_dir, f"ctl_scene_{key}.bin")
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    import torch
+    ok = 0
+    if local_rank == 0:
+        hs, desc = compile_scene(ctl, a, threads)
+        try:
+            scene_cache.save(desc, path)
+            ok = 1
+        except OSError as e:          # no room in /dev/shm: every rank compiles
+            log(f"[rank {rank}] scene cache not written ({e}); the other ranks compile")
+    # every rank learns whether a cache was written (a rank whose node has none finds no file)
+    flag = torch.tensor([ok], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=cpu)
+    if local_rank == 0:
+        dist.barrier(group=cpu)   # the others have mapped it
+        try:
+            os.remove(path)       # the maps keep the pages until the ranks exit
+        except OSError:
+            pass
+        return hs, desc, "compiled (cache written)" if ok else "compiled"
+    if int(flag.item()) == 1 and os.path.exists(path):
+        cached = scene_cache.load(path)
+        dist.barrier(group=cpu)
+        return cached, cached.desc, "mapped from the node's scene cache"
+    dist.barrier(group=cpu)
+    hs, desc = compile_scene(ctl, a, threads)
+    return hs, desc, "compiled"
+
+
 def apply_bvh(ctl, desc, bvh):
     """The device tree format --bvh selects (a scene flag of the desc)."""
     desc.flags |= {"wide": 0, "binary": ctl.CTL_SCENE_BINARY_BVH, "wideq": ctl._abi.CTL_SCENE_WIDE_QUANT}[bvh]
 
 
-def rank_report(dist, world, elapsed_s, steps, reduce_ms, dev):
+SCENE_SOURCES = ["compiled", "compiled (cache written)", "mapped from the node's scene cache"]
+
+
+def host_peak_rss_gb():
+    """Peak resident host memory of this process (getrusage ru_maxrss, KiB on
+    Linux): a mapped scene cache counts the pages this rank touched."""
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0 ** 2
+
+
+def rank_report(dist, world, elapsed_s, steps, reduce_ms, dev, build_s=0.0, source="compiled"):
     """Every rank's wall time per step of the timed region (its own bracket,
     the framebuffer reduce included) and the time of its reduce alone, plus the
     world size and backend the process group runs: the N-GPU line's `ranks`
     record, so a scaling run explains itself (slowest rank, reduce share).
+    Also each rank's scene source (build-once: compiled, or mapped from the
+    node's cache), its scene time and its peak host RSS.
     Collective: every rank calls it."""
     import torch
-    mine = torch.tensor([elapsed_s * 1e3 / max(1, steps), -1.0 if reduce_ms is None else float(reduce_ms)],
-                        dtype=torch.float64, device=dev)
+    src = SCENE_SOURCES.index(source) if source in SCENE_SOURCES else 0
+    mine = torch.tensor([elapsed_s * 1e3 / max(1, steps), -1.0 if reduce_ms is None else float(reduce_ms),
+                         float(build_s), host_peak_rss_gb(), float(src)], dtype=torch.float64, device=dev)
     if world > 1:
         allv = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allv, mine)
@@ -679,8 +754,12 @@ def rank_report(dist, world, elapsed_s, steps, reduce_ms, dev):
             "backend": dist.get_backend() if world > 1 else None,
             "ms_per_step": ms, "ms_per_step_min": min(ms), "ms_per_step_max": max(ms),
             "reduce_ms": [round(float(v[1]), 4) for v in allv] if world > 1 else None,
+            "scene_s": [round(float(v[2]), 2) for v in allv],
+            "scene_source": [SCENE_SOURCES[int(v[4])] for v in allv],
+            "host_peak_rss_gb": [round(float(v[3]), 2) for v in allv],
             "note": "per rank: its timed-region wall time / steps (the reduce included) and the framebuffer "
-                    "reduce alone (HIP events around shard.reduce_framebuffer); value uses the max over ranks"}
+                    "reduce alone (HIP events around shard.reduce_framebuffer); value uses the max over ranks; "
+                    "scene_s / scene_source / host_peak_rss_gb: the build-once scene (bench.build_scene_once)"}
 
 
 def launch_check(a, world, rank):
@@ -689,6 +768,7 @@ def launch_check(a, world, rank):
     shard.reduce_framebuffer and report their times like the bench's N-GPU
     line (`ranks`); rank 0 prints the line shape, with n_gpus = the ranks that
     reported.  No GPU, no scene."""
+    import ctypes as C
     import torch
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -710,10 +790,33 @@ def launch_check(a, world, rank):
         if rank == 0 and not bool((img == 1.0).all()):
             raise RuntimeError("launch-check: the reduced framebuffer is not the union of the shards")
     elapsed = time.perf_counter() - t0
-    ranks = rank_report(dist, world, elapsed, 1, red_ms, torch.device("cpu"))
+    # the build-once scene path on a small scene: local rank 0 compiles and writes
+    # the cache, the others map it; every rank's desc must be byte-identical
+    scene = None
+    t_build, source = 0.0, "compiled"
+    if a.launch_check_scene:
+        import hashlib
+        import cudatracerlib_amd as ctl
+        b = argparse.Namespace(**vars(a))
+        b.config, b.scale, b.width, b.height = 2, 0.02, 64, 64
+        tb = time.perf_counter()
+        owner, desc, source = build_scene_once(ctl, b, rank, world, dist, 2)
+        t_build = time.perf_counter() - tb
+        from cudatracerlib_amd import scene_cache
+        h = hashlib.sha256(bytes(desc.camera))
+        for name, (et, count) in scene_cache._ARRAYS.items():
+            p = scene_cache._addr(getattr(desc, name))
+            if p:
+                h.update(C.string_at(p, C.sizeof(et) * int(count(desc))))
+        digest = torch.tensor(list(h.digest()[:8]), dtype=torch.int64)
+        alld = [torch.zeros_like(digest) for _ in range(world)] if world > 1 else [digest]
+        if world > 1:
+            dist.all_gather(alld, digest)
+        scene = {"triangles": int(desc.n_tri_data), "identical_on_every_rank": all(torch.equal(x, alld[0]) for x in alld)}
+    ranks = rank_report(dist, world, elapsed, 1, red_ms, torch.device("cpu"), t_build, source)
     if rank == 0:
         print(json.dumps({"metric": "launch-check", "n_gpus": int(t.item()), "world_size": world,
-                          "gpus_requested": a.gpus, "ranks": ranks}), flush=True)
+                          "gpus_requested": a.gpus, "ranks": ranks, "scene": scene}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -772,15 +875,11 @@ def main(argv=None):
     threads = max(1, int(os.environ.get("OMP_NUM_THREADS", "8")))
 
     t0 = time.perf_counter()
-    hs = ctl.HostScene().generate(a.config, a.scale, a.width, a.height)
-    if a.split_alpha is not None or a.bins or a.max_leaf:
-        hs.set_bvh_params(a.split_alpha, a.split_depth, a.bins, a.max_leaf)
-    hs.set_bvh_builder(a.builder, a.sbvh_alpha)
-    desc = hs.compile(threads=threads)
+    hs, desc, scene_source = build_scene_once(ctl, a, rank, world, dist, threads)
     apply_bvh(ctl, desc, a.bvh)
     t_build = time.perf_counter() - t0
     log(f"[rank {rank}] scene config {a.config}: {desc.n_tri_data} tris, {desc.n_bvh_nodes} BVH nodes, "
-        f"built in {t_build:.1f}s with {threads} threads")
+        f"{scene_source} in {t_build:.1f}s with {threads} threads")
 
     pt = ctl.PathTracer(local, max_path_length=a.max_path_length, rr_start_depth=a.rr_start,
                         shadow_any_hit=bool(a.shadow_any_hit), tile_size=64, num_ranks=shards, rank=tile_rank,
@@ -915,7 +1014,8 @@ def main(argv=None):
         except Exception as e:
             c5 = {"error": f"{type(e).__name__}: {e}"}
     red = dev if a.backend == "nccl" else torch.device("cpu")
-    ranks = rank_report(dist, world, elapsed, a.steps, red0.elapsed_time(red1) if red0 is not None else None, red)
+    ranks = rank_report(dist, world, elapsed, a.steps, red0.elapsed_time(red1) if red0 is not None else None, red,
+                        t_build, scene_source)
     tt = torch.tensor([elapsed], dtype=torch.float64, device=red)
     rr = torch.tensor([rays, 1], dtype=torch.int64, device=red)   # rays, ranks that rendered
     if world > 1:
@@ -960,19 +1060,28 @@ def main(argv=None):
             ce = measure_ceilings(local, lanes)
             node_steps_s = st[1] * passes_per_launch / (per_launch_ms * 1e-3)
             ce["path_kernel_node_steps_per_s"] = round(node_steps_s, 1)
-            ce["frac_chain"] = round(node_steps_s / ce["node_chain"]["l2_resident"]["lane_steps_per_s"], 4)
-            ce["frac_chain_64_lanes"] = round(node_steps_s / ce["node_chain"]["l2_resident_64_lanes"]["lane_steps_per_s"],
-                                              4)
+            nc = ce["node_chain"]
+            # against every probe: incoherent lanes (each its own random line: a floor the
+            # kernel's coherence lifts it above), coherent lanes over L2 (the chain at the L2
+            # hit latency, every step a miss in L1), coherent lanes over L1 (at the L1 latency)
+            ce["frac_chain_by_probe"] = {k: round(node_steps_s / v["lane_steps_per_s"], 4) for k, v in nc.items()}
+            ce["frac_chain"] = ce["frac_chain_by_probe"]["l2_resident_coherent"]
             # triangle tests are dependent fetches too (three 16-B loads against the node's seven)
             ce["frac_chain_with_tri_fetches"] = round(
                 (st[1] + st[2] * 3.0 / 7.0) * passes_per_launch / (per_launch_ms * 1e-3)
-                / ce["node_chain"]["l2_resident"]["lane_steps_per_s"], 4)
+                / nc["l2_resident_coherent"]["lane_steps_per_s"], 4)
             if rl.get("achieved"):
                 ce["frac_hbm_of_measured_read"] = round(rl["achieved"] / ce["hbm_read_gbs"], 4)
             ce["note"] = ("frac_chain = the path kernel's 4-wide node steps per second (STATS pass x passes per "
-                          "launch / its HIP-event launch time) over the L2-resident dependent-chain ceiling at "
-                          "the kernel's lane activity and occupancy; the kernel also shades, tests triangles "
-                          "and idles in divergence, which the probe does not")
+                          "launch / its HIP-event launch time) over the dependent-chain probe at the kernel's lane "
+                          "activity and occupancy with the wave's lanes on one chain of L2-resident nodes (one line "
+                          "per load instruction; the kernel's L2 requests per vector-memory instruction are "
+                          "l2_requests_per_vmem_inst); the kernel also shades, tests triangles and idles in "
+                          "divergence, which the probe does not.  frac_chain_by_probe: against every probe")
+            pkk = ((prof[0] or {}).get("kernels") or {}).get(fam, {})
+            vm = (pkk.get("counters_per_launch") or {}).get("SQ_INSTS_VMEM_RD")
+            if pkk.get("l2_read_bytes") and vm:
+                ce["l2_requests_per_vmem_inst"] = round(pkk["l2_read_bytes"] / 128.0 / vm, 3)
             rl["ceilings"] = ce
             rl["hbm_ceiling_gbs"] = ce["hbm_read_gbs"]
             rl["frac_chain"] = ce["frac_chain"]

@@ -11,10 +11,11 @@
 //               node's seven 16-B loads (traverse.h), the next node a hash of the
 //               loaded bytes, so step k+1 cannot issue before step k lands.  A
 //               active lanes of every wave (the path kernel's measured lane
-//               activity), W waves per SIMD, the node array either L2-resident
-//               (2 MiB: the path kernel's 99 % L2 hit rate) or the C3 wide tree's
-//               size (0.65 GB: every step a far fetch).  Result: lane node steps
-//               per second for the chip.
+//               activity), W waves per SIMD, each lane on its own chain or all
+//               lanes of a wave on one (coherent rays share the top of the tree),
+//               the node array L1-resident (16 KiB), L2-resident (2 MiB: the path
+//               kernel's 99 % L2 hit rate) or the C3 wide tree's size (0.54 GB:
+//               every step a far fetch).  Result: lane node steps per second.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,10 +50,12 @@ __global__ __launch_bounds__(kBlock) void hbm_read_kernel(const uint4* __restric
 }
 
 __global__ __launch_bounds__(kBlock) void node_chain_kernel(const uint4* __restrict__ nodes, uint32_t mask,
-                                                            int steps, int active, uint32_t* out) {
+                                                            int steps, int active, int share, uint32_t* out) {
     const int lane = threadIdx.x & 63;
     if (lane >= active) return;
-    uint32_t idx = mix32(blockIdx.x * kBlock + threadIdx.x) & mask;
+    // lanes in groups of `share` walk the same chain (share 64: the wave's active
+    // lanes read one node per step, as coherent rays near the root do)
+    uint32_t idx = mix32(blockIdx.x * kBlock + (threadIdx.x & ~63) + lane / share) & mask;
     uint32_t acc = 0;
     for (int s = 0; s < steps; s++) {
         const uint4* q = nodes + (size_t)idx * 8;
@@ -129,15 +132,16 @@ __attribute__((visibility("default"))) int ctl_ceiling_hbm_read(int device, uint
 }
 
 // Dependent walks over `bytes` (rounded down to a power of two) of random 128-B
-// nodes (seven 16-B loads per step), `active` lanes of 64 per wave,
-// `waves_per_simd` waves on each SIMD (4 SIMDs per CU), `steps` steps per lane.
-// out[0] = lane node steps per second (best of `reps`), out[1] = ns per wave
-// step on one SIMD (best), out[2] = the node array's bytes.  Returns 0 or -1.
-__attribute__((visibility("default"))) int ctl_ceiling_node_chain(int device, uint64_t bytes, int active,
+// nodes (seven 16-B loads per step), `active` lanes of 64 per wave, lanes in
+// groups of `share` on one chain, `waves_per_simd` waves on each SIMD (4 SIMDs
+// per CU), `steps` steps per lane.  out[0] = lane node steps per second (best
+// of `reps`), out[1] = ns per wave step on one SIMD (best), out[2] = the node
+// array's bytes.  Returns 0 or -1.
+__attribute__((visibility("default"))) int ctl_ceiling_node_chain(int device, uint64_t bytes, int active, int share,
                                                                   int waves_per_simd, int steps, int reps,
                                                                   double* out) {
-    if (!out || bytes < 128 * 64 || active < 1 || active > 64 || waves_per_simd < 1 || waves_per_simd > 8 ||
-        steps < 1 || reps < 1)
+    if (!out || bytes < 128 * 2 || active < 1 || active > 64 || share < 1 || share > 64 || waves_per_simd < 1 ||
+        waves_per_simd > 8 || steps < 1 || reps < 1)
         return -1;
     Dev g(device);
     uint64_t n_nodes64 = 1;
@@ -156,7 +160,8 @@ __attribute__((visibility("default"))) int ctl_ceiling_node_chain(int device, ui
     const int blocks = cus * waves_per_simd;
     float best = 0, mean = 0;
     const int r = time_reps(reps, [&] {
-        hipLaunchKernelGGL(node_chain_kernel, dim3(blocks), dim3(kBlock), 0, 0, p, n_nodes - 1, steps, active, o);
+        hipLaunchKernelGGL(node_chain_kernel, dim3(blocks), dim3(kBlock), 0, 0, p, n_nodes - 1, steps, active, share,
+                           o);
     }, &best, &mean);
     hipFree(p);
     hipFree(o);

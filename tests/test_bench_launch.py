@@ -38,6 +38,22 @@ def test_gpus_n_without_launcher_spawns_n_ranks(n):
     assert all(0.0 <= x <= y for x, y in zip(rk["reduce_ms"], rk["ms_per_step"]))
 
 
+def test_build_once_scene_two_ranks(tmp_path):
+    """The N-GPU bench compiles the scene once per node: local rank 0 compiles
+    and writes the scene cache, rank 1 waits at a gloo barrier and maps it; the
+    two descs are byte-identical and the ranks record their scene source, time
+    and peak host RSS."""
+    r = _run(["--gpus", "2", "--launch-check", "--launch-check-scene", "--backend", "gloo", "--scene-cache-dir",
+              str(tmp_path)])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    rk = line["ranks"]
+    assert rk["scene_source"] == ["compiled (cache written)", "mapped from the node's scene cache"], rk
+    assert line["scene"]["identical_on_every_rank"] and line["scene"]["triangles"] > 1000
+    assert len(rk["host_peak_rss_gb"]) == 2 and all(x > 0 for x in rk["host_peak_rss_gb"])
+    assert not list(tmp_path.iterdir())     # the cache file is gone once every rank mapped it
+
+
 def test_single_gpu_runs_in_process():
     r = _run(["--gpus", "1", "--launch-check"])
     assert r.returncode == 0, r.stderr[-2000:]

@@ -33,5 +33,8 @@ for name, j in (("N=1", a), ("rank 5 of 8", b)):
     r = j["primary_rays"]["roofline"]
     print(name, "primary rays", j["primary_rays"]["rays_per_launch"], "frac_hbm", r.get("frac_hbm"),
           "traffic/ray", r.get("traffic_per_unit"), "matches", r.get("profile_matches_binary"))
+    r = j["roofline"]
+    print(name, "path kernel frac", r.get("frac"), "traffic", r.get("traffic"), "per unit", r.get("traffic_per_unit"),
+          "scaled by", r.get("scaled_by"), "frac_chain", r.get("frac_chain"))
 print("ranks (rehearsal):", json.dumps(last("gpurun_out/rehearsal_2rank.json").get("ranks")))
 PY
