@@ -48,7 +48,7 @@ struct MeshRebuild {
     uint32_t n_leaf = 0;
     uint4* d_leaf = nullptr;            // {holder << 1 | slot, first entry, entries, wide node << 2 | slot}
     uint32_t* d_leaf_of = nullptr;      // per entry of the mesh: the record of the leaf starting there
-    int32_t* d_objects = nullptr;       // numLeafs (bvhNodeData) per binary node
+    float* d_nrec = nullptr;            // per binary node: its box (6) and numLeafs (bvhNodeData), 32 B
     uint32_t* d_cnt = nullptr;          // arrival counters per binary node (0 between launches)
     uint32_t n_wide = 0;                // 4-wide nodes of the mesh (0: binary scene)
     uint32_t* d_wup = nullptr;          // per wide node: parent << 2 | slot (0xffffffff: the root)
@@ -183,12 +183,6 @@ __device__ __forceinline__ float cld(const float* p) {
 __device__ __forceinline__ void cst(float* p, float a) {
     __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ int32_t cldi(const int32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void csti(int32_t* p, int32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // BVHNodeData child slots (TriIntersectorData.h:44-88)
 __device__ __forceinline__ DBox slot_box(const float* nd, int c) {
@@ -216,7 +210,7 @@ struct RebuildArgs {
     float4* woop;               // the mesh's TriIntersectorData entries
     uint4* leaf;
     const uint32_t* leaf_of;
-    int32_t* objects;
+    float* nrec;                // per node {lo xyz, hi xyz, objects, 0}: written when the node is rebuilt
     uint32_t* cnt;
     const uint32_t* wup;
     uint32_t* wcnt;
@@ -241,16 +235,26 @@ __device__ __forceinline__ int leaf_objects(const uint32_t* idx, uint32_t first)
     return n;
 }
 
+// The record of a rebuilt node: getBox (the union of its two slots) and numLeafs
+// in 32 B, so a parent reads four words instead of both slots and the count.
+__device__ __forceinline__ void rec_load(const float* r, DBox& b, int& n) {
+    const float2 a = cld2(r), c = cld2(r + 2), d = cld2(r + 4), e = cld2(r + 6);
+    b = DBox{{a.x, a.y, c.x}, {c.y, d.x, d.y}};
+    n = __float_as_int(e.x);
+}
+__device__ __forceinline__ void rec_store(float* r, const DBox& b, int n) {
+    cst2(r, b.lo[0], b.lo[1]);
+    cst2(r + 2, b.lo[2], b.hi[0]);
+    cst2(r + 4, b.hi[1], b.hi[2]);
+    cst2(r + 6, __int_as_float(n), 0.0f);
+}
+
 // getBox / numLeafs of child value v held in slot c of node `holder`
 __device__ __forceinline__ void child_info(const RebuildArgs& A, const float* holder, int c, int32_t v, DBox& b,
                                            int& n) {
     if (v == kSent) { b = dbox_identity(); n = 0; }
     else if (v < 0) { b = slot_box(holder, c); n = leaf_objects(A.idx, (uint32_t)~v); }
-    else {
-        const float* y = A.bin + 16 * (size_t)((uint32_t)v >> 2);
-        b = dbox_union(slot_box(y, 0), slot_box(y, 1));
-        n = cldi(A.objects + ((uint32_t)v >> 2));
-    }
+    else rec_load(A.nrec + 8 * (size_t)((uint32_t)v >> 2), b, n);
 }
 
 // BVHRebuilder::setChild's array writes for a moved child: the parent word of
@@ -266,12 +270,13 @@ __device__ void rebuild_node(const RebuildArgs& A, uint32_t x) {
     float* X = A.bin + 16 * (size_t)x;
     int32_t c[2];
     kids(X, c);
-    DBox cb[2], gb[2][2];
+    DBox cb[2], gb[2][2], sb[2];
     int cn[2], gn[2][2];
     int32_t g[2][2];
     bool can[2];
     for (int i = 0; i < 2; i++) {
         child_info(A, X, i, c[i], cb[i], cn[i]);
+        sb[i] = c[i] == kSent ? slot_box(X, i) : cb[i];          // the stored slot (an empty one as stored)
         if (c[i] >= 0 && c[i] != kSent) set_slot(X, i, cb[i]);   // node->setLeft / setRight(newBox)
         can[i] = false;
         if (c[i] >= 0 && c[i] != kSent) {
@@ -295,7 +300,12 @@ __device__ void rebuild_node(const RebuildArgs& A, uint32_t x) {
     for (int i = 1; i < 4; i++)
         if (rot[i] < rot[best]) best = i;   // std::min_element: the first smallest
     const float now = dbox_area(cb[0]) * (float)cn[0] + dbox_area(cb[1]) * (float)cn[1];
-    if (!(rot[best] < now)) return;
+    float* xr = A.nrec + 8 * (size_t)x;
+    const int xn = __float_as_int(cld2(xr + 6).x);   // numLeafs(x): no rotation at x changes it
+    if (!(rot[best] < now)) {
+        rec_store(xr, dbox_union(sb[0], sb[1]), xn);
+        return;
+    }
     // swapChildren(idx, lc, lg) (:691-702): child c[lc] and grandchild g[1-lc][lg] trade places
     const int lc = best < 2 ? 1 : 0, lg = (best == 1 || best == 2) ? 1 : 0, o = 1 - lc;
     const uint32_t other = (uint32_t)c[o] >> 2;
@@ -309,7 +319,9 @@ __device__ void rebuild_node(const RebuildArgs& A, uint32_t x) {
     set_kid(X, lc, g[o][lg]);
     set_slot(X, lc, gb[o][lg]);
     moved_to(A, g[o][lg], x, lc);
-    csti(A.objects + other, cldi(A.objects + other) + cn[lc] - gn[o][lg]);   // BVHNodeInfo::changeCount, net
+    // BVHNodeInfo::changeCount, net: the other child's objects change by the swap
+    rec_store(A.nrec + 8 * (size_t)other, ob, cn[o] + cn[lc] - gn[o][lg]);
+    rec_store(xr, lc == 0 ? dbox_union(gb[o][lg], ob) : dbox_union(ob, gb[o][lg]), xn);
 }
 
 // One thread per leaf: Woop data and the leaf's box, then up both trees.
@@ -495,6 +507,9 @@ bool plan_mesh(AnimState* A, MeshRebuild& R, const ctl_bvh_node* nodes, uint32_t
             else for (uint32_t e = (uint32_t)~v;; e++) { objects[k]++; if (idx[e] & 1) break; }
         }
     }
+    // node records: the box is written when the node is rebuilt, the objects persist
+    std::vector<float> nrec(8ull * n_nodes, 0.0f);
+    for (uint32_t k = 0; k < n_nodes; k++) std::memcpy(&nrec[8ull * k + 6], &objects[k], 4);
     std::sort(leaves.begin(), leaves.end(), [](uint4 a, uint4 b) { return a.y < b.y; });
     std::vector<uint32_t> leaf_of(n_entries, 0xffffffffu);
     for (size_t i = 0; i < leaves.size(); i++) leaf_of[leaves[i].y] = (uint32_t)i;
@@ -527,7 +542,7 @@ bool plan_mesh(AnimState* A, MeshRebuild& R, const ctl_bvh_node* nodes, uint32_t
     R.n_wide = n_wide;
     if (!anim_upload(A, &R.d_leaf, leaves.data(), leaves.size()) ||
         !anim_upload(A, &R.d_leaf_of, leaf_of.data(), leaf_of.size()) ||
-        !anim_upload(A, &R.d_objects, objects.data(), objects.size()) || !anim_alloc(A, &R.d_cnt, n_nodes) ||
+        !anim_upload(A, &R.d_nrec, nrec.data(), nrec.size()) || !anim_alloc(A, &R.d_cnt, n_nodes) ||
         hipMemset(R.d_cnt, 0, n_nodes * sizeof(uint32_t)) != hipSuccess ||
         (n_wide && (!anim_upload(A, &R.d_wup, wup.data(), wup.size()) || !anim_alloc(A, &R.d_wcnt, n_wide) ||
                     hipMemset(R.d_wcnt, 0, n_wide * sizeof(uint32_t)) != hipSuccess))) {
@@ -758,7 +773,7 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         R.woop = const_cast<float4*>(S.woop) + P.km.bvh_triangle_offset;
         R.leaf = P.rb.d_leaf;
         R.leaf_of = P.rb.d_leaf_of;
-        R.objects = P.rb.d_objects;
+        R.nrec = P.rb.d_nrec;
         R.cnt = P.rb.d_cnt;
         R.wup = P.rb.d_wup;
         R.wcnt = P.rb.d_wcnt;
