@@ -49,6 +49,8 @@ struct MeshRebuild {
     uint4* d_leaf = nullptr;            // {holder << 1 | slot, first entry, entries, wide node << 2 | slot}
     uint32_t* d_leaf_of = nullptr;      // per entry of the mesh: the record of the leaf starting there
     float* d_nrec = nullptr;            // per binary node: its box (6) and numLeafs (bvhNodeData), 32 B
+    float* d_lrec = nullptr;            // per leaf: its box and entries, 32 B
+    float* d_wrec = nullptr;            // per 4-wide node: its box, 32 B
     uint32_t* d_cnt = nullptr;          // arrival counters per binary node (0 between launches)
     uint32_t n_wide = 0;                // 4-wide nodes of the mesh (0: binary scene)
     uint32_t* d_wup = nullptr;          // per wide node: parent << 2 | slot (0xffffffff: the root)
@@ -160,15 +162,19 @@ __device__ __forceinline__ float dbox_area(const DBox& b) {
     const float x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
     return 2.0f * (x * y + x * z + y * z);
 }
-// Words another thread of the same launch reads or writes go through
-// agent-scope relaxed atomics (global_load / global_store with sc1 on gfx950):
-// each access is coherent across the XCDs' L2s by itself.  An acquire /
-// release at agent scope would instead write back and invalidate the whole L2
-// at every arrival (buffer_wbl2 / buffer_inv sc1), which made the rebuild 30x
-// slower than the refit it replaced.  The arrival orders the accesses instead:
-// a thread's coherent stores complete (s_waitcnt vmcnt(0)) before its arrival
-// increments the counter, and the last arriver's loads are issued after the
-// counter's value came back.
+// What one thread of the launch hands to another goes through small records
+// written and read with agent-scope relaxed atomics (global_store / global_load
+// with sc1 on gfx950), each access coherent across the XCDs' L2s by itself:
+// per leaf its box and objects (lrec), per binary node its box and objects
+// (nrec), per 4-wide node its box (wrec), and the child words of a node a
+// rotation rewrites.  The node arrays themselves (slots, parent words, the
+// 4-wide slots) are written with plain stores: no thread of the launch reads
+// them back.  An acquire / release at agent scope would instead write back and
+// invalidate the whole L2 at every arrival (buffer_wbl2 / buffer_inv sc1): the
+// first version did, 7.85 ms per animate.  The arrival orders the accesses: a
+// thread's records complete (s_waitcnt vmcnt(0)) before its arrival increments
+// the counter, and the last arriver's loads are issued after the counter's
+// value came back.
 __device__ __forceinline__ float2 cld2(const float* p) {
     const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return make_float2(__uint_as_float((uint32_t)v), __uint_as_float((uint32_t)(v >> 32)));
@@ -177,66 +183,32 @@ __device__ __forceinline__ void cst2(float* p, float a, float b) {
     const uint64_t v = (uint64_t)__float_as_uint(a) | ((uint64_t)__float_as_uint(b) << 32);
     __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ float cld(const float* p) {
-    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void cst(float* p, float a) {
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
-// BVHNodeData child slots (TriIntersectorData.h:44-88)
+// BVHNodeData child slots (TriIntersectorData.h:44-88), plain accesses
 __device__ __forceinline__ DBox slot_box(const float* nd, int c) {
-    const float2 a = cld2(nd + 4 * c), b = cld2(nd + 4 * c + 2), z = cld2(nd + 8 + 2 * c);
-    return DBox{{a.x, b.x, z.x}, {a.y, b.y, z.y}};
+    const float4 q = reinterpret_cast<const float4*>(nd)[c];
+    const float2 z = reinterpret_cast<const float2*>(nd + 8)[c];
+    return DBox{{q.x, q.z, z.x}, {q.y, q.w, z.y}};
 }
 __device__ __forceinline__ void set_slot(float* nd, int c, const DBox& b) {
-    cst2(nd + 4 * c, b.lo[0], b.hi[0]);
-    cst2(nd + 4 * c + 2, b.lo[1], b.hi[1]);
-    cst2(nd + 8 + 2 * c, b.lo[2], b.hi[2]);
+    reinterpret_cast<float4*>(nd)[c] = make_float4(b.lo[0], b.hi[0], b.lo[1], b.hi[1]);
+    reinterpret_cast<float2*>(nd + 8)[c] = make_float2(b.lo[2], b.hi[2]);
 }
-__device__ __forceinline__ void kids(const float* nd, int32_t k[2]) {
+// a node's child words: plain when no rotation of this launch can have moved
+// them yet, coherent otherwise
+__device__ __forceinline__ void kids_plain(const float* nd, int32_t k[2]) {
+    const float2 v = reinterpret_cast<const float2*>(nd + 12)[0];
+    k[0] = __float_as_int(v.x);
+    k[1] = __float_as_int(v.y);
+}
+__device__ __forceinline__ void kids_coherent(const float* nd, int32_t k[2]) {
     const float2 v = cld2(nd + 12);
     k[0] = __float_as_int(v.x);
     k[1] = __float_as_int(v.y);
 }
-__device__ __forceinline__ void set_kid(float* nd, int c, int32_t v) { cst(nd + 12 + c, __int_as_float(v)); }
+__device__ __forceinline__ void set_kids(float* nd, int32_t a, int32_t b) { cst2(nd + 12, __int_as_float(a), __int_as_float(b)); }
 
-struct RebuildArgs {
-    float* bin;                 // the mesh tree's node 0
-    WideNode* wide;             // its first 4-wide node (nullptr: no wide copy)
-    const uint32_t* idx;        // the mesh's TriIntersectorData2 entries
-    const uint32_t* tris;       // the mesh's triangles (skinned vertex indices)
-    const float4* P;            // skinned positions
-    float4* woop;               // the mesh's TriIntersectorData entries
-    uint4* leaf;
-    const uint32_t* leaf_of;
-    float* nrec;                // per node {lo xyz, hi xyz, objects, 0}: written when the node is rebuilt
-    uint32_t* cnt;
-    const uint32_t* wup;
-    uint32_t* wcnt;
-    float* mesh_box;            // m_sLocalBox: 6 floats
-    uint32_t n_leaf;
-};
-
-// The last of `need` arrivals at counter k goes on (and leaves the counter at
-// 0 for the next launch).  The caller's coherent stores complete first.
-__device__ __forceinline__ bool arrive(uint32_t* cnt, uint32_t k, uint32_t need) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t old = __hip_atomic_fetch_add(cnt + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("" ::: "memory");   // no load of the arrivals' words is hoisted above the counter
-    if (old + 1 < need) return false;
-    __hip_atomic_store(cnt + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
-}
-
-__device__ __forceinline__ int leaf_objects(const uint32_t* idx, uint32_t first) {
-    int n = 1;
-    while (!(idx[first + n - 1] & 1u)) n++;
-    return n;
-}
-
-// The record of a rebuilt node: getBox (the union of its two slots) and numLeafs
-// in 32 B, so a parent reads four words instead of both slots and the count.
+// A record: getBox and numLeafs (bvhNodeData) in 32 B
 __device__ __forceinline__ void rec_load(const float* r, DBox& b, int& n) {
     const float2 a = cld2(r), c = cld2(r + 2), d = cld2(r + 4), e = cld2(r + 6);
     b = DBox{{a.x, a.y, c.x}, {c.y, d.x, d.y}};
@@ -249,40 +221,66 @@ __device__ __forceinline__ void rec_store(float* r, const DBox& b, int n) {
     cst2(r + 6, __int_as_float(n), 0.0f);
 }
 
-// getBox / numLeafs of child value v held in slot c of node `holder`
-__device__ __forceinline__ void child_info(const RebuildArgs& A, const float* holder, int c, int32_t v, DBox& b,
-                                           int& n) {
+struct RebuildArgs {
+    float* bin;                 // the mesh tree's node 0
+    WideNode* wide;             // its first 4-wide node (nullptr: no wide copy)
+    const uint32_t* idx;        // the mesh's TriIntersectorData2 entries
+    const uint32_t* tris;       // the mesh's triangles (skinned vertex indices)
+    const float4* P;            // skinned positions
+    float4* woop;               // the mesh's TriIntersectorData entries
+    uint4* leaf;
+    const uint32_t* leaf_of;
+    float* nrec;                // per binary node {lo xyz, hi xyz, objects, 0}: written when the node is rebuilt
+    float* lrec;                // per leaf record, the same: written by the leaf's thread
+    float* wrec;                // per 4-wide node, its box: written when the node is refit
+    uint32_t* cnt;
+    const uint32_t* wup;
+    uint32_t* wcnt;
+    float* mesh_box;            // m_sLocalBox: 6 floats
+    uint32_t n_leaf;
+};
+
+// The last of `need` arrivals at counter k goes on (and leaves the counter at
+// 0 for the next launch).  The caller's coherent stores complete first.
+__device__ __forceinline__ bool arrive(uint32_t* cnt, uint32_t k, uint32_t need) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(cnt + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::: "memory");   // no load of the arrivals' records is hoisted above the counter
+    if (old + 1 < need) return false;
+    __hip_atomic_store(cnt + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+// getBox / numLeafs of child value v (from the child's record)
+__device__ __forceinline__ void child_info(const RebuildArgs& A, int32_t v, DBox& b, int& n) {
     if (v == kSent) { b = dbox_identity(); n = 0; }
-    else if (v < 0) { b = slot_box(holder, c); n = leaf_objects(A.idx, (uint32_t)~v); }
+    else if (v < 0) rec_load(A.lrec + 8 * (size_t)A.leaf_of[(uint32_t)~v], b, n);
     else rec_load(A.nrec + 8 * (size_t)((uint32_t)v >> 2), b, n);
 }
 
-// BVHRebuilder::setChild's array writes for a moved child: the parent word of
-// an inner node, the holder of a leaf's record (read by the next launch)
+// BVHRebuilder::setChild's array writes for a moved child (read by the next
+// launch): the parent word of an inner node, the holder of a leaf's record
 __device__ __forceinline__ void moved_to(const RebuildArgs& A, int32_t v, uint32_t node, int slot) {
     if (v == kSent) return;
-    if (v >= 0) cst(A.bin + 16 * (size_t)((uint32_t)v >> 2) + 14, __int_as_float((int32_t)(node << 2)));
+    if (v >= 0) A.bin[16 * (size_t)((uint32_t)v >> 2) + 14] = __int_as_float((int32_t)(node << 2));
     else A.leaf[A.leaf_of[(uint32_t)~v]].x = node << 1 | (uint32_t)slot;
 }
 
-// recomputeNode (BVHRebuilder.cpp:281-340) of node x, its subtree done
-__device__ void rebuild_node(const RebuildArgs& A, uint32_t x) {
+// recomputeNode (BVHRebuilder.cpp:281-340) of node x, its subtree done.
+// Returns x's box (BVHNodeData::getBox: both slots).
+__device__ DBox rebuild_node(const RebuildArgs& A, uint32_t x, const int32_t c[2]) {
     float* X = A.bin + 16 * (size_t)x;
-    int32_t c[2];
-    kids(X, c);
     DBox cb[2], gb[2][2], sb[2];
     int cn[2], gn[2][2];
     int32_t g[2][2];
     bool can[2];
     for (int i = 0; i < 2; i++) {
-        child_info(A, X, i, c[i], cb[i], cn[i]);
-        sb[i] = c[i] == kSent ? slot_box(X, i) : cb[i];          // the stored slot (an empty one as stored)
-        if (c[i] >= 0 && c[i] != kSent) set_slot(X, i, cb[i]);   // node->setLeft / setRight(newBox)
+        child_info(A, c[i], cb[i], cn[i]);
+        sb[i] = c[i] == kSent ? slot_box(X, i) : cb[i];   // the stored slot (an empty one as stored)
         can[i] = false;
         if (c[i] >= 0 && c[i] != kSent) {
-            const float* Y = A.bin + 16 * (size_t)((uint32_t)c[i] >> 2);
-            kids(Y, g[i]);
-            for (int j = 0; j < 2; j++) child_info(A, Y, j, g[i][j], gb[i][j], gn[i][j]);
+            kids_coherent(A.bin + 16 * (size_t)((uint32_t)c[i] >> 2), g[i]);   // the child's rotation may have moved them
+            for (int j = 0; j < 2; j++) child_info(A, g[i][j], gb[i][j], gn[i][j]);
             can[i] = g[i][0] != kSent && g[i][1] != kSent;   // numberGrandchildren == 2
         }
     }
@@ -303,25 +301,32 @@ __device__ void rebuild_node(const RebuildArgs& A, uint32_t x) {
     float* xr = A.nrec + 8 * (size_t)x;
     const int xn = __float_as_int(cld2(xr + 6).x);   // numLeafs(x): no rotation at x changes it
     if (!(rot[best] < now)) {
-        rec_store(xr, dbox_union(sb[0], sb[1]), xn);
-        return;
+        // node->setLeft / setRight(newBox) for the recomputed children
+        for (int i = 0; i < 2; i++)
+            if (c[i] != kSent) set_slot(X, i, cb[i]);
+        const DBox xb = dbox_union(sb[0], sb[1]);
+        rec_store(xr, xb, xn);
+        return xb;
     }
     // swapChildren(idx, lc, lg) (:691-702): child c[lc] and grandchild g[1-lc][lg] trade places
     const int lc = best < 2 ? 1 : 0, lg = (best == 1 || best == 2) ? 1 : 0, o = 1 - lc;
     const uint32_t other = (uint32_t)c[o] >> 2;
     float* O = A.bin + 16 * (size_t)other;
-    set_kid(O, lg, c[lc]);
+    set_kids(O, lg == 0 ? c[lc] : g[o][0], lg == 0 ? g[o][1] : c[lc]);
     set_slot(O, lg, cb[lc]);
+    set_slot(O, 1 - lg, gb[o][1 - lg]);
     moved_to(A, c[lc], other, lg);
     // propagateBBChange(other -> x): the other child's box, its slots in order
     const DBox ob = lg == 0 ? dbox_union(cb[lc], gb[o][1]) : dbox_union(gb[o][0], cb[lc]);
+    set_kids(X, lc == 0 ? g[o][lg] : c[0], lc == 0 ? c[1] : g[o][lg]);
     set_slot(X, o, ob);
-    set_kid(X, lc, g[o][lg]);
     set_slot(X, lc, gb[o][lg]);
     moved_to(A, g[o][lg], x, lc);
     // BVHNodeInfo::changeCount, net: the other child's objects change by the swap
     rec_store(A.nrec + 8 * (size_t)other, ob, cn[o] + cn[lc] - gn[o][lg]);
-    rec_store(xr, lc == 0 ? dbox_union(gb[o][lg], ob) : dbox_union(ob, gb[o][lg]), xn);
+    const DBox xb = lc == 0 ? dbox_union(gb[o][lg], ob) : dbox_union(ob, gb[o][lg]);
+    rec_store(xr, xb, xn);
+    return xb;
 }
 
 // One thread per leaf: Woop data and the leaf's box, then up both trees.
@@ -345,14 +350,15 @@ __global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
         box_extend(lo, hi, q0, q1);
     }
     const DBox lb{{lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}};
+    rec_store(A.lrec + 8 * (size_t)i, lb, (int)lf.z);
     // the 4-wide copy: its leaf slot, then every node whose slots have all arrived
     if (A.wide) {
         uint32_t w = lf.w >> 2, sl = lf.w & 3u;
         DBox b = lb;
         for (;;) {
             WideNode& W = A.wide[w];
-            cst(&W.lo_x[sl], b.lo[0]); cst(&W.lo_y[sl], b.lo[1]); cst(&W.lo_z[sl], b.lo[2]);
-            cst(&W.hi_x[sl], b.hi[0]); cst(&W.hi_y[sl], b.hi[1]); cst(&W.hi_z[sl], b.hi[2]);
+            W.lo_x[sl] = b.lo[0]; W.lo_y[sl] = b.lo[1]; W.lo_z[sl] = b.lo[2];
+            W.hi_x[sl] = b.hi[0]; W.hi_y[sl] = b.hi[1]; W.hi_z[sl] = b.hi[2];
             const int4 ch = *reinterpret_cast<const int4*>(W.child);   // the topology: fixed since the upload
             const uint32_t need = (ch.x != kSent) + (ch.y != kSent) + (ch.z != kSent) + (ch.w != kSent);
             if (!arrive(A.wcnt, w, need)) break;
@@ -360,10 +366,15 @@ __global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
             if (up == 0xffffffffu) break;
             const int32_t chk[4] = {ch.x, ch.y, ch.z, ch.w};
             b = dbox_identity();
-            for (int k = 0; k < 4; k++)
-                if (chk[k] != kSent)
-                    b = dbox_union(b, DBox{{cld(&W.lo_x[k]), cld(&W.lo_y[k]), cld(&W.lo_z[k])},
-                                           {cld(&W.hi_x[k]), cld(&W.hi_y[k]), cld(&W.hi_z[k])}});
+            for (int k = 0; k < 4; k++) {
+                if (chk[k] == kSent) continue;
+                DBox cbx;
+                int n;
+                if (chk[k] >= 0) rec_load(A.wrec + 8 * (size_t)chk[k], cbx, n);
+                else rec_load(A.lrec + 8 * (size_t)A.leaf_of[(uint32_t)~chk[k] >> 3], cbx, n);
+                b = dbox_union(b, cbx);
+            }
+            rec_store(A.wrec + 8 * (size_t)w, b, 0);
             w = up >> 2;
             sl = up & 3u;
         }
@@ -374,14 +385,13 @@ __global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
     for (;;) {
         float* X = A.bin + 16 * (size_t)x;
         int32_t k[2];
-        kids(X, k);   // unchanged until this node is rebuilt (by the last arrival)
+        kids_plain(X, k);   // unchanged until this node is rebuilt (by the last arrival)
         const uint32_t need = (k[0] != kSent) + (k[1] != kSent);
         if (!arrive(A.cnt, x, need)) return;
-        rebuild_node(A, x);
-        const int32_t p = __float_as_int(cld(X + 14));
+        const DBox xb = rebuild_node(A, x, k);
+        const int32_t p = __float_as_int(X[14]);
         if (p < 0) {   // the root: m_sLocalBox = BVHNodeData::getBox, both slots
-            const DBox r = dbox_union(slot_box(X, 0), slot_box(X, 1));
-            for (int k = 0; k < 3; k++) { A.mesh_box[k] = r.lo[k]; A.mesh_box[3 + k] = r.hi[k]; }
+            for (int q = 0; q < 3; q++) { A.mesh_box[q] = xb.lo[q]; A.mesh_box[3 + q] = xb.hi[q]; }
             return;
         }
         x = (uint32_t)p >> 2;
@@ -543,6 +553,8 @@ bool plan_mesh(AnimState* A, MeshRebuild& R, const ctl_bvh_node* nodes, uint32_t
     if (!anim_upload(A, &R.d_leaf, leaves.data(), leaves.size()) ||
         !anim_upload(A, &R.d_leaf_of, leaf_of.data(), leaf_of.size()) ||
         !anim_upload(A, &R.d_nrec, nrec.data(), nrec.size()) || !anim_alloc(A, &R.d_cnt, n_nodes) ||
+        !anim_alloc(A, &R.d_lrec, 8 * std::max<size_t>(1, leaves.size())) ||
+        (n_wide && !anim_alloc(A, &R.d_wrec, 8ull * n_wide)) ||
         hipMemset(R.d_cnt, 0, n_nodes * sizeof(uint32_t)) != hipSuccess ||
         (n_wide && (!anim_upload(A, &R.d_wup, wup.data(), wup.size()) || !anim_alloc(A, &R.d_wcnt, n_wide) ||
                     hipMemset(R.d_wcnt, 0, n_wide * sizeof(uint32_t)) != hipSuccess))) {
@@ -774,6 +786,8 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         R.leaf = P.rb.d_leaf;
         R.leaf_of = P.rb.d_leaf_of;
         R.nrec = P.rb.d_nrec;
+        R.lrec = P.rb.d_lrec;
+        R.wrec = P.rb.d_wrec;
         R.cnt = P.rb.d_cnt;
         R.wup = P.rb.d_wup;
         R.wcnt = P.rb.d_wcnt;
