@@ -166,10 +166,11 @@ __device__ __forceinline__ float dbox_area(const DBox& b) {
 // written and read with agent-scope relaxed atomics (global_store / global_load
 // with sc1 on gfx950), each access coherent across the XCDs' L2s by itself:
 // per leaf its box and objects (lrec), per binary node its box and objects
-// (nrec), per 4-wide node its box (wrec), and the child words of a node a
-// rotation rewrites.  The node arrays themselves (slots, parent words, the
-// 4-wide slots) are written with plain stores: no thread of the launch reads
-// them back.  An acquire / release at agent scope would instead write back and
+// (nrec), per 4-wide node its box (wrec).  Words two threads of the launch may
+// write (binary slots, child and parent words, a leaf's holder) are stored the
+// same way, so the last writer wins whatever the XCDs' write-back order; the
+// 4-wide slots have one writer each and take plain stores.  An acquire /
+// release at agent scope would instead write back and
 // invalidate the whole L2 at every arrival (buffer_wbl2 / buffer_inv sc1): the
 // first version did, 7.85 ms per animate.  The arrival orders the accesses: a
 // thread's records complete (s_waitcnt vmcnt(0)) before its arrival increments
@@ -184,15 +185,20 @@ __device__ __forceinline__ void cst2(float* p, float a, float b) {
     __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// BVHNodeData child slots (TriIntersectorData.h:44-88), plain accesses
+// BVHNodeData child slots (TriIntersectorData.h:44-88).  A slot can be written
+// by two threads of one launch (the node's own rebuild, then a rotation at its
+// parent that makes it the `other` child), so its stores are coherent: a plain
+// store could sit dirty in one XCD's L2 and be written back after the other.
+// Reads are plain: only empty slots are read, which nothing rewrites.
 __device__ __forceinline__ DBox slot_box(const float* nd, int c) {
     const float4 q = reinterpret_cast<const float4*>(nd)[c];
     const float2 z = reinterpret_cast<const float2*>(nd + 8)[c];
     return DBox{{q.x, q.z, z.x}, {q.y, q.w, z.y}};
 }
 __device__ __forceinline__ void set_slot(float* nd, int c, const DBox& b) {
-    reinterpret_cast<float4*>(nd)[c] = make_float4(b.lo[0], b.hi[0], b.lo[1], b.hi[1]);
-    reinterpret_cast<float2*>(nd + 8)[c] = make_float2(b.lo[2], b.hi[2]);
+    cst2(nd + 4 * c, b.lo[0], b.hi[0]);
+    cst2(nd + 4 * c + 2, b.lo[1], b.hi[1]);
+    cst2(nd + 8 + 2 * c, b.lo[2], b.hi[2]);
 }
 // a node's child words: plain when no rotation of this launch can have moved
 // them yet, coherent otherwise
@@ -259,11 +265,16 @@ __device__ __forceinline__ void child_info(const RebuildArgs& A, int32_t v, DBox
 }
 
 // BVHRebuilder::setChild's array writes for a moved child (read by the next
-// launch): the parent word of an inner node, the holder of a leaf's record
+// launch; a child can move twice in one launch): the parent word of an inner
+// node, the holder of a leaf's record
 __device__ __forceinline__ void moved_to(const RebuildArgs& A, int32_t v, uint32_t node, int slot) {
     if (v == kSent) return;
-    if (v >= 0) A.bin[16 * (size_t)((uint32_t)v >> 2) + 14] = __int_as_float((int32_t)(node << 2));
-    else A.leaf[A.leaf_of[(uint32_t)~v]].x = node << 1 | (uint32_t)slot;
+    if (v >= 0)
+        __hip_atomic_store(reinterpret_cast<int32_t*>(A.bin + 16 * (size_t)((uint32_t)v >> 2) + 14), (int32_t)(node << 2),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        __hip_atomic_store(&A.leaf[A.leaf_of[(uint32_t)~v]].x, node << 1 | (uint32_t)slot, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // recomputeNode (BVHRebuilder.cpp:281-340) of node x, its subtree done.
@@ -314,7 +325,6 @@ __device__ DBox rebuild_node(const RebuildArgs& A, uint32_t x, const int32_t c[2
     float* O = A.bin + 16 * (size_t)other;
     set_kids(O, lg == 0 ? c[lc] : g[o][0], lg == 0 ? g[o][1] : c[lc]);
     set_slot(O, lg, cb[lc]);
-    set_slot(O, 1 - lg, gb[o][1 - lg]);
     moved_to(A, c[lc], other, lg);
     // propagateBBChange(other -> x): the other child's box, its slots in order
     const DBox ob = lg == 0 ? dbox_union(cb[lc], gb[o][1]) : dbox_union(gb[o][0], cb[lc]);
@@ -379,9 +389,9 @@ __global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
             sl = up & 3u;
         }
     }
-    // the binary tree: the leaf's slot, then each node whose children have all arrived
+    // the binary tree: each node whose children have all arrived (the holder writes
+    // the leaf's slot from its record)
     uint32_t x = lf.x >> 1;
-    set_slot(A.bin + 16 * (size_t)x, (int)(lf.x & 1u), lb);
     for (;;) {
         float* X = A.bin + 16 * (size_t)x;
         int32_t k[2];

@@ -480,6 +480,41 @@ def test_animate_large_grid_bit_exact(ctl, orc, dev, bvh):
 
 
 @pytest.mark.gpu
+def test_rebuild_deterministic_across_contexts(ctl, dev):
+    """The rebuild's threads climb the tree in whatever order they arrive, on every
+    XCD: the result must not depend on it.  Two contexts animate the 512 x 512
+    skinned grid through the same 4 frames (each frame from the last one's tree);
+    their node arrays, Woop data, 4-wide trees and mesh boxes are identical after
+    every frame."""
+    A = ctl._abi
+    V, N, BI, BW, T, UV = skinned_grid(512)
+    s = ctl.HostScene()
+    s.add_animated_mesh(V, N, BI, BW, T, [ctl.diffuse_material(0.5, 0.5, 0.5)], uvs=UV)
+    s.add_node(0)
+    s.add_node(0, [1, 0, 0, 25, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1])
+    s.set_camera([0, 8, -20], [0, 0, 0], [0, 1, 0], 50, 16, 16)
+    d = s.compile()
+    nw = ctl.host_wide_trees(d)[0].shape[0]
+    pts = [ctl.PathTracer(0), ctl.PathTracer(0)]
+    try:
+        for pt in pts:
+            pt.upload_scene(d)
+        for t in (0.4, 1.3, 2.2, 3.1):
+            got = []
+            for pt in pts:
+                pt.animate(0, grid_frames(16, 0.0), grid_frames(16, t), 0.9)
+                got.append((pt.read_array(A.CTL_ARRAY_BVH_NODES, 0, d.n_bvh_nodes, np.uint32, 16),
+                            pt.read_array(A.CTL_ARRAY_WOOP, 0, d.n_woop_tris, np.uint32, 12),
+                            pt.read_array(A.CTL_ARRAY_MESH_BOXES, 0, d.n_meshes, np.uint32, 6),
+                            pt.read_array(A.CTL_ARRAY_WIDE_BVH, 0, nw, np.uint32, 32)))
+            for a, b in zip(*got):
+                assert np.array_equal(a, b), t
+    finally:
+        for pt in pts:
+            pt.close()
+
+
+@pytest.mark.gpu
 def test_animate_rejects_bad_bones(ctl, dev):
     s = build_scene(ctl)
     d = s.compile()
