@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get("CTL_LIB") or os.path.join(_HERE, "_lib", "libctl_trac
 
 # CTL_ABI_VERSION of the include/ctl_trace.h these bindings mirror; load()
 # refuses a library that reports another (mismatched struct layouts).
-ABI_VERSION = 3
+ABI_VERSION = 4
 CTL_OK = 0
 CTL_SCENE_HALF_HOST_QUIRK = 1
 CTL_SCENE_BINARY_BVH = 2

@@ -41,9 +41,11 @@
 extern "C" {
 #endif
 
-#define CTL_ABI_VERSION 3   /* 2: round 4 (ctl_env_light 112 B, ctl_fb_reduce d_out, wide-tree reads);
+#define CTL_ABI_VERSION 4   /* 2: round 4 (ctl_env_light 112 B, ctl_fb_reduce d_out, wide-tree reads);
                                3: round 5 (ctl_occluded; CTL_SCENE_WIDE8 / CTL_ARRAY_W8_* / ctl_host_w8_tree
-                               removed) */
+                               removed);
+                               4: round 6 (CTL_PT_RENDER_AHEAD, CTL_ARRAY_CULL_BOUND; ctl_scene_animate /
+                               ctl_scene_set_transform rebuild trees with BVHRebuilder's rotations) */
 
 #if defined(_WIN32)
 #define CTL_API __declspec(dllexport)

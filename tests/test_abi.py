@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     # round 5: ctl_occluded; the 8-wide tree's flag, arrays and ctl_host_w8_tree gone
-    assert abi.load().ctl_abi_version() == 3 == abi.ABI_VERSION
+    assert abi.load().ctl_abi_version() == 4 == abi.ABI_VERSION
 
 
 def test_load_refuses_another_abi_version(tmp_path, monkeypatch):
