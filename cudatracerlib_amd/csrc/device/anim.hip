@@ -7,20 +7,24 @@
 //   tris     g_ComputeTriangles -> TriangleData::setData (TriangleData.cu:35-63)
 //   rebuild  the mesh tree as BVHRebuilder::Build(&p, true) leaves it
 //            (AnimatedMesh.cpp:174-176, BVHRebuilder.cpp:281-340, 365-450): one
-//            thread per leaf writes its entries' Woop data (AnimProvider::
-//            setObject, AnimatedMesh.cpp:113-117) and the union of their
-//            triangles' boxes into the slot that holds the leaf, then climbs:
-//            the last of a node's children to arrive (an atomic counter per
-//            node) recomputes the node -- its inner children's boxes, the best
-//            of the four child/grandchild rotations by SAH if strictly cheaper
-//            (host/bvh_rebuild.h states the rules), the moved subtrees' parent
-//            words and leaf records -- and moves on to its parent.  A node is
-//            recomputed after its whole subtree, as in the reference's
+//            thread per leaf (or per pair of leaves under one node) writes its
+//            entries' Woop data (AnimProvider::setObject, AnimatedMesh.cpp:
+//            113-117) and the leaf's box record, then climbs: the last of a
+//            node's children to arrive (an atomic counter per node) recomputes
+//            the node -- the best of the four child/grandchild rotations by SAH
+//            if strictly cheaper (host/bvh_rebuild.h states the rules), the
+//            moved subtrees' child and parent words, the box records -- and
+//            moves on to its parent, carrying the node's view (box, objects,
+//            children and theirs) so that only the sibling's is read back.  A
+//            node is recomputed after its whole subtree, as in the reference's
 //            post-order recursion, and nodes of disjoint subtrees never touch
 //            the same words, so the result is the recursion's.  The tree's
-//            shape persists from frame to frame, as the reference's does.  The
-//            4-wide copy keeps the topology the upload collapsed and is refit in
-//            the same launch, bottom-up by arrival counts from the same leaves.
+//            shape persists from frame to frame, as the reference's does.
+//   slots    every node's two slots from its children's final records, and
+//            each leaf's holder and pairing for the next frame (one launch)
+//   4-wide   the 4-wide copy keeps the topology the upload collapsed and is
+//            refit by height: one launch per height below the top, the top
+//            (<= 2048 nodes) in one block through LDS.
 //   scene    instance boxes (mesh box x node transform) and the scene box ->
 //            m_rayTraceEps on the device; the instance tree rebuilt on the host
 //            along the moved instances' paths (SceneBVH::Build, the same
@@ -46,15 +50,18 @@ namespace ctl {
 struct MeshRebuild {
     uint32_t n_nodes = 0;               // binary nodes of the mesh tree
     uint32_t n_leaf = 0;
-    uint4* d_leaf = nullptr;            // {holder << 1 | slot, first entry, entries, wide node << 2 | slot}
+    uint4* d_leaf = nullptr;            // {holder << 1 | slot, first entry, entries, pairing} (anim_rebuild_kernel)
     uint32_t* d_leaf_of = nullptr;      // per entry of the mesh: the record of the leaf starting there
     float* d_nrec = nullptr;            // per binary node: its box (6) and numLeafs (bvhNodeData), 32 B
     float* d_lrec = nullptr;            // per leaf: its box and entries, 32 B
-    float* d_wrec = nullptr;            // per 4-wide node: its box, 32 B
-    uint32_t* d_cnt = nullptr;          // arrival counters per binary node (0 between launches)
+    uint32_t* d_cnt = nullptr;          // arrival counters per binary node (even between launches)
     uint32_t n_wide = 0;                // 4-wide nodes of the mesh (0: binary scene)
-    uint32_t* d_wup = nullptr;          // per wide node: parent << 2 | slot (0xffffffff: the root)
-    uint32_t* d_wcnt = nullptr;         // arrival counters per wide node
+    float* d_wrec = nullptr;            // per 4-wide node: its box, 32 B
+    uint32_t* d_worder = nullptr;       // 4-wide nodes by height (children first)
+    uint32_t* d_woff = nullptr;         // per height: its first entry of d_worder (and the end)
+    std::vector<uint32_t> woff;         // the same on the host
+    uint32_t wtop = 0;                  // the first height of the one-block top
+    uint4* d_wcode = nullptr;           // per 4-wide node: its child codes (WideArgs)
 };
 
 struct AnimMeshPlan {
@@ -162,74 +169,71 @@ __device__ __forceinline__ float dbox_area(const DBox& b) {
     const float x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
     return 2.0f * (x * y + x * z + y * z);
 }
-// What one thread of the launch hands to another goes through small records
-// written and read with agent-scope relaxed atomics (global_store / global_load
-// with sc1 on gfx950), each access coherent across the XCDs' L2s by itself:
-// per leaf its box and objects (lrec), per binary node its box and objects
-// (nrec), per 4-wide node its box (wrec).  Words two threads of the launch may
-// write (binary slots, child and parent words, a leaf's holder) are stored the
-// same way, so the last writer wins whatever the XCDs' write-back order; the
-// 4-wide slots have one writer each and take plain stores.  An acquire /
-// release at agent scope would instead write back and
-// invalidate the whole L2 at every arrival (buffer_wbl2 / buffer_inv sc1): the
-// first version did, 7.85 ms per animate.  The arrival orders the accesses: a
-// thread's records complete (s_waitcnt vmcnt(0)) before its arrival increments
-// the counter, and the last arriver's loads are issued after the counter's
-// value came back.
-__device__ __forceinline__ float2 cld2(const float* p) {
-    const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_float2(__uint_as_float((uint32_t)v), __uint_as_float((uint32_t)(v >> 32)));
+// What one thread of the climb hands to another goes through 32-B records: per
+// leaf its box and objects (lrec), per binary node the same (nrec).  They are
+// written and read with the SC1 cache policy (buffer_load / buffer_store
+// dwordx4 sc1: coherent across the XCDs' L2s access by access), 16 B per access.
+// Words two threads of the launch may write (a moved subtree's parent word, a
+// moved leaf's holder, a rotated node's child words) are stored the same way,
+// so the last writer wins whatever the XCDs' write-back order.  The node slots
+// are not written by the climb at all: a second launch (anim_slot_kernel)
+// stores every node's two slots from its children's final records, plain and
+// whole, and the 4-wide copy is refit by height after that (anim_wide_kernel),
+// both reading what the climb left after a launch boundary.  An acquire /
+// release at agent scope would instead write back and invalidate the whole L2
+// at every arrival (buffer_wbl2 / buffer_inv sc1): the first version did, 7.85
+// ms per animate.  The arrival orders the accesses: a thread's records complete
+// (s_waitcnt vmcnt(0)) before its arrival increments the counter, and the last
+// arriver's loads are issued after the counter's value came back.
+constexpr int kSC1 = 16;   // cache-policy operand of the buffer intrinsics: SC1
+
+struct Coh {               // buffer descriptors of the arrays the climb shares
+    __amdgpu_buffer_rsrc_t bin, nrec, lrec;
+};
+__device__ __forceinline__ float4 cld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSC1));
 }
-__device__ __forceinline__ void cst2(float* p, float a, float b) {
-    const uint64_t v = (uint64_t)__float_as_uint(a) | ((uint64_t)__float_as_uint(b) << 32);
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void cst4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
+    using v4u = __attribute__((ext_vector_type(4))) unsigned int;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, off, 0, kSC1);
+}
+__device__ __forceinline__ void cld_kids(__amdgpu_buffer_rsrc_t bin, uint32_t node, int32_t k[2]) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(bin, node * 64u + 48u, 0, kSC1);
+    k[0] = (int32_t)v[0];
+    k[1] = (int32_t)v[1];
+}
+__device__ __forceinline__ void cst_kids(__amdgpu_buffer_rsrc_t bin, uint32_t node, int32_t a, int32_t b) {
+    using v2u = __attribute__((ext_vector_type(2))) unsigned int;
+    __builtin_amdgcn_raw_buffer_store_b64(v2u{(unsigned)a, (unsigned)b}, bin, node * 64u + 48u, 0, kSC1);
 }
 
-// BVHNodeData child slots (TriIntersectorData.h:44-88).  A slot can be written
-// by two threads of one launch (the node's own rebuild, then a rotation at its
-// parent that makes it the `other` child), so its stores are coherent: a plain
-// store could sit dirty in one XCD's L2 and be written back after the other.
-// Reads are plain: only empty slots are read, which nothing rewrites.
+// BVHNodeData child slots (TriIntersectorData.h:44-88): {lo.x hi.x lo.y hi.y}
+// per slot at 0 / 16 B, {lo.z hi.z} per slot at 32 / 40 B
 __device__ __forceinline__ DBox slot_box(const float* nd, int c) {
     const float4 q = reinterpret_cast<const float4*>(nd)[c];
     const float2 z = reinterpret_cast<const float2*>(nd + 8)[c];
     return DBox{{q.x, q.z, z.x}, {q.y, q.w, z.y}};
 }
-__device__ __forceinline__ void set_slot(float* nd, int c, const DBox& b) {
-    cst2(nd + 4 * c, b.lo[0], b.hi[0]);
-    cst2(nd + 4 * c + 2, b.lo[1], b.hi[1]);
-    cst2(nd + 8 + 2 * c, b.lo[2], b.hi[2]);
-}
-// a node's child words: plain when no rotation of this launch can have moved
-// them yet, coherent otherwise
+// a node's child words as the last launch left them (the climb reads a node's
+// own words before anything of this launch can have moved them)
 __device__ __forceinline__ void kids_plain(const float* nd, int32_t k[2]) {
     const float2 v = reinterpret_cast<const float2*>(nd + 12)[0];
     k[0] = __float_as_int(v.x);
     k[1] = __float_as_int(v.y);
 }
-__device__ __forceinline__ void kids_coherent(const float* nd, int32_t k[2]) {
-    const float2 v = cld2(nd + 12);
-    k[0] = __float_as_int(v.x);
-    k[1] = __float_as_int(v.y);
-}
-__device__ __forceinline__ void set_kids(float* nd, int32_t a, int32_t b) { cst2(nd + 12, __int_as_float(a), __int_as_float(b)); }
 
-// A record: getBox and numLeafs (bvhNodeData) in 32 B
-__device__ __forceinline__ void rec_load(const float* r, DBox& b, int& n) {
-    const float2 a = cld2(r), c = cld2(r + 2), d = cld2(r + 4), e = cld2(r + 6);
-    b = DBox{{a.x, a.y, c.x}, {c.y, d.x, d.y}};
-    n = __float_as_int(e.x);
+// A record: getBox and numLeafs (bvhNodeData), {lo xyz, hi.x} {hi.yz, objects, 0}
+__device__ __forceinline__ void rec_unpack(float4 a, float4 c, DBox& b, int& n) {
+    b = DBox{{a.x, a.y, a.z}, {a.w, c.x, c.y}};
+    n = __float_as_int(c.z);
 }
-__device__ __forceinline__ void rec_store(float* r, const DBox& b, int n) {
-    cst2(r, b.lo[0], b.lo[1]);
-    cst2(r + 2, b.lo[2], b.hi[0]);
-    cst2(r + 4, b.hi[1], b.hi[2]);
-    cst2(r + 6, __int_as_float(n), 0.0f);
+__device__ __forceinline__ void rec_store(__amdgpu_buffer_rsrc_t r, uint32_t i, const DBox& b, int n) {
+    cst4(r, 32u * i, make_float4(b.lo[0], b.lo[1], b.lo[2], b.hi[0]));
+    cst4(r, 32u * i + 16u, make_float4(b.hi[1], b.hi[2], __int_as_float(n), 0.0f));
 }
 
 struct RebuildArgs {
     float* bin;                 // the mesh tree's node 0
-    WideNode* wide;             // its first 4-wide node (nullptr: no wide copy)
     const uint32_t* idx;        // the mesh's TriIntersectorData2 entries
     const uint32_t* tris;       // the mesh's triangles (skinned vertex indices)
     const float4* P;            // skinned positions
@@ -238,116 +242,171 @@ struct RebuildArgs {
     const uint32_t* leaf_of;
     float* nrec;                // per binary node {lo xyz, hi xyz, objects, 0}: written when the node is rebuilt
     float* lrec;                // per leaf record, the same: written by the leaf's thread
-    float* wrec;                // per 4-wide node, its box: written when the node is refit
     uint32_t* cnt;
-    const uint32_t* wup;
-    uint32_t* wcnt;
     float* mesh_box;            // m_sLocalBox: 6 floats
-    uint32_t n_leaf;
+    uint32_t n_leaf, n_nodes;
 };
 
-// The last of `need` arrivals at counter k goes on (and leaves the counter at
-// 0 for the next launch).  The caller's coherent stores complete first.
+__device__ __forceinline__ Coh coh_of(const RebuildArgs& A) {
+    return Coh{__builtin_amdgcn_make_buffer_rsrc(A.bin, 0, (int)(64u * A.n_nodes), 0x00020000),
+               __builtin_amdgcn_make_buffer_rsrc(A.nrec, 0, (int)(32u * A.n_nodes), 0x00020000),
+               __builtin_amdgcn_make_buffer_rsrc(A.lrec, 0, (int)(32u * A.n_leaf), 0x00020000)};
+}
+
+// The last of `need` (1 or 2, fixed for a node: no rotation moves an empty
+// slot) arrivals at counter k goes on.  Every launch adds `need` to the counter,
+// so the last arrival is the one that makes it a multiple of `need`; nothing
+// resets it.  The caller's coherent stores complete first.
 __device__ __forceinline__ bool arrive(uint32_t* cnt, uint32_t k, uint32_t need) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t old = __hip_atomic_fetch_add(cnt + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("" ::: "memory");   // no load of the arrivals' records is hoisted above the counter
-    if (old + 1 < need) return false;
-    __hip_atomic_store(cnt + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
+    return need == 1 || (old & 1u) != 0;
 }
 
-// getBox / numLeafs of child value v (from the child's record)
-__device__ __forceinline__ void child_info(const RebuildArgs& A, int32_t v, DBox& b, int& n) {
-    if (v == kSent) { b = dbox_identity(); n = 0; }
-    else if (v < 0) rec_load(A.lrec + 8 * (size_t)A.leaf_of[(uint32_t)~v], b, n);
-    else rec_load(A.nrec + 8 * (size_t)((uint32_t)v >> 2), b, n);
-}
+// A finished subtree as its parent's recomputation reads it: getBox and numLeafs,
+// and for an inner node its children with theirs.  The climbing thread carries
+// the one it just finished; the sibling's comes from the records.
+struct View {
+    DBox b;
+    int n;
+    int32_t k[2];
+    DBox kb[2];
+    int kn[2];
+};
 
-// BVHRebuilder::setChild's array writes for a moved child (read by the next
-// launch; a child can move twice in one launch): the parent word of an inner
-// node, the holder of a leaf's record
-__device__ __forceinline__ void moved_to(const RebuildArgs& A, int32_t v, uint32_t node, int slot) {
-    if (v == kSent) return;
-    if (v >= 0)
-        __hip_atomic_store(reinterpret_cast<int32_t*>(A.bin + 16 * (size_t)((uint32_t)v >> 2) + 14), (int32_t)(node << 2),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        __hip_atomic_store(&A.leaf[A.leaf_of[(uint32_t)~v]].x, node << 1 | (uint32_t)slot, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+// field-wise selects (a conditional over whole structs would select their
+// addresses and put them in scratch)
+__device__ __forceinline__ DBox bsel(bool a, const DBox& x, const DBox& y) {
+    DBox r;
+    for (int k = 0; k < 3; k++) { r.lo[k] = a ? x.lo[k] : y.lo[k]; r.hi[k] = a ? x.hi[k] : y.hi[k]; }
+    return r;
 }
-
-// recomputeNode (BVHRebuilder.cpp:281-340) of node x, its subtree done.
-// Returns x's box (BVHNodeData::getBox: both slots).
-__device__ DBox rebuild_node(const RebuildArgs& A, uint32_t x, const int32_t c[2]) {
-    float* X = A.bin + 16 * (size_t)x;
-    DBox cb[2], gb[2][2], sb[2];
-    int cn[2], gn[2][2];
-    int32_t g[2][2];
-    bool can[2];
-    for (int i = 0; i < 2; i++) {
-        child_info(A, c[i], cb[i], cn[i]);
-        sb[i] = c[i] == kSent ? slot_box(X, i) : cb[i];   // the stored slot (an empty one as stored)
-        can[i] = false;
-        if (c[i] >= 0 && c[i] != kSent) {
-            kids_coherent(A.bin + 16 * (size_t)((uint32_t)c[i] >> 2), g[i]);   // the child's rotation may have moved them
-            for (int j = 0; j < 2; j++) child_info(A, g[i][j], gb[i][j], gn[i][j]);
-            can[i] = g[i][0] != kSent && g[i][1] != kSent;   // numberGrandchildren == 2
-        }
+__device__ __forceinline__ View vsel(bool a, const View& x, const View& y) {
+    View r;
+    r.b = bsel(a, x.b, y.b);
+    r.n = a ? x.n : y.n;
+    for (int j = 0; j < 2; j++) {
+        r.k[j] = a ? x.k[j] : y.k[j];
+        r.kb[j] = bsel(a, x.kb[j], y.kb[j]);
+        r.kn[j] = a ? x.kn[j] : y.kn[j];
     }
+    return r;
+}
+
+// getBox / numLeafs of child value v (AABB::Identity and 0 for an empty slot)
+__device__ __forceinline__ void child_info(const RebuildArgs& A, const Coh& C, int32_t v, DBox& b, int& n) {
+    if (v == kSent) { b = dbox_identity(); n = 0; return; }
+    const bool leaf = v < 0;
+    const uint32_t i = leaf ? A.leaf_of[(uint32_t)~v] : (uint32_t)v >> 2;
+    const __amdgpu_buffer_rsrc_t r = leaf ? C.lrec : C.nrec;
+    rec_unpack(cld4(r, 32u * i), cld4(r, 32u * i + 16u), b, n);
+}
+__device__ __forceinline__ View load_view(const RebuildArgs& A, const Coh& C, int32_t v) {
+    View w;
+    child_info(A, C, v, w.b, w.n);
+    w.k[0] = w.k[1] = kSent;
+    if (v >= 0 && v != kSent) cld_kids(C.bin, (uint32_t)v >> 2, w.k);   // its own rotation may have moved them
+    for (int j = 0; j < 2; j++) child_info(A, C, w.k[j], w.kb[j], w.kn[j]);
+    return w;
+}
+
+// BVHRebuilder::setChild's parent word of a moved inner child (read by the
+// next launch; a child can move twice in one launch).  A moved leaf's holder
+// is written by anim_slot_kernel, which sees every leaf's final slot.
+__device__ __forceinline__ void moved_to(const RebuildArgs& A, int32_t v, uint32_t node) {
+    if (v < 0 || v == kSent) return;
+    __hip_atomic_store(reinterpret_cast<int32_t*>(A.bin + 16 * (size_t)((uint32_t)v >> 2) + 14), (int32_t)(node << 2),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// recomputeNode (BVHRebuilder.cpp:281-340) of node x, its subtree done, with
+// its children's views v[0], v[1].  Returns x's.
+__device__ __forceinline__ View recompute_node(const RebuildArgs& A, const Coh& C, uint32_t x, const int32_t c[2],
+                                               const View v[2]) {
+    const float* X = A.bin + 16 * (size_t)x;
+    bool can[2];
+    for (int i = 0; i < 2; i++)
+        can[i] = c[i] >= 0 && c[i] != kSent && v[i].k[0] != kSent && v[i].k[1] != kSent;   // numberGrandchildren == 2
     // sah(idx, child, grandchild) (:624-638) for the four rotations
     float rot[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
     if (can[0]) {
-        rot[0] = dbox_area(dbox_union(cb[1], gb[0][1])) * (float)(cn[1] + gn[0][1]) + dbox_area(gb[0][0]) * (float)gn[0][0];
-        rot[1] = dbox_area(dbox_union(cb[1], gb[0][0])) * (float)(cn[1] + gn[0][0]) + dbox_area(gb[0][1]) * (float)gn[0][1];
+        rot[0] = dbox_area(dbox_union(v[1].b, v[0].kb[1])) * (float)(v[1].n + v[0].kn[1]) + dbox_area(v[0].kb[0]) * (float)v[0].kn[0];
+        rot[1] = dbox_area(dbox_union(v[1].b, v[0].kb[0])) * (float)(v[1].n + v[0].kn[0]) + dbox_area(v[0].kb[1]) * (float)v[0].kn[1];
     }
     if (can[1]) {
-        rot[2] = dbox_area(dbox_union(cb[0], gb[1][0])) * (float)(cn[0] + gn[1][0]) + dbox_area(gb[1][1]) * (float)gn[1][1];
-        rot[3] = dbox_area(dbox_union(cb[0], gb[1][1])) * (float)(cn[0] + gn[1][1]) + dbox_area(gb[1][0]) * (float)gn[1][0];
+        rot[2] = dbox_area(dbox_union(v[0].b, v[1].kb[0])) * (float)(v[0].n + v[1].kn[0]) + dbox_area(v[1].kb[1]) * (float)v[1].kn[1];
+        rot[3] = dbox_area(dbox_union(v[0].b, v[1].kb[1])) * (float)(v[0].n + v[1].kn[1]) + dbox_area(v[1].kb[0]) * (float)v[1].kn[0];
     }
     int best = 0;
+    float bestv = rot[0];
     for (int i = 1; i < 4; i++)
-        if (rot[i] < rot[best]) best = i;   // std::min_element: the first smallest
-    const float now = dbox_area(cb[0]) * (float)cn[0] + dbox_area(cb[1]) * (float)cn[1];
-    float* xr = A.nrec + 8 * (size_t)x;
-    const int xn = __float_as_int(cld2(xr + 6).x);   // numLeafs(x): no rotation at x changes it
-    if (!(rot[best] < now)) {
-        // node->setLeft / setRight(newBox) for the recomputed children
-        for (int i = 0; i < 2; i++)
-            if (c[i] != kSent) set_slot(X, i, cb[i]);
-        const DBox xb = dbox_union(sb[0], sb[1]);
-        rec_store(xr, xb, xn);
-        return xb;
+        if (rot[i] < bestv) { best = i; bestv = rot[i]; }   // std::min_element: the first smallest
+    const float now = dbox_area(v[0].b) * (float)v[0].n + dbox_area(v[1].b) * (float)v[1].n;
+    View r;
+    r.n = v[0].n + v[1].n;   // numLeafs(x): no rotation at x changes it
+    if (!(bestv < now)) {
+        // getBox: both stored slots, an empty one as stored (both loaded, then
+        // selected: a select of a load and a register became a scratch round trip)
+        r.b = dbox_union(v[0].b, v[1].b);
+        if (c[0] == kSent || c[1] == kSent) {
+            const DBox s0 = slot_box(X, 0), s1 = slot_box(X, 1);
+            r.b = dbox_union(bsel(c[0] == kSent, s0, v[0].b), bsel(c[1] == kSent, s1, v[1].b));
+        }
+        for (int i = 0; i < 2; i++) { r.k[i] = c[i]; r.kb[i] = v[i].b; r.kn[i] = v[i].n; }
+        rec_store(C.nrec, x, r.b, r.n);
+        return r;
     }
-    // swapChildren(idx, lc, lg) (:691-702): child c[lc] and grandchild g[1-lc][lg] trade places
-    const int lc = best < 2 ? 1 : 0, lg = (best == 1 || best == 2) ? 1 : 0, o = 1 - lc;
-    const uint32_t other = (uint32_t)c[o] >> 2;
-    float* O = A.bin + 16 * (size_t)other;
-    set_kids(O, lg == 0 ? c[lc] : g[o][0], lg == 0 ? g[o][1] : c[lc]);
-    set_slot(O, lg, cb[lc]);
-    moved_to(A, c[lc], other, lg);
+    // swapChildren(idx, lc, lg) (:691-702): child c[lc] and grandchild (c[o]'s lg) trade places
+    const int lc = best < 2 ? 1 : 0, lg = (best == 1 || best == 2) ? 1 : 0;
+    const View L = vsel(lc == 0, v[0], v[1]);   // the child pushed down
+    const View O = vsel(lc == 0, v[1], v[0]);   // the other child
+    const int32_t g = lg == 0 ? O.k[0] : O.k[1], og = lg == 0 ? O.k[1] : O.k[0];
+    const DBox gb = bsel(lg == 0, O.kb[0], O.kb[1]), ogb = bsel(lg == 0, O.kb[1], O.kb[0]);
+    const int gn = lg == 0 ? O.kn[0] : O.kn[1];
+    const int32_t cl = lc == 0 ? c[0] : c[1], co = lc == 0 ? c[1] : c[0];
+    const uint32_t other = (uint32_t)co >> 2;
+    cst_kids(C.bin, other, lg == 0 ? cl : og, lg == 0 ? og : cl);
+    moved_to(A, cl, other);
     // propagateBBChange(other -> x): the other child's box, its slots in order
-    const DBox ob = lg == 0 ? dbox_union(cb[lc], gb[o][1]) : dbox_union(gb[o][0], cb[lc]);
-    set_kids(X, lc == 0 ? g[o][lg] : c[0], lc == 0 ? c[1] : g[o][lg]);
-    set_slot(X, o, ob);
-    set_slot(X, lc, gb[o][lg]);
-    moved_to(A, g[o][lg], x, lc);
-    // BVHNodeInfo::changeCount, net: the other child's objects change by the swap
-    rec_store(A.nrec + 8 * (size_t)other, ob, cn[o] + cn[lc] - gn[o][lg]);
-    const DBox xb = lc == 0 ? dbox_union(gb[o][lg], ob) : dbox_union(ob, gb[o][lg]);
-    rec_store(xr, xb, xn);
-    return xb;
+    const DBox ob = bsel(lg == 0, dbox_union(L.b, ogb), dbox_union(ogb, L.b));
+    const int on = O.n + L.n - gn;   // BVHNodeInfo::changeCount, net
+    cst_kids(C.bin, x, lc == 0 ? g : co, lc == 0 ? co : g);
+    moved_to(A, g, x);
+    rec_store(C.nrec, other, ob, on);
+    r.b = bsel(lc == 0, dbox_union(gb, ob), dbox_union(ob, gb));
+    r.k[0] = lc == 0 ? g : co;   r.k[1] = lc == 0 ? co : g;
+    r.kb[0] = bsel(lc == 0, gb, ob); r.kb[1] = bsel(lc == 0, ob, gb);
+    r.kn[0] = lc == 0 ? gn : on; r.kn[1] = lc == 0 ? on : gn;
+    rec_store(C.nrec, x, r.b, r.n);
+    return r;
 }
 
-// One thread per leaf: Woop data and the leaf's box, then up both trees.
-__global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
-    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
-    if (i >= A.n_leaf) return;
-    const uint4 lf = A.leaf[i];
+// The same, the thread having arrived from child slot `from` with that child's
+// view; the sibling's comes from the records.
+__device__ __forceinline__ View rebuild_node(const RebuildArgs& A, const Coh& C, uint32_t x, const int32_t c[2], int from,
+                                             const View& me) {
+    const View sib = load_view(A, C, from == 0 ? c[1] : c[0]);
+    View v[2];
+    v[0] = vsel(from == 0, me, sib);
+    v[1] = vsel(from == 0, sib, me);
+    return recompute_node(A, C, x, c, v);
+}
+
+// A leaf record: {holder << 1 | slot, first entry, entries, mode}; the mode
+// (set by the plan, then by each launch's anim_slot_kernel for the next one)
+// pairs the two leaves of a node whose children are both leaves: the one in
+// slot 0 takes both and recomputes their node without an arrival, the other
+// has nothing to do.
+constexpr uint32_t kLeafSingle = 0xffffffffu, kLeafPartner = 0xfffffffeu;   // else: the partner's record
+
+// AnimProvider::setObject (AnimatedMesh.cpp:113-117) for a leaf's entries, and
+// the leaf's box (its triangles' boxes extended from AABB::Identity)
+__device__ __forceinline__ View leaf_view(const RebuildArgs& A, const Coh& C, uint32_t i, uint32_t first, uint32_t count) {
     float lo[3], hi[3];
     box_empty(lo, hi);
 #pragma unroll 2
-    for (uint32_t e = lf.y; e < lf.y + lf.z; e++) {
+    for (uint32_t e = first; e < first + count; e++) {
         const uint32_t t = A.idx[e] >> 1;
         const f3 a = ld3(A.P, A.tris[3 * t]), b = ld3(A.P, A.tris[3 * t + 1]), c = ld3(A.P, A.tris[3 * t + 2]);
         float w[12];
@@ -359,52 +418,181 @@ __global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
         const float q1[3] = {tmax(tmax(a.x, b.x), c.x), tmax(tmax(a.y, b.y), c.y), tmax(tmax(a.z, b.z), c.z)};
         box_extend(lo, hi, q0, q1);
     }
-    const DBox lb{{lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}};
-    rec_store(A.lrec + 8 * (size_t)i, lb, (int)lf.z);
-    // the 4-wide copy: its leaf slot, then every node whose slots have all arrived
-    if (A.wide) {
-        uint32_t w = lf.w >> 2, sl = lf.w & 3u;
-        DBox b = lb;
-        for (;;) {
-            WideNode& W = A.wide[w];
-            W.lo_x[sl] = b.lo[0]; W.lo_y[sl] = b.lo[1]; W.lo_z[sl] = b.lo[2];
-            W.hi_x[sl] = b.hi[0]; W.hi_y[sl] = b.hi[1]; W.hi_z[sl] = b.hi[2];
-            const int4 ch = *reinterpret_cast<const int4*>(W.child);   // the topology: fixed since the upload
-            const uint32_t need = (ch.x != kSent) + (ch.y != kSent) + (ch.z != kSent) + (ch.w != kSent);
-            if (!arrive(A.wcnt, w, need)) break;
-            const uint32_t up = A.wup[w];
-            if (up == 0xffffffffu) break;
-            const int32_t chk[4] = {ch.x, ch.y, ch.z, ch.w};
-            b = dbox_identity();
-            for (int k = 0; k < 4; k++) {
-                if (chk[k] == kSent) continue;
-                DBox cbx;
-                int n;
-                if (chk[k] >= 0) rec_load(A.wrec + 8 * (size_t)chk[k], cbx, n);
-                else rec_load(A.lrec + 8 * (size_t)A.leaf_of[(uint32_t)~chk[k] >> 3], cbx, n);
-                b = dbox_union(b, cbx);
-            }
-            rec_store(A.wrec + 8 * (size_t)w, b, 0);
-            w = up >> 2;
-            sl = up & 3u;
-        }
+    View me;
+    me.b = DBox{{lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}};
+    me.n = (int)count;
+    me.k[0] = me.k[1] = kSent;
+    me.kb[0] = me.kb[1] = dbox_identity();
+    me.kn[0] = me.kn[1] = 0;
+    rec_store(C.lrec, i, me.b, me.n);
+    return me;
+}
+
+// After node x: on to its parent (false at the root, whose box is m_sLocalBox =
+// BVHNodeData::getBox, both slots).  The parent word is moved only by a
+// rotation above x, which comes later.
+__device__ __forceinline__ bool climb_up(const RebuildArgs& A, uint32_t& x, int32_t& prev, const View& me) {
+    const int32_t p = __float_as_int(A.bin[16 * (size_t)x + 14]);
+    if (p < 0) {
+        for (int q = 0; q < 3; q++) { A.mesh_box[q] = me.b.lo[q]; A.mesh_box[3 + q] = me.b.hi[q]; }
+        return false;
     }
-    // the binary tree: each node whose children have all arrived (the holder writes
-    // the leaf's slot from its record)
+    prev = (int32_t)(x << 2);
+    x = (uint32_t)p >> 2;
+    return true;
+}
+
+// One thread per leaf (or leaf pair): Woop data and the leaf's box, then up the binary tree.
+__global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
+    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
+    if (i >= A.n_leaf) return;
+    const uint4 lf = A.leaf[i];
+    if (lf.w == kLeafPartner) return;
+    const Coh C = coh_of(A);
+    View me = leaf_view(A, C, i, lf.y, lf.z);
+    int32_t prev = (int32_t)~lf.y;   // the child value the thread comes from
     uint32_t x = lf.x >> 1;
+    if (lf.w != kLeafSingle) {   // both children of x: no arrival, no records to read
+        const uint4 pf = A.leaf[lf.w];
+        View v[2];
+        v[0] = me;
+        v[1] = leaf_view(A, C, lf.w, pf.y, pf.z);
+        const int32_t c[2] = {(int32_t)~lf.y, (int32_t)~pf.y};
+        me = recompute_node(A, C, x, c, v);
+        if (!climb_up(A, x, prev, me)) return;
+    }
+    // each node whose children have all arrived, recomputed by the last arrival
     for (;;) {
-        float* X = A.bin + 16 * (size_t)x;
         int32_t k[2];
-        kids_plain(X, k);   // unchanged until this node is rebuilt (by the last arrival)
+        kids_plain(A.bin + 16 * (size_t)x, k);   // unchanged until this node is rebuilt (by the last arrival)
         const uint32_t need = (k[0] != kSent) + (k[1] != kSent);
         if (!arrive(A.cnt, x, need)) return;
-        const DBox xb = rebuild_node(A, x, k);
-        const int32_t p = __float_as_int(X[14]);
-        if (p < 0) {   // the root: m_sLocalBox = BVHNodeData::getBox, both slots
-            for (int q = 0; q < 3; q++) { A.mesh_box[q] = xb.lo[q]; A.mesh_box[3 + q] = xb.hi[q]; }
-            return;
+        me = rebuild_node(A, C, x, k, k[0] == prev ? 0 : 1, me);
+        if (!climb_up(A, x, prev, me)) return;
+    }
+}
+
+// node->setLeft / setRight for every node: its two slots from its children's
+// final records (an empty slot keeps what it holds), three whole 16-B stores;
+// and each leaf child's holder and pairing for the next launch.
+__global__ __launch_bounds__(kAB) void anim_slot_kernel(float* bin, const float* nrec, const float* lrec,
+                                                       const uint32_t* leaf_of, uint4* leaf, uint32_t n_nodes) {
+    const uint32_t x = blockIdx.x * kAB + threadIdx.x;
+    if (x >= n_nodes) return;
+    float4* X = reinterpret_cast<float4*>(bin + 16 * (size_t)x);
+    const int4 k4 = reinterpret_cast<const int4*>(X)[3];
+    const int32_t k[2] = {k4.x, k4.y};
+    float4 s[2] = {}, z = {};
+    if (k[0] == kSent || k[1] == kSent) { s[0] = X[0]; s[1] = X[1]; z = X[2]; }
+    float zz[4] = {z.x, z.y, z.z, z.w};
+    uint32_t lr[2] = {kLeafSingle, kLeafSingle};
+    for (int c = 0; c < 2; c++) {
+        if (k[c] == kSent) continue;
+        const bool lv = k[c] < 0;
+        if (lv) lr[c] = leaf_of[(uint32_t)~k[c]];
+        const float* r = lv ? lrec + 8 * (size_t)lr[c] : nrec + 8 * (size_t)((uint32_t)k[c] >> 2);
+        const float4 a = reinterpret_cast<const float4*>(r)[0], b = reinterpret_cast<const float4*>(r)[1];
+        s[c] = make_float4(a.x, a.w, a.y, b.x);   // {lo.x hi.x lo.y hi.y}
+        zz[2 * c] = a.z;
+        zz[2 * c + 1] = b.y;
+    }
+    X[0] = s[0];
+    X[1] = s[1];
+    X[2] = make_float4(zz[0], zz[1], zz[2], zz[3]);
+    const bool pair = lr[0] != kLeafSingle && lr[1] != kLeafSingle;
+    for (int c = 0; c < 2; c++) {
+        if (lr[c] == kLeafSingle) continue;
+        leaf[lr[c]].x = x << 1 | (uint32_t)c;
+        leaf[lr[c]].w = !pair ? kLeafSingle : c == 0 ? lr[1] : kLeafPartner;
+    }
+}
+
+// The 4-wide copy, refit in the topology the upload collapsed.  Per node, the
+// plan's child codes: an empty slot 0xffffffff, a leaf its lrec record << 2 | 1,
+// an inner child its node << 2 (its box in wrec) or, between nodes of the
+// one-block top, its position there << 2 | 2 (its box in LDS).
+struct WideArgs {
+    WideNode* wide;
+    float* wrec;               // per node: the union of its slots, for its parent
+    const float* lrec;
+    const uint4* code;
+    const uint32_t* order;     // nodes by height, children first
+};
+constexpr uint32_t kNoChild = 0xffffffffu;
+__device__ __forceinline__ DBox rec6(const float* base, uint32_t i) {
+    const float4* r = reinterpret_cast<const float4*>(base + 8 * (size_t)i);
+    const float4 a = r[0], c = r[1];
+    return DBox{{a.x, a.y, a.z}, {a.w, c.x, c.y}};
+}
+// each occupied slot gets its child's box, an empty one keeps what it holds
+// (whole 16-B stores: lo_x .. hi_z over the four slots); returns the union of
+// the occupied slots in slot order
+__device__ __forceinline__ DBox wide_write(WideNode* W, const uint32_t c[4], DBox cb[4]) {
+    DBox b = dbox_identity();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (c[q] == kNoChild)
+            cb[q] = DBox{{W->lo_x[q], W->lo_y[q], W->lo_z[q]}, {W->hi_x[q], W->hi_y[q], W->hi_z[q]}};
+        else
+            b = dbox_union(b, cb[q]);
+    }
+    float4* F = reinterpret_cast<float4*>(W);
+    for (int k = 0; k < 3; k++) {
+        F[2 * k] = make_float4(cb[0].lo[k], cb[1].lo[k], cb[2].lo[k], cb[3].lo[k]);
+        F[2 * k + 1] = make_float4(cb[0].hi[k], cb[1].hi[k], cb[2].hi[k], cb[3].hi[k]);
+    }
+    return b;
+}
+// one height below the top (its children are lower: earlier launches)
+__global__ __launch_bounds__(kAB) void anim_wide_kernel(WideArgs A, uint32_t first, uint32_t n) {
+    const uint32_t j = blockIdx.x * kAB + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t w = A.order[first + j];
+    const uint4 cd = A.code[w];
+    const uint32_t c[4] = {cd.x, cd.y, cd.z, cd.w};
+    DBox cb[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if (c[q] != kNoChild) cb[q] = rec6((c[q] & 1) ? A.lrec : A.wrec, c[q] >> 2);
+    const DBox b = wide_write(A.wide + w, c, cb);
+    float4* R = reinterpret_cast<float4*>(A.wrec + 8 * (size_t)w);
+    R[0] = make_float4(b.lo[0], b.lo[1], b.lo[2], b.hi[0]);
+    R[1] = make_float4(b.hi[1], b.hi[2], 0.0f, 0.0f);
+}
+// the top heights (at most kTopMax nodes), height after height in one block:
+// their nodes and child codes staged in LDS first, their boxes handed up there
+constexpr int kTopWide = 1024;
+constexpr uint32_t kTopMax = 2048;
+__global__ __launch_bounds__(kTopWide) void anim_wide_top_kernel(WideArgs A, const uint32_t* off, uint32_t n_heights) {
+    __shared__ float box[6 * kTopMax];
+    __shared__ uint4 code[kTopMax];
+    __shared__ uint32_t node[kTopMax];
+    const uint32_t base = off[0], n = off[n_heights] - base;
+    for (uint32_t j = threadIdx.x; j < n; j += kTopWide) {
+        node[j] = A.order[base + j];
+        code[j] = A.code[node[j]];
+    }
+    __syncthreads();
+    for (uint32_t h = 0; h < n_heights; h++) {
+        for (uint32_t j = off[h] - base + threadIdx.x; j < off[h + 1] - base; j += kTopWide) {
+            const uint4 cd = code[j];
+            const uint32_t c[4] = {cd.x, cd.y, cd.z, cd.w};
+            DBox cb[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (c[q] == kNoChild) continue;
+                if ((c[q] & 3) == 2) {
+                    const float* l = box + 6 * (c[q] >> 2);
+                    cb[q] = DBox{{l[0], l[1], l[2]}, {l[3], l[4], l[5]}};
+                } else {
+                    cb[q] = rec6((c[q] & 1) ? A.lrec : A.wrec, c[q] >> 2);
+                }
+            }
+            const DBox b = wide_write(A.wide + node[j], c, cb);
+            float* l = box + 6 * j;
+            for (int k = 0; k < 3; k++) { l[k] = b.lo[k]; l[3 + k] = b.hi[k]; }
         }
-        x = (uint32_t)p >> 2;
+        __syncthreads();
     }
 }
 
@@ -478,16 +666,15 @@ bool anim_upload(AnimState* A, T** dst, const T* src, size_t n) {
 }
 
 // The rebuild plan of a mesh tree (the compiled tree the upload put on the
-// device): its leaves with the slots that hold them, the objects under every
-// node, and the 4-wide copy's parent links and leaf slots.
+// device): its leaves with the slots that hold them, and the 4-wide copy's
+// nodes by height.
 bool plan_mesh(AnimState* A, MeshRebuild& R, const ctl_bvh_node* nodes, uint32_t n_nodes, uint32_t n_entries,
                const uint32_t* idx, const WideNode* wn, uint32_t n_wide, std::string& err) {
     R.n_nodes = n_nodes;
     if (n_nodes == 0) { err = "rebuild plan: empty tree"; return false; }
     std::vector<uint4> leaves;
-    std::vector<int32_t> objects(n_nodes, 0);
     std::vector<uint8_t> seen(n_entries, 0), node_seen(n_nodes, 0);
-    // pre-order from the root, then the objects children first
+    // pre-order from the root: every node reached once, its parent word its parent
     std::vector<uint32_t> pre, st{0};
     node_seen[0] = 1;
     while (!st.empty()) {
@@ -513,61 +700,116 @@ bool plan_mesh(AnimState* A, MeshRebuild& R, const ctl_bvh_node* nodes, uint32_t
                 seen[e] = 1;
                 if (idx[e] & 1) break;
             }
-            leaves.push_back(make_uint4(k << 1 | (uint32_t)c, (uint32_t)~v, e + 1 - (uint32_t)~v, 0xffffffffu));
+            leaves.push_back(make_uint4(k << 1 | (uint32_t)c, (uint32_t)~v, e + 1 - (uint32_t)~v, kLeafSingle));
         }
     }
     if (rb_parent(nodes[0]) >= 0) { err = "rebuild plan: the root has a parent word"; return false; }
     if (std::find(seen.begin(), seen.end(), 0) != seen.end()) { err = "rebuild plan: an entry lies in no leaf"; return false; }
-    for (size_t i = pre.size(); i-- > 0;) {
-        const uint32_t k = pre[i];
-        for (int c = 0; c < 2; c++) {
-            const int32_t v = rb_kid(nodes[k], c);
-            if (v == kSent) continue;
-            if (v >= 0) objects[k] += objects[(uint32_t)v >> 2];
-            else for (uint32_t e = (uint32_t)~v;; e++) { objects[k]++; if (idx[e] & 1) break; }
-        }
-    }
-    // node records: the box is written when the node is rebuilt, the objects persist
-    std::vector<float> nrec(8ull * n_nodes, 0.0f);
-    for (uint32_t k = 0; k < n_nodes; k++) std::memcpy(&nrec[8ull * k + 6], &objects[k], 4);
+    if (64ull * n_nodes > 0xffffffffull) { err = "rebuild plan: a mesh tree of more than 64 M nodes"; return false; }
     std::sort(leaves.begin(), leaves.end(), [](uint4 a, uint4 b) { return a.y < b.y; });
     std::vector<uint32_t> leaf_of(n_entries, 0xffffffffu);
     for (size_t i = 0; i < leaves.size(); i++) leaf_of[leaves[i].y] = (uint32_t)i;
-    // the 4-wide copy: every leaf slot is one binary leaf (counted: first entry << 3 | count)
-    std::vector<uint32_t> wup(n_wide, 0xffffffffu);
+    for (uint4& l : leaves) l.w = kLeafSingle;
+    for (uint32_t k = 0; k < n_nodes; k++) {   // a node's two leaf children: the pairing of anim_slot_kernel
+        const int32_t a = rb_kid(nodes[k], 0), b = rb_kid(nodes[k], 1);
+        if (a >= 0 || b >= 0 || a == kSent || b == kSent || !node_seen[k]) continue;
+        leaves[leaf_of[(uint32_t)~a]].w = leaf_of[(uint32_t)~b];
+        leaves[leaf_of[(uint32_t)~b]].w = kLeafPartner;
+    }
+    // the 4-wide copy: every leaf slot is one binary leaf (counted: first entry << 3 | count),
+    // every node but the root one node's child; its nodes ordered by height
+    std::vector<uint32_t> worder;
+    std::vector<uint4> wcode;
+    R.woff.clear();
     if (n_wide) {
-        std::vector<uint32_t> wide_leaf(n_entries, 0xffffffffu);
+        std::vector<uint32_t> up(n_wide, 0xffffffffu), height(n_wide, 0);
+        std::vector<uint8_t> wleaf(n_entries, 0);
         for (uint32_t i = 0; i < n_wide; i++)
             for (int q = 0; q < 4; q++) {
                 const int32_t v = wn[i].child[q];
                 if (v == kSent) continue;
                 if (v >= 0) {
-                    if ((uint32_t)v >= n_wide || wup[v] != 0xffffffffu) { err = "rebuild plan: malformed 4-wide tree"; return false; }
-                    wup[v] = i << 2 | (uint32_t)q;
-                } else {
-                    const uint32_t first = (uint32_t)~v >> 3;
-                    if (first >= n_entries || leaf_of[first] == 0xffffffffu) {
-                        err = "rebuild plan: a 4-wide leaf is no binary leaf";
+                    if ((uint32_t)v >= n_wide || up[v] != 0xffffffffu || (uint32_t)v == i) {
+                        err = "rebuild plan: malformed 4-wide tree";
                         return false;
                     }
-                    wide_leaf[first] = i << 2 | (uint32_t)q;
+                    up[v] = i;
+                } else {
+                    const uint32_t first = (uint32_t)~v >> 3;
+                    if (first >= n_entries || leaf_of[first] == 0xffffffffu || wleaf[first]) {
+                        err = "rebuild plan: a 4-wide leaf is no binary leaf, or repeats";
+                        return false;
+                    }
+                    wleaf[first] = 1;
                 }
             }
-        for (uint4& l : leaves) {
-            l.w = wide_leaf[l.y];
-            if (l.w == 0xffffffffu) { err = "rebuild plan: a binary leaf is in no 4-wide leaf slot"; return false; }
+        for (const uint4& l : leaves)
+            if (!wleaf[l.y]) { err = "rebuild plan: a binary leaf is in no 4-wide leaf slot"; return false; }
+        // heights from one root, children first (iterative post-order)
+        uint32_t root = 0xffffffffu;
+        for (uint32_t i = 0; i < n_wide; i++)
+            if (up[i] == 0xffffffffu) {
+                if (root != 0xffffffffu) { err = "rebuild plan: the 4-wide tree has two roots"; return false; }
+                root = i;
+            }
+        if (root == 0xffffffffu) { err = "rebuild plan: the 4-wide tree has no root"; return false; }
+        std::vector<uint32_t> post, st{root};
+        while (!st.empty()) {
+            const uint32_t k = st.back();
+            st.pop_back();
+            post.push_back(k);
+            for (int q = 0; q < 4; q++) {
+                const int32_t v = wn[k].child[q];
+                if (v >= 0 && v != kSent) st.push_back((uint32_t)v);
+            }
+        }
+        if (post.size() != n_wide) { err = "rebuild plan: 4-wide nodes unreachable from the root"; return false; }
+        uint32_t hmax = 0;
+        for (size_t j = post.size(); j-- > 0;) {
+            const uint32_t k = post[j];
+            uint32_t h = 1;
+            for (int q = 0; q < 4; q++) {
+                const int32_t v = wn[k].child[q];
+                if (v >= 0 && v != kSent) h = std::max(h, height[v] + 1);
+            }
+            height[k] = h;
+            hmax = std::max(hmax, h);
+        }
+        R.woff.assign(hmax + 1, 0);   // heights 1..hmax -> woff[h - 1] .. woff[h]
+        for (uint32_t i = 0; i < n_wide; i++) R.woff[height[i]]++;
+        for (uint32_t h = 1; h <= hmax; h++) R.woff[h] += R.woff[h - 1];
+        worder.resize(n_wide);
+        std::vector<uint32_t> fill(R.woff.begin(), R.woff.end() - 1), pos(n_wide);
+        for (uint32_t i = 0; i < n_wide; i++) {
+            pos[i] = fill[height[i] - 1]++;
+            worder[pos[i]] = i;
+        }
+        // the top: the highest heights while they hold at most kTopMax nodes together
+        R.wtop = hmax;
+        while (R.wtop > 0 && n_wide - R.woff[R.wtop - 1] <= kTopMax) R.wtop--;
+        const uint32_t top0 = R.woff[R.wtop];
+        wcode.resize(n_wide);
+        for (uint32_t i = 0; i < n_wide; i++) {
+            uint32_t c[4];
+            for (int q = 0; q < 4; q++) {
+                const int32_t v = wn[i].child[q];
+                c[q] = v == kSent ? kNoChild
+                       : v < 0    ? leaf_of[(uint32_t)~v >> 3] << 2 | 1u
+                       : pos[i] >= top0 && pos[v] >= top0 ? (pos[v] - top0) << 2 | 2u
+                                                          : (uint32_t)v << 2;
+            }
+            wcode[i] = make_uint4(c[0], c[1], c[2], c[3]);
         }
     }
     R.n_leaf = (uint32_t)leaves.size();
     R.n_wide = n_wide;
     if (!anim_upload(A, &R.d_leaf, leaves.data(), leaves.size()) ||
-        !anim_upload(A, &R.d_leaf_of, leaf_of.data(), leaf_of.size()) ||
-        !anim_upload(A, &R.d_nrec, nrec.data(), nrec.size()) || !anim_alloc(A, &R.d_cnt, n_nodes) ||
-        !anim_alloc(A, &R.d_lrec, 8 * std::max<size_t>(1, leaves.size())) ||
-        (n_wide && !anim_alloc(A, &R.d_wrec, 8ull * n_wide)) ||
+        !anim_upload(A, &R.d_leaf_of, leaf_of.data(), leaf_of.size()) || !anim_alloc(A, &R.d_nrec, 8ull * n_nodes) ||
+        !anim_alloc(A, &R.d_cnt, n_nodes) || !anim_alloc(A, &R.d_lrec, 8 * std::max<size_t>(1, leaves.size())) ||
         hipMemset(R.d_cnt, 0, n_nodes * sizeof(uint32_t)) != hipSuccess ||
-        (n_wide && (!anim_upload(A, &R.d_wup, wup.data(), wup.size()) || !anim_alloc(A, &R.d_wcnt, n_wide) ||
-                    hipMemset(R.d_wcnt, 0, n_wide * sizeof(uint32_t)) != hipSuccess))) {
+        (n_wide && (!anim_alloc(A, &R.d_wrec, 8ull * n_wide) || !anim_upload(A, &R.d_worder, worder.data(), n_wide) ||
+                    !anim_upload(A, &R.d_woff, R.woff.data(), R.woff.size()) ||
+                    !anim_upload(A, &R.d_wcode, wcode.data(), n_wide)))) {
         err = "rebuild plan: upload failed";
         return false;
     }
@@ -788,7 +1030,6 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
     if (P.rb.n_leaf) {
         RebuildArgs R;
         R.bin = reinterpret_cast<float*>(const_cast<float4*>(S.bvh)) + 4ull * P.km.bvh_node_offset;
-        R.wide = S.wide && P.rb.n_wide ? reinterpret_cast<WideNode*>(const_cast<float4*>(S.wbvh)) + P.wide_base : nullptr;
         R.idx = S.tri_idx + P.km.bvh_indices_offset;
         R.tris = tris;
         R.P = A->d_P;
@@ -797,13 +1038,25 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         R.leaf_of = P.rb.d_leaf_of;
         R.nrec = P.rb.d_nrec;
         R.lrec = P.rb.d_lrec;
-        R.wrec = P.rb.d_wrec;
         R.cnt = P.rb.d_cnt;
-        R.wup = P.rb.d_wup;
-        R.wcnt = P.rb.d_wcnt;
         R.mesh_box = A->d_mesh_boxes + 6 * P.am.mesh;
         R.n_leaf = P.rb.n_leaf;
+        R.n_nodes = P.rb.n_nodes;
         hipLaunchKernelGGL(anim_rebuild_kernel, dim3((P.rb.n_leaf + kAB - 1) / kAB), dim3(kAB), 0, s, R);
+        hipLaunchKernelGGL(anim_slot_kernel, dim3((P.rb.n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, R.bin, R.nrec, R.lrec,
+                           R.leaf_of, R.leaf, P.rb.n_nodes);
+        if (S.wide && P.rb.n_wide) {
+            // the 4-wide copy: a launch per height below the top, the top in one block
+            const WideArgs W{reinterpret_cast<WideNode*>(const_cast<float4*>(S.wbvh)) + P.wide_base, P.rb.d_wrec, R.lrec,
+                             P.rb.d_wcode, P.rb.d_worder};
+            const uint32_t nh = (uint32_t)P.rb.woff.size() - 1;
+            for (uint32_t h = 0; h < P.rb.wtop; h++) {
+                const uint32_t n = P.rb.woff[h + 1] - P.rb.woff[h];
+                hipLaunchKernelGGL(anim_wide_kernel, dim3((n + kAB - 1) / kAB), dim3(kAB), 0, s, W, P.rb.woff[h], n);
+            }
+            hipLaunchKernelGGL(anim_wide_top_kernel, dim3(1), dim3(kTopWide), 0, s, W, P.rb.d_woff + P.rb.wtop,
+                               nh - P.rb.wtop);
+        }
     }
     if (hipGetLastError() != hipSuccess) { c->err = "scene_animate: launch failed"; return CTL_ERR_HIP; }
     // instances of the mesh, the instance tree, epsilon (DynamicScene::AnimateMesh invalidates the node)

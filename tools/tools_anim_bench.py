@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--bones", type=int, default=16)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--binary", action="store_true", help="CTL_SCENE_BINARY_BVH: no 4-wide copy to refit")
     a = ap.parse_args()
     import ctypes as C
     import torch
@@ -62,6 +63,8 @@ def main():
     s.add_node(0)
     s.set_camera([0, 8, -20], [0, 0, 0], [0, 1, 0], 50, 64, 64)
     d = s.compile()
+    if a.binary:
+        d.flags |= ctl.CTL_SCENE_BINARY_BVH
     t_build = time.perf_counter() - t0
     pt = ctl.PathTracer(0)
     pt.upload_scene(d)
@@ -85,7 +88,8 @@ def main():
     alg = nv * 72 + nt * (12 + 64 + 96) + ne * (4 + 12 + 48 + 48) + nn * 128 + nt * 60 + (nn // 2) * 256
     per = sorted(ms)[len(ms) // 2]
     print(json.dumps({
-        "workload": f"skinned grid {a.n}x{a.n} quads: {nv} vertices, {nt} triangles, {a.bones} bones, 4 influences",
+        "workload": f"skinned grid {a.n}x{a.n} quads: {nv} vertices, {nt} triangles, {a.bones} bones, 4 influences"
+                    + (", binary tree only" if a.binary else ""),
         "ms_per_animate_median": round(per, 4), "ms_min": round(min(ms), 4),
         "mtris_per_s": round(nt / per / 1e3, 1),
         "alg_bytes_per_animate": int(alg), "alg_GBps": round(alg / (per * 1e-3) / 1e9, 1),
