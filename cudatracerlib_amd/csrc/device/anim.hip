@@ -185,10 +185,15 @@ __device__ __forceinline__ float dbox_area(const DBox& b) {
 // ms per animate.  The arrival orders the accesses: a thread's records complete
 // (s_waitcnt vmcnt(0)) before its arrival increments the counter, and the last
 // arriver's loads are issued after the counter's value came back.
-constexpr int kSC1 = 16;   // cache-policy operand of the buffer intrinsics: SC1
+// CTL_REBUILD_DIAG (timing-only builds, never shipped): 1 leaves out the climb, 2 drops SC1 from the shared records and every
+// rotation (so no stale read can reach a child word), 3 drops the rotations
+#ifndef CTL_REBUILD_DIAG
+#define CTL_REBUILD_DIAG 0
+#endif
+constexpr int kSC1 = CTL_REBUILD_DIAG == 2 ? 0 : 16;   // cache-policy operand of the buffer intrinsics: SC1
 
 struct Coh {               // buffer descriptors of the arrays the climb shares
-    __amdgpu_buffer_rsrc_t bin, nrec, lrec;
+    __amdgpu_buffer_rsrc_t bin, nrec;
 };
 __device__ __forceinline__ float4 cld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSC1));
@@ -241,7 +246,7 @@ struct RebuildArgs {
     uint4* leaf;
     const uint32_t* leaf_of;
     float* nrec;                // per binary node {lo xyz, hi xyz, objects, 0}: written when the node is rebuilt
-    float* lrec;                // per leaf record, the same: written by the leaf's thread
+    float* lrec;                // per leaf record, the same: written by anim_leaf_kernel
     uint32_t* cnt;
     float* mesh_box;            // m_sLocalBox: 6 floats
     uint32_t n_leaf, n_nodes;
@@ -249,8 +254,7 @@ struct RebuildArgs {
 
 __device__ __forceinline__ Coh coh_of(const RebuildArgs& A) {
     return Coh{__builtin_amdgcn_make_buffer_rsrc(A.bin, 0, (int)(64u * A.n_nodes), 0x00020000),
-               __builtin_amdgcn_make_buffer_rsrc(A.nrec, 0, (int)(32u * A.n_nodes), 0x00020000),
-               __builtin_amdgcn_make_buffer_rsrc(A.lrec, 0, (int)(32u * A.n_leaf), 0x00020000)};
+               __builtin_amdgcn_make_buffer_rsrc(A.nrec, 0, (int)(32u * A.n_nodes), 0x00020000)};
 }
 
 // The last of `need` (1 or 2, fixed for a node: no rotation moves an empty
@@ -297,10 +301,13 @@ __device__ __forceinline__ View vsel(bool a, const View& x, const View& y) {
 // getBox / numLeafs of child value v (AABB::Identity and 0 for an empty slot)
 __device__ __forceinline__ void child_info(const RebuildArgs& A, const Coh& C, int32_t v, DBox& b, int& n) {
     if (v == kSent) { b = dbox_identity(); n = 0; return; }
-    const bool leaf = v < 0;
-    const uint32_t i = leaf ? A.leaf_of[(uint32_t)~v] : (uint32_t)v >> 2;
-    const __amdgpu_buffer_rsrc_t r = leaf ? C.lrec : C.nrec;
-    rec_unpack(cld4(r, 32u * i), cld4(r, 32u * i + 16u), b, n);
+    if (v < 0) {   // a leaf's record: from the leaf launch, plain
+        const float4* r = reinterpret_cast<const float4*>(A.lrec + 8 * (size_t)A.leaf_of[(uint32_t)~v]);
+        rec_unpack(r[0], r[1], b, n);
+        return;
+    }
+    const uint32_t i = (uint32_t)v >> 2;
+    rec_unpack(cld4(C.nrec, 32u * i), cld4(C.nrec, 32u * i + 16u), b, n);
 }
 __device__ __forceinline__ View load_view(const RebuildArgs& A, const Coh& C, int32_t v) {
     View w;
@@ -345,7 +352,7 @@ __device__ __forceinline__ View recompute_node(const RebuildArgs& A, const Coh& 
     const float now = dbox_area(v[0].b) * (float)v[0].n + dbox_area(v[1].b) * (float)v[1].n;
     View r;
     r.n = v[0].n + v[1].n;   // numLeafs(x): no rotation at x changes it
-    if (!(bestv < now)) {
+    if (!(bestv < now) || CTL_REBUILD_DIAG >= 2) {
         // getBox: both stored slots, an empty one as stored (both loaded, then
         // selected: a select of a load and a register became a scratch round trip)
         r.b = dbox_union(v[0].b, v[1].b);
@@ -400,31 +407,14 @@ __device__ __forceinline__ View rebuild_node(const RebuildArgs& A, const Coh& C,
 // has nothing to do.
 constexpr uint32_t kLeafSingle = 0xffffffffu, kLeafPartner = 0xfffffffeu;   // else: the partner's record
 
-// AnimProvider::setObject (AnimatedMesh.cpp:113-117) for a leaf's entries, and
-// the leaf's box (its triangles' boxes extended from AABB::Identity)
-__device__ __forceinline__ View leaf_view(const RebuildArgs& A, const Coh& C, uint32_t i, uint32_t first, uint32_t count) {
-    float lo[3], hi[3];
-    box_empty(lo, hi);
-#pragma unroll 2
-    for (uint32_t e = first; e < first + count; e++) {
-        const uint32_t t = A.idx[e] >> 1;
-        const f3 a = ld3(A.P, A.tris[3 * t]), b = ld3(A.P, A.tris[3 * t + 1]), c = ld3(A.P, A.tris[3 * t + 2]);
-        float w[12];
-        woop_set_hd(a, b, c, w);
-        A.woop[3 * e] = make_float4(w[0], w[1], w[2], w[3]);
-        A.woop[3 * e + 1] = make_float4(w[4], w[5], w[6], w[7]);
-        A.woop[3 * e + 2] = make_float4(w[8], w[9], w[10], w[11]);
-        const float q0[3] = {tmin(tmin(a.x, b.x), c.x), tmin(tmin(a.y, b.y), c.y), tmin(tmin(a.z, b.z), c.z)};
-        const float q1[3] = {tmax(tmax(a.x, b.x), c.x), tmax(tmax(a.y, b.y), c.y), tmax(tmax(a.z, b.z), c.z)};
-        box_extend(lo, hi, q0, q1);
-    }
+// A leaf's view: its record, written by anim_leaf_kernel (an earlier launch)
+__device__ __forceinline__ View leaf_view(const RebuildArgs& A, uint32_t i) {
     View me;
-    me.b = DBox{{lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}};
-    me.n = (int)count;
+    const float4* r = reinterpret_cast<const float4*>(A.lrec + 8 * (size_t)i);
+    rec_unpack(r[0], r[1], me.b, me.n);
     me.k[0] = me.k[1] = kSent;
     me.kb[0] = me.kb[1] = dbox_identity();
     me.kn[0] = me.kn[1] = 0;
-    rec_store(C.lrec, i, me.b, me.n);
     return me;
 }
 
@@ -442,21 +432,49 @@ __device__ __forceinline__ bool climb_up(const RebuildArgs& A, uint32_t& x, int3
     return true;
 }
 
-// One thread per leaf (or leaf pair): Woop data and the leaf's box, then up the binary tree.
-__global__ __launch_bounds__(kAB) void anim_rebuild_kernel(RebuildArgs A) {
+// One thread per leaf: AnimProvider::setObject (AnimatedMesh.cpp:113-117) for
+// its entries, and its record: the box (its triangles' boxes extended from
+// AABB::Identity) and the entries.
+__global__ __launch_bounds__(kAB) void anim_leaf_kernel(RebuildArgs A) {
     const uint32_t i = blockIdx.x * kAB + threadIdx.x;
     if (i >= A.n_leaf) return;
     const uint4 lf = A.leaf[i];
+    float lo[3], hi[3];
+    box_empty(lo, hi);
+#pragma unroll 2
+    for (uint32_t e = lf.y; e < lf.y + lf.z; e++) {
+        const uint32_t t = A.idx[e] >> 1;
+        const f3 a = ld3(A.P, A.tris[3 * t]), b = ld3(A.P, A.tris[3 * t + 1]), c = ld3(A.P, A.tris[3 * t + 2]);
+        float w[12];
+        woop_set_hd(a, b, c, w);
+        A.woop[3 * e] = make_float4(w[0], w[1], w[2], w[3]);
+        A.woop[3 * e + 1] = make_float4(w[4], w[5], w[6], w[7]);
+        A.woop[3 * e + 2] = make_float4(w[8], w[9], w[10], w[11]);
+        const float q0[3] = {tmin(tmin(a.x, b.x), c.x), tmin(tmin(a.y, b.y), c.y), tmin(tmin(a.z, b.z), c.z)};
+        const float q1[3] = {tmax(tmax(a.x, b.x), c.x), tmax(tmax(a.y, b.y), c.y), tmax(tmax(a.z, b.z), c.z)};
+        box_extend(lo, hi, q0, q1);
+    }
+    float4* r = reinterpret_cast<float4*>(A.lrec + 8 * (size_t)i);
+    r[0] = make_float4(lo[0], lo[1], lo[2], hi[0]);
+    r[1] = make_float4(hi[1], hi[2], __int_as_float((int)lf.z), 0.0f);
+}
+
+// One thread per leaf (or leaf pair) whose record the leaf launch wrote, up the
+// binary tree.  96 VGPRs, 5 waves per SIMD (the compiler's choice was 100 and 4).
+__global__ __launch_bounds__(kAB) __attribute__((amdgpu_waves_per_eu(5))) void anim_rebuild_kernel(RebuildArgs A) {
+    const uint32_t i = blockIdx.x * kAB + threadIdx.x;
+    if (i >= A.n_leaf || CTL_REBUILD_DIAG == 1) return;
+    const uint4 lf = A.leaf[i];
     if (lf.w == kLeafPartner) return;
     const Coh C = coh_of(A);
-    View me = leaf_view(A, C, i, lf.y, lf.z);
+    View me = leaf_view(A, i);
     int32_t prev = (int32_t)~lf.y;   // the child value the thread comes from
     uint32_t x = lf.x >> 1;
     if (lf.w != kLeafSingle) {   // both children of x: no arrival, no records to read
         const uint4 pf = A.leaf[lf.w];
         View v[2];
         v[0] = me;
-        v[1] = leaf_view(A, C, lf.w, pf.y, pf.z);
+        v[1] = leaf_view(A, lf.w);
         const int32_t c[2] = {(int32_t)~lf.y, (int32_t)~pf.y};
         me = recompute_node(A, C, x, c, v);
         if (!climb_up(A, x, prev, me)) return;
@@ -1042,6 +1060,7 @@ CTL_API ctl_status ctl_scene_animate(ctl_ctx* c, uint32_t anim, const ctl_float4
         R.mesh_box = A->d_mesh_boxes + 6 * P.am.mesh;
         R.n_leaf = P.rb.n_leaf;
         R.n_nodes = P.rb.n_nodes;
+        hipLaunchKernelGGL(anim_leaf_kernel, dim3((P.rb.n_leaf + kAB - 1) / kAB), dim3(kAB), 0, s, R);
         hipLaunchKernelGGL(anim_rebuild_kernel, dim3((P.rb.n_leaf + kAB - 1) / kAB), dim3(kAB), 0, s, R);
         hipLaunchKernelGGL(anim_slot_kernel, dim3((P.rb.n_nodes + kAB - 1) / kAB), dim3(kAB), 0, s, R.bin, R.nrec, R.lrec,
                            R.leaf_of, R.leaf, P.rb.n_nodes);

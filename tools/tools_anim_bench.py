@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--bones", type=int, default=16)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--binary", action="store_true", help="CTL_SCENE_BINARY_BVH: no 4-wide copy to refit")
+    ap.add_argument("--shape", action="store_true", help="also report the tree's depth and the nodes one animate rotates")
     a = ap.parse_args()
     import ctypes as C
     import torch
@@ -82,6 +83,23 @@ def main():
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
     nv, nt, ne, nn = V.shape[0], T.shape[0], int(d.n_woop_tris), int(d.n_bvh_nodes)
+    shape = {}
+    if a.shape:
+        from cudatracerlib_amd import _abi
+        before = pt.read_array(_abi.CTL_ARRAY_BVH_NODES, 0, nn, np.int32, 16)
+        pt.animate(0, f0, f1, 0.37)
+        after = pt.read_array(_abi.CTL_ARRAY_BVH_NODES, 0, nn, np.int32, 16)
+        shape["nodes_with_new_children"] = int(np.any(before[:, 12:14] != after[:, 12:14], axis=1).sum())
+        kids = after[:, 12:14]
+        depth = np.zeros(nn, np.int64)   # node depth from the root, by the parent words (d.z)
+        order = [0]
+        for k in order:
+            for c in kids[k]:
+                if 0 <= c and c != 0x76543210:
+                    depth[c >> 2] = depth[k] + 1
+                    order.append(int(c >> 2))
+        leaf_depth = [depth[k] + 1 for k in range(nn) for c in kids[k] if c < 0]
+        shape.update(max_leaf_depth=int(max(leaf_depth)), mean_leaf_depth=round(float(np.mean(leaf_depth)), 2))
     # algorithmic bytes: skin 40 in + 32 out per vertex; tris 12 idx + 32 in/out + 6 x 16 gathers;
     # woop 4 idx + 12 tri + 3 x 16 gathers + 48 out; refit binary 64 in + 64 out per node + leaf
     # gathers (12 + 48 per triangle), wide about half the nodes at 128 B each
@@ -95,6 +113,7 @@ def main():
         "alg_bytes_per_animate": int(alg), "alg_GBps": round(alg / (per * 1e-3) / 1e9, 1),
         "bvh_nodes": nn, "scene_build_s": round(t_build, 2),
         "note": "includes the epsilon readback (one stream sync) and 2 x 1 KB bone uploads",
+        **shape,
     }), flush=True)
     pt.close()
 
