@@ -526,3 +526,127 @@ def test_animate_rejects_bad_bones(ctl, dev):
     with pytest.raises(ctl.CTLError):
         pt.animate(1, eye, eye, 0.5)         # one animated mesh only
     pt.close()
+
+
+def expected_wide(upload, wbase, d, nodes):
+    """The 4-wide mesh trees as the rebuild must leave them: the upload's
+    topology, each leaf slot the leaf's box (read from the binary tree's slot
+    that holds it: BVHNodeData's leaf box is its triangles' boxes extended from
+    AABB::Identity), each inner slot the union of the child node's occupied slots
+    in slot order (from AABB::Identity, `a < b ? a : b`), empty slots as
+    uploaded."""
+    out = upload.copy()
+    wi = out.view(np.int32)
+    f = nodes.view(np.float32).reshape(-1, 16)
+    n = nodes.view(np.int32).reshape(-1, 16)
+    nw = upload.shape[0]
+    for m in range(d.n_meshes):
+        k0 = d.meshes[m].bvh_node_offset // 4
+        k1 = d.meshes[m + 1].bvh_node_offset // 4 if m + 1 < d.n_meshes else d.n_bvh_nodes
+        w0, w1 = int(wbase[m]), int(wbase[m + 1]) if m + 1 < d.n_meshes else nw
+        leaf = {}
+        for k in range(k0, k1):
+            for c in range(2):
+                v = n[k, 12 + c]
+                if v < 0:
+                    leaf[~v] = (f[k, [0, 2, 8]] if c == 0 else f[k, [4, 6, 10]],
+                                f[k, [1, 3, 9]] if c == 0 else f[k, [5, 7, 11]])
+        post, st = [], [w0]
+        while st:
+            k = st.pop()
+            post.append(k)
+            st += [w0 + v for v in wi[k, 24:28] if 0 <= v != 0x76543210]
+        for k in reversed(post):
+            for q in range(4):
+                v = wi[k, 24 + q]
+                if v == 0x76543210:
+                    continue
+                if v < 0:
+                    lo, hi = leaf[(~v) >> 3]
+                else:
+                    ch = w0 + v
+                    lo = np.full(3, np.finfo(np.float32).max, np.float32)
+                    hi = -lo
+                    for r in range(4):
+                        if wi[ch, 24 + r] == 0x76543210:
+                            continue
+                        clo, chi = out[ch, [r, 8 + r, 16 + r]], out[ch, [4 + r, 12 + r, 20 + r]]
+                        lo, hi = np.where(lo < clo, lo, clo), np.where(hi > chi, hi, chi)
+                out[k, [q, 8 + q, 16 + q]] = lo
+                out[k, [4 + q, 12 + q, 20 + q]] = hi
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bvh", ["wide", "binary"])
+def test_small_and_several_animated_meshes_bit_exact(ctl, orc, dev, bvh):
+    """Three animated meshes (1 triangle: a root with one empty slot; 3
+    triangles; the tube) animated in turn over three rounds, each frame from the
+    last one's trees: every array equals the oracle's, and the 4-wide copy equals
+    its upload topology refit from the oracle's leaf boxes (expected_wide)."""
+    A = ctl._abi
+    s = ctl.HostScene()
+    one = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32)
+    three = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0], [1, 1, 0.5], [2, 0, 0.2]], np.float32)
+    small = []
+    for V, T in ((one, [[0, 1, 2]]), (three, [[0, 1, 2], [1, 3, 2], [1, 4, 3]])):
+        nv = V.shape[0]
+        bi = np.zeros((nv, 8), np.uint8)
+        bi[:, 1] = 1
+        bw = np.zeros((nv, 8), np.uint8)
+        bw[:, 0], bw[:, 1] = 200, 55
+        nrm = np.tile(np.array([[0, 0, 1]], np.float32), (nv, 1))
+        small.append(s.add_animated_mesh(V, nrm, bi, bw, np.array(T, np.uint32), [ctl.diffuse_material(0.6, 0.6, 0.6)],
+                                         uvs=V[:, :2].copy()))
+    v, nrm, bi, bw, tris, uv = skinned_tube()
+    m_tube = s.add_animated_mesh(v, nrm, bi, bw, tris, [ctl.diffuse_material(0.7, 0.5, 0.3)], uvs=uv)
+    ground = np.array([[-6, -0.5, -6], [6, -0.5, -6], [6, -0.5, 6], [-6, -0.5, 6]], np.float32)
+    m_g = s.add_mesh(ground, [[0, 2, 1], [0, 3, 2]], [ctl.diffuse_material(0.5, 0.5, 0.5)])
+    for i, m in enumerate(small + [m_tube]):
+        s.add_node(m, [1, 0, 0, 2.0 * i, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1])
+    nl = s.add_node(m_g)
+    s.add_area_light(nl, 0, [5.0, 5.0, 5.0])
+    s.set_camera([1.2, 2.5, -9], [1.2, 1.8, 0], [0, 1, 0], 50, 32, 24)
+    d = s.compile()
+    if bvh == "binary":
+        d = binary_bvh(d)
+    f0, f1 = frames()
+    pt = ctl.PathTracer(0)
+    pt.upload_scene(d)
+    upload = None if bvh == "binary" else pt.wide_trees(d)
+    keep = None
+    for rnd in range(3):
+        for anim in range(3):
+            lerp = 0.2 + 0.25 * rnd + 0.05 * anim
+            pt.animate(anim, f0, f1, lerp)
+            tri = _arr(d.tri_data, C.c_uint32, d.n_tri_data * 8) if keep is None else keep[0]
+            woop = _arr(d.woop_tris, C.c_float, d.n_woop_tris * 12) if keep is None else keep[1]
+            if keep is None:
+                nodes = _arr(d.bvh_nodes, C.c_float, d.n_bvh_nodes * 16)
+                scene = _arr(d.scene_bvh_nodes, C.c_float, max(1, d.n_scene_bvh_nodes) * 16)
+                boxes = _arr(d.mesh_boxes, C.c_float, d.n_meshes * 6)
+            else:
+                nodes, scene, boxes = keep[2], keep[3], keep[4]
+            eps = np.zeros(1, np.float32)
+            orc.oracle_animate(C.byref(d), anim, oracle.ptr(f0), oracle.ptr(f1), lerp, oracle.ptr(tri),
+                               oracle.ptr(woop), oracle.ptr(nodes), oracle.ptr(scene), oracle.ptr(boxes),
+                               oracle.ptr(eps))
+            keep = (tri, woop, nodes, scene, boxes)
+            got = pt.read_array(A.CTL_ARRAY_BVH_NODES, 0, d.n_bvh_nodes, np.uint32, 16)
+            assert np.array_equal(got.ravel(), nodes.view(np.uint32)), (rnd, anim)
+            got = pt.read_array(A.CTL_ARRAY_WOOP, 0, d.n_woop_tris, np.uint32, 12)
+            assert np.array_equal(got.ravel(), woop.view(np.uint32)), (rnd, anim)
+            got = pt.read_array(A.CTL_ARRAY_TRI_DATA, 0, d.n_tri_data, np.uint32, 8)
+            assert np.array_equal(got.ravel(), tri), (rnd, anim)
+            got = pt.read_array(A.CTL_ARRAY_SCENE_BVH, 0, d.n_scene_bvh_nodes, np.uint32, 16)
+            assert np.array_equal(got.ravel(), scene[:d.n_scene_bvh_nodes * 16].view(np.uint32)), (rnd, anim)
+            got = pt.read_array(A.CTL_ARRAY_MESH_BOXES, 0, d.n_meshes, np.float32, 6)
+            assert np.array_equal(got.ravel().view(np.uint32), boxes.view(np.uint32)), (rnd, anim)
+            assert pt.read_array(A.CTL_ARRAY_RAY_EPS, 0, 1, np.float32, 1)[0, 0] == eps[0]
+            if upload is not None:
+                mesh, wbase, _ = pt.wide_trees(d)
+                want = expected_wide(upload[0], upload[1], d, nodes)
+                assert np.array_equal(mesh.view(np.uint32), want.view(np.uint32)), (rnd, anim)
+    n = nodes.view(np.int32).reshape(-1, 16)
+    assert (n[:, 12:14] == 0x76543210).any()   # the 1-triangle mesh's root keeps an empty slot
+    pt.close()
