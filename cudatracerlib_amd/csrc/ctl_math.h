@@ -45,20 +45,6 @@ CTL_HD float fracf_ref(float f) { return f - floorf(f); }                 // Mat
 #else
 #define CTL_CR CTL_HD
 #endif
-#if defined(CTL_CR_FAST_TIMING) && defined(__HIP_DEVICE_COMPILE__)
-// timing-only builds (never shipped, not bit-exact): the fp32 library instead,
-// the upper bound of a faster exact implementation
-CTL_CR float cr_sin(float x) { return sinf(x); }
-CTL_CR float cr_cos(float x) { return cosf(x); }
-CTL_CR float cr_tan(float x) { return tanf(x); }
-CTL_CR float cr_acos(float x) { return acosf(x); }
-CTL_CR float cr_atan2(float y, float x) { return atan2f(y, x); }
-CTL_CR float cr_atan(float x) { return atanf(x); }
-CTL_CR float cr_exp(float x) { return expf(x); }
-CTL_CR float cr_log(float x) { return logf(x); }
-CTL_CR float cr_log2(float x) { return log2f(x); }
-CTL_CR float cr_pow(float a, float b) { return powf(a, b); }
-#else
 CTL_CR float cr_sin(float x) { return (float)sin((double)x); }
 CTL_CR float cr_cos(float x) { return (float)cos((double)x); }
 CTL_CR float cr_tan(float x) { return (float)tan((double)x); }
@@ -69,7 +55,6 @@ CTL_CR float cr_exp(float x) { return (float)exp((double)x); }
 CTL_CR float cr_log(float x) { return (float)log((double)x); }
 CTL_CR float cr_log2(float x) { return (float)log2((double)x); }
 CTL_CR float cr_pow(float a, float b) { return (float)pow((double)a, (double)b); }
-#endif
 
 struct f2 { float x, y; };
 struct f3 { float x, y, z; };

@@ -516,7 +516,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SINGLE ?
     wave_add_u64(&counters[12], ts.inner_r);
     wave_add_u64(&counters[13], ts.rounds);
     wave_add_u64(&counters[14], ts.leafphase_in);
-    wave_add_u64(&counters[15], ts.uni_waves);
 #endif
 }
 
@@ -1211,7 +1210,7 @@ static ctl_status render_pass_speculative(ctl_ctx* c, const ctl_pt_params* param
 CTL_API ctl_status ctl_render_pass(ctl_ctx* c, const ctl_pt_params* params, ctl_pixel* d_fb, void* stream) {
 #ifdef CTL_PROFILE_TRACE
     ctl_status r = launch_pass(c, params, d_fb, false, stream);
-    unsigned long long v[11];
+    unsigned long long v[10];
     if (hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)) == hipSuccess &&
         hipMemcpy(v, c->d_counters + 5, sizeof(v), hipMemcpyDeviceToHost) == hipSuccess) {
         fprintf(stderr, "[profile] trace/total wave time %.4f (%llu / %llu); inner loop: %llu wave iterations, "
@@ -1219,8 +1218,7 @@ CTL_API ctl_status ctl_render_pass(ctl_ctx* c, const ctl_pt_params* params, ctl_
                 (double)v[0] / (double)v[1], v[0], v[1], v[4], (double)v[3] / (double)v[4], v[6],
                 (double)v[5] / (double)v[6]);
         fprintf(stderr, "[profile] lanes in the round per inner iteration %.1f; rounds %llu, lanes holding a leaf at the "
-                        "leaf phase %.1f; 4-wide inner iterations with one node for the wave %.3f\n",
-                (double)v[7] / (double)v[4], v[8], (double)v[9] / (double)v[8], (double)v[10] / (double)v[4]);
+                        "leaf phase %.1f\n", (double)v[7] / (double)v[4], v[8], (double)v[9] / (double)v[8]);
         (void)hipMemset(c->d_counters + 5, 0, sizeof(v));
     }
     return r;

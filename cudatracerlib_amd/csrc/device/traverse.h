@@ -121,7 +121,6 @@ struct TraceStats {
     // in; per wave (counted on the first active lane), iterations executed
     uint32_t inner_lanes = 0, inner_waves = 0, leaf_lanes = 0, leaf_waves = 0;
     uint32_t round_r = 0, inner_r = 0, rounds = 0, leafphase_in = 0;
-    uint32_t uni_waves = 0;   // 4-wide inner iterations whose active lanes all fetch one node
 #endif
 };
 #ifdef CTL_PROFILE_TRACE
@@ -542,14 +541,6 @@ struct Traverser4 {
             const int top1 = ctl_lds_stack[max(min(sp - 1, kLdsStack - 1), 0) * kStackBlock + st.tid];
             const int top2 = ctl_lds_stack[max(min(sp - 2, kLdsStack - 1), 0) * kStackBlock + st.tid];
             CTL_PROF_COUNT(stats, inner_lanes, inner_waves);
-#ifdef CTL_PROFILE_TRACE
-            {
-                const uint32_t mine = nodeBase + (uint32_t)nodeAddr;
-                const uint32_t first = __builtin_amdgcn_readfirstlane(mine);
-                if (__ballot(mine != first) == 0 && (int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1)
-                    stats->uni_waves++;
-            }
-#endif
             if (STATS) stats->nodes++;
             int k0, k1, k2, k3;
             const uint32_t off = (nodeBase + (uint32_t)nodeAddr) << 7;
