@@ -61,6 +61,7 @@ def parse(argv=None):
     ap.add_argument("--closest-shadow-passes", type=int, default=4,
                     help="passes of the leg with the reference's closest-hit Occluded shadow rays (0: skip)")
     ap.add_argument("--prim-passes", type=int, default=16, help="C1 PrimTracer leg passes (0: skip)")
+    ap.add_argument("--anim-iters", type=int, default=20, help="animation leg: timed ctl_scene_animate calls (0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--schedule", default="persistent", choices=["persistent", "megakernel", "wavefront"])
@@ -619,6 +620,51 @@ def c1_prim_leg(ctl, dev, torch, passes):
             "note": "plumbing config: 65 k rays per pass, launch-latency bound"}
 
 
+def animation_leg(ctl, dev, torch, iters, n=1024):
+    """SURVEY 8(f) row 4: ctl_scene_animate (AnimatedMesh::k_ComputeState with
+    BVHRebuilder::Build(&p, true)'s recompute and SAH rotations) on the skinned grid
+    of tools/tools_anim_bench.py (n x n quads, 2 n^2 triangles, 16 bones), on its
+    own context: three untimed calls (the tree's shape carries over), then `iters`
+    calls each bracketed by HIP events on the stream they run on.  A call includes
+    the skinning, TriangleData, Woop data, the mesh tree's rebuild, the 4-wide copy,
+    the instance boxes / epsilon and their read-back (one stream sync)."""
+    import importlib.util
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("tools_anim_bench", os.path.join(here, "tools", "tools_anim_bench.py"))
+    tab = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tab)
+    V, N, BI, BW, T, UV = tab.grid(n, 16)
+    s = ctl.HostScene()
+    s.add_animated_mesh(V, N, BI, BW, T, [ctl.diffuse_material(0.5, 0.5, 0.5)], uvs=UV)
+    s.add_node(0)
+    s.set_camera([0, 8, -20], [0, 0, 0], [0, 1, 0], 50, 64, 64)
+    d = s.compile()
+    pt = ctl.PathTracer(dev.index or 0)
+    try:
+        pt.upload_scene(d)
+        f0, f1 = tab.frames(16, 0.0), tab.frames(16, 1.0)
+        for _ in range(3):
+            pt.animate(0, f0, f1, 0.5)
+        torch.cuda.synchronize()
+        ms = []
+        for k in range(iters):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            pt.animate(0, f0, f1, (k + 0.5) / iters)
+            e1.record()
+            torch.cuda.synchronize()
+            ms.append(e0.elapsed_time(e1))
+    finally:
+        pt.close()
+    med = sorted(ms)[len(ms) // 2]
+    return {"workload": f"skinned grid {n}x{n} quads: {V.shape[0]} vertices, {T.shape[0]} triangles, 16 bones, "
+                        f"{int(d.n_bvh_nodes)} binary nodes rebuilt with rotations, the 4-wide copy refit",
+            "calls": iters, "ms_per_animate_median": round(med, 4), "ms_min": round(min(ms), 4),
+            "mtris_per_s": round(T.shape[0] / med / 1e3, 1),
+            "note": "ctl_scene_animate per call (HIP events); the reference runs BVHRebuilder on the host after a "
+                    "device-to-host copy (AnimatedMesh.cpp:170-180)"}
+
+
 def c5_leg(ctl, dev, torch, stream, sptr, a, threads):
     """BASELINE configs[4] (C5, the textured / rough-material scene) on its own
     context: the full-shading path kernel (path_kernel_persistent FULL=1) at the
@@ -1013,6 +1059,12 @@ def main(argv=None):
             c5 = c5_leg(ctl, dev, torch, stream, sptr, a, threads)
         except Exception as e:
             c5 = {"error": f"{type(e).__name__}: {e}"}
+    anim = None
+    if rank == 0 and a.anim_iters > 0:
+        try:   # a side leg, like C1; last, so that it perturbs no other leg
+            anim = animation_leg(ctl, dev, torch, a.anim_iters)
+        except Exception as e:
+            anim = {"error": f"{type(e).__name__}: {e}"}
     red = dev if a.backend == "nccl" else torch.device("cpu")
     ranks = rank_report(dist, world, elapsed, a.steps, red0.elapsed_time(red1) if red0 is not None else None, red,
                         t_build, scene_source)
@@ -1128,6 +1180,7 @@ def main(argv=None):
             "parity_vs_reference_order": reference_order_record(),
             "wavefront_tracer": wpt,
             "prim_tracer_c1": c1,
+            "animation": anim,
             "path_tracer_c5": c5,
             "image_weight_sum": wsum,
             "scene_build_s": round(t_build, 2),

@@ -5,7 +5,7 @@
 set -o pipefail
 LIBS=${LIBS:-"base=_ab/base.so new=cudatracerlib_amd/_lib/libctl_trace.so"}
 mkdir -p gpurun_out/ab_libs
-ARGS="--steps 20 --warmup 5 --no-cpu-baseline --wpt-passes 0 --closest-shadow-passes 0 --prim-passes 0 --binary-passes 0 --one-pass-leg 0 --dopass-leg 0 --c5-passes 0"
+ARGS="--steps 20 --warmup 5 --no-cpu-baseline --wpt-passes 0 --closest-shadow-passes 0 --prim-passes 0 --binary-passes 0 --one-pass-leg 0 --dopass-leg 0 --c5-passes 0 --anim-iters 0"
 for i in 1 2; do
   for kv in $LIBS; do
     tag=${kv%%=*}; lib=${kv#*=}

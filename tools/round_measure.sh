@@ -21,7 +21,7 @@ export CTL_PMC_PROFILE=gpurun_out/pmc/pmc.json   # box-local: the runs below rea
 fi
 timeout -k 10 900 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { echo "BENCH FAILED"; tail -20 gpurun_out/bench_full.err; exit 1; }
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --emulate-ranks 8 --emulate-rank 5 --no-cpu-baseline \
-    --wpt-passes 0 --prim-passes 0 --c5-passes 0 --closest-shadow-passes 0 > gpurun_out/emul_rank5_of_8.json 2> gpurun_out/emul.err || { echo "EMULATED RANK FAILED"; tail -20 gpurun_out/emul.err; exit 1; }
+    --wpt-passes 0 --prim-passes 0 --c5-passes 0 --closest-shadow-passes 0 --anim-iters 0 > gpurun_out/emul_rank5_of_8.json 2> gpurun_out/emul.err || { echo "EMULATED RANK FAILED"; tail -20 gpurun_out/emul.err; exit 1; }
 bash tools/rehearsal_2rank.sh > gpurun_out/rehearsal.log 2>&1 || { echo "REHEARSAL FAILED"; tail -20 gpurun_out/rehearsal.log; exit 1; }
 python3 tools/bench_summary.py gpurun_out/bench_full.json
 python3 - <<'PY'

@@ -6,7 +6,7 @@
 set -o pipefail
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS="--steps 8 --warmup 0 --ceiling 0 --no-cpu-baseline --binary-passes 0 --wpt-passes 0 --closest-shadow-passes 0 --one-pass-leg 0 --prim-passes 0 --c5-passes 0 --dopass-leg 0 $*"
+ARGS="--steps 8 --warmup 0 --ceiling 0 --no-cpu-baseline --binary-passes 0 --wpt-passes 0 --closest-shadow-passes 0 --one-pass-leg 0 --prim-passes 0 --c5-passes 0 --dopass-leg 0 --anim-iters 0 $*"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCC_HIT_sum TCC_MISS_sum" \
