@@ -169,24 +169,26 @@ __device__ __forceinline__ float dbox_area(const DBox& b) {
     const float x = b.hi[0] - b.lo[0], y = b.hi[1] - b.lo[1], z = b.hi[2] - b.lo[2];
     return 2.0f * (x * y + x * z + y * z);
 }
-// What one thread of the climb hands to another goes through 32-B records: per
-// leaf its box and objects (lrec), per binary node the same (nrec).  They are
-// written and read with the SC1 cache policy (buffer_load / buffer_store
-// dwordx4 sc1: coherent across the XCDs' L2s access by access), 16 B per access.
-// Words two threads of the launch may write (a moved subtree's parent word, a
-// moved leaf's holder, a rotated node's child words) are stored the same way,
-// so the last writer wins whatever the XCDs' write-back order.  The node slots
-// are not written by the climb at all: a second launch (anim_slot_kernel)
-// stores every node's two slots from its children's final records, plain and
-// whole, and the 4-wide copy is refit by height after that (anim_wide_kernel),
-// both reading what the climb left after a launch boundary.  An acquire /
-// release at agent scope would instead write back and invalidate the whole L2
-// at every arrival (buffer_wbl2 / buffer_inv sc1): the first version did, 7.85
-// ms per animate.  The arrival orders the accesses: a thread's records complete
-// (s_waitcnt vmcnt(0)) before its arrival increments the counter, and the last
-// arriver's loads are issued after the counter's value came back.
-// CTL_REBUILD_DIAG (timing-only builds, never shipped): 1 leaves out the climb, 2 drops SC1 from the shared records and every
-// rotation (so no stale read can reach a child word), 3 drops the rotations
+// What one thread of the climb hands to another goes through 32-B records (box
+// and objects) per binary node (nrec), written and read with the SC1 cache
+// policy (buffer_load / buffer_store dwordx4 sc1: coherent across the XCDs' L2s
+// access by access), 16 B per access.  Words two threads of the launch may
+// write (a moved subtree's parent word, a rotated node's child words) are
+// stored the same way, so the last writer wins whatever the XCDs' write-back
+// order.  The leaf records (lrec) come from the leaf launch before and are read
+// plain.  The climb writes no node slot and no leaf holder: a later launch
+// (anim_slot_kernel) stores every node's two slots from its children's final
+// records, plain and whole, and each leaf's holder and pairing, and the 4-wide
+// copy is refit by height after that (anim_wide_kernel), all reading what the
+// climb left after a launch boundary.  An acquire / release at agent scope
+// would instead write back and invalidate the whole L2 at every arrival
+// (buffer_wbl2 / buffer_inv sc1): the first version did, 7.85 ms per animate.
+// The arrival orders the accesses: a thread's records complete (s_waitcnt
+// vmcnt(0)) before its arrival increments the counter, and the last arriver's
+// loads are issued after the counter's value came back.
+// CTL_REBUILD_DIAG (timing-only builds, never shipped): 1 leaves out the climb,
+// 2 drops SC1 from the shared records and every rotation (so no stale read can
+// reach a child word), 3 drops the rotations
 #ifndef CTL_REBUILD_DIAG
 #define CTL_REBUILD_DIAG 0
 #endif
