@@ -45,9 +45,11 @@ constexpr int kStackMax = 128;
 // lanes of the wave still look for a leaf (1 = the reference's rule: none;
 // C3 sweep: 1 -> 2098, 2 -> 2164, 4 -> 2225, 6 -> 2237, 8 -> 2216, 16 -> 2146 Mrays/s;
 // later, with the current kernel, 5 / 6 / 7 agree within run-to-run noise, ~2250;
-// round 3 with the LDS-parked path state: 3 / 4 / 5 / 7 -> 3185 / 3187 / 3170 / 3151).
+// round 3 with the LDS-parked path state: 3 / 4 / 5 / 7 -> 3185 / 3187 / 3170 / 3151;
+// round 6, interleaved on one box: 1 / 2 / 3 / 4 / 6 / 8 -> 3139 / 3228 / 3235 / 3216 /
+// 3166 / 3134, C5 7.99 / 7.87 / 7.87 / 7.93 / 8.03 / 8.10 ms per pass).
 #ifndef CTL_LEAF_BREAK
-#define CTL_LEAF_BREAK 4
+#define CTL_LEAF_BREAK 3
 #endif
 
 // Per-ray visit order (round 4).  Every traversal is a function of its ray
